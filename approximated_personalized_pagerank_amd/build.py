@@ -1,0 +1,36 @@
+"""In-tree build of libppr_hip.so for gfx950 (hipcc, no JIT cache, no torch extension)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+from ._lib import LIB_PATH, PKG_DIR
+
+CSRC = os.path.join(PKG_DIR, "csrc")
+SOURCES = ["grank.hip", "host_graph.cpp"]
+HEADERS = ["ppr_device.h", os.path.join("..", "..", "include", "ppr_hip.h")]
+ARCH = os.environ.get("PPR_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    for f in SOURCES + HEADERS:
+        if os.path.getmtime(os.path.join(CSRC, f)) > t:
+            return True
+    return False
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB_PATH
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-result", "-Wno-unused-value",
+           "-o", LIB_PATH + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-lpthread"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH

@@ -1,0 +1,217 @@
+// host_graph.cpp -- host-side graph preparation behind the C ABI (include/ppr_hip.h).
+//
+//  * ppr_find_partitions_csr: the BFS 2-colouring GRank alternates over
+//    (reference include/internal/pprInternal.h:29-99), on the dense CSR whose ids follow the
+//    graph's iteration order, so it reproduces the reference's partitions exactly.
+//  * ppr_execution_order_csr: MCCompletePathV2's node order (include/mccompletepathv2.h:36-113).
+//  * ppr_rmat_generate: the synthetic RMAT graphs the benchmarks run on (Graph500 a/b/c/d
+//    quadrant recursion, counter-based RNG, vertex labels scrambled by a bijection, duplicate
+//    edges removed, self-loops kept, successors ascending).
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/ppr_hip.h"
+
+namespace {
+
+inline uint64_t splitmix64(uint64_t& s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+// bijection on `bits`-bit integers: odd multiplies and xor-shifts modulo 2^bits
+inline uint64_t scramble(uint64_t x, int bits, uint64_t seed) {
+  if (bits == 0) return 0;
+  const uint64_t mask = bits >= 64 ? ~0ULL : ((1ULL << bits) - 1);
+  uint64_t s = seed ^ 0xD1B54A32D192ED03ULL;
+  for (int r = 0; r < 3; r++) {
+    uint64_t mul = splitmix64(s) | 1ULL;
+    uint64_t add = splitmix64(s);
+    x = (x * mul + add) & mask;
+    x ^= x >> ((bits + 1) / 2);
+  }
+  return x & mask;
+}
+
+template <class F>
+void parallel_for(int64_t n, int nthreads, F f) {
+  if (nthreads <= 1 || n < 4096) { f(0, n, 0); return; }
+  std::vector<std::thread> th;
+  int64_t chunk = (n + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; t++) {
+    int64_t b = t * chunk, e = std::min<int64_t>(n, b + chunk);
+    if (b >= e) break;
+    th.emplace_back(f, b, e, t);
+  }
+  for (auto& t : th) t.join();
+}
+
+int hw_threads() {
+  unsigned h = std::thread::hardware_concurrency();
+  if (h == 0) h = 1;
+  return (int)std::min<unsigned>(h, 16);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ppr_find_partitions_csr(const ppr_csr* g, uint8_t* part) {
+  if (!g || !part || g->n < 0) return PPR_ERR_ARG;
+  const int64_t n = g->n;
+  if (n == 0) return PPR_OK;
+  const int64_t* rp = g->row_ptr;
+  const int32_t* col = g->col;
+  const int64_t m = rp[n];
+  // predecessor lists in graph-iteration order (pprInternal.h:38-47)
+  std::vector<int64_t> prp(n + 1, 0);
+  for (int64_t e = 0; e < m; e++) {
+    if (col[e] < 0 || col[e] >= n) return PPR_ERR_GRAPH;
+    prp[col[e] + 1]++;
+  }
+  for (int64_t i = 0; i < n; i++) prp[i + 1] += prp[i];
+  std::vector<int32_t> pcol(m > 0 ? m : 1);
+  {
+    std::vector<int64_t> fill(prp.begin(), prp.end() - 1);
+    for (int64_t v = 0; v < n; v++)
+      for (int64_t e = rp[v]; e < rp[v + 1]; e++) pcol[fill[col[e]]++] = (int32_t)v;
+  }
+  std::vector<uint8_t> vis(n, 0);
+  std::vector<int32_t> q(n);
+  for (int64_t r = 0; r < n; r++) {
+    if (vis[r]) continue;
+    int64_t qh = 0, qt = 0;
+    vis[r] = 1; part[r] = 0; q[qt++] = (int32_t)r;   // root joins partitions.first (:57-63)
+    while (qh < qt) {
+      const int32_t x = q[qh++];
+      const uint8_t c = part[x] ^ 1;                  // opposite colour (:69-70)
+      for (int64_t e = rp[x]; e < rp[x + 1]; e++) {
+        const int32_t s = col[e];
+        if (!vis[s]) { vis[s] = 1; part[s] = c; q[qt++] = s; }
+      }
+      for (int64_t e = prp[x]; e < prp[x + 1]; e++) {
+        const int32_t s = pcol[e];
+        if (!vis[s]) { vis[s] = 1; part[s] = c; q[qt++] = s; }
+      }
+    }
+  }
+  return PPR_OK;
+}
+
+int ppr_execution_order_csr(const ppr_csr* g, int32_t* order) {
+  if (!g || !order || g->n < 0) return PPR_ERR_ARG;
+  const int64_t n = g->n;
+  if (n == 0) return PPR_OK;
+  const int64_t* rp = g->row_ptr;
+  const int32_t* col = g->col;
+  const int64_t m = rp[n];
+  std::vector<int64_t> prp(n + 1, 0);
+  for (int64_t e = 0; e < m; e++) prp[col[e] + 1]++;
+  for (int64_t i = 0; i < n; i++) prp[i + 1] += prp[i];
+  std::vector<int32_t> pcol(m > 0 ? m : 1);
+  {
+    std::vector<int64_t> fill(prp.begin(), prp.end() - 1);
+    for (int64_t v = 0; v < n; v++)
+      for (int64_t e = rp[v]; e < rp[v + 1]; e++) pcol[fill[col[e]]++] = (int32_t)v;
+  }
+  // sort by (indegree desc, outdegree asc) (include/mccompletepathv2.h:52-62); std::sort is not
+  // stable, so equal (in,out) pairs keep an implementation-defined order in the reference. We
+  // use a stable sort (graph order within equal pairs): a documented, deterministic choice.
+  std::vector<int32_t> sorted(n);
+  for (int64_t i = 0; i < n; i++) sorted[i] = (int32_t)i;
+  std::stable_sort(sorted.begin(), sorted.end(), [&](int32_t a, int32_t b) {
+    int64_t ia = prp[a + 1] - prp[a], ib = prp[b + 1] - prp[b];
+    if (ia != ib) return ia > ib;
+    return (rp[a + 1] - rp[a]) < (rp[b + 1] - rp[b]);
+  });
+  // predecessor-release BFS (:64-111)
+  std::vector<int64_t> wait(n);
+  for (int64_t v = 0; v < n; v++) wait[v] = rp[v + 1] - rp[v];
+  std::vector<uint8_t> vis(n, 0);
+  std::vector<int32_t> q(n);
+  int64_t out = 0;
+  for (int64_t i = 0; i < n; i++) {
+    const int32_t node = sorted[i];
+    if (vis[node]) continue;
+    int64_t qh = 0, qt = 0;
+    q[qt++] = node;
+    while (qh < qt) {
+      const int32_t x = q[qh++];
+      if (out >= n) return PPR_ERR_GRAPH;
+      order[out++] = x;
+      vis[x] = 1;
+      for (int64_t e = prp[x]; e < prp[x + 1]; e++) {
+        const int32_t p = pcol[e];
+        if (wait[p]-- > 0) {
+          if (wait[p] == 0 && !vis[p]) q[qt++] = p;
+        }
+      }
+    }
+  }
+  // every node is emitted exactly once: released at most once (wait hits 0 once) and taken as
+  // a root only when unvisited with an empty queue
+  return (int)(out == n ? PPR_OK : PPR_ERR_GRAPH);
+}
+
+int64_t ppr_rmat_generate(int32_t scale, int32_t edge_factor, double a, double b, double c,
+                          uint64_t seed, int64_t* row_ptr, int32_t* col, int64_t col_cap) {
+  if (scale < 0 || scale > 30 || edge_factor < 0 || !row_ptr) return -PPR_ERR_ARG;
+  const int64_t n = 1LL << scale;
+  const int64_t m0 = (int64_t)edge_factor * n;
+  const int nth = hw_threads();
+  const double ab = a + b, abc = a + b + c;
+  std::vector<uint64_t> edges(m0);
+  parallel_for(m0, nth, [&](int64_t b0, int64_t e0, int) {
+    for (int64_t e = b0; e < e0; e++) {
+      uint64_t s = seed * 0x100000001B3ULL ^ (uint64_t)e * 0x9E3779B97F4A7C15ULL;
+      splitmix64(s);
+      uint64_t src = 0, dst = 0;
+      for (int l = 0; l < scale; l++) {
+        const double u = (double)(splitmix64(s) >> 11) * (1.0 / 9007199254740992.0);
+        const uint64_t bs = u >= ab, bd = (u >= a && u < ab) || u >= abc;
+        src = (src << 1) | bs;
+        dst = (dst << 1) | bd;
+      }
+      src = scramble(src, scale, seed);
+      dst = scramble(dst, scale, seed);
+      edges[e] = (src << 32) | dst;
+    }
+  });
+  // bucket by source (counting sort), then sort + unique each row
+  std::vector<int64_t> cnt(n + 1, 0);
+  for (int64_t e = 0; e < m0; e++) cnt[(edges[e] >> 32) + 1]++;
+  for (int64_t i = 0; i < n; i++) cnt[i + 1] += cnt[i];
+  std::vector<uint32_t> tmp(m0);
+  {
+    std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
+    for (int64_t e = 0; e < m0; e++) tmp[fill[edges[e] >> 32]++] = (uint32_t)(edges[e] & 0xffffffffu);
+  }
+  std::vector<uint64_t>().swap(edges);
+  std::vector<int64_t> deg(n, 0);
+  parallel_for(n, nth, [&](int64_t b0, int64_t e0, int) {
+    for (int64_t v = b0; v < e0; v++) {
+      uint32_t* p = tmp.data() + cnt[v];
+      int64_t k = cnt[v + 1] - cnt[v];
+      std::sort(p, p + k);
+      deg[v] = std::unique(p, p + k) - p;
+    }
+  });
+  row_ptr[0] = 0;
+  for (int64_t v = 0; v < n; v++) row_ptr[v + 1] = row_ptr[v] + deg[v];
+  const int64_t m = row_ptr[n];
+  if (!col) return m;          // size query
+  if (col_cap < m) return -PPR_ERR_ARG;
+  parallel_for(n, nth, [&](int64_t b0, int64_t e0, int) {
+    for (int64_t v = b0; v < e0; v++)
+      std::memcpy(col + row_ptr[v], tmp.data() + cnt[v], sizeof(int32_t) * deg[v]);
+  });
+  return m;
+}
+
+}  // extern "C"

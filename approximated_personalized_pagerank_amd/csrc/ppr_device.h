@@ -1,0 +1,300 @@
+// ppr_device.h -- wave-level device primitives of the basket-merge kernels (gfx950, wave64).
+//
+// Everything here is executed by ONE 64-lane wavefront and relies on the in-order execution of
+// a wave's LDS instructions; `wave_fence()` only stops the compiler from moving memory
+// operations across phase boundaries (it emits no instruction).
+//
+// Semantics implemented (reference file:line):
+//  * accumulation   include/grank.h:107-116  acc[k] = fma(s, d/deg, acc[k]) in successor order;
+//                   a key appears at most once per successor basket, so within a 64-candidate
+//                   group the only conflicts are the same key from different successors; they
+//                   are applied lowest lane (= earliest successor) first ("owner rounds").
+//  * top-L          include/internal/pprInternal.h:109-137 with the deterministic order
+//                   (score desc, dense id asc): radix select on the fp64 bit pattern (scores are
+//                   >= 0, so IEEE bits order like the values), ties resolved on ~id.
+//  * norm1          include/internal/pprInternal.h:147-165, summed in the fixed 64-lane pattern
+//                   restated in oracle/grank_oracle.c:norm1_rows.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pprd {
+
+constexpr int WAVE = 64;
+constexpr int EMPTY = -1;
+constexpr uint32_t NO_OWNER = 0xffffffffu;
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+__device__ __forceinline__ void wave_fence() { __asm__ __volatile__("" ::: "memory"); }
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const int l = lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+__device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
+__device__ __forceinline__ double bitsd(uint64_t x) { return __longlong_as_double((long long)x); }
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ int wave_incl_scan(int x) {
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane_id() >= o) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_or(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) x |= (uint64_t)__shfl_xor((unsigned long long)x, o);
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_and(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) x &= (uint64_t)__shfl_xor((unsigned long long)x, o);
+  return x;
+}
+__device__ __forceinline__ int wave_sum(int x) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS accumulation table: open addressing, linear probing, keys unique.
+struct LdsTable {
+  int* keys;
+  uint32_t* owner;
+  double* acc;
+  uint32_t mask;  // capacity - 1 (power of two)
+};
+
+__device__ __forceinline__ void table_clear(const LdsTable& t) {
+  for (uint32_t i = lane_id(); i <= t.mask; i += WAVE) { t.keys[i] = EMPTY; t.owner[i] = NO_OWNER; }
+  wave_fence();
+}
+
+// find-or-insert; an inserting lane zeroes the accumulator (reference: operator[] value-inits)
+__device__ __forceinline__ uint32_t table_slot(const LdsTable& t, int key) {
+  uint32_t h = hash32((uint32_t)key) & t.mask;
+  for (;;) {
+    const int cur = t.keys[h];
+    if (cur == key) return h;
+    if (cur == EMPTY) {
+      const int prev = atomicCAS(&t.keys[h], EMPTY, key);
+      if (prev == EMPTY) { t.acc[h] = 0.0; return h; }
+      if (prev == key) return h;
+    }
+    h = (h + 1) & t.mask;
+  }
+}
+
+// Apply one group of <= 64 ordered candidates (lane order == successor order).
+__device__ __forceinline__ void table_apply(const LdsTable& t, bool valid, int key, double s,
+                                            double factor) {
+  const uint32_t slot = valid ? table_slot(t, key) : 0u;
+  wave_fence();
+  bool pending = valid;
+  const uint32_t me = (uint32_t)lane_id();
+  while (__ballot(pending)) {
+    if (pending) atomicMin(&t.owner[slot], me);
+    wave_fence();
+    if (pending && t.owner[slot] == me) {
+      t.acc[slot] = fma(s, factor, t.acc[slot]);
+      t.owner[slot] = NO_OWNER;
+      pending = false;
+    }
+    wave_fence();
+  }
+}
+
+// In-place compaction of occupied slots to the front (keys[0..U), acc[0..U)); returns U.
+__device__ __forceinline__ int table_compact(const LdsTable& t) {
+  int U = 0;
+  for (uint32_t base = 0; base <= t.mask; base += WAVE) {
+    const uint32_t i = base + lane_id();
+    const int k = t.keys[i];
+    const double a = t.acc[i];
+    const bool occ = k != EMPTY;
+    const uint64_t m = __ballot(occ);
+    wave_fence();
+    if (occ) {
+      const int pos = U + __popcll(m & lanemask_lt());
+      t.keys[pos] = k;
+      t.acc[pos] = a;
+    }
+    wave_fence();
+    U += __popcll(m);
+  }
+  return U;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Top-`need` selection by (score desc, id asc) over n entries (keys[i], vals[i]) held in LDS or
+// global memory. Result: entry i is selected iff
+//     (v & ma) > pa  ||  ((v & ma) == pa && (!tie || (w & mb) >= pb))      v = bits(score), w = ~id
+struct SelCrit {
+  uint64_t pa, ma;
+  uint64_t pb, mb;
+  bool tie;
+};
+
+// radix select of the k-th largest 64-bit value among filtered entries (8-bit digits from the
+// highest bit that varies). On return: prefix/mask fix the boundary bucket; k = how many of the
+// boundary bucket are selected; resolved = boundary holds exactly-equal values with more than k
+// members (a tie that the caller must break on another field).
+template <class GetV, class Filt>
+__device__ __forceinline__ void radix_kth_desc(int n, int& k, GetV getv, Filt filt,
+                                               uint32_t* hist, uint64_t& prefix, uint64_t& mask,
+                                               bool& tie_left) {
+  uint64_t lor = 0, land = ~0ull;
+  int cnt = 0;
+  for (int i = lane_id(); i < n; i += WAVE)
+    if (filt(i)) { const uint64_t v = getv(i); lor |= v; land &= v; cnt++; }
+  lor = wave_or(lor);
+  land = wave_and(land);
+  cnt = wave_sum(cnt);
+  const uint64_t diff = lor ^ land;
+  if (diff == 0) {  // every filtered value equal
+    prefix = land; mask = ~0ull; tie_left = cnt > k;
+    return;
+  }
+  const int top = 63 - __clzll((long long)diff);
+  mask = top == 63 ? 0ull : ~((2ull << top) - 1ull);
+  prefix = land & mask;
+  int shift = top >= 7 ? top - 7 : 0;
+  for (;;) {
+    for (int b = lane_id(); b < 256; b += WAVE) hist[b] = 0;
+    wave_fence();
+    for (int i = lane_id(); i < n; i += WAVE) {
+      if (!filt(i)) continue;
+      const uint64_t v = getv(i);
+      if ((v & mask) == prefix) atomicAdd(&hist[(uint32_t)(v >> shift) & 255u], 1u);
+    }
+    wave_fence();
+    // lane l owns bins 255-4l .. 252-4l (descending), scan finds the boundary bin
+    const int l = lane_id();
+    uint32_t c[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) c[j] = hist[255 - 4 * l - j];
+    const int s = (int)(c[0] + c[1] + c[2] + c[3]);
+    const int incl = wave_incl_scan(s);
+    int run = incl - s;
+    int bin = -1, above = 0, hb = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (bin < 0 && run < k && run + (int)c[j] >= k) { bin = 255 - 4 * l - j; above = run; hb = (int)c[j]; }
+      run += (int)c[j];
+    }
+    const uint64_t who = __ballot(bin >= 0);
+    const int src = __ffsll((long long)who) - 1;
+    bin = __shfl(bin, src);
+    above = __shfl(above, src);
+    hb = __shfl(hb, src);
+    k -= above;
+    prefix |= (uint64_t)bin << shift;
+    mask |= 255ull << shift;
+    wave_fence();
+    if (hb == k) { tie_left = false; return; }
+    if (shift == 0) { tie_left = true; return; }
+    shift = shift >= 8 ? shift - 8 : 0;
+  }
+}
+
+template <class KeyAt, class ValAt>
+__device__ __forceinline__ SelCrit select_top(int n, int need, KeyAt keyat, ValAt valat,
+                                              uint32_t* hist) {
+  SelCrit c;
+  c.tie = false; c.pb = 0; c.mb = 0;
+  int k = need;
+  bool tie = false;
+  radix_kth_desc(n, k, [&](int i) { return dbits(valat(i)); }, [&](int) { return true; },
+                 hist, c.pa, c.ma, tie);
+  if (tie) {
+    // all boundary entries carry exactly the same score: keep the k smallest ids
+    const uint64_t pa = c.pa;
+    bool tie2 = false;
+    radix_kth_desc(n, k, [&](int i) { return (uint64_t)(uint32_t)~keyat(i); },
+                   [&](int i) { return dbits(valat(i)) == pa; }, hist, c.pb, c.mb, tie2);
+    c.tie = true;
+  }
+  return c;
+}
+
+__device__ __forceinline__ bool sel_test(const SelCrit& c, uint64_t v, uint32_t w) {
+  const uint64_t va = v & c.ma;
+  if (va != c.pa) return va > c.pa;
+  return !c.tie || ((uint64_t)w & c.mb) >= c.pb;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row buffer (LDS): rv = score bits, rk = id; bitonic sort, (score desc, id asc).
+__device__ __forceinline__ bool row_less(uint64_t av, int ak, uint64_t bv, int bk) {
+  // "a ranks below b"
+  return av < bv || (av == bv && (uint32_t)~ak < (uint32_t)~bk);
+}
+
+__device__ __forceinline__ void row_sort(uint64_t* rv, int* rk, int cnt, int Lp) {
+  for (int i = cnt + lane_id(); i < Lp; i += WAVE) { rv[i] = 0; rk[i] = -1; }  // sentinels last
+  wave_fence();
+  for (int k = 2; k <= Lp; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = lane_id(); t < (Lp >> 1); t += WAVE) {
+        const int i = ((t / j) * 2 * j) + (t % j);
+        const int p = i + j;
+        const uint64_t av = rv[i], bv = rv[p];
+        const int ak = rk[i], bk = rk[p];
+        // descending overall: blocks with (i & k) == 0 descend
+        const bool desc = (i & k) == 0;
+        const bool swap = desc ? row_less(av, ak, bv, bk) : row_less(bv, bk, av, ak);
+        if (swap) { rv[i] = bv; rv[p] = av; rk[i] = bk; rk[p] = ak; }
+      }
+      wave_fence();
+    }
+  }
+}
+
+// norm1 between the new row (LDS rv/rk, cnt) and the old row (global ids/scores, olen), with
+// the fixed lane pattern of oracle/grank_oracle.c:norm1_rows. hk/hv: LDS hash of 2*Lp slots,
+// mf: LDS flags (Lp).
+__device__ __forceinline__ double row_norm1(const uint64_t* rv, const int* rk, int cnt,
+                                            const int* oid, const double* osc, int olen,
+                                            int* hk, int* hv, int* mf, int hsize) {
+  const uint32_t hmask = (uint32_t)hsize - 1;
+  for (int i = lane_id(); i < hsize; i += WAVE) hk[i] = EMPTY;
+  for (int j = lane_id(); j < olen; j += WAVE) mf[j] = 0;
+  wave_fence();
+  for (int j = lane_id(); j < olen; j += WAVE) {
+    const int key = oid[j];
+    uint32_t h = hash32((uint32_t)key) & hmask;
+    for (;;) {
+      const int prev = atomicCAS(&hk[h], EMPTY, key);
+      if (prev == EMPTY) { hv[h] = j; break; }
+      h = (h + 1) & hmask;
+    }
+  }
+  wave_fence();
+  double p = 0.0;
+  for (int i = lane_id(); i < cnt; i += WAVE) {
+    const int key = rk[i];
+    uint32_t h = hash32((uint32_t)key) & hmask;
+    double o = 0.0;
+    for (;;) {
+      const int cur = hk[h];
+      if (cur == key) { const int j = hv[h]; o = osc[j]; mf[j] = 1; break; }
+      if (cur == EMPTY) break;
+      h = (h + 1) & hmask;
+    }
+    p += fabs(bitsd(rv[i]) - o);
+  }
+  wave_fence();
+  for (int j = lane_id(); j < olen; j += WAVE)
+    if (!mf[j]) p += osc[j];
+#pragma unroll
+  for (int o = 32; o; o >>= 1) p = p + __shfl_xor(p, o);
+  return p;
+}
+
+}  // namespace pprd

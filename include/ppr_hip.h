@@ -1,0 +1,137 @@
+/*
+ * ppr_hip.h -- C ABI of the MI355X-native all-sources approximate PPR engine (libppr_hip.so).
+ *
+ * The reference (fruttasecca/approximated_personalized_pagerank) has no FFI: its surface is the
+ * C++ templates ppr::grank / ppr::grankMulti / ppr::mccompletepathv2. This ABI is what those
+ * templates bind to in the drop-in headers include/ppr/grank.h, include/ppr/grankMulti.h and
+ * include/ppr/mccompletepathv2.h (same signatures as the reference), and what the Python mirror
+ * binds with ctypes. Plain pointers and sizes only; no torch / HIP types in signatures
+ * (streams are passed as void*).
+ *
+ * Dense ids: node i is the i-th key of the graph in its iteration order; col[] keeps each
+ * node's successor order (the reference sums contributions in that order,
+ * include/grank.h:107-116, and its partitions depend on the iteration order,
+ * include/internal/pprInternal.h:57-63).
+ *
+ * All entry points are synchronous unless stated, thread-safe per call, and keep no globals.
+ * Return value: PPR_OK (0) or a PPR_ERR_* code; ppr_strerror() names it.
+ */
+#ifndef PPR_HIP_H
+#define PPR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  PPR_OK = 0,
+  PPR_ERR_ARG = 1,       /* bad pointer / size */
+  PPR_ERR_K = 2,         /* "K must be positive"          include/grank.h:51 */
+  PPR_ERR_L = 3,         /* "L must be positive"          include/grank.h:52 */
+  PPR_ERR_KL = 4,        /* "K must be <= L"              include/grank.h:53 */
+  PPR_ERR_ITERS = 5,     /* "iterations must be positive" include/grank.h:54 */
+  PPR_ERR_DAMPING = 6,   /* "damping must be [0,1]"       include/grank.h:55 */
+  PPR_ERR_THREADS = 7,   /* "nThreads must be positive"   header-only/grankMulti.h:304 */
+  PPR_ERR_GRAPH = 8,     /* successor id out of range (UB in the reference, README.md:69-73) */
+  PPR_ERR_HIP = 9,       /* HIP runtime failure (no device, launch failure, ...) */
+  PPR_ERR_OOM = 10,      /* device allocation failed */
+  PPR_ERR_RANGE = 11     /* L / K / node count beyond what the kernels support */
+};
+
+/* graph in dense CSR form (borrowed; host memory unless a *_dev entry point says otherwise) */
+typedef struct ppr_csr {
+  int64_t n;               /* nodes */
+  const int64_t* row_ptr;  /* [n+1], row_ptr[0] = 0, edges m = row_ptr[n] */
+  const int32_t* col;      /* [m] dense successor ids, successor order preserved */
+} ppr_csr;
+
+typedef struct ppr_opts {
+  int32_t device;          /* HIP device ordinal; -1 = current device */
+  int32_t flags;           /* PPR_FLAG_* */
+  void* stream;            /* hipStream_t to run on; NULL = library-owned stream */
+} ppr_opts;
+
+enum {
+  PPR_FLAG_STATS = 1       /* collect candidate counts / algorithmic bytes per iteration */
+};
+
+#define PPR_MAX_ITER_STATS 256
+
+typedef struct ppr_stats {
+  int32_t iterations_run;          /* iterations actually executed (tolerance may stop early) */
+  int32_t reserved;
+  double max_diff[PPR_MAX_ITER_STATS];   /* maxDiff of the partition updated in iteration i */
+  double device_ms;                /* init + iterations + final top-K, device events */
+  double merge_ms;                 /* basket-merge kernels only (sum over iterations) */
+  int64_t candidates;              /* sum over iterations of candidates (PPR_FLAG_STATS) */
+  int64_t algo_bytes;              /* SURVEY s8d algorithmic bytes over iterations (STATS) */
+  int64_t merge_launches;          /* number of merge-kernel launches */
+} ppr_stats;
+
+const char* ppr_strerror(int code);
+
+/* ---- host-side graph preparation (no GPU) ---- */
+
+/* BFS 2-colouring of include/internal/pprInternal.h:29-99; part[i] = 0 for partitions.first */
+int ppr_find_partitions_csr(const ppr_csr* g, uint8_t* part);
+
+/* MCCompletePathV2 node order, include/mccompletepathv2.h:36-113 (stable on ties) */
+int ppr_execution_order_csr(const ppr_csr* g, int32_t* order);
+
+/* Synthetic RMAT graph (Graph500 recursion, scrambled labels, deduped, successors ascending).
+ * Call with col = NULL to get m (row_ptr[n+1] is filled either way); returns m or -error. */
+int64_t ppr_rmat_generate(int32_t scale, int32_t edge_factor, double a, double b, double c,
+                          uint64_t seed, int64_t* row_ptr, int32_t* col, int64_t col_cap);
+
+/* ---- GRank (ppr::grank / ppr::grankMulti, include/grank.h:42-150) ----
+ * One call: upload, init, iterate, final top-K, download. out_ids / out_scores are n*K
+ * (row v = the K best (id, score) of source v, score desc, id asc; unused slots id -1),
+ * out_len is n. part: partition bits from ppr_find_partitions_csr (or NULL to compute). */
+int ppr_grank_csr(const ppr_csr* g, const uint8_t* part, uint32_t K, uint32_t L,
+                  uint32_t iterations, double damping, double tolerance, const ppr_opts* o,
+                  int32_t* out_ids, double* out_scores, int32_t* out_len, ppr_stats* st);
+
+/* ---- device-resident plan (benchmarks, multi-GPU source sharding) ---- */
+typedef struct ppr_plan ppr_plan;
+
+/* Uploads the CSR and partition lists to HBM and allocates the two L-wide basket slabs. */
+int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part, uint32_t K, uint32_t L,
+                          double damping, const ppr_opts* o, ppr_plan** out);
+void ppr_grank_plan_destroy(ppr_plan* p);
+
+/* Whole device phase: init baskets, run up to `iterations` with the reference's stopping rule,
+ * final top-K into the plan's device output. Inputs are already resident. */
+int ppr_grank_plan_run(ppr_plan* p, uint32_t iterations, double tolerance, ppr_stats* st);
+
+/* Step-level entry points (multi-GPU sharding; each is asynchronous on the plan's stream):
+ *   init:    initial baskets of every node
+ *   iterate: merge the active sources with index [begin, end) of iteration `it`'s active list
+ *            (the list orders sources by descending work so contiguous ranges balance), writing
+ *            their new rows into the next-slot slab and folding norm1 into a device max
+ *   finish:  final top-K of every node into the device output */
+int ppr_grank_plan_init(ppr_plan* p);
+int ppr_grank_plan_active_count(ppr_plan* p, int32_t it, int64_t* count);
+int ppr_grank_plan_iterate(ppr_plan* p, int32_t it, int64_t begin, int64_t end);
+int ppr_grank_plan_read_maxdiff(ppr_plan* p, int32_t it, double* maxdiff); /* syncs */
+int ppr_grank_plan_finish(ppr_plan* p, int32_t iterations_run);
+
+/* Row exchange for source sharding: device pointers (ids int32[L], scores f64[L], len int32)
+ * of the basket rows iteration `it` wrote, plus pack/unpack of active-list ranges into a
+ * contiguous device buffer of rows (row = L*4 + L*8 + 8 bytes). */
+int ppr_grank_plan_row_bytes(ppr_plan* p, int64_t* bytes);
+int ppr_grank_plan_pack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* dev_buf);
+int ppr_grank_plan_unpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* dev_buf);
+
+/* Downloads: final top-K (n*K) and the current L-slab (n*L, rows sorted, len per node). */
+int ppr_grank_plan_fetch(ppr_plan* p, int32_t* out_ids, double* out_scores, int32_t* out_len);
+int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, int32_t* ids, double* scores,
+                              int32_t* len);
+/* Device stream the plan runs on (hipStream_t as void*), for event timing by the caller. */
+void* ppr_grank_plan_stream(ppr_plan* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPR_HIP_H */

@@ -1,0 +1,259 @@
+/*
+ * oracle/grank_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, single-threaded restatement of the reference's GRank hot path, used as the parity
+ * checker for the MI355X HIP path (tests/, __graft_entry__.smoke(), bench.py cpu_baseline only).
+ * It is never linked into, called by, or shipped with the product library.
+ *
+ * Pinned against the compiled reference (oracle/_ref/ref_driver, built from /root/reference by
+ * oracle/Makefile) through the golden vectors in tests/golden/ (tests/test_oracle_golden.py):
+ * bit-exact where the reference has no top-L truncation (ring G1, RMAT-10 L>=|V| G2, the
+ * known-answer graphs), tie-aware statistics elsewhere.
+ *
+ * Semantics restated (reference file:line):
+ *   init         include/grank.h:64-83       B[v] = {v: 1-d}; B[v][s] += d/deg for s in succ(v);
+ *                                             keepTop(L)
+ *   partitions   include/internal/pprInternal.h:29-99   BFS 2-colouring, roots in graph order,
+ *                                             successors then predecessors get the opposite colour
+ *   iteration    include/grank.h:90-141      Jacobi sweep over the active partition, then swap
+ *   merge        include/grank.h:96-126      acc = {v: 1-d}; for u in succ(v) (CSR order), for
+ *                                             (k,s) in B[u]: acc[k] = fma(s, d/deg, acc[k])
+ *                                             (-O3 -march=native contracts this into an FMA)
+ *   keepTop      include/internal/pprInternal.h:109-137  keep L largest; the reference breaks
+ *                                             ties by unordered_map order + nth_element; this
+ *                                             restatement (and the HIP path) uses the documented
+ *                                             deterministic rule (score desc, dense id asc) and
+ *                                             stores rows in that order
+ *   norm1        include/internal/pprInternal.h:147-165  sum |new-old| over the key union; the
+ *                                             summation order here is the HIP kernel's fixed
+ *                                             64-lane pattern (see norm1_rows) so maxDiff is
+ *                                             bit-identical too
+ *   stop rule    include/grank.h:90-94,140   maxDiff[2] = {tol, tol}; loop while
+ *                                             i < iterations && max(maxDiff) >= tol
+ *   final top-K  include/grank.h:143-147      first min(K, len) entries of each sorted row
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct { int32_t key; double sc; } ent_t;
+
+static int cmp_ent(const void* a, const void* b) {
+  const ent_t* x = (const ent_t*)a;
+  const ent_t* y = (const ent_t*)b;
+  if (x->sc > y->sc) return -1;
+  if (x->sc < y->sc) return 1;
+  return (x->key < y->key) ? -1 : (x->key > y->key);
+}
+
+/* ---- open-addressing accumulator (keys unique, insertion-order independent) ---- */
+typedef struct {
+  int64_t cap;
+  int32_t* keys;
+  double* acc;
+  int64_t used;
+  int64_t* slots; /* occupied slot list, for cheap reset */
+} acc_t;
+
+static uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+static void acc_init(acc_t* a, int64_t need) {
+  int64_t cap = 16;
+  while (cap < 2 * need + 2) cap <<= 1;
+  if (cap > a->cap) {
+    free(a->keys); free(a->acc); free(a->slots);
+    a->cap = cap;
+    a->keys = (int32_t*)malloc(sizeof(int32_t) * cap);
+    a->acc = (double*)malloc(sizeof(double) * cap);
+    a->slots = (int64_t*)malloc(sizeof(int64_t) * cap);
+    for (int64_t i = 0; i < cap; i++) a->keys[i] = -1;
+    a->used = 0;
+  }
+}
+
+static void acc_reset(acc_t* a) {
+  for (int64_t i = 0; i < a->used; i++) a->keys[a->slots[i]] = -1;
+  a->used = 0;
+}
+
+static double* acc_find(acc_t* a, int32_t key) {
+  uint64_t mask = (uint64_t)a->cap - 1;
+  uint64_t h = mix32((uint32_t)key) & mask;
+  for (;;) {
+    if (a->keys[h] == key) return &a->acc[h];
+    if (a->keys[h] == -1) {
+      a->keys[h] = key;
+      a->acc[h] = 0.0;
+      a->slots[a->used++] = (int64_t)h;
+      return &a->acc[h];
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+static void acc_free(acc_t* a) { free(a->keys); free(a->acc); free(a->slots); memset(a, 0, sizeof(*a)); }
+
+/* collect, order by (score desc, key asc), keep first L -> out row; returns len */
+static int32_t acc_top(acc_t* a, int32_t L, ent_t** buf, int64_t* bufcap, int32_t* ids, double* sc) {
+  if (a->used > *bufcap) { free(*buf); *bufcap = a->used; *buf = (ent_t*)malloc(sizeof(ent_t) * (*bufcap)); }
+  ent_t* e = *buf;
+  for (int64_t i = 0; i < a->used; i++) { int64_t s = a->slots[i]; e[i].key = a->keys[s]; e[i].sc = a->acc[s]; }
+  qsort(e, (size_t)a->used, sizeof(ent_t), cmp_ent);
+  int32_t len = a->used < L ? (int32_t)a->used : L;
+  for (int32_t i = 0; i < len; i++) { ids[i] = e[i].key; sc[i] = e[i].sc; }
+  return len;
+}
+
+/* norm1 with the HIP kernel's fixed summation pattern: 64 lane partials, entry i of the new row
+ * goes to lane i%64 (in increasing i), then old entries j absent from the new row go to lane
+ * j%64 (in increasing j), then an xor butterfly 32,16,8,4,2,1. */
+static double norm1_rows(const int32_t* nid, const double* nsc, int32_t nlen,
+                         const int32_t* oid, const double* osc, int32_t olen) {
+  double p[64];
+  for (int l = 0; l < 64; l++) p[l] = 0.0;
+  for (int32_t i = 0; i < nlen; i++) {
+    double o = 0.0;
+    for (int32_t j = 0; j < olen; j++) if (oid[j] == nid[i]) { o = osc[j]; break; }
+    p[i & 63] += fabs(nsc[i] - o);
+  }
+  for (int32_t j = 0; j < olen; j++) {
+    int found = 0;
+    for (int32_t i = 0; i < nlen; i++) if (nid[i] == oid[j]) { found = 1; break; }
+    if (!found) p[j & 63] += osc[j];
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    double q[64];
+    for (int l = 0; l < 64; l++) q[l] = p[l] + p[l ^ off];
+    memcpy(p, q, sizeof(p));
+  }
+  return p[0];
+}
+
+/* ---- partitions: include/internal/pprInternal.h:29-99 in dense (graph-iteration) order ---- */
+int oracle_find_partitions(int64_t n, const int64_t* rp, const int32_t* col, uint8_t* part) {
+  int64_t m = n ? rp[n] : 0;
+  int64_t* prp = (int64_t*)calloc((size_t)n + 1, sizeof(int64_t));
+  int32_t* pcol = (int32_t*)malloc(sizeof(int32_t) * (size_t)(m ? m : 1));
+  char* vis = (char*)calloc((size_t)(n ? n : 1), 1);
+  int32_t* q = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n ? n : 1));
+  if (!prp || !pcol || !vis || !q) return -1;
+  /* predecessors[s] in the order nodes are iterated (pprInternal.h:38-47) */
+  for (int64_t e = 0; e < m; e++) prp[col[e] + 1]++;
+  for (int64_t i = 0; i < n; i++) prp[i + 1] += prp[i];
+  int64_t* fill = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n ? n : 1));
+  for (int64_t i = 0; i < n; i++) fill[i] = prp[i];
+  for (int64_t v = 0; v < n; v++)
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) pcol[fill[col[e]]++] = (int32_t)v;
+  free(fill);
+  for (int64_t r = 0; r < n; r++) {
+    int64_t qh = 0, qt = 0;
+    if (!vis[r]) { vis[r] = 1; q[qt++] = (int32_t)r; part[r] = 0; }
+    while (qh < qt) {
+      int32_t nx = q[qh++];
+      uint8_t c = part[nx] == 0 ? 1 : 0; /* pprInternal.h:79-80 */
+      for (int64_t e = rp[nx]; e < rp[nx + 1]; e++) {
+        int32_t s = col[e];
+        if (!vis[s]) { vis[s] = 1; part[s] = c; q[qt++] = s; }
+      }
+      for (int64_t e = prp[nx]; e < prp[nx + 1]; e++) {
+        int32_t s = pcol[e];
+        if (!vis[s]) { vis[s] = 1; part[s] = c; q[qt++] = s; }
+      }
+    }
+  }
+  free(prp); free(pcol); free(vis); free(q);
+  return 0;
+}
+
+/* ---- GRank on a fixed-width |V| x L slab ----
+ * Inputs: CSR in dense order (successor order preserved), partition bits (0 = first).
+ * Outputs (all optional except out_*): final top-K rows, the final L-slab, maxDiff history.
+ * Returns 0 on success. */
+int oracle_grank(int64_t n, const int64_t* rp, const int32_t* col, const uint8_t* part,
+                 int32_t K, int32_t L, int32_t iterations, double damping, double tolerance,
+                 int32_t* out_ids, double* out_sc, int32_t* out_len,
+                 int32_t* slab_ids, double* slab_sc, int32_t* slab_len,
+                 double* maxdiff_hist, int32_t* iters_run) {
+  if (K <= 0 || L <= 0 || K > L || iterations < 0 || damping < 0 || damping > 1) return -2;  /* 0 = init only (diagnostics) */
+  int32_t* ci = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n * L + 1));
+  double* cs = (double*)malloc(sizeof(double) * (size_t)(n * L + 1));
+  int32_t* cl = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n + 1));
+  int32_t* ni = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n * L + 1));
+  double* ns = (double*)malloc(sizeof(double) * (size_t)(n * L + 1));
+  int32_t* nl = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n + 1));
+  if (!ci || !cs || !cl || !ni || !ns || !nl) return -1;
+  acc_t a; memset(&a, 0, sizeof(a));
+  ent_t* buf = NULL; int64_t bufcap = 0;
+  const double self = 1.0 - damping;
+
+  /* init: include/grank.h:64-83 */
+  for (int64_t v = 0; v < n; v++) {
+    int64_t deg = rp[v + 1] - rp[v];
+    double factor = damping / (double)deg;
+    acc_init(&a, deg + 1);
+    *acc_find(&a, (int32_t)v) = self;
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
+      double* p = acc_find(&a, col[e]);
+      *p = *p + factor;
+    }
+    cl[v] = acc_top(&a, L, &buf, &bufcap, ci + v * L, cs + v * L);
+    acc_reset(&a);
+  }
+
+  double md[2] = {tolerance, tolerance};
+  int32_t it;
+  for (it = 0; it < iterations && (md[0] > md[1] ? md[0] : md[1]) >= tolerance; it++) {
+    uint8_t active = (uint8_t)(it & 1); /* partitions.first at even iterations */
+    md[0] = 0.0;
+    for (int64_t v = 0; v < n; v++) {
+      if (part[v] != active) continue;
+      int64_t deg = rp[v + 1] - rp[v];
+      double factor = damping / (double)deg;
+      int64_t cand = 1;
+      for (int64_t e = rp[v]; e < rp[v + 1]; e++) cand += cl[col[e]];
+      acc_init(&a, cand);
+      *acc_find(&a, (int32_t)v) = self;
+      for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
+        int32_t u = col[e];
+        const int32_t* ui = ci + (int64_t)u * L;
+        const double* us = cs + (int64_t)u * L;
+        for (int32_t j = 0; j < cl[u]; j++) {
+          double* p = acc_find(&a, ui[j]);
+          *p = fma(us[j], factor, *p);
+        }
+      }
+      nl[v] = acc_top(&a, L, &buf, &bufcap, ni + v * L, ns + v * L);
+      acc_reset(&a);
+      double d1 = norm1_rows(ni + v * L, ns + v * L, nl[v], ci + v * L, cs + v * L, cl[v]);
+      if (d1 > md[0]) md[0] = d1;
+    }
+    for (int64_t v = 0; v < n; v++) {
+      if (part[v] != active) continue;
+      memcpy(ci + v * L, ni + v * L, sizeof(int32_t) * (size_t)nl[v]);
+      memcpy(cs + v * L, ns + v * L, sizeof(double) * (size_t)nl[v]);
+      cl[v] = nl[v];
+    }
+    if (maxdiff_hist) maxdiff_hist[it] = md[0];
+    double t = md[0]; md[0] = md[1]; md[1] = t;
+  }
+  if (iters_run) *iters_run = it;
+
+  for (int64_t v = 0; v < n; v++) {
+    int32_t k = cl[v] < K ? cl[v] : K;
+    out_len[v] = k;
+    for (int32_t j = 0; j < K; j++) {
+      out_ids[v * K + j] = j < k ? ci[v * L + j] : -1;
+      out_sc[v * K + j] = j < k ? cs[v * L + j] : 0.0;
+    }
+  }
+  if (slab_ids) memcpy(slab_ids, ci, sizeof(int32_t) * (size_t)(n * L));
+  if (slab_sc) memcpy(slab_sc, cs, sizeof(double) * (size_t)(n * L));
+  if (slab_len) memcpy(slab_len, cl, sizeof(int32_t) * (size_t)n);
+  free(ci); free(cs); free(cl); free(ni); free(ns); free(nl); free(buf);
+  acc_free(&a);
+  return 0;
+}

@@ -1,0 +1,62 @@
+"""Shared helpers for the parity tests (fixtures, tie-aware comparisons)."""
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# fixtures whose reference run never truncates a basket at a tie: bit-exact targets (P2)
+EXACT = [
+    "g1_ring100", "g1_ring100_multi", "g2_rmat8_full", "g5_noedges10", "g5_single", "g5_single_loop",
+    "g5_two_linked", "g5_ring6", "g5_ring6_k3l4", "g5_star", "g5_star_loop", "g5_ring100_k10_l10",
+    "g5_ring100_k10_l20", "g5_ring100_full", "g5_instar_full", "g5_instar_loop_full",
+    "g5_instar_all_full", "g5_random5000_full", "g5_complete_full",
+]
+# truncating runs: statistical parity (P3/P4), thresholds = measured restatement-vs-reference
+# agreement with margin, next to the reference-vs-relabelled-reference ceiling of SURVEY s0.4
+STAT = {
+    "g3_rmat12_k16_l32": 0.88,
+    "g3_rmat14_k32_l64": 0.96,
+    "g4_eat_k50_l100": 0.99,
+}
+
+
+def load(name: str):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    K, L, it, d, tol = z["params"]
+    return dict(z=z, K=int(K), L=int(L), iters=int(it), damping=float(d), tol=float(tol),
+                rp=z["rp"], col=z["col"], part=z["part"])
+
+
+def all_names():
+    return sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def ref_rows(f):
+    z = f["z"]
+    cnt = np.minimum(z["cnt"], f["K"])
+    return z["ids"], z["scores"], cnt, (z["sample"] if "sample" in z else None)
+
+
+def jaccard_rows(ai, al, bi, bl):
+    js = np.empty(len(al))
+    for v in range(len(al)):
+        a = set(ai[v, : al[v]].tolist())
+        b = set(bi[v, : bl[v]].tolist())
+        js[v] = 1.0 if not (a or b) else len(a & b) / len(a | b)
+    return js
+
+
+def tie_aware_recall(ai, asc, al, bi, bsc, bl, tol=1e-12):
+    """fraction of b's entries whose score is matched by some a entry within tol (ties allowed)"""
+    hit = tot = 0
+    for v in range(len(al)):
+        sa = np.sort(asc[v, : al[v]])
+        for s in bsc[v, : bl[v]]:
+            tot += 1
+            j = np.searchsorted(sa, s - tol)
+            hit += j < len(sa) and abs(sa[j] - s) <= tol * max(1.0, abs(s))
+    return hit / max(tot, 1)

@@ -1,0 +1,89 @@
+"""CPU-only checks of the product library's host side and ABI (no device calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import approximated_personalized_pagerank_amd as ppr
+from approximated_personalized_pagerank_amd import _lib
+from helpers import all_names, load
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "ppr_hip.h")).read()
+    return sorted(set(re.findall(r"\b(ppr_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_abi_exports_every_declared_symbol():
+    L = _lib.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), s
+
+
+def test_strerror_messages_match_reference():
+    L = _lib.lib()
+    # include/grank.h:51-55, header-only/grankMulti.h:304
+    for code, msg in [(2, "K must be positive"), (3, "L must be positive"), (4, "K must be <= L"),
+                      (5, "iterations must be positive"), (6, "damping must be [0,1]"),
+                      (7, "nThreads must be positive")]:
+        assert L.ppr_strerror(code).decode() == msg
+        assert _lib.ERRORS[code] == msg
+
+
+@pytest.mark.parametrize("args,msg", [((0, 3, 42, 0.5, 1e-4), "K must be positive"),
+                                      ((2, 0, 32, 0.85, 1e-4), "L must be positive"),
+                                      ((2, 1, 10, 0.5, 1e-4), "K must be <= L"),
+                                      ((2, 2, 0, 0.5, 1e-4), "iterations must be positive"),
+                                      ((2, 2, 10, 1.5, 1e-4), r"damping must be \[0,1\]"),
+                                      ((2, 2, 10, -1.5, 1e-4), r"damping must be \[0,1\]")])
+def test_bad_parameters(args, msg):
+    # test/grankTest.cc:20-29 (validation happens before any device work)
+    with pytest.raises(ppr.PprError, match=msg):
+        ppr.grank({}, *args)
+    with pytest.raises(ppr.PprError, match="nThreads must be positive"):
+        ppr.grank_multi({}, 2, 2, 10, 0.5, 1e-4, 0)
+
+
+def test_abi_param_validation_without_device():
+    L = _lib.lib()
+    c = _lib.PprCsr(0, None, None)
+    out = ctypes.c_void_p()
+    assert L.ppr_grank_plan_create(ctypes.byref(c), None, 0, 3, 0.85, None, ctypes.byref(out)) == 2
+    assert L.ppr_grank_plan_create(ctypes.byref(c), None, 4, 3, 0.85, None, ctypes.byref(out)) == 4
+    assert L.ppr_grank_csr(ctypes.byref(c), None, 2, 2, 0, 0.85, 0.0, None, None, None, None, None) == 5
+    # empty graph: nothing to do, no device needed
+    assert L.ppr_grank_csr(ctypes.byref(c), None, 2, 2, 3, 0.85, 0.0, None, None, None, None, None) == 0
+
+
+@pytest.mark.parametrize("name", all_names())
+def test_product_partitions_match_reference(name):
+    f = load(name)
+    assert np.array_equal(ppr.Csr(f["rp"], f["col"]).partitions(), f["part"])
+
+
+def test_rmat_shape_and_determinism():
+    g1 = ppr.rmat(12, seed=42)
+    g2 = ppr.rmat(12, seed=42)
+    assert np.array_equal(g1.row_ptr, g2.row_ptr) and np.array_equal(g1.col, g2.col)
+    assert g1.n == 4096 and 0.75 * 16 * 4096 < g1.m <= 16 * 4096
+    for v in range(0, g1.n, 97):  # successors ascending and unique
+        s = g1.col[g1.row_ptr[v]:g1.row_ptr[v + 1]]
+        assert np.all(np.diff(s) > 0)
+    assert not np.array_equal(ppr.rmat(12, seed=43).col[:100], g1.col[:100])
+
+
+def test_execution_order_is_permutation():
+    g = ppr.rmat(11, seed=1)
+    o = g.execution_order()
+    assert np.array_equal(np.sort(o), np.arange(g.n))
+
+
+def test_from_dict_rejects_unknown_successor():
+    with pytest.raises(ppr.PprError):
+        ppr.Csr.from_dict({0: [1]})

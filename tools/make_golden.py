@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ by running the compiled reference.
+
+Runs oracle/_ref/ref_driver (built by `make -C oracle ref` from the unmodified reference headers
+in /root/reference) on graphs produced here, and stores inputs + reference outputs as .npz
+fixtures (data only; no reference source travels). Run from the repo root:
+
+    python tools/make_golden.py
+
+Each fixture holds, in the REFERENCE's graph iteration order (its unordered_map order, which
+defines the dense ids the engine uses): the dense CSR (rp, col), the reference's partition bits
+(findPartitions), the parameters, and the reference result rows sorted by (score desc, id asc).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+EAT = "/root/reference/example.txt"
+
+
+def write_graph_bin(path, keys, succ_lists):
+    n = len(keys)
+    rp = np.zeros(n + 1, dtype=np.int64)
+    flat = []
+    for i, s in enumerate(succ_lists):
+        flat.extend(s)
+        rp[i + 1] = len(flat)
+    with open(path, "wb") as f:
+        np.array([n, len(flat)], dtype=np.int64).tofile(f)
+        np.asarray(keys, dtype=np.int32).tofile(f)
+        rp.tofile(f)
+        np.asarray(flat, dtype=np.int32).tofile(f)
+
+
+def read_out(path, K):
+    with open(path, "rb") as f:
+        buf = f.read()
+    off = 0
+
+    def take(dtype, count):
+        nonlocal off
+        a = np.frombuffer(buf, dtype=dtype, count=count, offset=off)
+        off += a.nbytes
+        return a.copy()
+
+    n = int(take(np.int64, 1)[0])
+    order = take(np.int32, n)
+    m = int(take(np.int64, 1)[0])
+    rp = take(np.int64, n + 1)
+    col = take(np.int32, m)
+    part = take(np.uint8, n)
+    exec_order = take(np.int32, n)
+    ms = float(take(np.float64, 1)[0])
+    ids = np.full((n, K), -1, dtype=np.int32)
+    sc = np.zeros((n, K), dtype=np.float64)
+    cnt = np.zeros(n, dtype=np.int32)
+    rec = np.dtype([("k", "<i4"), ("s", "<f8")])
+    for v in range(n):
+        c = int(take(np.int32, 1)[0])
+        if c:
+            r = np.frombuffer(buf, dtype=rec, count=c, offset=off)
+            off += r.nbytes
+            o = np.lexsort((r["k"], -r["s"]))  # score desc, id asc
+            kk = min(c, K)
+            ids[v, :kk] = r["k"][o][:kk]
+            sc[v, :kk] = r["s"][o][:kk]
+            cnt[v] = c
+    return dict(order=order, rp=rp, col=col, part=part, exec_order=exec_order, ms=ms, ids=ids,
+                scores=sc, cnt=cnt)
+
+
+def run_ref(mode, graph_path, K, L, iters, d, tol, threads=1):
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "out.bin")
+        subprocess.run([DRIVER, mode, graph_path, out, str(K), str(L), str(iters), repr(d), repr(tol),
+                        str(threads)], check=True)
+        return read_out(out, K)
+
+
+def save(name, res, params, sample=None, extra=None):
+    d = dict(order=res["order"], rp=res["rp"], col=res["col"], part=res["part"],
+             params=np.array(params, dtype=np.float64))
+    if sample is None:
+        d.update(ids=res["ids"], scores=res["scores"], cnt=res["cnt"])
+    else:
+        d.update(sample=sample, ids=res["ids"][sample], scores=res["scores"][sample], cnt=res["cnt"][sample])
+    if extra:
+        d.update(extra)
+    path = os.path.join(GOLDEN, name + ".npz")
+    np.savez_compressed(path, **d)
+    print(f"{name}: n={len(res['order'])} m={len(res['col'])} -> {os.path.getsize(path) / 1024:.0f} KiB")
+
+
+def gen_graph(name, keys, succ, K, L, iters, d, tol, mode="grank", threads=1, sample=None, extra_modes=()):
+    with tempfile.TemporaryDirectory() as td:
+        gp = os.path.join(td, "g.bin")
+        write_graph_bin(gp, keys, succ)
+        res = run_ref(mode, gp, K, L, iters, d, tol, threads)
+        extra = {}
+        for em, eK, eL, eit, etol in extra_modes:
+            r2 = run_ref(em, gp, eK, eL, eit, d, etol, 1)
+            extra[f"{em}_ids"] = r2["ids"]
+            extra[f"{em}_scores"] = r2["scores"]
+            extra[f"{em}_cnt"] = r2["cnt"]
+        save(name, res, [K, L, iters, d, tol], sample, extra)
+        return res
+
+
+def rmat_lists(scale, seed=42):
+    from approximated_personalized_pagerank_amd.graph import rmat
+    g = rmat(scale, seed=seed)
+    keys = list(range(g.n))
+    succ = [g.col[g.row_ptr[i]:g.row_ptr[i + 1]].tolist() for i in range(g.n)]
+    return keys, succ
+
+
+def main():
+    os.makedirs(GOLDEN, exist_ok=True)
+    if not os.path.exists(DRIVER):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    rng = np.random.default_rng(12345)
+
+    # G1: README ring of 100 (README.md "GRank" example), K50 L100 30 it tol 1e-3
+    ring = [[(i + 1) % 100] for i in range(100)]
+    gen_graph("g1_ring100", list(range(100)), ring, 50, 100, 30, 0.85, 1e-3)
+    gen_graph("g1_ring100_multi", list(range(100)), ring, 50, 100, 30, 0.85, 1e-3, mode="grankmulti", threads=4)
+
+    # G2: no truncation (L >= |V|): bit-exact target
+    keys, succ = rmat_lists(8)
+    gen_graph("g2_rmat8_full", keys, succ, 256, 256, 10, 0.85, -1.0)
+
+    # G3: truncating RMAT runs
+    keys, succ = rmat_lists(12)
+    gen_graph("g3_rmat12_k16_l32", keys, succ, 16, 32, 10, 0.85, -1.0)
+    keys, succ = rmat_lists(14)
+    sample = np.sort(rng.choice(1 << 14, 2048, replace=False)).astype(np.int64)
+    gen_graph("g3_rmat14_k32_l64", keys, succ, 32, 64, 20, 0.85, -1.0, mode="grankmulti", threads=8,
+              sample=sample)
+
+    # G4: EAT (example.txt), grankMulti K50 L100 30 it 1e-4 (src/main.cc:37), 3000-source sample
+    if os.path.exists(EAT):
+        with tempfile.TemporaryDirectory() as td:
+            out = os.path.join(td, "out.bin")
+            subprocess.run([DRIVER, "grankmulti", EAT, out, "50", "100", "30", "0.85", "0.0001", "4"], check=True)
+            res = read_out(out, 50)
+        n = len(res["order"])
+        sample = np.sort(rng.choice(n, 3000, replace=False)).astype(np.int64)
+        save("g4_eat_k50_l100", res, [50, 100, 30, 0.85, 1e-4], sample)
+
+    # G5: the reference tests' known-answer graphs (test/grankTest.cc), reference outputs + exact
+    # PPR (pprSingleSource) where the test compares against it.
+    def kg(name, n, edges, K, L, iters, tol, pprss=False):
+        succ = [[] for _ in range(n)]
+        for a, b in edges:
+            succ[a].append(b)
+        extra = [("pprss", n, 0, 100, -1.0)] if pprss else ()
+        gen_graph(name, list(range(n)), succ, K, L, iters, 0.85, tol, extra_modes=extra)
+
+    kg("g5_noedges10", 10, [], 10, 30, 100, 1e-4)
+    kg("g5_single", 1, [], 10, 30, 100, 1e-4)
+    kg("g5_single_loop", 1, [(0, 0)], 10, 30, 100, 1e-4)
+    kg("g5_two_linked", 2, [(0, 1), (1, 0)], 10, 30, 100, 1e-4)
+    kg("g5_ring6", 6, [(i, (i + 1) % 6) for i in range(6)], 10, 30, 100, 1e-4)
+    kg("g5_ring6_k3l4", 6, [(i, (i + 1) % 6) for i in range(6)], 3, 4, 100, 1e-4)
+    kg("g5_star", 6, [(i, 0) for i in range(1, 6)], 10, 30, 100, 1e-4)
+    kg("g5_star_loop", 6, [(i, 0) for i in range(1, 6)] + [(0, 0)], 10, 30, 100, 1e-4)
+    ring100 = [(i, i + 1) for i in range(99)] + [(99, 0)]
+    kg("g5_ring100_k10_l10", 100, ring100, 10, 10, 100, 1e-4)
+    kg("g5_ring100_k10_l20", 100, ring100, 10, 20, 100, 1e-4)
+    kg("g5_ring100_full", 100, ring100, 100, 100, 100, -1.0, pprss=True)
+    instar = [(i, 0) for i in range(99)]
+    kg("g5_instar_full", 100, instar, 100, 100, 100, -1.0, pprss=True)
+    kg("g5_instar_loop_full", 100, instar + [(0, 0)], 100, 100, 100, -1.0, pprss=True)
+    kg("g5_instar_all_full", 100, instar + [(0, 0)] + [(0, i) for i in range(99)], 100, 100, 100, -1.0,
+       pprss=True)
+    rnd = [(int(a), int(b)) for a, b in rng.integers(0, 100, size=(5000, 2))]
+    kg("g5_random5000_full", 100, rnd, 100, 100, 100, -1.0, pprss=True)
+    kg("g5_complete_full", 100, [(i, u) for i in range(100) for u in range(100)], 100, 100, 100, -1.0,
+       pprss=True)
+
+
+if __name__ == "__main__":
+    main()
