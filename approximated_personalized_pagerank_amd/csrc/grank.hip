@@ -34,6 +34,7 @@
 
 #include "../../include/ppr_hip.h"
 #include "ppr_device.h"
+#include "wg_merge.h"
 
 using namespace pprd;
 
@@ -48,7 +49,13 @@ using namespace pprd;
 
 namespace {
 
-constexpr int NT = 4;                 // LDS table tiers
+constexpr int NT = 4;                 // single-wave LDS table tiers
+constexpr int TIER_WG = NT;           // workgroup tier (k_merge_wg)
+constexpr int TIER_BIG = NT + 1;      // beyond the workgroup tier
+constexpr int NLISTS = NT + 2;
+constexpr int WG_T = 7168;            // workgroup table slots
+constexpr int WG_PASS_CAP = 4096;     // expected distinct keys per key-bucket pass
+constexpr int WG_PL = 1024;           // partial-list entries (P * L)
 constexpr int MAX_L = 4096;           // widest basket the kernels accept
 constexpr int WAVES_PER_BLOCK = 4;
 
@@ -85,32 +92,44 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
                                                   const int32_t* tier_cap, int32_t* tier_lists,
                                                   uint32_t* tier_cnt, int64_t list_cap,
                                                   int32_t* cand, unsigned long long* stats) {
-  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
-  if (w >= count) return;
-  const int v = list[w];
-  const int64_t b = g.rp[v], e = g.rp[v + 1];
-  int64_t c = 0;
-  if (a.unit) {
-    c = e - b;
-  } else {
-    for (int64_t i = b + lane_id(); i < e; i += WAVE) {
-      const int32_t cx = g.colx[i];
-      c += s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)];
-    }
+  __shared__ unsigned long long red[2][WAVES_PER_BLOCK];
+  const int wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
+  unsigned long long my_c = 0, my_b = 0;
+  if (w < count) {
+    const int v = list[w];
+    const int64_t b = g.rp[v], e = g.rp[v + 1];
+    int64_t c = 0;
+    if (a.unit) {
+      c = e - b;
+    } else {
+      for (int64_t i = b + lane_id(); i < e; i += WAVE) {
+        const int32_t cx = g.colx[i];
+        c += s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)];
+      }
 #pragma unroll
-    for (int o = 32; o; o >>= 1) c += __shfl_xor((long long)c, o);
-  }
-  if (lane_id() == 0) {
-    const int64_t need = c + 1;
-    cand[v] = (int32_t)(need > 0x7fffffff ? 0x7fffffff : need);
-    int t = 0;
-    while (t < NT && need > tier_cap[t]) t++;
-    const uint32_t pos = atomicAdd(&tier_cnt[t], 1u);
-    tier_lists[(int64_t)t * list_cap + pos] = v;
-    if (a.stats) {
+      for (int o = 32; o; o >>= 1) c += __shfl_xor((long long)c, o);
+    }
+    if (lane_id() == 0) {
+      const int64_t need = c + 1;
+      cand[v] = (int32_t)(need > 0x7fffffff ? 0x7fffffff : need);
+      int t = 0;
+      while (t < NT + 1 && need > tier_cap[t]) t++;
+      const uint32_t pos = atomicAdd(&tier_cnt[t], 1u);
+      tier_lists[(int64_t)t * list_cap + pos] = v;
       const int ownlen = a.unit ? 0 : s.len[s.lrow(a.active == 0 ? a.sA : a.sB, v)];
-      atomicAdd(&stats[0], (unsigned long long)c);
-      atomicAdd(&stats[1], (unsigned long long)(8 + 8 * (e - b) + 12 * c + 12 * ownlen));
+      my_c = (unsigned long long)c;
+      my_b = (unsigned long long)(8 + 8 * (e - b) + 12 * c + 12 * ownlen);
+    }
+  }
+  if (a.stats) {
+    if (lane_id() == 0) { red[0][wv] = my_c; red[1][wv] = my_b; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long sc = 0, sb = 0;
+      for (int i = 0; i < WAVES_PER_BLOCK; i++) { sc += red[0][i]; sb += red[1][i]; }
+      if (sc) atomicAdd(&stats[0], sc);
+      if (sb) atomicAdd(&stats[1], sb);
     }
   }
 }
@@ -263,6 +282,124 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
 }
 
 // ---------------------------------------------------------------------------------------------
+// one workgroup (8 waves) per source, shared LDS table, P key-bucket passes (wg_merge.h)
+__global__ void __launch_bounds__(WG_THREADS) k_merge_wg(DevGraph g, DevSlab s, IterArgs a,
+                                                         const int32_t* list, int64_t count,
+                                                         const int32_t* cand, int Lp,
+                                                         unsigned long long* maxdiff,
+                                                         unsigned long long* stats,
+                                                         int32_t* ovf_list, uint32_t* ovf_cnt) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int64_t w = blockIdx.x;
+  if (w >= count) return;
+  const WgLds L = wg_carve(smem, WG_T, Lp, WG_PL);
+  const int wv = threadIdx.x >> 6;
+  const int l = lane_id();
+  const int v = list[w];
+  const int64_t b = g.rp[v], e = g.rp[v + 1];
+  const double factor = a.damping / (double)(e - b);
+  const int need = cand[v];
+  const int P = (need + WG_PASS_CAP - 1) / WG_PASS_CAP;
+  const uint32_t T = WG_T, budget = WG_T - 512;
+  const int Lw = s.L;
+  if (threadIdx.x == 0) { L.misc[M_PLEN] = 0; L.misc[M_OVF] = 0; }
+
+  for (int pass = 0; pass < P; pass++) {
+    for (int i = threadIdx.x; i < (int)T; i += WG_THREADS) { L.keys[i] = EMPTY; L.owner[i] = NO_OWNER; }
+    if (threadIdx.x == 0) L.misc[M_FILL] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0 && (P == 1 || (int)(hash_b((uint32_t)v) % (uint32_t)P) == pass)) {
+      const uint32_t sl = wg_slot(L.keys, L.acc, T, (uint32_t)(((uint64_t)hash32((uint32_t)v) * T) >> 32), v,
+                                  reinterpret_cast<uint32_t*>(&L.misc[M_FILL]), budget);
+      L.acc[sl] = 1.0 - a.damping;
+    }
+    __syncthreads();
+    auto inpass = [&](int key) { return P == 1 || (int)(hash_b((uint32_t)key) % (uint32_t)P) == pass; };
+    if (a.unit) {
+      const int64_t deg = e - b;
+      for (int64_t c0 = 0; c0 < deg; c0 += WG_CHUNK) {
+        const int64_t q0 = c0 + wv * 128 + l, q1 = q0 + 64;
+        const bool v0 = q0 < deg, v1 = q1 < deg;
+        const int k0 = v0 ? (g.colx[b + q0] & 0x7fffffff) : 0;
+        const int k1 = v1 ? (g.colx[b + q1] & 0x7fffffff) : 0;
+        wg_route_apply(L, T, budget, v0 && inpass(k0), k0, 1.0, v1 && inpass(k1), k1, 1.0, factor);
+      }
+    } else {
+      for (int64_t wb = b; wb < e; wb += WG_WIN) {
+        const int64_t i = wb + threadIdx.x;
+        int u = 0, sl = 0, ln = 0;
+        if (i < e) {
+          const int32_t cx = g.colx[i];
+          u = cx & 0x7fffffff;
+          sl = read_slot(a, cx);
+          ln = s.len[s.lrow(sl, u)];
+        }
+        const int incl = wg_incl_scan(ln, L.cnt);
+        L.wpre[threadIdx.x] = incl;
+        L.wu[threadIdx.x] = u;
+        L.wsl[threadIdx.x] = sl;
+        __syncthreads();
+        const int W = L.wpre[WG_WIN - 1];
+        for (int c0 = 0; c0 < W; c0 += WG_CHUNK) {
+          int kk[2] = {0, 0};
+          double ss[2] = {0.0, 0.0};
+          bool vv[2] = {false, false};
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const int q = c0 + wv * 128 + h * 64 + l;
+            if (q < W) {
+              int j = 0;
+#pragma unroll
+              for (int step = WG_WIN / 2; step; step >>= 1)
+                if (L.wpre[j + step - 1] <= q) j += step;
+              const int ex = j > 0 ? L.wpre[j - 1] : 0;
+              const int64_t r = s.row(L.wsl[j], L.wu[j]) + (q - ex);
+              kk[h] = s.ids[r];
+              ss[h] = s.sc[r];
+              vv[h] = inpass(kk[h]);
+            }
+          }
+          wg_route_apply(L, T, budget, vv[0], kk[0], ss[0], vv[1], kk[1], ss[1], factor);
+        }
+        __syncthreads();  // window arrays are rewritten next
+      }
+    }
+    if (L.misc[M_OVF]) break;  // uniform: read after the last barrier of wg_route_apply
+    // this pass's top-L (by the global rule) goes to the partial list
+    const int U = L.misc[M_FILL];
+    auto occ = [&](int i) { return L.keys[i] != EMPTY; };
+    if (U <= Lw) {
+      for (int i = threadIdx.x; i < (int)T; i += WG_THREADS)
+        if (occ(i)) { const int pos = atomicAdd(&L.misc[M_PLEN], 1); L.pk[pos] = L.keys[i]; L.pv[pos] = L.acc[i]; }
+    } else {
+      const SelCrit c = wg_select_top(L, (int)T, Lw, [&](int i) { return L.keys[i]; },
+                                      [&](int i) { return L.acc[i]; }, occ);
+      for (int i = threadIdx.x; i < (int)T; i += WG_THREADS) {
+        if (!occ(i)) continue;
+        const int key = L.keys[i];
+        if (sel_test(c, dbits(L.acc[i]), (uint32_t)~key)) {
+          const int pos = atomicAdd(&L.misc[M_PLEN], 1);
+          L.pk[pos] = key;
+          L.pv[pos] = L.acc[i];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (L.misc[M_OVF]) {
+    if (threadIdx.x == 0) { const uint32_t pos = atomicAdd(ovf_cnt, 1u); ovf_list[pos] = v; }
+    return;
+  }
+  if (wv == 0) {
+    const int n = L.misc[M_PLEN];
+    const int* pk = L.pk;
+    const double* pv = L.pv;
+    finish_source(v, n, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; }, s, a, L.hist,
+                  L.rv, L.rk, Lp, L.hk, L.hv, L.mf, maxdiff, stats);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // big sources: one wave per source, table in HBM scratch (per-source region of T slots)
 struct GlbWork {
   int32_t v;
@@ -402,11 +539,13 @@ struct ppr_plan {
   int32_t* d_act[2] = {nullptr, nullptr};
   int64_t nact[2] = {0, 0};
   int32_t* d_cand = nullptr;
-  int32_t* d_tier_lists = nullptr;   // (NT+1) * n
-  uint32_t* d_tier_cnt = nullptr;    // NT+1
-  int32_t* d_tier_cap = nullptr;     // NT
+  int32_t* d_tier_lists = nullptr;   // NLISTS * n
+  uint32_t* d_tier_cnt = nullptr;    // NLISTS (+1: workgroup overflow count)
+  int32_t* d_tier_cap = nullptr;     // NT + 1
+  int32_t* d_ovf = nullptr;          // sources the workgroup tier could not hold
   int tierT[NT] = {0, 0, 0, 0};
-  int tierCap[NT] = {0, 0, 0, 0};
+  int tierCap[NT + 1] = {0, 0, 0, 0, 0};
+  size_t wg_lds = 0;
   unsigned long long* d_maxdiff = nullptr;  // PPR_MAX_ITER_STATS + 1
   unsigned long long* d_stats = nullptr;    // 2
   GlbWork* d_work = nullptr;
@@ -418,7 +557,8 @@ struct ppr_plan {
   int32_t* d_out_len = nullptr;
   int flags = 0;
   int64_t merge_launches = 0;
-  hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
+  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_m0 = nullptr, ev_m1 = nullptr;
 };
 
 static void plan_free(ppr_plan* p) {
@@ -426,10 +566,13 @@ static void plan_free(ppr_plan* p) {
   hipFree(p->d_rp); hipFree(p->d_colx); hipFree(p->d_part); hipFree(p->d_ids); hipFree(p->d_sc);
   hipFree(p->d_len); hipFree(p->d_all); hipFree(p->d_act[0]); hipFree(p->d_act[1]);
   hipFree(p->d_cand); hipFree(p->d_tier_lists); hipFree(p->d_tier_cnt); hipFree(p->d_tier_cap);
+  hipFree(p->d_ovf);
   hipFree(p->d_maxdiff); hipFree(p->d_stats); hipFree(p->d_work); hipFree(p->d_scratch);
   hipFree(p->d_out_ids); hipFree(p->d_out_sc); hipFree(p->d_out_len);
   if (p->ev_a) hipEventDestroy(p->ev_a);
   if (p->ev_b) hipEventDestroy(p->ev_b);
+  if (p->ev_m0) hipEventDestroy(p->ev_m0);
+  if (p->ev_m1) hipEventDestroy(p->ev_m1);
   if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
   delete p;
 }
@@ -482,19 +625,34 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
     if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
     p->own_stream = true;
   }
-  if (hipEventCreate(&p->ev_a) != hipSuccess || hipEventCreate(&p->ev_b) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
+  if (hipEventCreate(&p->ev_a) != hipSuccess || hipEventCreate(&p->ev_b) != hipSuccess ||
+      hipEventCreate(&p->ev_m0) != hipSuccess || hipEventCreate(&p->ev_m1) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
 
   // tiers: T = 256 << t; capacity 3/4 T; a block of 4 waves must fit the 160 KB LDS
-  // (PPR_MAX_LDS_TIERS=k keeps only the first k tiers: diagnostics / tests of the HBM path)
+  // PPR_TIER_MASK (diagnostics / tests): bit t enables wave tier t, bit NT the workgroup tier;
+  // disabled tiers fall through to the next enabled one, ultimately the HBM-table path
   {
-    const char* env = getenv("PPR_MAX_LDS_TIERS");
-    const int max_tiers = env ? atoi(env) : NT;
+    const char* env = getenv("PPR_TIER_MASK");
+    const int mask = env ? (int)strtol(env, nullptr, 0) : 0xff;
     int T0 = 256;
     for (int t = 0; t < NT; t++) {
       const int T = T0 << t;
-      if (t >= max_tiers || lds_wave_bytes(T, p->Lp) * WAVES_PER_BLOCK > 160 * 1024) { p->tierT[t] = 0; p->tierCap[t] = 0; continue; }
+      if (!((mask >> t) & 1) || lds_wave_bytes(T, p->Lp) * WAVES_PER_BLOCK > 160 * 1024) { p->tierT[t] = 0; p->tierCap[t] = 0; continue; }
       p->tierT[t] = T;
       p->tierCap[t] = T / 4 * 3;
+    }
+    // workgroup tier: P = ceil(need / WG_PASS_CAP) key-bucket passes with P * L <= WG_PL
+    p->tierCap[NT] = 0;
+    p->wg_lds = wg_lds_bytes(WG_T, p->Lp, WG_PL);
+    const int pmax = WG_PL / (int)L;
+    if (((mask >> NT) & 1) && pmax >= 1 && p->wg_lds <= 160 * 1024)
+      p->tierCap[NT] = std::min(pmax, 8) * WG_PASS_CAP;
+    // a disabled tier has cap 0 (k_classify skips it); enabled caps must be non-decreasing
+    int run = 0;
+    for (int t = 0; t <= NT; t++) {
+      if (!p->tierCap[t]) continue;
+      if (p->tierCap[t] < run) p->tierCap[t] = 0;
+      else run = p->tierCap[t];
     }
   }
 
@@ -520,9 +678,10 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
   TRY(dalloc(&p->d_act[0], p->nact[0]));
   TRY(dalloc(&p->d_act[1], p->nact[1]));
   TRY(dalloc(&p->d_cand, n));
-  TRY(dalloc(&p->d_tier_lists, (size_t)(NT + 1) * (n > 0 ? n : 1)));
-  TRY(dalloc(&p->d_tier_cnt, NT + 1));
-  TRY(dalloc(&p->d_tier_cap, NT));
+  TRY(dalloc(&p->d_tier_lists, (size_t)NLISTS * (n > 0 ? n : 1)));
+  TRY(dalloc(&p->d_tier_cnt, NLISTS + 1));
+  TRY(dalloc(&p->d_tier_cap, NT + 1));
+  TRY(dalloc(&p->d_ovf, n));
   TRY(dalloc(&p->d_maxdiff, PPR_MAX_ITER_STATS + 1));
   TRY(dalloc(&p->d_stats, 2));
   TRY(dalloc(&p->d_out_ids, (size_t)n * K));
@@ -539,8 +698,8 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
       plan_free(p); return PPR_ERR_HIP;
     }
   }
-  int32_t caps[NT];
-  for (int t = 0; t < NT; t++) caps[t] = p->tierCap[t];
+  int32_t caps[NT + 1];
+  for (int t = 0; t <= NT; t++) caps[t] = p->tierCap[t];
   if (hipMemcpyAsync(p->d_tier_cap, caps, sizeof(caps), hipMemcpyHostToDevice, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
   for (int t = 0; t < NT; t++)
@@ -549,6 +708,8 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
       if (bytes > 64 * 1024)
         hipFuncSetAttribute((const void*)k_merge_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     }
+  if (p->tierCap[NT])
+    hipFuncSetAttribute((const void*)k_merge_wg, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   *out = p;
   return PPR_OK;
 }
@@ -568,24 +729,40 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   return a;
 }
 
-// classify + launch all tiers for `count` sources of `list`
+static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
+                          unsigned long long* maxdiff);
+
+// classify + launch all tiers for `count` sources of `list`; the span is timed with events on
+// the plan's stream and added to merge_ms (iterations only, not init)
 static int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
                      unsigned long long* maxdiff) {
   if (count <= 0) return PPR_OK;
+  HIP_OK(hipEventRecord(p->ev_m0, p->stream));
+  int rc = run_merge_impl(p, a, list, count, maxdiff);
+  if (rc) return rc;
+  HIP_OK(hipEventRecord(p->ev_m1, p->stream));
+  HIP_OK(hipEventSynchronize(p->ev_m1));
+  float ms = 0.f;
+  HIP_OK(hipEventElapsedTime(&ms, p->ev_m0, p->ev_m1));
+  if (!a.unit) p->merge_ms += ms;
+  return PPR_OK;
+}
+
+static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
+                          unsigned long long* maxdiff) {
   hipStream_t st = p->stream;
   DevGraph g{p->d_rp, p->d_colx, p->n};
   DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
-  HIP_OK(hipMemsetAsync(p->d_tier_cnt, 0, sizeof(uint32_t) * (NT + 1), st));
+  HIP_OK(hipMemsetAsync(p->d_tier_cnt, 0, sizeof(uint32_t) * (NLISTS + 1), st));
   const int64_t nb = (count + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(256), 0, st, g, s, a, list, count,
                      p->d_tier_cap, p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats);
   HIP_OK(hipGetLastError());
-  uint32_t cnt[NT + 1];
+  uint32_t cnt[NLISTS + 1];
   HIP_OK(hipMemcpyAsync(cnt, p->d_tier_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   for (int t = 0; t < NT; t++) {
-    if (!cnt[t]) continue;
-    if (!p->tierT[t]) { cnt[NT] += 0; continue; }
+    if (!cnt[t] || !p->tierT[t]) continue;
     const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * WAVES_PER_BLOCK;
     const int64_t blocks = ((int64_t)cnt[t] + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     hipLaunchKernelGGL(k_merge_lds, dim3((unsigned)blocks), dim3(256), bytes, st, g, s, a,
@@ -594,17 +771,29 @@ static int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_
     HIP_OK(hipGetLastError());
     p->merge_launches++;
   }
-  // sources beyond the largest LDS tier (including tiers disabled by a large L)
+  if (cnt[TIER_WG]) {
+    hipLaunchKernelGGL(k_merge_wg, dim3(cnt[TIER_WG]), dim3(WG_THREADS), p->wg_lds, st, g, s, a,
+                       p->d_tier_lists + (int64_t)TIER_WG * p->n, (int64_t)cnt[TIER_WG], p->d_cand,
+                       p->Lp, maxdiff, p->d_stats, p->d_ovf, p->d_tier_cnt + NLISTS);
+    HIP_OK(hipGetLastError());
+    p->merge_launches++;
+    HIP_OK(hipMemcpyAsync(&cnt[NLISTS], p->d_tier_cnt + NLISTS, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
+  // sources beyond the workgroup tier, plus workgroup-tier overflows
   std::vector<int32_t> big;
-  for (int t = 0; t <= NT; t++) {
-    if (!cnt[t]) continue;
-    if (t < NT && p->tierT[t]) continue;
-    std::vector<int32_t> tmp(cnt[t]);
-    HIP_OK(hipMemcpyAsync(tmp.data(), p->d_tier_lists + (int64_t)t * p->n, 4 * (size_t)cnt[t],
-                          hipMemcpyDeviceToHost, st));
+  auto pull = [&](const int32_t* dptr, uint32_t k) -> int {
+    if (!k) return PPR_OK;
+    std::vector<int32_t> tmp(k);
+    HIP_OK(hipMemcpyAsync(tmp.data(), dptr, 4 * (size_t)k, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     big.insert(big.end(), tmp.begin(), tmp.end());
-  }
+    return PPR_OK;
+  };
+  for (int t = 0; t < NT; t++)
+    if (cnt[t] && !p->tierT[t]) { int r = pull(p->d_tier_lists + (int64_t)t * p->n, cnt[t]); if (r) return r; }
+  { int r = pull(p->d_tier_lists + (int64_t)TIER_BIG * p->n, cnt[TIER_BIG]); if (r) return r; }
+  { int r = pull(p->d_ovf, cnt[NLISTS]); if (r) return r; }
   if (big.empty()) return PPR_OK;
   std::vector<int32_t> cand(p->n);
   HIP_OK(hipMemcpyAsync(cand.data(), p->d_cand, 4 * (size_t)p->n, hipMemcpyDeviceToHost, st));
@@ -711,6 +900,7 @@ extern "C" int ppr_grank_plan_run(ppr_plan* p, uint32_t iterations, double toler
   HIP_OK(hipMemsetAsync(p->d_maxdiff, 0, 8 * (PPR_MAX_ITER_STATS + 1), s));
   HIP_OK(hipMemsetAsync(p->d_stats, 0, 16, s));
   p->merge_launches = 0;
+  p->merge_ms = 0.0;
   HIP_OK(hipEventRecord(p->ev_a, s));
   int rc = ppr_grank_plan_init(p);
   if (rc) return rc;
@@ -739,7 +929,7 @@ extern "C" int ppr_grank_plan_run(ppr_plan* p, uint32_t iterations, double toler
     hipEventElapsedTime(&ms, p->ev_a, p->ev_b);
     st->iterations_run = (int32_t)it;
     st->device_ms = ms;
-    st->merge_ms = 0;
+    st->merge_ms = p->merge_ms;
     unsigned long long sv[2];
     HIP_OK(hipMemcpyAsync(sv, p->d_stats, 16, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));

@@ -44,6 +44,7 @@ class GrankResult:
     iterations_run: int = 0
     max_diff: Optional[np.ndarray] = None
     device_ms: float = 0.0
+    merge_ms: float = 0.0
     candidates: int = 0
     algo_bytes: int = 0
 
@@ -59,6 +60,7 @@ def _stats_to(res: GrankResult, st: _lib.PprStats) -> None:
     res.iterations_run = int(st.iterations_run)
     res.max_diff = np.array(st.max_diff[: min(st.iterations_run, _lib.PPR_MAX_ITER_STATS)])
     res.device_ms = float(st.device_ms)
+    res.merge_ms = float(st.merge_ms)
     res.candidates = int(st.candidates)
     res.algo_bytes = int(st.algo_bytes)
 

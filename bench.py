@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""bench.py -- GRank all-sources approximate PPR on synthetic RMAT (BASELINE.json metric).
+
+Metric: source-nodes/sec of ppr::grank K=64 L=128 30 iterations on RMAT-22 (configs[2]),
+whole-job throughput with the graph already resident in HBM: one "step" = one complete GRank
+job on the device (init baskets + 30 iterations of the basket merge + final top-K).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scale 22] [--K 64] [--L 128] [--iters 30]
+
+N > 1 (torch.distributed.run, one rank per GPU over RCCL): every rank holds the graph and a
+slab replica, merges a contiguous shard of each iteration's active sources, and the updated
+basket rows are all-gathered (approximated_personalized_pagerank_amd/shard.py).
+value = |V| * steps / max-over-ranks time; scaling "strong" (the job is fixed, sources split).
+
+Extra objects on the JSON line (DESIGN.md "measurement"):
+  roofline      merge phase: SURVEY s8d algorithmic bytes / merge-phase time (hipEvents on the
+                plan's stream), against 8 TB/s HBM
+  cpu_baseline  the reference's own combineMaps (oracle/_ref/ref_driver, compiled from
+                /root/reference) timed on a stratified sample of the end-state workload on this
+                host, extrapolated to the whole job
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ------------------------------------------------------------------------------------------
+# CPU baseline: reference combineMaps on a stratified sample (rank 0, N=1 only)
+def cpu_baseline(g, part, slab, L, damping, iters, threads, budget, seed=0):
+    drv = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+    if not os.path.exists(drv):
+        return None
+    ids, sc, lens = slab
+    rp, col = g.row_ptr, g.col
+    deg = np.diff(rp)
+    src_of_edge = np.repeat(np.arange(g.n, dtype=np.int64), deg)
+    cand = np.bincount(src_of_edge, weights=lens[col].astype(np.float64), minlength=g.n)
+    work = cand + deg
+    rng = np.random.default_rng(seed)
+    strata = []  # (partition, population count, sample array)
+    n_strata = 4
+    for p in (0, 1):
+        act = np.nonzero((part == p) & (deg > 0))[0]
+        if len(act) == 0:
+            continue
+        order = act[np.argsort(-work[act], kind="stable")]
+        cw = np.cumsum(work[order])
+        cuts = np.searchsorted(cw, cw[-1] * np.arange(1, n_strata) / n_strata)
+        bounds = [0] + sorted(set(int(c) + 1 for c in cuts)) + [len(order)]
+        bounds = sorted(set(min(b, len(order)) for b in bounds))
+        for h in range(len(bounds) - 1):
+            pop = order[bounds[h]:bounds[h + 1]]
+            if len(pop) == 0:
+                continue
+            mean_w = work[pop].mean()
+            k = int(min(len(pop), max(2, np.ceil(budget / (2 * n_strata) / max(mean_w, 1.0)))))
+            smp = pop if k == len(pop) else rng.choice(pop, k, replace=False)
+            strata.append((p, len(pop), np.sort(smp)))
+    src = np.concatenate([s for _, _, s in strata]).astype(np.int32)
+    off = np.cumsum([0] + [len(s) for _, _, s in strata]).astype(np.int64)
+    srp = np.zeros(len(src) + 1, dtype=np.int64)
+    srp[1:] = np.cumsum(deg[src])
+    succ = np.concatenate([col[rp[v]:rp[v + 1]] for v in src]).astype(np.int32)
+    need = np.unique(np.concatenate([src, succ]))
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "sample.bin")
+        with open(path, "wb") as f:
+            np.array([L], dtype=np.int32).tofile(f)
+            np.array([len(src)], dtype=np.int64).tofile(f)
+            src.tofile(f)
+            srp.tofile(f)
+            succ.tofile(f)
+            np.array([len(need)], dtype=np.int64).tofile(f)
+            for v in need:
+                ln = int(lens[v])
+                np.array([v, ln], dtype=np.int32).tofile(f)
+                ids[v, :ln].tofile(f)
+                sc[v, :ln].tofile(f)
+            np.array([len(strata)], dtype=np.int64).tofile(f)
+            off.tofile(f)
+        t0 = time.time()
+        out = subprocess.run([drv, "bench_combine", path, str(threads), repr(damping)], check=True,
+                             capture_output=True, text=True).stdout
+        wall = time.time() - t0
+    rows = [json.loads(x) for x in out.splitlines() if x.startswith("{")]
+    per_part = {0: 0.0, 1: 0.0}
+    sampled_ms = 0.0
+    for (p, pop, smp), r in zip(strata, rows):
+        per_part[p] += pop / len(smp) * r["ms"]
+        sampled_ms += r["ms"]
+    iters_p = {0: (iters + 1) // 2, 1: iters // 2}
+    job_ms = sum(iters_p[p] * per_part[p] for p in (0, 1))
+    n_act = int(((deg > 0)).sum())
+    return {
+        "value": g.n / (job_ms / 1e3),
+        "unit": "source-nodes/s",
+        "cores": threads,
+        "kind": "reference",
+        "sample": (f"reference grankMultiInternal::combineMaps (header-only/grankMulti.h:230-268, "
+                   f"-O3 -march=x86-64-v3) on {len(src)} of {n_act} active sources: {len(strata)} work "
+                   f"strata (4 per partition), end-state L={L} baskets; {sampled_ms / 1e3:.1f} s timed of "
+                   f"{wall:.1f} s wall; whole job extrapolated as {iters_p[0]} A + {iters_p[1]} B "
+                   f"iterations = {job_ms / 1e3:.0f} s (init, partitions and the final top-K excluded)"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scale", type=int, default=22)
+    ap.add_argument("--K", type=int, default=64)
+    ap.add_argument("--L", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--damping", type=float, default=0.85)
+    ap.add_argument("--tol", type=float, default=-1.0)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-budget", type=float, default=2e8, help="sampled candidates for cpu_baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import approximated_personalized_pagerank_amd as ppr
+    from approximated_personalized_pagerank_amd import build as _build
+    if rank == 0:
+        _build.build()
+
+    t = time.time()
+    g = ppr.rmat(args.scale, seed=args.seed)
+    part = g.partitions()
+    deg = g.degrees()
+    log(f"[rank {rank}] RMAT-{args.scale}: n={g.n} m={g.m} dangling={(deg == 0).sum()} "
+        f"|A|={(part == 0).sum()} |B|={(part == 1).sum()} prep {time.time() - t:.1f}s")
+
+    if world > 1:
+        from approximated_personalized_pagerank_amd.shard import run_distributed_bench
+        res = run_distributed_bench(g, part, args, rank, world, local)
+        if rank != 0:
+            return
+        elapsed, stats = res
+        cpu = None
+    else:
+        plan = ppr.GrankPlan(g, args.K, args.L, args.damping, part=part, device=local, stats=True)
+        for _ in range(args.warmup):
+            plan.run(args.iters, args.tol)
+        merge_ms = algo = dev_ms = 0.0
+        launches = 0
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            st = plan.run(args.iters, args.tol)  # synchronous: ends with an event sync
+            merge_ms += st.merge_ms
+            algo += st.algo_bytes
+            dev_ms += st.device_ms
+            launches += st.merge_launches
+        elapsed = time.perf_counter() - t0
+        stats = dict(merge_ms=merge_ms, algo_bytes=algo, device_ms=dev_ms, iterations=st.iterations_run,
+                     launches=launches)
+        cpu = None
+        if not args.no_cpu_baseline:
+            try:
+                slab = plan.fetch_slab()
+                plan.close()
+                cpu = cpu_baseline(g, part, slab, args.L, args.damping, args.iters, args.cpu_threads,
+                                   args.cpu_budget)
+            except Exception as exc:  # reported, never fatal
+                log(f"cpu_baseline failed: {exc!r}")
+                cpu = None
+
+    steps = args.steps
+    value = g.n * steps / elapsed
+    achieved = stats["algo_bytes"] / 1e9 / (stats["merge_ms"] / 1e3) if stats["merge_ms"] > 0 else 0.0
+    line = {
+        "metric": "source-nodes/sec grank K=64 L=128 on RMAT-22; 1/2/4/8 MI355X + HBM GB/s",
+        "value": value,
+        "unit": "source-nodes/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic RMAT (Graph500 a=.57 b=.19 c=.19, edge factor 16, seed %d, dedup)" % args.seed,
+        "config": {"workload": f"grank RMAT-{args.scale} K={args.K} L={args.L} iters={args.iters} "
+                               f"damping={args.damping} tol={args.tol}",
+                   "nodes": g.n, "edges": g.m, "iterations_run": stats["iterations"],
+                   "parallelism": f"source-shard x{world}" if world > 1 else "1 GPU"},
+        "roofline": {"bound": "hbm", "kernel": "merge phase (k_classify + k_merge_lds + k_merge_glb)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "algo_bytes_per_step": stats["algo_bytes"] / steps,
+                     "merge_ms_per_step": stats["merge_ms"] / steps,
+                     "merge_launches_per_step": stats["launches"] / steps,
+                     "traffic": None},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

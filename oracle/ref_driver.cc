@@ -5,7 +5,8 @@
 // to oracle/_ref/ (git-ignored). It is used to
 //   (1) generate the golden vectors under tests/golden/ (tools/make_golden.py), and
 //   (2) time the reference's own per-source merge (grankMultiInternal::combineMaps,
-//       header-only/grankMulti.h:230-268) on a bounded sample for bench.py's cpu_baseline.
+//       header-only/grankMulti.h:230-268) on a bounded, stratified sample of sources for
+//       bench.py's cpu_baseline (mode bench_combine).
 //
 // No reference source is copied here: the algorithms are #included from the reference tree.
 //
@@ -136,61 +137,65 @@ static void write_out(const char* path, const Graph& g, const Dense& d, const Re
 }
 
 // bench mode: time the reference's per-source merge, grankMultiInternal::combineMaps
-// (header-only/grankMulti.h:230-268), over a sample of sources, with the reference's own
-// containers, split over nThreads exactly as grankMulti does (:379-396).
-// state file: int64 n, int32 L, int32 len[n], int32 ids[n*L], double sc[n*L] (dense ids; the
-// basket state the MI355X path held at some iteration). sample file: int64 s, int32 src[s].
-static int bench_combine(const char* graph_path, const char* state_path, const char* sample_path,
-                         int nthreads, double damping) {
-  Graph g = read_graph_bin(graph_path);
-  // graph keys in the bench graphs are the dense ids themselves (keys[i] == i)
-  FILE* f = fopen(state_path, "rb");
-  if (!f) die("cannot open state");
-  int64_t n; int32_t L;
-  if (fread(&n, 8, 1, f) != 1 || fread(&L, 4, 1, f) != 1) die("short state");
-  std::vector<int32_t> len(n);
-  if (fread(len.data(), 4, n, f) != (size_t)n) die("short len");
-  FILE* fs = fopen(sample_path, "rb");
-  if (!fs) die("cannot open sample");
-  int64_t s;
-  if (fread(&s, 8, 1, fs) != 1) die("short sample");
+// (header-only/grankMulti.h:230-268), over stratified samples of sources, with the reference's
+// own containers, split over nThreads exactly as grankMulti does (:379-396).
+// sample file (dense ids, written by bench.py):
+//   int32 L, int64 s, int32 src[s], int64 rp[s+1], int32 succ[rp[s]],
+//   int64 nb, nb x { int32 id, int32 len, int32 ids[len], double sc[len] }   (baskets of every
+//   sampled source and of every successor), int64 nstrata, int64 off[nstrata+1]
+// prints one JSON line per stratum: {"stratum": h, "sources": k, "ms": t}
+template <class T> static void rd(FILE* f, T* p, size_t n) {
+  if (n && fread(p, sizeof(T), n, f) != n) die("short sample file");
+}
+static int bench_combine(const char* sample_path, int nthreads, double damping) {
+  FILE* f = fopen(sample_path, "rb");
+  if (!f) die("cannot open sample");
+  int32_t L; int64_t s;
+  rd(f, &L, 1); rd(f, &s, 1);
   std::vector<int32_t> src(s);
-  if (fread(src.data(), 4, s, fs) != (size_t)s) die("short sample2");
-  fclose(fs);
-  // baskets needed: the sources themselves and all their successors
-  std::vector<char> need(n, 0);
-  for (int32_t v : src) { need[v] = 1; for (int u : g[v]) need[u] = 1; }
+  std::vector<int64_t> rp(s + 1);
+  rd(f, src.data(), s); rd(f, rp.data(), s + 1);
+  std::vector<int32_t> succ(rp[s]);
+  rd(f, succ.data(), rp[s]);
+  Graph g;
+  for (int64_t i = 0; i < s; i++) g[src[i]] = std::vector<int>(succ.begin() + rp[i], succ.begin() + rp[i + 1]);
+  int64_t nb; rd(f, &nb, 1);
   Result scores, next;
-  scores.reserve(n); next.reserve(n);
-  for (int64_t v = 0; v < n; v++) { scores[(int)v]; next[(int)v]; }
-  long off_ids = ftell(f);
-  std::vector<int32_t> ids(L);
-  std::vector<double> sc(L);
-  for (int64_t v = 0; v < n; v++) {
-    if (!need[v]) continue;
-    fseek(f, off_ids + (long)(v * L * 4), SEEK_SET);
-    if (fread(ids.data(), 4, L, f) != (size_t)L) die("short ids");
-    fseek(f, off_ids + (long)(n * L * 4) + (long)(v * L * 8), SEEK_SET);
-    if (fread(sc.data(), 8, L, f) != (size_t)L) die("short sc");
-    auto& mp = scores[(int)v];
-    for (int32_t i = 0; i < len[v]; i++) mp[ids[i]] = sc[i];
+  scores.reserve(nb); next.reserve(s);
+  std::vector<int32_t> ids; std::vector<double> sc;
+  for (int64_t b = 0; b < nb; b++) {
+    int32_t id, len; rd(f, &id, 1); rd(f, &len, 1);
+    ids.resize(len); sc.resize(len);
+    rd(f, ids.data(), len); rd(f, sc.data(), len);
+    auto& mp = scores[id];
+    mp.reserve(len);
+    for (int32_t i = 0; i < len; i++) mp[ids[i]] = sc[i];
   }
+  for (int64_t i = 0; i < s; i++) next[src[i]];
+  int64_t ns; rd(f, &ns, 1);
+  std::vector<int64_t> off(ns + 1);
+  rd(f, off.data(), ns + 1);
   fclose(f);
-  std::vector<double> maxDiffs(nthreads, 0);
-  std::vector<std::thread> th;
-  auto t0 = std::chrono::steady_clock::now();
-  size_t chunk = src.size() / nthreads;
-  for (int t = 0; t < nthreads; t++) {
-    auto b = src.begin() + chunk * t;
-    auto e = (t == nthreads - 1) ? src.end() : src.begin() + chunk * (t + 1);
-    th.emplace_back(ppr::grankMultiInternal::combineMaps<int, std::vector<int32_t>::iterator>,
-                    b, e, std::ref(g), std::ref(scores), std::ref(next), std::ref(maxDiffs[t]),
-                    (size_t)L, damping);
+  for (int64_t h = 0; h < ns; h++) {
+    std::vector<double> maxDiffs(nthreads, 0);
+    std::vector<std::thread> th;
+    auto b0 = src.begin() + off[h], e0 = src.begin() + off[h + 1];
+    size_t chunk = (size_t)(off[h + 1] - off[h]) / nthreads;
+    auto t0 = std::chrono::steady_clock::now();
+    for (int t = 0; t < nthreads; t++) {
+      auto b = b0 + chunk * t;
+      auto e = (t == nthreads - 1) ? e0 : b0 + chunk * (t + 1);
+      th.emplace_back(ppr::grankMultiInternal::combineMaps<int, std::vector<int32_t>::iterator>,
+                      b, e, std::cref(g), std::cref(scores), std::ref(next), std::ref(maxDiffs[t]),
+                      (size_t)L, damping);
+    }
+    for (auto& t : th) t.join();
+    auto t1 = std::chrono::steady_clock::now();
+    double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    printf("{\"stratum\": %lld, \"sources\": %lld, \"ms\": %.3f, \"threads\": %d}\n", (long long)h,
+           (long long)(off[h + 1] - off[h]), ms, nthreads);
+    fflush(stdout);
   }
-  for (auto& t : th) t.join();
-  auto t1 = std::chrono::steady_clock::now();
-  double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-  printf("{\"sources\": %lld, \"ms\": %.3f, \"threads\": %d}\n", (long long)s, ms, nthreads);
   return 0;
 }
 
@@ -198,8 +203,8 @@ int main(int argc, char** argv) {
   if (argc < 2) die("usage: ref_driver MODE ...");
   std::string mode = argv[1];
   if (mode == "bench_combine") {
-    if (argc < 7) die("bench_combine graph state sample nthreads damping");
-    return bench_combine(argv[2], argv[3], argv[4], atoi(argv[5]), atof(argv[6]));
+    if (argc < 5) die("bench_combine sample nthreads damping");
+    return bench_combine(argv[2], atoi(argv[3]), atof(argv[4]));
   }
   // algorithm modes: MODE in.{bin|csv} out.bin K L iters damping tol threads
   if (argc < 10) die("MODE in out K L iters damping tol threads");

@@ -98,3 +98,18 @@ def test_gpu_deterministic_and_multi_equal():
     m1 = ppr.grank_multi(d, 32, 64, 6, 0.85, -1.0, 4)
     m2 = ppr.grank(d, 32, 64, 6, 0.85, -1.0)
     assert m1 == m2
+
+
+@pytest.mark.parametrize("mask", ["0x10", "0x0", "0x11", "0x3"])
+def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
+    """every merge path alone (workgroup tier / HBM-table path / mixes) matches the oracle"""
+    monkeypatch.setenv("PPR_TIER_MASK", mask)
+    for scale, K, L, it in [(10, 16, 32, 5), (11, 8, 64, 4)]:
+        g = ppr.rmat(scale, seed=77 + scale)
+        part = g.partitions()
+        r = ppr.grank_csr(g, K, L, it, 0.85, -1.0, part=part, device=0)
+        o = oracle.grank(g.row_ptr, g.col, part, K, L, it, 0.85, -1.0)
+        assert np.array_equal(r.max_diff, o["max_diff"])
+        assert np.array_equal(r.lens, o["lens"])
+        assert np.array_equal(r.ids, o["ids"])
+        assert np.array_equal(r.scores, o["scores"])
