@@ -33,10 +33,12 @@
 #include <vector>
 
 #include "../../include/ppr_hip.h"
-#include "ppr_device.h"
+#include "merge_wave.h"
 #include "wg_merge.h"
+#include "merge_hub.h"
+#include "merge_glb.h"
 
-using namespace pprd;
+using namespace pprk;
 
 #define HIP_OK(expr)                                  \
   do {                                                \
@@ -48,476 +50,15 @@ using namespace pprd;
   } while (0)
 
 namespace {
-
-constexpr int NT = 4;                 // single-wave LDS table tiers
-constexpr int TIER_WG = NT;           // workgroup tier (k_merge_wg)
-constexpr int TIER_BIG = NT + 1;      // beyond the workgroup tier
-constexpr int NLISTS = NT + 2;
-constexpr int WG_T = 7168;            // workgroup table slots
-constexpr int WG_PASS_CAP = 4096;     // expected distinct keys per key-bucket pass
-constexpr int WG_PL = 1024;           // partial-list entries (P * L)
-constexpr int MAX_L = 4096;           // widest basket the kernels accept
-constexpr int WAVES_PER_BLOCK = 4;
-
-struct DevGraph {
-  const int64_t* rp;
-  const int32_t* colx;
-  int64_t n;
-};
-
-struct DevSlab {
-  int32_t* ids;
-  double* sc;
-  int32_t* len;
-  int64_t n;
-  int32_t L;
-  __device__ __forceinline__ int64_t row(int slot, int64_t u) const { return ((int64_t)slot * n + u) * L; }
-  __device__ __forceinline__ int64_t lrow(int slot, int64_t u) const { return (int64_t)slot * n + u; }
-};
-
-struct IterArgs {
-  int sA, sB;        // read slot of partition 0 / 1 nodes
-  int active;        // partition updated in this iteration (-1 = init)
-  double damping;
-  uint32_t unit;     // init mode
-  uint32_t stats;
-};
-
-__device__ __forceinline__ int read_slot(const IterArgs& a, int32_t cx) { return (cx < 0) ? a.sB : a.sA; }
-
-// ---------------------------------------------------------------------------------------------
-// classification: C_v = number of candidates of source v (+1 for its own key)
-__global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArgs a,
-                                                  const int32_t* list, int64_t count,
-                                                  const int32_t* tier_cap, int32_t* tier_lists,
-                                                  uint32_t* tier_cnt, int64_t list_cap,
-                                                  int32_t* cand, unsigned long long* stats) {
-  __shared__ unsigned long long red[2][WAVES_PER_BLOCK];
-  const int wv = threadIdx.x >> 6;
-  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
-  unsigned long long my_c = 0, my_b = 0;
-  if (w < count) {
-    const int v = list[w];
-    const int64_t b = g.rp[v], e = g.rp[v + 1];
-    int64_t c = 0;
-    if (a.unit) {
-      c = e - b;
-    } else {
-      for (int64_t i = b + lane_id(); i < e; i += WAVE) {
-        const int32_t cx = g.colx[i];
-        c += s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)];
-      }
-#pragma unroll
-      for (int o = 32; o; o >>= 1) c += __shfl_xor((long long)c, o);
-    }
-    if (lane_id() == 0) {
-      const int64_t need = c + 1;
-      cand[v] = (int32_t)(need > 0x7fffffff ? 0x7fffffff : need);
-      int t = 0;
-      while (t < NT + 1 && need > tier_cap[t]) t++;
-      const uint32_t pos = atomicAdd(&tier_cnt[t], 1u);
-      tier_lists[(int64_t)t * list_cap + pos] = v;
-      const int ownlen = a.unit ? 0 : s.len[s.lrow(a.active == 0 ? a.sA : a.sB, v)];
-      my_c = (unsigned long long)c;
-      my_b = (unsigned long long)(8 + 8 * (e - b) + 12 * c + 12 * ownlen);
-    }
-  }
-  if (a.stats) {
-    if (lane_id() == 0) { red[0][wv] = my_c; red[1][wv] = my_b; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long sc = 0, sb = 0;
-      for (int i = 0; i < WAVES_PER_BLOCK; i++) { sc += red[0][i]; sb += red[1][i]; }
-      if (sc) atomicAdd(&stats[0], sc);
-      if (sb) atomicAdd(&stats[1], sb);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// finish one source from a compacted candidate set (keys/vals, U entries, LDS or global):
-// select top-L, sort, write the next-slot row, norm1 against the old row, maxDiff.
-template <class KeyAt, class ValAt>
-__device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt valat,
-                                              const DevSlab& s, const IterArgs& a, uint32_t* hist,
-                                              uint64_t* rv, int* rk, int Lp, int* hk, int* hv,
-                                              int* mf, unsigned long long* maxdiff,
-                                              unsigned long long* stats) {
-  const int L = s.L;
-  int cnt;
-  if (U <= L) {
-    for (int i = lane_id(); i < U; i += WAVE) { rv[i] = dbits(valat(i)); rk[i] = keyat(i); }
-    cnt = U;
-  } else {
-    const SelCrit c = select_top(U, L, keyat, valat, hist);
-    int base = 0;
-    for (int i0 = 0; i0 < U; i0 += WAVE) {
-      const int i = i0 + lane_id();
-      bool sel = false;
-      uint64_t vb = 0;
-      int key = 0;
-      if (i < U) { key = keyat(i); vb = dbits(valat(i)); sel = sel_test(c, vb, (uint32_t)~key); }
-      const uint64_t m = __ballot(sel);
-      if (sel) { const int pos = base + __popcll(m & lanemask_lt()); rv[pos] = vb; rk[pos] = key; }
-      base += __popcll(m);
-    }
-    cnt = L;
-  }
-  wave_fence();
-  row_sort(rv, rk, cnt, Lp);
-  const int cur = (a.active == 1) ? a.sB : a.sA;
-  if (a.unit) {
-    // init: slot 0; dangling sources never update, so their basket is valid in both slots
-    const int nslots = 2;
-    for (int sl = 0; sl < nslots; sl++) {
-      const int64_t r = s.row(sl, v);
-      for (int i = lane_id(); i < cnt; i += WAVE) { s.ids[r + i] = rk[i]; s.sc[r + i] = bitsd(rv[i]); }
-      if (lane_id() == 0) s.len[s.lrow(sl, v)] = cnt;
-    }
-    return;
-  }
-  const int nxt = cur ^ 1;
-  const int64_t r = s.row(nxt, v);
-  for (int i = lane_id(); i < cnt; i += WAVE) { s.ids[r + i] = rk[i]; s.sc[r + i] = bitsd(rv[i]); }
-  if (lane_id() == 0) s.len[s.lrow(nxt, v)] = cnt;
-  const int64_t ro = s.row(cur, v);
-  const int olen = s.len[s.lrow(cur, v)];
-  const double d1 = row_norm1(rv, rk, cnt, s.ids + ro, s.sc + ro, olen, hk, hv, mf, 2 * Lp);
-  if (lane_id() == 0) {
-    atomicMax(maxdiff, (unsigned long long)dbits(d1));
-    if (a.stats) atomicAdd(&stats[1], (unsigned long long)(12 * cnt + 4));
-  }
-}
-
-// per-wave LDS bytes for table size T and padded width Lp
-// layout: acc f64[T] | keys i32[T] | owner u32[T] | rv u64[Lp] | rk i32[Lp] | hist u32[256] |
-//         hk i32[2Lp] | hv i32[2Lp] | mf i32[Lp]
-__host__ __device__ constexpr size_t lds_wave_bytes(int T, int Lp) {
-  return (size_t)T * 16 + (size_t)Lp * 12 + 1024 + (size_t)Lp * 20;
-}
-
-// ---------------------------------------------------------------------------------------------
-// one wave per source, LDS table of T slots (dynamic LDS: WAVES_PER_BLOCK regions)
-__global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterArgs a,
-                                                   const int32_t* list, int64_t count, int T,
-                                                   int Lp, unsigned long long* maxdiff,
-                                                   unsigned long long* stats) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int wv = threadIdx.x >> 6;
-  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
-  if (w >= count) return;
-  unsigned char* base = smem + (size_t)wv * lds_wave_bytes(T, Lp);
-  LdsTable t;
-  t.acc = reinterpret_cast<double*>(base);
-  t.keys = reinterpret_cast<int*>(base + (size_t)T * 8);
-  t.owner = reinterpret_cast<uint32_t*>(base + (size_t)T * 12);
-  t.mask = (uint32_t)T - 1;
-  uint64_t* rv = reinterpret_cast<uint64_t*>(base + (size_t)T * 16);
-  int* rk = reinterpret_cast<int*>(base + (size_t)T * 16 + (size_t)Lp * 8);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 16 + (size_t)Lp * 12);
-
-  const int v = list[w];
-  const int64_t b = g.rp[v], e = g.rp[v + 1];
-  const double factor = a.damping / (double)(e - b);
-
-  table_clear(t);
-  if (lane_id() == 0) { const uint32_t sl = table_slot(t, v); t.acc[sl] = 1.0 - a.damping; }
-  wave_fence();
-
-  if (a.unit) {
-    for (int64_t e0 = b; e0 < e; e0 += WAVE) {
-      const int64_t i = e0 + lane_id();
-      const bool valid = i < e;
-      const int key = valid ? (g.colx[i] & 0x7fffffff) : 0;
-      table_apply(t, valid, key, 1.0, factor);
-    }
-  } else {
-    for (int64_t e0 = b; e0 < e; e0 += WAVE) {
-      const int64_t i = e0 + lane_id();
-      int u = 0, sl = 0, ln = 0;
-      if (i < e) {
-        const int32_t cx = g.colx[i];
-        u = cx & 0x7fffffff;
-        sl = read_slot(a, cx);
-        ln = s.len[s.lrow(sl, u)];
-      }
-      const int incl = wave_incl_scan(ln);
-      const int total = __shfl(incl, WAVE - 1);
-      for (int g0 = 0; g0 < total; g0 += WAVE) {
-        const int c = g0 + lane_id();
-        const bool valid = c < total;
-        // successor j = number of window entries whose inclusive prefix is <= c
-        int j = 0;
-#pragma unroll
-        for (int step = 32; step; step >>= 1) {
-          const int pv = __shfl(incl, j + step - 1);
-          if (pv <= c) j += step;
-        }
-        const int jj = j < WAVE ? j : WAVE - 1;
-        // every lane must execute the bpermute (an inactive source lane reads back 0)
-        const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
-        const int ex = jj > 0 ? exv : 0;
-        const int uj = __shfl(u, jj);
-        const int sj = __shfl(sl, jj);
-        int key = 0;
-        double sv = 0.0;
-        if (valid) {
-          const int64_t r = s.row(sj, uj) + (c - ex);
-          key = s.ids[r];
-          sv = s.sc[r];
-        }
-        table_apply(t, valid, key, sv, factor);
-      }
-    }
-  }
-  wave_fence();
-  const int U = table_compact(t);
-  int* hk = reinterpret_cast<int*>(base + (size_t)T * 16 + (size_t)Lp * 12 + 1024);
-  int* hv = hk + 2 * Lp;
-  int* mf = hv + 2 * Lp;
-  const int* keys = t.keys;
-  const double* acc = t.acc;
-  finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, s, a, hist,
-                rv, rk, Lp, hk, hv, mf, maxdiff, stats);
-}
-
-// ---------------------------------------------------------------------------------------------
-// one workgroup (8 waves) per source, shared LDS table, P key-bucket passes (wg_merge.h)
-__global__ void __launch_bounds__(WG_THREADS) k_merge_wg(DevGraph g, DevSlab s, IterArgs a,
-                                                         const int32_t* list, int64_t count,
-                                                         const int32_t* cand, int Lp,
-                                                         unsigned long long* maxdiff,
-                                                         unsigned long long* stats,
-                                                         int32_t* ovf_list, uint32_t* ovf_cnt) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int64_t w = blockIdx.x;
-  if (w >= count) return;
-  const WgLds L = wg_carve(smem, WG_T, Lp, WG_PL);
-  const int wv = threadIdx.x >> 6;
-  const int l = lane_id();
-  const int v = list[w];
-  const int64_t b = g.rp[v], e = g.rp[v + 1];
-  const double factor = a.damping / (double)(e - b);
-  const int need = cand[v];
-  const int P = (need + WG_PASS_CAP - 1) / WG_PASS_CAP;
-  const uint32_t T = WG_T, budget = WG_T - 512;
-  const int Lw = s.L;
-  if (threadIdx.x == 0) { L.misc[M_PLEN] = 0; L.misc[M_OVF] = 0; }
-
-  for (int pass = 0; pass < P; pass++) {
-    for (int i = threadIdx.x; i < (int)T; i += WG_THREADS) { L.keys[i] = EMPTY; L.owner[i] = NO_OWNER; }
-    if (threadIdx.x == 0) L.misc[M_FILL] = 0;
-    __syncthreads();
-    if (threadIdx.x == 0 && (P == 1 || (int)(hash_b((uint32_t)v) % (uint32_t)P) == pass)) {
-      const uint32_t sl = wg_slot(L.keys, L.acc, T, (uint32_t)(((uint64_t)hash32((uint32_t)v) * T) >> 32), v,
-                                  reinterpret_cast<uint32_t*>(&L.misc[M_FILL]), budget);
-      L.acc[sl] = 1.0 - a.damping;
-    }
-    __syncthreads();
-    auto inpass = [&](int key) { return P == 1 || (int)(hash_b((uint32_t)key) % (uint32_t)P) == pass; };
-    if (a.unit) {
-      const int64_t deg = e - b;
-      for (int64_t c0 = 0; c0 < deg; c0 += WG_CHUNK) {
-        const int64_t q0 = c0 + wv * 128 + l, q1 = q0 + 64;
-        const bool v0 = q0 < deg, v1 = q1 < deg;
-        const int k0 = v0 ? (g.colx[b + q0] & 0x7fffffff) : 0;
-        const int k1 = v1 ? (g.colx[b + q1] & 0x7fffffff) : 0;
-        wg_route_apply(L, T, budget, v0 && inpass(k0), k0, 1.0, v1 && inpass(k1), k1, 1.0, factor);
-      }
-    } else {
-      for (int64_t wb = b; wb < e; wb += WG_WIN) {
-        const int64_t i = wb + threadIdx.x;
-        int u = 0, sl = 0, ln = 0;
-        if (i < e) {
-          const int32_t cx = g.colx[i];
-          u = cx & 0x7fffffff;
-          sl = read_slot(a, cx);
-          ln = s.len[s.lrow(sl, u)];
-        }
-        const int incl = wg_incl_scan(ln, L.cnt);
-        L.wpre[threadIdx.x] = incl;
-        L.wu[threadIdx.x] = u;
-        L.wsl[threadIdx.x] = sl;
-        __syncthreads();
-        const int W = L.wpre[WG_WIN - 1];
-        for (int c0 = 0; c0 < W; c0 += WG_CHUNK) {
-          int kk[2] = {0, 0};
-          double ss[2] = {0.0, 0.0};
-          bool vv[2] = {false, false};
-#pragma unroll
-          for (int h = 0; h < 2; h++) {
-            const int q = c0 + wv * 128 + h * 64 + l;
-            if (q < W) {
-              int j = 0;
-#pragma unroll
-              for (int step = WG_WIN / 2; step; step >>= 1)
-                if (L.wpre[j + step - 1] <= q) j += step;
-              const int ex = j > 0 ? L.wpre[j - 1] : 0;
-              const int64_t r = s.row(L.wsl[j], L.wu[j]) + (q - ex);
-              kk[h] = s.ids[r];
-              ss[h] = s.sc[r];
-              vv[h] = inpass(kk[h]);
-            }
-          }
-          wg_route_apply(L, T, budget, vv[0], kk[0], ss[0], vv[1], kk[1], ss[1], factor);
-        }
-        __syncthreads();  // window arrays are rewritten next
-      }
-    }
-    if (L.misc[M_OVF]) break;  // uniform: read after the last barrier of wg_route_apply
-    // this pass's top-L (by the global rule) goes to the partial list
-    const int U = L.misc[M_FILL];
-    auto occ = [&](int i) { return L.keys[i] != EMPTY; };
-    if (U <= Lw) {
-      for (int i = threadIdx.x; i < (int)T; i += WG_THREADS)
-        if (occ(i)) { const int pos = atomicAdd(&L.misc[M_PLEN], 1); L.pk[pos] = L.keys[i]; L.pv[pos] = L.acc[i]; }
-    } else {
-      const SelCrit c = wg_select_top(L, (int)T, Lw, [&](int i) { return L.keys[i]; },
-                                      [&](int i) { return L.acc[i]; }, occ);
-      for (int i = threadIdx.x; i < (int)T; i += WG_THREADS) {
-        if (!occ(i)) continue;
-        const int key = L.keys[i];
-        if (sel_test(c, dbits(L.acc[i]), (uint32_t)~key)) {
-          const int pos = atomicAdd(&L.misc[M_PLEN], 1);
-          L.pk[pos] = key;
-          L.pv[pos] = L.acc[i];
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (L.misc[M_OVF]) {
-    if (threadIdx.x == 0) { const uint32_t pos = atomicAdd(ovf_cnt, 1u); ovf_list[pos] = v; }
-    return;
-  }
-  if (wv == 0) {
-    const int n = L.misc[M_PLEN];
-    const int* pk = L.pk;
-    const double* pv = L.pv;
-    finish_source(v, n, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; }, s, a, L.hist,
-                  L.rv, L.rk, Lp, L.hk, L.hv, L.mf, maxdiff, stats);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// big sources: one wave per source, table in HBM scratch (per-source region of T slots)
-struct GlbWork {
-  int32_t v;
-  int32_t pad;
-  int64_t off;   // slot offset into the scratch arrays
-  int64_t T;     // table slots (power of two)
-};
-
-__global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArgs a,
-                                                  const GlbWork* work, int64_t count,
-                                                  int32_t* gkeys, double* gacc, int32_t* ckeys,
-                                                  double* cacc, int Lp,
-                                                  unsigned long long* maxdiff,
-                                                  unsigned long long* stats) {
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int64_t w = blockIdx.x;
-  if (w >= count) return;
-  const GlbWork wk = work[w];
-  const int v = wk.v;
-  int32_t* keys = gkeys + wk.off;
-  double* acc = gacc + wk.off;
-  const uint64_t mask = (uint64_t)wk.T - 1;
-  uint64_t* rv = reinterpret_cast<uint64_t*>(smem);
-  int* rk = reinterpret_cast<int*>(smem + (size_t)Lp * 8);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + (size_t)Lp * 12);
-  int* hk = reinterpret_cast<int*>(smem + (size_t)Lp * 12 + 1024);
-  int* hv = hk + 2 * Lp;
-  int* mf = hv + 2 * Lp;
-
-  for (int64_t i = lane_id(); i < wk.T; i += WAVE) keys[i] = EMPTY;
-  __threadfence_block();
-  const int64_t b = g.rp[v], e = g.rp[v + 1];
-  const double factor = a.damping / (double)(e - b);
-
-  auto slot_of = [&](int key) -> uint64_t {
-    uint64_t h = hash32((uint32_t)key) & mask;
-    for (;;) {
-      const int prev = atomicCAS(&keys[h], EMPTY, key);
-      if (prev == EMPTY) {
-        __hip_atomic_store(&acc[h], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return h;
-      }
-      if (prev == key) return h;
-      h = (h + 1) & mask;
-    }
-  };
-  if (lane_id() == 0) {
-    const uint64_t h = slot_of(v);
-    __hip_atomic_store(&acc[h], 1.0 - a.damping, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __threadfence_block();
-  // one successor basket per step: its keys are distinct, so lanes never collide within a step
-  for (int64_t i = b; i < e; i++) {
-    const int32_t cx = g.colx[i];
-    const int u = cx & 0x7fffffff;
-    int ln;
-    int64_t r = 0;
-    if (a.unit) ln = 1;
-    else { const int sl = read_slot(a, cx); ln = s.len[s.lrow(sl, u)]; r = s.row(sl, u); }
-    for (int j = lane_id(); j < ln; j += WAVE) {
-      const int key = a.unit ? u : s.ids[r + j];
-      const double sv = a.unit ? 1.0 : s.sc[r + j];
-      const uint64_t h = slot_of(key);
-      const double cur = __hip_atomic_load(&acc[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&acc[h], fma(sv, factor, cur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __threadfence_block();
-  }
-  // compact into ckeys/cacc
-  int32_t* ck = ckeys + wk.off;
-  double* ca = cacc + wk.off;
-  int U = 0;
-  for (int64_t base = 0; base < wk.T; base += WAVE) {
-    const int64_t i = base + lane_id();
-    const int k = __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool occ = k != EMPTY;
-    const uint64_t m = __ballot(occ);
-    if (occ) {
-      const int pos = U + __popcll(m & lanemask_lt());
-      ck[pos] = k;
-      ca[pos] = __hip_atomic_load(&acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    U += __popcll(m);
-  }
-  __threadfence_block();
-  finish_source(v, U, [&](int i) { return ck[i]; }, [&](int i) { return ca[i]; }, s, a, hist, rv,
-                rk, Lp, hk, hv, mf, maxdiff, stats);
-}
-
-// ---------------------------------------------------------------------------------------------
-// final top-K (include/grank.h:143-147): rows are sorted, so top-K is the first min(K, len)
-__global__ void k_topk(DevSlab s, const uint8_t* part, int sA, int sB, int K, int32_t* oid,
-                       double* osc, int32_t* olen) {
-  const int64_t v = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
-  if (v >= s.n) return;
-  const int sl = part[v] ? sB : sA;
-  const int len = s.len[s.lrow(sl, v)];
-  const int k = len < K ? len : K;
-  const int64_t r = s.row(sl, v);
-  for (int i = lane_id(); i < K; i += WAVE) {
-    oid[v * K + i] = i < k ? s.ids[r + i] : -1;
-    osc[v * K + i] = i < k ? s.sc[r + i] : 0.0;
-  }
-  if (lane_id() == 0) olen[v] = k;
-}
-
-__global__ void k_zero_u64(unsigned long long* p, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = 0ull;
-}
+constexpr int WG_TIER_PASSES = 3;
 
 int pow2_at_least(int64_t x) {
   int p = 1;
   while (p < x) p <<= 1;
   return p;
 }
-
 }  // namespace
+
 
 // ================================================================================================
 // plan
@@ -546,6 +87,7 @@ struct ppr_plan {
   int tierT[NT] = {0, 0, 0, 0};
   int tierCap[NT + 1] = {0, 0, 0, 0, 0};
   size_t wg_lds = 0;
+  bool hub_enabled = true;
   unsigned long long* d_maxdiff = nullptr;  // PPR_MAX_ITER_STATS + 1
   unsigned long long* d_stats = nullptr;    // 2
   GlbWork* d_work = nullptr;
@@ -556,6 +98,8 @@ struct ppr_plan {
   double* d_out_sc = nullptr;
   int32_t* d_out_len = nullptr;
   int flags = 0;
+  std::vector<int64_t> h_rp;       // host row pointers (hub planning)
+  size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0;
   int64_t merge_launches = 0;
   double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_m0 = nullptr, ev_m1 = nullptr;
@@ -641,12 +185,14 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
       p->tierT[t] = T;
       p->tierCap[t] = T / 4 * 3;
     }
-    // workgroup tier: P = ceil(need / WG_PASS_CAP) key-bucket passes with P * L <= WG_PL
+    // workgroup tier: up to WG_TIER_PASSES key-bucket passes over the slab stream; beyond that
+    // the hub pipeline's one partition pass is cheaper than re-reading the stream
     p->tierCap[NT] = 0;
-    p->wg_lds = wg_lds_bytes(WG_T, p->Lp, WG_PL);
-    const int pmax = WG_PL / (int)L;
+    p->wg_lds = wg_lds_bytes(WG_T, p->Lp, wg_pl(p->Lp));
+    const int pmax = WG_TIER_PASSES;
+    p->hub_enabled = ((mask >> (NT + 1)) & 1) && pmax >= 1 && p->wg_lds <= 160 * 1024;
     if (((mask >> NT) & 1) && pmax >= 1 && p->wg_lds <= 160 * 1024)
-      p->tierCap[NT] = std::min(pmax, 8) * WG_PASS_CAP;
+      p->tierCap[NT] = pmax * WG_PASS_CAP;
     // a disabled tier has cap 0 (k_classify skips it); enabled caps must be non-decreasing
     int run = 0;
     for (int t = 0; t <= NT; t++) {
@@ -664,6 +210,7 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
     all[v] = (int32_t)v;
     if (g->row_ptr[v + 1] > g->row_ptr[v]) act[part[v]].push_back((int32_t)v);
   }
+  p->h_rp.assign(g->row_ptr, g->row_ptr + n + 1);
   p->nact[0] = (int64_t)act[0].size();
   p->nact[1] = (int64_t)act[1].size();
 
@@ -710,6 +257,12 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
     }
   if (p->tierCap[NT])
     hipFuncSetAttribute((const void*)k_merge_wg, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  p->hub_lds_wg = wg_lds_bytes(WG_T, p->Lp, wg_pl(p->Lp));
+  p->hub_lds_final = wg_lds_bytes(0, p->Lp, 0);
+  hipFuncSetAttribute((const void*)k_hub_bucket, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_count, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   *out = p;
   return PPR_OK;
 }
@@ -731,6 +284,132 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
 
 static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
                           unsigned long long* maxdiff);
+
+static int ensure_scratch(ppr_plan* p, size_t need) {
+  if (need <= p->scratch_bytes) return PPR_OK;
+  HIP_OK(hipStreamSynchronize(p->stream));
+  hipFree(p->d_scratch);
+  p->d_scratch = nullptr;
+  p->scratch_bytes = 0;
+  if (hipMalloc(&p->d_scratch, need) != hipSuccess) return PPR_ERR_OOM;
+  p->scratch_bytes = need;
+  return PPR_OK;
+}
+
+static int ceil_log2(int64_t x) { int k = 0; while ((1LL << k) < x) k++; return k; }
+
+// Hub pipeline over `big` (sources beyond the workgroup tier). Sources whose buckets overflow
+// the workgroup accumulator are appended to `fallback` (HBM-table path).
+static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& big,
+                    const std::vector<int32_t>& cand, unsigned long long* maxdiff,
+                    std::vector<int32_t>& fallback) {
+  hipStream_t st = p->stream;
+  DevGraph g{p->d_rp, p->d_colx, p->n};
+  DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
+  const int64_t L = p->L;
+  const int64_t budget = 1LL << 28;  // staged candidates per batch (3 GiB of keys + scores)
+  size_t i0 = 0;
+  while (i0 < big.size()) {
+    std::vector<HubDesc> desc;
+    std::vector<HubTask> tiles, buckets;
+    int64_t cm = 0, stg = 0, pt = 0, bkn = 0;
+    int maxP = 1;
+    size_t i = i0;
+    while (i < big.size()) {
+      const int v = big[i];
+      const int64_t need = cand[v];
+      const int64_t deg = p->h_rp[v + 1] - p->h_rp[v];
+      if (!desc.empty() && stg + need > budget) break;
+      int logP = ceil_log2((need + HUB_BUCKET - 1) / HUB_BUCKET);
+      logP = std::max(1, std::min(HUB_MAX_LOGP, logP));
+      const int P = 1 << logP;
+      const int T = (int)((deg + HUB_TILE - 1) / HUB_TILE);
+      const int idx = (int)desc.size();
+      desc.push_back(HubDesc{v, logP, T, (int32_t)need, cm, stg, pt, bkn});
+      for (int t = 0; t < T; t++) tiles.push_back(HubTask{idx, t});
+      for (int b = 0; b < P; b++) buckets.push_back(HubTask{idx, b});
+      cm += (int64_t)P * T;
+      stg += need - 1;
+      pt += (int64_t)P * L;
+      bkn += 2 * P + 1;
+      maxP = std::max(maxP, P);
+      i++;
+    }
+    // scratch layout
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t off = 0;
+    const size_t o_desc = off; off = al(off + sizeof(HubDesc) * desc.size());
+    const size_t o_tile = off; off = al(off + sizeof(HubTask) * tiles.size());
+    const size_t o_buck = off; off = al(off + sizeof(HubTask) * buckets.size());
+    const size_t o_cm = off;   off = al(off + 4 * (size_t)cm);
+    const size_t o_bk = off;   off = al(off + 4 * (size_t)bkn);
+    const size_t o_sk = off;   off = al(off + 4 * (size_t)stg);
+    const size_t o_ss = off;   off = al(off + 8 * (size_t)stg);
+    const size_t o_pk = off;   off = al(off + 4 * (size_t)pt);
+    const size_t o_ps = off;   off = al(off + 8 * (size_t)pt);
+    const size_t o_ovf = off;  off = al(off + 4 * (buckets.size() + 1));
+    int rc = ensure_scratch(p, off);
+    if (rc) return rc;
+    char* base = (char*)p->d_scratch;
+    HubDesc* d_desc = (HubDesc*)(base + o_desc);
+    HubTask* d_tile = (HubTask*)(base + o_tile);
+    HubTask* d_buck = (HubTask*)(base + o_buck);
+    int32_t* d_cm = (int32_t*)(base + o_cm);
+    int32_t* d_bk = (int32_t*)(base + o_bk);
+    int32_t* d_sk = (int32_t*)(base + o_sk);
+    double* d_ss = (double*)(base + o_ss);
+    int32_t* d_pk = (int32_t*)(base + o_pk);
+    double* d_ps = (double*)(base + o_ps);
+    int32_t* d_ovf = (int32_t*)(base + o_ovf);
+    uint32_t* d_ovf_cnt = (uint32_t*)(d_ovf + buckets.size());
+    HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * desc.size(), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_tile, tiles.data(), sizeof(HubTask) * tiles.size(), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(d_buck, buckets.data(), sizeof(HubTask) * buckets.size(), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(d_ovf_cnt, 0, 4, st));
+    const int64_t ntiles = (int64_t)tiles.size();
+    const size_t lds_tile = (size_t)WAVES_PER_BLOCK * maxP * 4;
+    const unsigned tb = (unsigned)((ntiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(k_hub_scan, dim3((unsigned)desc.size()), dim3(1024), 0, st, d_desc, d_cm, d_bk);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
+                       d_cm, d_sk, d_ss);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(k_hub_bucket, dim3((unsigned)buckets.size()), dim3(WG_THREADS), p->hub_lds_wg, st, s, a, g,
+                       d_desc, d_buck, d_bk, d_sk, d_ss, d_pk, d_ps, d_bk, p->Lp, d_ovf, d_ovf_cnt);
+    HIP_OK(hipGetLastError());
+    uint32_t novf = 0;
+    HIP_OK(hipMemcpyAsync(&novf, d_ovf_cnt, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (novf) {
+      // sources with an overflowing bucket skip the final merge and take the HBM-table path:
+      // give them an empty descriptor range (logP stays, but their final is not launched)
+      std::vector<int32_t> ov(novf);
+      HIP_OK(hipMemcpyAsync(ov.data(), d_ovf, 4 * (size_t)novf, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      std::vector<char> bad(desc.size(), 0);
+      for (int32_t x : ov) bad[-x - 1] = 1;
+      std::vector<HubDesc> keep;
+      for (size_t k = 0; k < desc.size(); k++) {
+        if (bad[k]) fallback.push_back(desc[k].v);
+        else keep.push_back(desc[k]);
+      }
+      desc.swap(keep);
+      if (!desc.empty())
+        HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * desc.size(), hipMemcpyHostToDevice, st));
+    }
+    if (!desc.empty()) {
+      hipLaunchKernelGGL(k_hub_final, dim3((unsigned)desc.size()), dim3(WG_THREADS), p->hub_lds_final, st, s, a,
+                         d_desc, d_bk, d_pk, d_ps, p->Lp, maxdiff, p->d_stats);
+      HIP_OK(hipGetLastError());
+    }
+    p->merge_launches += 5;
+    HIP_OK(hipStreamSynchronize(st));  // scratch is reused by the next batch
+    i0 = i;
+  }
+  return PPR_OK;
+}
 
 // classify + launch all tiers for `count` sources of `list`; the span is timed with events on
 // the plan's stream and added to merge_ms (iterations only, not init)
@@ -792,8 +471,21 @@ static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, i
   };
   for (int t = 0; t < NT; t++)
     if (cnt[t] && !p->tierT[t]) { int r = pull(p->d_tier_lists + (int64_t)t * p->n, cnt[t]); if (r) return r; }
-  { int r = pull(p->d_tier_lists + (int64_t)TIER_BIG * p->n, cnt[TIER_BIG]); if (r) return r; }
   { int r = pull(p->d_ovf, cnt[NLISTS]); if (r) return r; }
+  if (cnt[TIER_BIG]) {
+    std::vector<int32_t> hubs(cnt[TIER_BIG]);
+    HIP_OK(hipMemcpyAsync(hubs.data(), p->d_tier_lists + (int64_t)TIER_BIG * p->n, 4 * (size_t)cnt[TIER_BIG],
+                          hipMemcpyDeviceToHost, st));
+    std::vector<int32_t> hcand(p->n);
+    HIP_OK(hipMemcpyAsync(hcand.data(), p->d_cand, 4 * (size_t)p->n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (p->hub_enabled) {
+      int r = run_hubs(p, a, hubs, hcand, maxdiff, big);
+      if (r) return r;
+    } else {
+      big.insert(big.end(), hubs.begin(), hubs.end());
+    }
+  }
   if (big.empty()) return PPR_OK;
   std::vector<int32_t> cand(p->n);
   HIP_OK(hipMemcpyAsync(cand.data(), p->d_cand, 4 * (size_t)p->n, hipMemcpyDeviceToHost, st));
@@ -863,7 +555,17 @@ extern "C" int ppr_grank_plan_iterate(ppr_plan* p, int32_t it, int64_t begin, in
   if (end <= begin) return PPR_OK;
   IterArgs a = iter_args(p, it, false);
   unsigned long long* md = p->d_maxdiff + (it < PPR_MAX_ITER_STATS ? it : PPR_MAX_ITER_STATS);
-  return run_merge(p, a, p->d_act[part] + begin, end - begin, md);
+  int rc = run_merge(p, a, p->d_act[part] + begin, end - begin, md);
+  if (rc) return rc;
+  if (a.stats) {  // bytes of the rows this iteration wrote (outside the timed merge span)
+    DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
+    const int64_t cnt = end - begin;
+    const unsigned blocks = (unsigned)std::min<int64_t>((cnt + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_stat_written, dim3(blocks), dim3(256), 0, p->stream, s, a,
+                       p->d_act[part] + begin, cnt, p->d_stats);
+    HIP_OK(hipGetLastError());
+  }
+  return PPR_OK;
 }
 
 extern "C" int ppr_grank_plan_read_maxdiff(ppr_plan* p, int32_t it, double* maxdiff) {

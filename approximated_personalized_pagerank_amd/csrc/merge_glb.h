@@ -1,0 +1,123 @@
+// merge_glb.h -- last-resort path: one wave per source with its hash table in HBM scratch
+// (one successor basket per step; the keys of one basket are distinct, so lanes never collide
+// within a step and the per-key order is the successor order). Used only for sources whose
+// key-bucket passes still overflow the workgroup table, and for tier tests.
+#pragma once
+#include "ppr_common.h"
+
+namespace pprk {
+
+// ---------------------------------------------------------------------------------------------
+// big sources: one wave per source, table in HBM scratch (per-source region of T slots)
+struct GlbWork {
+  int32_t v;
+  int32_t pad;
+  int64_t off;   // slot offset into the scratch arrays
+  int64_t T;     // table slots (power of two)
+};
+
+__global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArgs a,
+                                                  const GlbWork* work, int64_t count,
+                                                  int32_t* gkeys, double* gacc, int32_t* ckeys,
+                                                  double* cacc, int Lp,
+                                                  unsigned long long* maxdiff,
+                                                  unsigned long long* stats) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int64_t w = blockIdx.x;
+  if (w >= count) return;
+  const GlbWork wk = work[w];
+  const int v = wk.v;
+  int32_t* keys = gkeys + wk.off;
+  double* acc = gacc + wk.off;
+  const uint64_t mask = (uint64_t)wk.T - 1;
+  uint64_t* rv = reinterpret_cast<uint64_t*>(smem);
+  int* rk = reinterpret_cast<int*>(smem + (size_t)Lp * 8);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + (size_t)Lp * 12);
+  int* hk = reinterpret_cast<int*>(smem + (size_t)Lp * 12 + 1024);
+  int* hv = hk + 2 * Lp;
+  int* mf = hv + 2 * Lp;
+
+  for (int64_t i = lane_id(); i < wk.T; i += WAVE) keys[i] = EMPTY;
+  __threadfence_block();
+  const int64_t b = g.rp[v], e = g.rp[v + 1];
+  const double factor = a.damping / (double)(e - b);
+
+  auto slot_of = [&](int key) -> uint64_t {
+    uint64_t h = hash32((uint32_t)key) & mask;
+    for (;;) {
+      const int prev = atomicCAS(&keys[h], EMPTY, key);
+      if (prev == EMPTY) {
+        __hip_atomic_store(&acc[h], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return h;
+      }
+      if (prev == key) return h;
+      h = (h + 1) & mask;
+    }
+  };
+  if (lane_id() == 0) {
+    const uint64_t h = slot_of(v);
+    __hip_atomic_store(&acc[h], 1.0 - a.damping, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __threadfence_block();
+  // one successor basket per step: its keys are distinct, so lanes never collide within a step
+  for (int64_t i = b; i < e; i++) {
+    const int32_t cx = g.colx[i];
+    const int u = cx & 0x7fffffff;
+    int ln;
+    int64_t r = 0;
+    if (a.unit) ln = 1;
+    else { const int sl = read_slot(a, cx); ln = s.len[s.lrow(sl, u)]; r = s.row(sl, u); }
+    for (int j = lane_id(); j < ln; j += WAVE) {
+      const int key = a.unit ? u : s.ids[r + j];
+      const double sv = a.unit ? 1.0 : s.sc[r + j];
+      const uint64_t h = slot_of(key);
+      const double cur = __hip_atomic_load(&acc[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&acc[h], fma(sv, factor, cur), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __threadfence_block();
+  }
+  // compact into ckeys/cacc
+  int32_t* ck = ckeys + wk.off;
+  double* ca = cacc + wk.off;
+  int U = 0;
+  for (int64_t base = 0; base < wk.T; base += WAVE) {
+    const int64_t i = base + lane_id();
+    const int k = __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool occ = k != EMPTY;
+    const uint64_t m = __ballot(occ);
+    if (occ) {
+      const int pos = U + __popcll(m & lanemask_lt());
+      ck[pos] = k;
+      ca[pos] = __hip_atomic_load(&acc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    U += __popcll(m);
+  }
+  __threadfence_block();
+  finish_source(v, U, [&](int i) { return ck[i]; }, [&](int i) { return ca[i]; }, s, a, hist, rv,
+                rk, Lp, hk, hv, mf, maxdiff, stats);
+}
+
+// ---------------------------------------------------------------------------------------------
+// final top-K (include/grank.h:143-147): rows are sorted, so top-K is the first min(K, len)
+__global__ void k_topk(DevSlab s, const uint8_t* part, int sA, int sB, int K, int32_t* oid,
+                       double* osc, int32_t* olen) {
+  const int64_t v = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
+  if (v >= s.n) return;
+  const int sl = part[v] ? sB : sA;
+  const int len = s.len[s.lrow(sl, v)];
+  const int k = len < K ? len : K;
+  const int64_t r = s.row(sl, v);
+  for (int i = lane_id(); i < K; i += WAVE) {
+    oid[v * K + i] = i < k ? s.ids[r + i] : -1;
+    osc[v * K + i] = i < k ? s.sc[r + i] : 0.0;
+  }
+  if (lane_id() == 0) olen[v] = k;
+}
+
+__global__ void k_zero_u64(unsigned long long* p, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0ull;
+}
+
+
+}  // namespace pprk

@@ -1,0 +1,277 @@
+// merge_hub.h -- sources beyond the workgroup tier ("hubs"): stable key-bucket partition.
+#pragma once
+#include "wg_merge.h"
+
+namespace pprk {
+
+// ---------------------------------------------------------------------------------------------
+// Hub pipeline (sources beyond the workgroup tier). A source's candidate stream (successor order)
+// is split by key into P = 2^logP buckets with a STABLE partition, so each key's contributions
+// keep their successor order inside its bucket; every bucket is then accumulated by the
+// workgroup kernel (one key set per bucket, disjoint across buckets) and the per-bucket top-L
+// lists are merged by one workgroup per source.
+//   k_hub_count    wave per tile (64 successors): per-bucket counts -> cm[b][t]
+//   k_hub_scan     block per source: exclusive scan of cm in (b, t) order -> scatter offsets
+//   k_hub_scatter  wave per tile: ballot ranks inside a group + running per-bucket counters
+//   k_hub_bucket   workgroup per bucket: k_merge_wg's accumulation on the bucket stream
+//   k_hub_final    workgroup per source: top-L of the bucket lists, row, norm1
+constexpr int HUB_TILE = 64;          // successors per tile (one wave)
+constexpr int HUB_BUCKET = 4096;      // target candidates per bucket
+constexpr int HUB_MAX_LOGP = 12;
+
+struct HubDesc {
+  int32_t v;
+  int32_t logP;
+  int32_t T;       // tiles
+  int32_t need;    // candidates + 1
+  int64_t cm_off;  // count matrix (P*T ints)
+  int64_t st_off;  // staging (need-1 keys / scores)
+  int64_t pt_off;  // bucket top-L lists (P*L)
+  int64_t bk_off;  // bucket starts [P+1] then list lengths [P]
+};
+struct HubTask { int32_t d; int32_t x; };   // (descriptor, tile or bucket)
+
+__device__ __forceinline__ uint32_t hub_digit(int key, int logP) {
+  return logP == 0 ? 0u : (hash_b((uint32_t)key) >> (32 - logP));
+}
+
+// walk the candidates of tile t of source d in successor order, 64 per step
+template <class F>
+__device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
+                                              int v, int t, F f) {
+  const int64_t b = g.rp[v], e = g.rp[v + 1];
+  const int64_t i = b + (int64_t)t * HUB_TILE + lane_id();
+  if (a.unit) {  // init: every successor contributes {u: 1.0}
+    const bool valid = i < e;
+    f(valid, valid ? (g.colx[i] & 0x7fffffff) : 0, 1.0);
+    return;
+  }
+  int u = 0, sl = 0, ln = 0;
+  if (i < e) {
+    const int32_t cx = g.colx[i];
+    u = cx & 0x7fffffff;
+    sl = read_slot(a, cx);
+    ln = s.len[s.lrow(sl, u)];
+  }
+  const int incl = wave_incl_scan(ln);
+  const int total = __shfl(incl, WAVE - 1);
+  for (int g0 = 0; g0 < total; g0 += WAVE) {
+    const int c = g0 + lane_id();
+    const bool valid = c < total;
+    int j = 0;
+#pragma unroll
+    for (int step = 32; step; step >>= 1) {
+      const int pv = __shfl(incl, j + step - 1);
+      if (pv <= c) j += step;
+    }
+    const int jj = j < WAVE ? j : WAVE - 1;
+    const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
+    const int ex = jj > 0 ? exv : 0;
+    const int uj = __shfl(u, jj);
+    const int sj = __shfl(sl, jj);
+    int key = 0;
+    double sv = 0.0;
+    if (valid) {
+      const int64_t r = s.row(sj, uj) + (c - ex);
+      key = s.ids[r];
+      sv = s.sc[r];
+    }
+    f(valid, key, sv);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterArgs a,
+                                                   const HubDesc* desc, const HubTask* tasks,
+                                                   int64_t ntasks, int maxP, int32_t* cm) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
+  if (w >= ntasks) return;
+  const HubTask tk = tasks[w];
+  const HubDesc d = desc[tk.d];
+  const int P = 1 << d.logP;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * maxP;
+  for (int i = lane_id(); i < P; i += WAVE) hist[i] = 0;
+  wave_fence();
+  hub_tile_walk(g, s, a, d.v, tk.x, [&](bool valid, int key, double) {
+    if (valid) atomicAdd(&hist[hub_digit(key, d.logP)], 1u);
+  });
+  wave_fence();
+  for (int i = lane_id(); i < P; i += WAVE) cm[d.cm_off + (int64_t)i * d.T + tk.x] = (int32_t)hist[i];
+}
+
+__global__ void __launch_bounds__(1024) k_hub_scan(const HubDesc* desc, int32_t* cm, int32_t* bk) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const HubDesc d = desc[blockIdx.x];
+  const int P = 1 << d.logP;
+  const int64_t n = (int64_t)P * d.T;
+  int32_t* c = cm + d.cm_off;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int x = i < n ? c[i] : 0;
+    const int incl = wave_incl_scan(x);
+    if (lane_id() == WAVE - 1) wsum[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    int add = carry;
+    for (int k = 0; k < (int)(threadIdx.x >> 6); k++) add += wsum[k];
+    if (i < n) c[i] = add + incl - x;   // exclusive
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = add + incl;
+    __syncthreads();
+  }
+  int32_t* b = bk + d.bk_off;
+  for (int i = threadIdx.x; i < P; i += 1024) b[i] = d.T ? c[(int64_t)i * d.T] : 0;
+  if (threadIdx.x == 0) b[P] = carry;
+}
+
+__global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, IterArgs a,
+                                                     const HubDesc* desc, const HubTask* tasks,
+                                                     int64_t ntasks, int maxP, const int32_t* cm,
+                                                     int32_t* st_key, double* st_sc) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
+  if (w >= ntasks) return;
+  const HubTask tk = tasks[w];
+  const HubDesc d = desc[tk.d];
+  const int P = 1 << d.logP;
+  uint32_t* run = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * maxP;
+  for (int i = lane_id(); i < P; i += WAVE) run[i] = 0;
+  wave_fence();
+  const uint64_t lt = lanemask_lt();
+  hub_tile_walk(g, s, a, d.v, tk.x, [&](bool valid, int key, double sv) {
+    const uint32_t dg = valid ? hub_digit(key, d.logP) : 0u;
+    // lanes holding the same digit: AND of per-bit ballots (stable rank = lower lanes first)
+    uint64_t match = __ballot(valid);
+    for (int bit = 0; bit < d.logP; bit++) {
+      const uint64_t bb = __ballot(valid && ((dg >> bit) & 1u));
+      match &= ((dg >> bit) & 1u) ? bb : ~bb;
+    }
+    const int rank = __popcll(match & lt);
+    const uint32_t base = valid ? run[dg] : 0u;
+    wave_fence();
+    if (valid) {
+      if (rank == 0) run[dg] = base + (uint32_t)__popcll(match);
+      const int64_t pos = d.st_off + cm[d.cm_off + (int64_t)dg * d.T + tk.x] + base + rank;
+      st_key[pos] = key;
+      st_sc[pos] = sv;
+    }
+    wave_fence();
+  });
+}
+
+__global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a,
+                                                           const DevGraph g, const HubDesc* desc,
+                                                           const HubTask* tasks, const int32_t* bk_all,
+                                                           const int32_t* st_key, const double* st_sc,
+                                                           int32_t* pt_key, double* pt_sc,
+                                                           int32_t* bk_len_all, int Lp,
+                                                           int32_t* ovf_list, uint32_t* ovf_cnt) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const HubTask tk = tasks[blockIdx.x];
+  const HubDesc d = desc[tk.d];
+  const WgLds L = wg_carve(smem, WG_T, Lp, wg_pl(Lp));
+  const int wv = threadIdx.x >> 6;
+  const int l = lane_id();
+  const int v = d.v;
+  const int P = 1 << d.logP;
+  const int32_t* bk = bk_all + d.bk_off;
+  const int64_t sb = d.st_off + bk[tk.x], nb = bk[tk.x + 1] - bk[tk.x];
+  const bool seed = (int)hub_digit(v, d.logP) == tk.x;
+  const double factor = a.damping / (double)(g.rp[v + 1] - g.rp[v]);
+  const int Lw = s.L;
+  // the bucket stream: staged (key, score) in successor order, next chunk loaded ahead
+  auto each = [&](auto&& fn) {
+    auto ld = [&](int64_t q, bool& vv, int& kk, double& ss) {
+      vv = q < nb;
+      kk = vv ? st_key[sb + q] : 0;
+      ss = vv ? st_sc[sb + q] : 0.0;
+    };
+    bool nv0, nv1;
+    int nk0, nk1;
+    double ns0, ns1;
+    ld(wv * 128 + l, nv0, nk0, ns0);
+    ld(wv * 128 + 64 + l, nv1, nk1, ns1);
+    for (int64_t c0 = 0; c0 < nb; c0 += WG_CHUNK) {
+      const bool cv0 = nv0, cv1 = nv1;
+      const int ck0 = nk0, ck1 = nk1;
+      const double cs0 = ns0, cs1 = ns1;
+      if (c0 + WG_CHUNK < nb) {
+        ld(c0 + WG_CHUNK + wv * 128 + l, nv0, nk0, ns0);
+        ld(c0 + WG_CHUNK + wv * 128 + 64 + l, nv1, nk1, ns1);
+      }
+      fn(cv0, ck0, cs0, cv1, ck1, cs1);
+    }
+  };
+  // optimistic single pass: a bucket dominated by a few hot keys holds few distinct keys
+  int Pp = 1;
+  for (;;) {
+    if (wg_accumulate(L, Pp, 0x51ed270bu, seed, v, 1.0 - a.damping, factor, Lw, each)) break;
+    Pp *= 2;
+    if (Pp > WG_MAX_PASSES) {
+      if (threadIdx.x == 0) { const uint32_t pos = atomicAdd(ovf_cnt, 1u); ovf_list[pos] = -(tk.d + 1); }
+      return;
+    }
+  }
+  if (wv == 0) {
+    const int n = L.misc[M_PLEN];
+    int32_t* ok = pt_key + d.pt_off + (int64_t)tk.x * Lw;
+    double* os = pt_sc + d.pt_off + (int64_t)tk.x * Lw;
+    for (int i = l; i < n; i += WAVE) { ok[i] = L.pk[i]; os[i] = L.pv[i]; }
+    if (l == 0) bk_len_all[d.bk_off + P + 1 + tk.x] = n;
+  }
+}
+
+__global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a, const HubDesc* desc,
+                                                          const int32_t* bk_all, const int32_t* pt_key,
+                                                          const double* pt_sc, int Lp,
+                                                          unsigned long long* maxdiff,
+                                                          unsigned long long* stats) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const HubDesc d = desc[blockIdx.x];
+  const WgLds L = wg_carve(smem, 0, Lp, 0);
+  const int P = 1 << d.logP;
+  const int Lw = s.L;
+  const int32_t* blen = bk_all + d.bk_off + P + 1;
+  const int32_t* pk = pt_key + d.pt_off;
+  const double* pv = pt_sc + d.pt_off;
+  const int n = P * Lw;  // flattened (bucket, slot) index; slot < blen[bucket] is valid
+  auto occ = [&](int i) { return (i % Lw) < blen[i / Lw]; };
+  int total = 0;
+  for (int b = threadIdx.x; b < P; b += WG_THREADS) total += blen[b];
+  total = wave_sum(total);
+  if (lane_id() == 0) L.misc[16 + (threadIdx.x >> 6)] = total;
+  if (threadIdx.x == 0) L.misc[M_PLEN] = 0;
+  __syncthreads();
+  total = 0;
+  for (int i = 0; i < WG_WAVES; i++) total += L.misc[16 + i];
+  __syncthreads();
+  if (total <= Lw) {
+    for (int i = threadIdx.x; i < n; i += WG_THREADS)
+      if (occ(i)) { const int pos = atomicAdd(&L.misc[M_PLEN], 1); L.rv[pos] = dbits(pv[i]); L.rk[pos] = pk[i]; }
+  } else {
+    const SelCrit c = wg_select_top(L, n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; }, occ);
+    for (int i = threadIdx.x; i < n; i += WG_THREADS) {
+      if (!occ(i)) continue;
+      if (sel_test(c, dbits(pv[i]), (uint32_t)~pk[i])) {
+        const int pos = atomicAdd(&L.misc[M_PLEN], 1);
+        L.rv[pos] = dbits(pv[i]);
+        L.rk[pos] = pk[i];
+      }
+    }
+  }
+  __syncthreads();
+  if ((threadIdx.x >> 6) == 0) {
+    const int cnt = L.misc[M_PLEN];
+    const uint64_t* rv = L.rv;
+    const int* rk = L.rk;
+    // rows already hold the final set: finish_source with U <= L only sorts/writes/norm1
+    finish_source(d.v, cnt, [&](int i) { return rk[i]; }, [&](int i) { return bitsd(rv[i]); }, s, a,
+                  L.hist, L.rv, L.rk, Lp, L.hk, L.hv, L.mf, maxdiff, stats);
+  }
+}
+
+}  // namespace pprk

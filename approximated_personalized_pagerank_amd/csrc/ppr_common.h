@@ -1,0 +1,109 @@
+// ppr_common.h -- device-side types shared by every merge kernel, and the per-source epilogue.
+//
+// HBM layout (DESIGN.md "data layout"):
+//   rp   int64 [n+1]        CSR row pointers (dense ids = graph iteration order)
+//   colx int32 [m]          successor id | partition-of-successor << 31
+//   ids  int32 [2][n][L]    basket slab, two slots per node (ping-pong per partition)
+//   sc   f64   [2][n][L]
+//   len  int32 [2][n]
+// A node of partition p has been updated upd(p,it) = p ? it/2 : (it+1)/2 times before
+// iteration `it`; its current basket lives in slot upd & 1 and an active node writes slot upd^1,
+// so the inactive partition's carry-over (include/grank.h:133-134) costs nothing.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ppr_device.h"
+
+namespace pprk {
+using namespace pprd;
+
+constexpr int NT = 4;                 // single-wave LDS table tiers (256 << t slots)
+constexpr int TIER_WG = NT;           // workgroup tier (k_merge_wg)
+constexpr int TIER_BIG = NT + 1;      // hub pipeline
+constexpr int NLISTS = NT + 2;
+constexpr int MAX_L = 4096;           // widest basket the kernels accept
+constexpr int WAVES_PER_BLOCK = 4;
+
+struct DevGraph {
+  const int64_t* rp;
+  const int32_t* colx;
+  int64_t n;
+};
+
+struct DevSlab {
+  int32_t* ids;
+  double* sc;
+  int32_t* len;
+  int64_t n;
+  int32_t L;
+  __device__ __forceinline__ int64_t row(int slot, int64_t u) const { return ((int64_t)slot * n + u) * L; }
+  __device__ __forceinline__ int64_t lrow(int slot, int64_t u) const { return (int64_t)slot * n + u; }
+};
+
+struct IterArgs {
+  int sA, sB;        // read slot of partition 0 / 1 nodes
+  int active;        // partition updated in this iteration (-1 = init)
+  double damping;
+  uint32_t unit;     // init mode: every successor contributes {u: 1.0}
+  uint32_t stats;
+};
+
+__device__ __forceinline__ int read_slot(const IterArgs& a, int32_t cx) { return (cx < 0) ? a.sB : a.sA; }
+
+// Epilogue of one source, run by ONE wave: select the top-L of U candidates (keys/vals in LDS
+// or HBM), sort the row, write it to the next slot, norm1 against the old row, fold maxDiff.
+template <class KeyAt, class ValAt>
+__device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt valat,
+                                              const DevSlab& s, const IterArgs& a, uint32_t* hist,
+                                              uint64_t* rv, int* rk, int Lp, int* hk, int* hv,
+                                              int* mf, unsigned long long* maxdiff,
+                                              unsigned long long* stats) {
+  const int L = s.L;
+  int cnt;
+  if (U <= L) {
+    for (int i = lane_id(); i < U; i += WAVE) { rv[i] = dbits(valat(i)); rk[i] = keyat(i); }
+    cnt = U;
+  } else {
+    const SelCrit c = select_top(U, L, keyat, valat, hist);
+    int base = 0;
+    for (int i0 = 0; i0 < U; i0 += WAVE) {
+      const int i = i0 + lane_id();
+      bool sel = false;
+      uint64_t vb = 0;
+      int key = 0;
+      if (i < U) { key = keyat(i); vb = dbits(valat(i)); sel = sel_test(c, vb, (uint32_t)~key); }
+      const uint64_t m = __ballot(sel);
+      if (sel) { const int pos = base + __popcll(m & lanemask_lt()); rv[pos] = vb; rk[pos] = key; }
+      base += __popcll(m);
+    }
+    cnt = L;
+  }
+  wave_fence();
+  row_sort(rv, rk, cnt, Lp);
+  if (a.unit) {
+    // init writes both slots: a dangling source never updates, so its basket must be valid in
+    // whichever slot its partition reads
+    for (int sl = 0; sl < 2; sl++) {
+      const int64_t r = s.row(sl, v);
+      for (int i = lane_id(); i < cnt; i += WAVE) { s.ids[r + i] = rk[i]; s.sc[r + i] = bitsd(rv[i]); }
+      if (lane_id() == 0) s.len[s.lrow(sl, v)] = cnt;
+    }
+    return;
+  }
+  const int cur = (a.active == 1) ? a.sB : a.sA;
+  const int nxt = cur ^ 1;
+  const int64_t r = s.row(nxt, v);
+  for (int i = lane_id(); i < cnt; i += WAVE) { s.ids[r + i] = rk[i]; s.sc[r + i] = bitsd(rv[i]); }
+  if (lane_id() == 0) s.len[s.lrow(nxt, v)] = cnt;
+  const int64_t ro = s.row(cur, v);
+  const int olen = s.len[s.lrow(cur, v)];
+  const double d1 = row_norm1(rv, rk, cnt, s.ids + ro, s.sc + ro, olen, hk, hv, mf, 2 * Lp);
+  if (lane_id() == 0) {
+    // maxDiff only grows: skip the contended atomic when a larger value is already published
+    const unsigned long long b = (unsigned long long)dbits(d1);
+    if (b > __hip_atomic_load(maxdiff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(maxdiff, b);
+  }
+  (void)stats;  // written-row bytes are summed by k_stat_written (no per-source atomics)
+}
+
+}  // namespace pprk

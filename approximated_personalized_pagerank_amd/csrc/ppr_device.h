@@ -7,8 +7,9 @@
 // Semantics implemented (reference file:line):
 //  * accumulation   include/grank.h:107-116  acc[k] = fma(s, d/deg, acc[k]) in successor order;
 //                   a key appears at most once per successor basket, so within a 64-candidate
-//                   group the only conflicts are the same key from different successors; they
-//                   are applied lowest lane (= earliest successor) first ("owner rounds").
+//                   group the only conflicts are the same key from different successors; lanes
+//                   sharing a slot are found with ballots over the slot bits and chained lowest
+//                   lane (= earliest successor) first in registers (apply_group).
 //  * top-L          include/internal/pprInternal.h:109-137 with the deterministic order
 //                   (score desc, dense id asc): radix select on the fp64 bit pattern (scores are
 //                   >= 0, so IEEE bits order like the values), ties resolved on ~id.
@@ -22,7 +23,6 @@ namespace pprd {
 
 constexpr int WAVE = 64;
 constexpr int EMPTY = -1;
-constexpr uint32_t NO_OWNER = 0xffffffffu;
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 __device__ __forceinline__ void wave_fence() { __asm__ __volatile__("" ::: "memory"); }
@@ -66,13 +66,13 @@ __device__ __forceinline__ int wave_sum(int x) {
 // LDS accumulation table: open addressing, linear probing, keys unique.
 struct LdsTable {
   int* keys;
-  uint32_t* owner;
   double* acc;
   uint32_t mask;  // capacity - 1 (power of two)
+  int nbits;      // log2(capacity)
 };
 
 __device__ __forceinline__ void table_clear(const LdsTable& t) {
-  for (uint32_t i = lane_id(); i <= t.mask; i += WAVE) { t.keys[i] = EMPTY; t.owner[i] = NO_OWNER; }
+  for (uint32_t i = lane_id(); i <= t.mask; i += WAVE) t.keys[i] = EMPTY;
   wave_fence();
 }
 
@@ -91,23 +91,58 @@ __device__ __forceinline__ uint32_t table_slot(const LdsTable& t, int key) {
   }
 }
 
-// Apply one group of <= 64 ordered candidates (lane order == successor order).
+__device__ __forceinline__ double readlane_d(double x, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// Apply one group of <= 64 ordered candidates (lane order == successor order) whose table slots
+// are resolved. Keys are distinct within one successor basket, so equal slots in a group come
+// from different successors: they are chained lowest lane first, in registers, and the slot is
+// read and written once. `nbits` bits of the slot index distinguish slots.
+__device__ __forceinline__ void apply_group(double* acc, bool valid, uint32_t slot, double s,
+                                            double factor, int nbits) {
+  const uint64_t vmask = __ballot(valid);
+  uint64_t m = vmask;
+  for (int b = 0; b < nbits; b++) {
+    const bool bit = (slot >> b) & 1u;
+    const uint64_t bb = __ballot(valid && bit);
+    m &= bit ? bb : ~bb;
+  }
+  if (!valid) m = 0;
+  const uint64_t me = 1ull << lane_id();
+  if (!__ballot((m & ~me) != 0)) {  // all keys of the group distinct
+    if (valid) acc[slot] = fma(s, factor, acc[slot]);
+    wave_fence();
+    return;
+  }
+  const bool leader = valid && (m & lanemask_lt()) == 0;
+  const int first = __ffsll((long long)vmask) - 1;
+  if (__shfl((unsigned long long)m, first) == vmask) {  // one key for the whole group
+    double a = acc[slot];  // same address in every valid lane
+    for (uint64_t r = vmask; r; r &= r - 1) a = fma(readlane_d(s, __ffsll((long long)r) - 1), factor, a);
+    if (leader) acc[slot] = a;
+    wave_fence();
+    return;
+  }
+  double a = 0.0;
+  if (leader) a = fma(s, factor, acc[slot]);
+  uint64_t rest = leader ? (m & ~me) : 0ull;
+  while (__ballot(rest != 0)) {
+    const int idx = rest ? (__ffsll((long long)rest) - 1) : lane_id();
+    const double sv = __shfl(s, idx);
+    if (rest) { a = fma(sv, factor, a); rest &= rest - 1; }
+  }
+  if (leader) acc[slot] = a;
+  wave_fence();
+}
+
 __device__ __forceinline__ void table_apply(const LdsTable& t, bool valid, int key, double s,
                                             double factor) {
   const uint32_t slot = valid ? table_slot(t, key) : 0u;
   wave_fence();
-  bool pending = valid;
-  const uint32_t me = (uint32_t)lane_id();
-  while (__ballot(pending)) {
-    if (pending) atomicMin(&t.owner[slot], me);
-    wave_fence();
-    if (pending && t.owner[slot] == me) {
-      t.acc[slot] = fma(s, factor, t.acc[slot]);
-      t.owner[slot] = NO_OWNER;
-      pending = false;
-    }
-    wave_fence();
-  }
+  apply_group(t.acc, valid, slot, s, factor, t.nbits);
 }
 
 // In-place compaction of occupied slots to the front (keys[0..U), acc[0..U)); returns U.

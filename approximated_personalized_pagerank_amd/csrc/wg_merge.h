@@ -7,14 +7,15 @@
 // owner waves through a stable LDS partition: per (wave, half) group counts by ballot, an
 // exclusive scan over groups, then ranks inside a group by ballot popcount.
 //
-// Sources with more distinct keys than one table holds are processed in P key-bucket passes
-// (bucket = second hash of the key mod P; each pass accumulates only its bucket's keys, so a
-// key's chain is still complete within one pass) and the per-pass top-L lists are merged at the
-// end: the top-L of the union of disjoint key sets is inside the union of their top-Ls.
+// Streams with more distinct keys than one table holds are processed in P key-bucket passes
+// (bucket = salted hash of the key mod P; each pass accumulates only its bucket's keys, so a
+// key's chain is still complete within one pass). The top-L of each pass is folded into a
+// running top-L: the top-L of a union of disjoint key sets lies inside the union of their
+// top-Ls. A pass that overflows the table restarts the stream with twice as many passes.
 #pragma once
-#include "ppr_device.h"
+#include "ppr_common.h"
 
-namespace pprd {
+namespace pprk {
 
 constexpr int WG_WAVES = 8;
 constexpr int WG_THREADS = WG_WAVES * WAVE;      // 512
@@ -44,7 +45,6 @@ struct WgLds {
   // table
   double* acc;      // [T]
   int* keys;        // [T]
-  uint32_t* owner;  // [T]
   // routing queue
   int* qk;          // [WG_CHUNK]
   double* qs;       // [WG_CHUNK]
@@ -68,8 +68,11 @@ struct WgLds {
   int* mf;          // [Lp]
 };
 
+// partial (running top-L) list capacity: the running L plus one pass's L
+__host__ __device__ constexpr int wg_pl(int Lp) { return 2 * Lp; }
+
 __host__ __device__ constexpr size_t wg_lds_bytes(int T, int Lp, int PL) {
-  return (size_t)T * 16 + (size_t)WG_CHUNK * 12 + 128 * 4 * 2 + 16 * 4 + (size_t)WG_WIN * 12 +
+  return (size_t)T * 12 + (size_t)WG_CHUNK * 12 + 128 * 4 * 2 + 16 * 4 + (size_t)WG_WIN * 12 +
          (size_t)PL * 12 + 1024 + 256 + (size_t)Lp * 12 + (size_t)Lp * 20 + 64;
 }
 
@@ -81,7 +84,6 @@ __device__ __forceinline__ WgLds wg_carve(unsigned char* base, int T, int Lp, in
   w.pv = reinterpret_cast<double*>(p); p += (size_t)PL * 8;
   w.rv = reinterpret_cast<uint64_t*>(p); p += (size_t)Lp * 8;
   w.keys = reinterpret_cast<int*>(p); p += (size_t)T * 4;
-  w.owner = reinterpret_cast<uint32_t*>(p); p += (size_t)T * 4;
   w.qk = reinterpret_cast<int*>(p); p += (size_t)WG_CHUNK * 4;
   w.cnt = reinterpret_cast<int*>(p); p += 128 * 4;
   w.pre = reinterpret_cast<int*>(p); p += 128 * 4;
@@ -141,32 +143,21 @@ __device__ __forceinline__ void wg_route_apply(const WgLds& w, uint32_t T, uint3
   __syncthreads();
   // owner wave wv applies its segment in order
   const int b = w.seg[wv], e = w.seg[wv + 1];
-  const uint32_t me = (uint32_t)l;
   for (int g0 = b; g0 < e; g0 += WAVE) {
     const int i = g0 + l;
     const bool valid = i < e;
     const int key = valid ? w.qk[i] : 0;
     const double s = valid ? w.qs[i] : 0.0;
     uint32_t slot = 0;
-    bool ok = true;
+    bool ok = valid;
     if (valid) {
       slot = wg_slot(w.keys, w.acc, T, (uint32_t)(((uint64_t)hash32((uint32_t)key) * T) >> 32), key,
                      reinterpret_cast<uint32_t*>(&w.misc[M_FILL]), budget);
       ok = slot != 0xffffffffu;
-      if (!ok) w.misc[M_OVF] = 1;
+      if (!ok) { w.misc[M_OVF] = 1; slot = 0; }
     }
     wave_fence();
-    bool pending = valid && ok;
-    while (__ballot(pending)) {
-      if (pending) atomicMin(&w.owner[slot], me);
-      wave_fence();
-      if (pending && w.owner[slot] == me) {
-        w.acc[slot] = fma(s, factor, w.acc[slot]);
-        w.owner[slot] = NO_OWNER;
-        pending = false;
-      }
-      wave_fence();
-    }
+    apply_group(w.acc, ok, slot, s, factor, 32 - __clz((int)T - 1));
   }
   __syncthreads();
 }
@@ -259,4 +250,175 @@ __device__ __forceinline__ int wg_incl_scan(int x, int* scratch) {
   return incl + add;
 }
 
-}  // namespace pprd
+
+constexpr int WG_T = 10240;           // workgroup table slots (12 B each)
+constexpr int WG_PASS_CAP = 6144;     // expected distinct keys per pass when sizing P
+constexpr int WG_MAX_PASSES = 64;
+
+// Accumulate one ordered candidate stream (`each` calls its callback once per chunk with two
+// candidates per lane, in stream order) in P key-bucket passes. On success pk/pv[0..M_PLEN)
+// hold the stream's top-L by (score desc, id asc) (all entries when there are fewer).
+template <class EachChunk>
+__device__ __forceinline__ bool wg_accumulate(const WgLds& L, int P, uint32_t salt, bool seed_here,
+                                              int v, double selfval, double factor, int Lw,
+                                              EachChunk each) {
+  const uint32_t T = WG_T, budget = WG_T - 1024;
+  if (threadIdx.x == 0) { L.misc[M_PLEN] = 0; L.misc[M_OVF] = 0; }
+  for (int pass = 0; pass < P; pass++) {
+    for (int i = threadIdx.x; i < (int)T; i += blockDim.x) L.keys[i] = EMPTY;
+    if (threadIdx.x == 0) L.misc[M_FILL] = 0;
+    __syncthreads();
+    auto inpass = [&](int key) { return P == 1 || (int)(hash32((uint32_t)key ^ salt) % (uint32_t)P) == pass; };
+    if (threadIdx.x == 0 && seed_here && inpass(v)) {
+      const uint32_t sl = wg_slot(L.keys, L.acc, T, (uint32_t)(((uint64_t)hash32((uint32_t)v) * T) >> 32), v,
+                                  reinterpret_cast<uint32_t*>(&L.misc[M_FILL]), budget);
+      L.acc[sl] = selfval;
+    }
+    __syncthreads();
+    each([&](bool v0, int k0, double s0, bool v1, int k1, double s1) {
+      wg_route_apply(L, T, budget, v0 && inpass(k0), k0, s0, v1 && inpass(k1), k1, s1, factor);
+    });
+    if (L.misc[M_OVF]) return false;  // uniform: written before the last barrier
+    const int U = L.misc[M_FILL];
+    auto occ = [&](int i) { return L.keys[i] != EMPTY; };
+    if (U <= Lw) {
+      for (int i = threadIdx.x; i < (int)T; i += blockDim.x)
+        if (occ(i)) { const int pos = atomicAdd(&L.misc[M_PLEN], 1); L.pk[pos] = L.keys[i]; L.pv[pos] = L.acc[i]; }
+    } else {
+      const SelCrit c = wg_select_top(L, (int)T, Lw, [&](int i) { return L.keys[i]; },
+                                      [&](int i) { return L.acc[i]; }, occ);
+      for (int i = threadIdx.x; i < (int)T; i += blockDim.x) {
+        if (!occ(i)) continue;
+        const int key = L.keys[i];
+        if (sel_test(c, dbits(L.acc[i]), (uint32_t)~key)) {
+          const int pos = atomicAdd(&L.misc[M_PLEN], 1);
+          L.pk[pos] = key;
+          L.pv[pos] = L.acc[i];
+        }
+      }
+    }
+    __syncthreads();
+    if (L.misc[M_PLEN] > Lw && threadIdx.x < WAVE) {  // fold the running list back to L
+      const int n = L.misc[M_PLEN];
+      const int* pk = L.pk;
+      const double* pv = L.pv;
+      const SelCrit c = select_top(n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; }, L.hist);
+      int base = 0;
+      for (int i0 = 0; i0 < n; i0 += WAVE) {
+        const int i = i0 + lane_id();
+        bool sel = false;
+        if (i < n) sel = sel_test(c, dbits(pv[i]), (uint32_t)~pk[i]);
+        const uint64_t m = __ballot(sel);
+        if (sel) { const int pos = base + __popcll(m & lanemask_lt()); L.rv[pos] = dbits(pv[i]); L.rk[pos] = pk[i]; }
+        base += __popcll(m);
+      }
+      wave_fence();
+      for (int i = lane_id(); i < Lw; i += WAVE) { L.pk[i] = L.rk[i]; L.pv[i] = bitsd(L.rv[i]); }
+      if (lane_id() == 0) L.misc[M_PLEN] = Lw;
+    }
+    __syncthreads();
+  }
+  return true;
+}
+
+// the ordered candidate stream of source v read from the basket slab: windows of 512
+// successors (block prefix scan of their basket lengths), chunks of 1024 candidates, the next
+// chunk's gathers issued before the current chunk is routed
+template <class F>
+__device__ __forceinline__ void wg_slab_stream(const WgLds& L, const DevGraph& g, const DevSlab& s,
+                                               const IterArgs& a, int v, F fn) {
+  const int wv = threadIdx.x >> 6;
+  const int l = lane_id();
+  const int64_t b = g.rp[v], e = g.rp[v + 1];
+  if (a.unit) {
+    const int64_t deg = e - b;
+    for (int64_t c0 = 0; c0 < deg; c0 += WG_CHUNK) {
+      const int64_t q0 = c0 + wv * 128 + l, q1 = q0 + 64;
+      const bool v0 = q0 < deg, v1 = q1 < deg;
+      fn(v0, v0 ? (g.colx[b + q0] & 0x7fffffff) : 0, 1.0, v1, v1 ? (g.colx[b + q1] & 0x7fffffff) : 0, 1.0);
+    }
+    return;
+  }
+  for (int64_t wb = b; wb < e; wb += WG_WIN) {
+    const int64_t i = wb + threadIdx.x;
+    int u = 0, sl = 0, ln = 0;
+    if (i < e) {
+      const int32_t cx = g.colx[i];
+      u = cx & 0x7fffffff;
+      sl = read_slot(a, cx);
+      ln = s.len[s.lrow(sl, u)];
+    }
+    const int incl = wg_incl_scan(ln, L.cnt);
+    L.wpre[threadIdx.x] = incl;
+    L.wu[threadIdx.x] = u;
+    L.wsl[threadIdx.x] = sl;
+    __syncthreads();
+    const int W = L.wpre[WG_WIN - 1];
+    auto fetch = [&](int q, bool& vv, int& kk, double& ss) {
+      vv = q < W;
+      kk = 0;
+      ss = 0.0;
+      if (vv) {
+        int j = 0;
+#pragma unroll
+        for (int step = WG_WIN / 2; step; step >>= 1)
+          if (L.wpre[j + step - 1] <= q) j += step;
+        const int ex = j > 0 ? L.wpre[j - 1] : 0;
+        const int64_t r = s.row(L.wsl[j], L.wu[j]) + (q - ex);
+        kk = s.ids[r];
+        ss = s.sc[r];
+      }
+    };
+    bool nv0, nv1;
+    int nk0, nk1;
+    double ns0, ns1;
+    fetch(wv * 128 + l, nv0, nk0, ns0);
+    fetch(wv * 128 + 64 + l, nv1, nk1, ns1);
+    for (int c0 = 0; c0 < W; c0 += WG_CHUNK) {
+      const bool cv0 = nv0, cv1 = nv1;
+      const int ck0 = nk0, ck1 = nk1;
+      const double cs0 = ns0, cs1 = ns1;
+      if (c0 + WG_CHUNK < W) {
+        fetch(c0 + WG_CHUNK + wv * 128 + l, nv0, nk0, ns0);
+        fetch(c0 + WG_CHUNK + wv * 128 + 64 + l, nv1, nk1, ns1);
+      }
+      fn(cv0, ck0, cs0, cv1, ck1, cs1);
+    }
+    __syncthreads();  // window arrays are rewritten next
+  }
+}
+
+// one workgroup (8 waves) per source read from the slab
+__global__ void __launch_bounds__(WG_THREADS) k_merge_wg(DevGraph g, DevSlab s, IterArgs a,
+                                                         const int32_t* list, int64_t count,
+                                                         const int32_t* cand, int Lp,
+                                                         unsigned long long* maxdiff,
+                                                         unsigned long long* stats,
+                                                         int32_t* ovf_list, uint32_t* ovf_cnt) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int64_t w = blockIdx.x;
+  if (w >= count) return;
+  const WgLds L = wg_carve(smem, WG_T, Lp, wg_pl(Lp));
+  const int v = list[w];
+  const double factor = a.damping / (double)(g.rp[v + 1] - g.rp[v]);
+  int P = (cand[v] + WG_PASS_CAP - 1) / WG_PASS_CAP;
+  for (;;) {
+    const bool ok = wg_accumulate(L, P, 0x9e3779b9u, true, v, 1.0 - a.damping, factor, s.L,
+                                  [&](auto&& fn) { wg_slab_stream(L, g, s, a, v, fn); });
+    if (ok) break;
+    P *= 2;
+    if (P > WG_MAX_PASSES) {
+      if (threadIdx.x == 0) { const uint32_t pos = atomicAdd(ovf_cnt, 1u); ovf_list[pos] = v; }
+      return;
+    }
+  }
+  if (threadIdx.x < WAVE) {
+    const int n = L.misc[M_PLEN];
+    const int* pk = L.pk;
+    const double* pv = L.pv;
+    finish_source(v, n, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; }, s, a, L.hist,
+                  L.rv, L.rk, Lp, L.hk, L.hv, L.mf, maxdiff, stats);
+  }
+}
+
+}  // namespace pprk

@@ -100,9 +100,10 @@ def test_gpu_deterministic_and_multi_equal():
     assert m1 == m2
 
 
-@pytest.mark.parametrize("mask", ["0x10", "0x0", "0x11", "0x3"])
+@pytest.mark.parametrize("mask", ["0x10", "0x0", "0x11", "0x3", "0x20", "0x21", "0x30"])
 def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
-    """every merge path alone (workgroup tier / HBM-table path / mixes) matches the oracle"""
+    """every merge path alone (wave tiers 0x1-0x8, workgroup tier 0x10, hub pipeline 0x20, HBM-table
+    path 0x0) and mixes of them match the oracle bit for bit"""
     monkeypatch.setenv("PPR_TIER_MASK", mask)
     for scale, K, L, it in [(10, 16, 32, 5), (11, 8, 64, 4)]:
         g = ppr.rmat(scale, seed=77 + scale)

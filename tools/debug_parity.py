@@ -12,16 +12,18 @@ def compare(tag, a, b):
     print(f"{tag}: {len(bad)} differing rows of {len(ln)}")
     for v in bad[:3]:
         print("  v", v, "gpu len", ln[v], "ora len", b["slab_lens"][v])
-        print("   gpu", list(zip(ids[v, :8].tolist(), sc[v, :8].round(6).tolist())))
-        print("   ora", list(zip(b["slab_ids"][v, :8].tolist(), b["slab_scores"][v, :8].round(6).tolist())))
+        d = np.nonzero((ids[v] != b["slab_ids"][v]) | (sc[v] != b["slab_scores"][v]))[0]
+        print("   first diff at", d[:5], "deg", g.row_ptr[v+1]-g.row_ptr[v], "part", part[v])
+        for i in d[:3]:
+            print("   gpu", ids[v, i], repr(sc[v, i]), " ora", b["slab_ids"][v, i], repr(b["slab_scores"][v, i]))
     return len(bad)
 
 scale, K, L = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
-g = ppr.rmat(scale, seed=7)
+g = ppr.rmat(scale, seed=int(sys.argv[5]) if len(sys.argv) > 5 else 7)
 part = g.partitions()
 deg = g.degrees()
 print("n", g.n, "m", g.m, "maxdeg", deg.max())
-for it in range(0, 4):
+for it in range(0, int(sys.argv[4]) if len(sys.argv) > 4 else 4):
     plan = ppr.GrankPlan(g, K, L, 0.85, part=part, device=0)
     plan.init()
     for i in range(it):
