@@ -99,7 +99,8 @@ struct ppr_plan {
   int32_t* d_out_len = nullptr;
   int flags = 0;
   std::vector<int64_t> h_rp;       // host row pointers (hub planning)
-  size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0;
+  size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0, hub_lds_wave = 0;
+  int hub_bucket = 512, hub_wave_t = 1024;
   int64_t merge_launches = 0;
   double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_m0 = nullptr, ev_m1 = nullptr;
@@ -177,7 +178,7 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
   // disabled tiers fall through to the next enabled one, ultimately the HBM-table path
   {
     const char* env = getenv("PPR_TIER_MASK");
-    const int mask = env ? (int)strtol(env, nullptr, 0) : 0xff;
+    const int mask = env ? (int)strtol(env, nullptr, 0) : 0xef;  // workgroup tier off by default
     int T0 = 256;
     for (int t = 0; t < NT; t++) {
       const int T = T0 << t;
@@ -259,6 +260,15 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
     hipFuncSetAttribute((const void*)k_merge_wg, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   p->hub_lds_wg = wg_lds_bytes(WG_T, p->Lp, wg_pl(p->Lp));
   p->hub_lds_final = wg_lds_bytes(0, p->Lp, 0);
+  {
+    const char* e1 = getenv("PPR_HUB_BUCKET");
+    const char* e2 = getenv("PPR_HUB_WAVE_T");
+    p->hub_bucket = e1 ? std::max(64, atoi(e1)) : HUB_BUCKET;
+    p->hub_wave_t = e2 ? pow2_at_least(std::max(256, atoi(e2))) : HUB_WAVE_T;
+    p->hub_wave_t = std::min(p->hub_wave_t, 8192);
+  }
+  p->hub_lds_wave = hub_wave_lds(p->hub_wave_t) * WAVES_PER_BLOCK;
+  hipFuncSetAttribute((const void*)k_hub_bucket_w, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_count, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -320,7 +330,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
       const int64_t need = cand[v];
       const int64_t deg = p->h_rp[v + 1] - p->h_rp[v];
       if (!desc.empty() && stg + need > budget) break;
-      int logP = ceil_log2((need + HUB_BUCKET - 1) / HUB_BUCKET);
+      int logP = ceil_log2((need + p->hub_bucket - 1) / p->hub_bucket);
       logP = std::max(1, std::min(HUB_MAX_LOGP, logP));
       const int P = 1 << logP;
       const int T = (int)((deg + HUB_TILE - 1) / HUB_TILE);
@@ -348,6 +358,9 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     const size_t o_pk = off;   off = al(off + 4 * (size_t)pt);
     const size_t o_ps = off;   off = al(off + 8 * (size_t)pt);
     const size_t o_ovf = off;  off = al(off + 4 * (buckets.size() + 1));
+    const size_t o_wl = off;   off = al(off + sizeof(HubTask) * (buckets.size() + 1));
+    const size_t o_gl = off;   off = al(off + sizeof(HubTask) * (buckets.size() + 1));
+    const size_t o_cnt = off;  off = al(off + 16);
     int rc = ensure_scratch(p, off);
     if (rc) return rc;
     char* base = (char*)p->d_scratch;
@@ -362,10 +375,14 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     double* d_ps = (double*)(base + o_ps);
     int32_t* d_ovf = (int32_t*)(base + o_ovf);
     uint32_t* d_ovf_cnt = (uint32_t*)(d_ovf + buckets.size());
+    HubTask* d_wl = (HubTask*)(base + o_wl);
+    HubTask* d_gl = (HubTask*)(base + o_gl);
+    uint32_t* d_lc = (uint32_t*)(base + o_cnt);  // [0] wave list, [1] workgroup list
     HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * desc.size(), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_tile, tiles.data(), sizeof(HubTask) * tiles.size(), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_buck, buckets.data(), sizeof(HubTask) * buckets.size(), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(d_ovf_cnt, 0, 4, st));
+    HIP_OK(hipMemsetAsync(d_lc, 0, 8, st));
     const int64_t ntiles = (int64_t)tiles.size();
     const size_t lds_tile = (size_t)WAVES_PER_BLOCK * maxP * 4;
     const unsigned tb = (unsigned)((ntiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
@@ -376,9 +393,25 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
                        d_cm, d_sk, d_ss);
     HIP_OK(hipGetLastError());
-    hipLaunchKernelGGL(k_hub_bucket, dim3((unsigned)buckets.size()), dim3(WG_THREADS), p->hub_lds_wg, st, s, a, g,
-                       d_desc, d_buck, d_bk, d_sk, d_ss, d_pk, d_ps, d_bk, p->Lp, d_ovf, d_ovf_cnt);
-    HIP_OK(hipGetLastError());
+    const int64_t nbuck = (int64_t)buckets.size();
+    // every bucket goes to a single wave first: a bucket made long by one hot key (a core node
+    // present in most successor baskets) still has few distinct keys, and its sequential fma
+    // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
+    uint32_t lc[2] = {(uint32_t)nbuck, 0u};
+    (void)d_wl;
+    if (lc[0]) {
+      hipLaunchKernelGGL(k_hub_bucket_w, dim3((lc[0] + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK), dim3(256),
+                         p->hub_lds_wave, st, s, a, g, d_desc, d_buck, (int64_t)lc[0], d_bk, d_sk, d_ss, d_pk, d_ps,
+                         d_bk, p->Lp, d_gl, d_lc + 1, p->hub_wave_t);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(&lc[1], d_lc + 1, 4, hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+    }
+    if (lc[1]) {
+      hipLaunchKernelGGL(k_hub_bucket, dim3(lc[1]), dim3(WG_THREADS), p->hub_lds_wg, st, s, a, g,
+                         d_desc, d_gl, (int64_t)lc[1], d_bk, d_sk, d_ss, d_pk, d_ps, d_bk, p->Lp, d_ovf, d_ovf_cnt);
+      HIP_OK(hipGetLastError());
+    }
     uint32_t novf = 0;
     HIP_OK(hipMemcpyAsync(&novf, d_ovf_cnt, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -404,7 +437,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
                          d_desc, d_bk, d_pk, d_ps, p->Lp, maxdiff, p->d_stats);
       HIP_OK(hipGetLastError());
     }
-    p->merge_launches += 5;
+    p->merge_launches += 7;
     HIP_OK(hipStreamSynchronize(st));  // scratch is reused by the next batch
     i0 = i;
   }

@@ -1,6 +1,7 @@
 // merge_hub.h -- sources beyond the workgroup tier ("hubs"): stable key-bucket partition.
 #pragma once
 #include "wg_merge.h"
+#include "merge_wave.h"
 
 namespace pprk {
 
@@ -13,11 +14,17 @@ namespace pprk {
 //   k_hub_count    wave per tile (64 successors): per-bucket counts -> cm[b][t]
 //   k_hub_scan     block per source: exclusive scan of cm in (b, t) order -> scatter offsets
 //   k_hub_scatter  wave per tile: ballot ranks inside a group + running per-bucket counters
-//   k_hub_bucket   workgroup per bucket: k_merge_wg's accumulation on the bucket stream
+//   k_hub_bucket_w wave per bucket, private LDS table, no barriers: a hot key's long fma chain
+//                  occupies one wave while the CU's other waves keep working
+//   k_hub_bucket   workgroup per bucket whose distinct keys overflow the wave table
 //   k_hub_final    workgroup per source: top-L of the bucket lists, row, norm1
 constexpr int HUB_TILE = 64;          // successors per tile (one wave)
-constexpr int HUB_BUCKET = 4096;      // target candidates per bucket
-constexpr int HUB_MAX_LOGP = 12;
+constexpr int HUB_BUCKET = 768;       // default target candidates per bucket (PPR_HUB_BUCKET)
+constexpr int HUB_MAX_LOGP = 12;      // per-wave LDS counters of the partition: 16 KB
+constexpr int HUB_WAVE_T = 1024;      // default wave bucket table slots, 12 B each (PPR_HUB_WAVE_T)
+
+// wave bucket LDS: table + radix histogram only (12 waves per CU at T = 1024)
+__host__ __device__ constexpr size_t hub_wave_lds(int T) { return (size_t)T * 12 + 1024; }
 
 struct HubDesc {
   int32_t v;
@@ -163,14 +170,116 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   });
 }
 
+__global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, DevGraph g,
+                                                      const HubDesc* desc, const HubTask* tasks,
+                                                      int64_t ntasks, const int32_t* bk_all,
+                                                      const int32_t* st_key, const double* st_sc,
+                                                      int32_t* pt_key, double* pt_sc,
+                                                      int32_t* bk_len_all, int Lp, HubTask* spill,
+                                                      uint32_t* spill_cnt, int T) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
+  if (w >= ntasks) return;
+  unsigned char* base = smem + (size_t)wv * hub_wave_lds(T);
+  LdsTable t;
+  t.acc = reinterpret_cast<double*>(base);
+  t.keys = reinterpret_cast<int*>(base + (size_t)T * 8);
+  t.mask = (uint32_t)T - 1;
+  t.nbits = 31 - __clz(T);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 12);
+  (void)Lp;
+  const HubTask tk = tasks[w];
+  const HubDesc d = desc[tk.d];
+  const int v = d.v;
+  const int P = 1 << d.logP;
+  const int32_t* bk = bk_all + d.bk_off;
+  const int64_t sb = d.st_off + bk[tk.x];
+  const int nb = bk[tk.x + 1] - bk[tk.x];
+  const double factor = a.damping / (double)(g.rp[v + 1] - g.rp[v]);
+  const int Lw = s.L;
+  const int budget = T / 4 * 3;
+  table_clear(t);
+  int fill = 0;
+  if ((int)hub_digit(v, d.logP) == tk.x) {
+    if (lane_id() == 0) { const uint32_t sl = table_slot(t, v); t.acc[sl] = 1.0 - a.damping; }
+    fill = 1;
+  }
+  wave_fence();
+  const int l = lane_id();
+  bool nv = l < nb;
+  int nk = nv ? st_key[sb + l] : 0;
+  double ns = nv ? st_sc[sb + l] : 0.0;
+  bool overflow = false;
+  for (int g0 = 0; g0 < nb; g0 += WAVE) {
+    const bool cv = nv;
+    const int ck = nk;
+    const double cs = ns;
+    if (g0 + WAVE < nb) {
+      const int q = g0 + WAVE + l;
+      nv = q < nb;
+      nk = nv ? st_key[sb + q] : 0;
+      ns = nv ? st_sc[sb + q] : 0.0;
+    }
+    if (fill + WAVE > budget) { overflow = true; break; }  // uniform
+    uint32_t slot = 0;
+    bool ins = false;
+    if (cv) {
+      uint32_t h = hash32((uint32_t)ck) & t.mask;
+      for (;;) {
+        const int cur = t.keys[h];
+        if (cur == ck) break;
+        if (cur == EMPTY) {
+          const int prev = atomicCAS(&t.keys[h], EMPTY, ck);
+          if (prev == EMPTY) { t.acc[h] = 0.0; ins = true; break; }
+          if (prev == ck) break;
+        }
+        h = (h + 1) & t.mask;
+      }
+      slot = h;
+    }
+    fill += __popcll(__ballot(ins));
+    wave_fence();
+    apply_group(t.acc, cv, slot, cs, factor, t.nbits);
+  }
+  if (overflow) {
+    if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = tk; }
+    return;
+  }
+  const int U = table_compact(t);
+  int32_t* ok = pt_key + d.pt_off + (int64_t)tk.x * Lw;
+  double* os = pt_sc + d.pt_off + (int64_t)tk.x * Lw;
+  int cnt = U;
+  if (U <= Lw) {
+    for (int i = l; i < U; i += WAVE) { ok[i] = t.keys[i]; os[i] = t.acc[i]; }
+  } else {
+    const int* keys = t.keys;
+    const double* acc = t.acc;
+    const SelCrit c = select_top(U, Lw, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, hist);
+    int pos0 = 0;
+    for (int i0 = 0; i0 < U; i0 += WAVE) {
+      const int i = i0 + l;
+      bool sel = false;
+      if (i < U) sel = sel_test(c, dbits(acc[i]), (uint32_t)~keys[i]);
+      const uint64_t m = __ballot(sel);
+      if (sel) { const int pos = pos0 + __popcll(m & lanemask_lt()); ok[pos] = keys[i]; os[pos] = acc[i]; }
+      pos0 += __popcll(m);
+    }
+    cnt = Lw;
+  }
+  if (l == 0) bk_len_all[d.bk_off + P + 1 + tk.x] = cnt;
+}
+
 __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a,
                                                            const DevGraph g, const HubDesc* desc,
-                                                           const HubTask* tasks, const int32_t* bk_all,
+                                                           const HubTask* tasks, int64_t ntasks,
+                                                           const int32_t* bk_all,
                                                            const int32_t* st_key, const double* st_sc,
                                                            int32_t* pt_key, double* pt_sc,
                                                            int32_t* bk_len_all, int Lp,
                                                            int32_t* ovf_list, uint32_t* ovf_cnt) {
   extern __shared__ __align__(16) unsigned char smem[];
+  if ((int64_t)blockIdx.x >= ntasks) return;
   const HubTask tk = tasks[blockIdx.x];
   const HubDesc d = desc[tk.d];
   const WgLds L = wg_carve(smem, WG_T, Lp, wg_pl(Lp));

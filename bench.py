@@ -134,7 +134,7 @@ def main():
     ap.add_argument("--tol", type=float, default=-1.0)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-budget", type=float, default=2e8, help="sampled candidates for cpu_baseline")
+    ap.add_argument("--cpu-budget", type=float, default=1.5e9, help="sampled candidates for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
