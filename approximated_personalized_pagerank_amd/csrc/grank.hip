@@ -725,12 +725,63 @@ extern "C" int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, in
 
 extern "C" int ppr_grank_plan_row_bytes(ppr_plan* p, int64_t* bytes) {
   if (!p || !bytes) return PPR_ERR_ARG;
-  *bytes = (int64_t)p->L * 12 + 8;
+  const int64_t Le = ((int64_t)p->L + 1) & ~1LL;
+  *bytes = 8 + 4 * Le + 8 * (int64_t)p->L;
   return PPR_OK;
 }
 
-extern "C" int ppr_grank_plan_pack(ppr_plan*, int32_t, int64_t, int64_t, void*) { return PPR_ERR_RANGE; }
-extern "C" int ppr_grank_plan_unpack(ppr_plan*, int32_t, int64_t, int64_t, const void*) { return PPR_ERR_RANGE; }
+static int pack_common(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* buf, bool pack) {
+  if (!p || it < 0 || (!buf && end > begin)) return PPR_ERR_ARG;
+  const int part = it & 1;
+  begin = std::max<int64_t>(0, begin);
+  end = std::min<int64_t>(p->nact[part], end);
+  if (end <= begin) return PPR_OK;
+  HIP_OK(hipSetDevice(p->device));
+  const IterArgs a = iter_args(p, it, false);
+  const int nxt = ((a.active == 1) ? a.sB : a.sA) ^ 1;
+  DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
+  int64_t rb = 0;
+  ppr_grank_plan_row_bytes(p, &rb);
+  const int Le = (int)(((int64_t)p->L + 1) & ~1LL);
+  const int64_t cnt = end - begin;
+  const unsigned blocks = (unsigned)((cnt + 3) / 4);
+  if (pack)
+    hipLaunchKernelGGL(k_pack_rows, dim3(blocks), dim3(256), 0, p->stream, s, nxt, p->d_act[part] + begin, cnt,
+                       (unsigned char*)buf, rb, Le);
+  else
+    hipLaunchKernelGGL(k_unpack_rows, dim3(blocks), dim3(256), 0, p->stream, s, nxt, p->d_act[part] + begin, cnt,
+                       (const unsigned char*)buf, rb, Le);
+  HIP_OK(hipGetLastError());
+  return PPR_OK;
+}
+
+extern "C" int ppr_grank_plan_pack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* dev_buf) {
+  return pack_common(p, it, begin, end, dev_buf, true);
+}
+
+extern "C" int ppr_grank_plan_unpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* dev_buf) {
+  return pack_common(p, it, begin, end, const_cast<void*>(dev_buf), false);
+}
+
+extern "C" int ppr_grank_plan_fold_maxdiff(ppr_plan* p, int32_t it, double maxdiff) {
+  // all-reduced maxDiff of a sharded iteration written back (ppr_grank_plan_finish-side reads)
+  if (!p || it < 0) return PPR_ERR_ARG;
+  unsigned long long b;
+  std::memcpy(&b, &maxdiff, 8);
+  HIP_OK(hipMemcpyAsync(p->d_maxdiff + (it < PPR_MAX_ITER_STATS ? it : PPR_MAX_ITER_STATS), &b, 8,
+                        hipMemcpyHostToDevice, p->stream));
+  HIP_OK(hipStreamSynchronize(p->stream));
+  return PPR_OK;
+}
+
+extern "C" int ppr_grank_plan_active_list(ppr_plan* p, int32_t it, int32_t* out) {
+  // host copy of iteration `it`'s active sources in list order (the order ranges refer to)
+  if (!p || !out || it < 0) return PPR_ERR_ARG;
+  const int part = it & 1;
+  if (p->nact[part])
+    HIP_OK(hipMemcpy(out, p->d_act[part], 4 * (size_t)p->nact[part], hipMemcpyDeviceToHost));
+  return PPR_OK;
+}
 
 extern "C" int ppr_grank_csr(const ppr_csr* g, const uint8_t* part, uint32_t K, uint32_t L,
                              uint32_t iterations, double damping, double tolerance,

@@ -114,6 +114,38 @@ __global__ void k_topk(DevSlab s, const uint8_t* part, int sA, int sB, int K, in
   if (lane_id() == 0) olen[v] = k;
 }
 
+// Row exchange for source sharding. Packed row r (of sources list[0..count)) occupies
+// row_bytes = 8 + 4*Le + 8*L bytes: int32 len, int32 pad, int32 ids[Le] (Le = L rounded up to
+// even, so the f64 scores stay 8-byte aligned), f64 scores[L]. Rows are the next-slot baskets
+// the iteration wrote.
+__global__ void k_pack_rows(DevSlab s, int nxt, const int32_t* list, int64_t count,
+                            unsigned char* buf, int64_t row_bytes, int Le) {
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
+  if (r >= count) return;
+  const int v = list[r];
+  unsigned char* row = buf + r * row_bytes;
+  const int len = s.len[s.lrow(nxt, v)];
+  int32_t* rid = reinterpret_cast<int32_t*>(row + 8);
+  double* rsc = reinterpret_cast<double*>(row + 8 + 4 * (int64_t)Le);
+  const int64_t src = s.row(nxt, v);
+  for (int i = lane_id(); i < len; i += WAVE) { rid[i] = s.ids[src + i]; rsc[i] = s.sc[src + i]; }
+  if (lane_id() == 0) { reinterpret_cast<int32_t*>(row)[0] = len; reinterpret_cast<int32_t*>(row)[1] = 0; }
+}
+
+__global__ void k_unpack_rows(DevSlab s, int nxt, const int32_t* list, int64_t count,
+                              const unsigned char* buf, int64_t row_bytes, int Le) {
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
+  if (r >= count) return;
+  const int v = list[r];
+  const unsigned char* row = buf + r * row_bytes;
+  const int len = reinterpret_cast<const int32_t*>(row)[0];
+  const int32_t* rid = reinterpret_cast<const int32_t*>(row + 8);
+  const double* rsc = reinterpret_cast<const double*>(row + 8 + 4 * (int64_t)Le);
+  const int64_t dst = s.row(nxt, v);
+  for (int i = lane_id(); i < len; i += WAVE) { s.ids[dst + i] = rid[i]; s.sc[dst + i] = rsc[i]; }
+  if (lane_id() == 0) s.len[s.lrow(nxt, v)] = len;
+}
+
 __global__ void k_zero_u64(unsigned long long* p, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 0ull;

@@ -108,7 +108,7 @@ int ppr_grank_plan_run(ppr_plan* p, uint32_t iterations, double tolerance, ppr_s
 /* Step-level entry points (multi-GPU sharding; each is asynchronous on the plan's stream):
  *   init:    initial baskets of every node
  *   iterate: merge the active sources with index [begin, end) of iteration `it`'s active list
- *            (the list orders sources by descending work so contiguous ranges balance), writing
+ *            (the partition's non-dangling nodes in dense-id order, see ppr_grank_plan_active_list), writing
  *            their new rows into the next-slot slab and folding norm1 into a device max
  *   finish:  final top-K of every node into the device output */
 int ppr_grank_plan_init(ppr_plan* p);
@@ -119,10 +119,15 @@ int ppr_grank_plan_finish(ppr_plan* p, int32_t iterations_run);
 
 /* Row exchange for source sharding: device pointers (ids int32[L], scores f64[L], len int32)
  * of the basket rows iteration `it` wrote, plus pack/unpack of active-list ranges into a
- * contiguous device buffer of rows (row = L*4 + L*8 + 8 bytes). */
+ * contiguous device buffer of rows: int32 len, int32 pad, int32 ids[Le], f64 scores[L] with Le
+ * = L rounded up to even (ppr_grank_plan_row_bytes). Asynchronous on the plan's stream. */
 int ppr_grank_plan_row_bytes(ppr_plan* p, int64_t* bytes);
 int ppr_grank_plan_pack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* dev_buf);
 int ppr_grank_plan_unpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* dev_buf);
+/* Active sources of iteration `it` in list order (host copy, nact entries), and the write-back of
+ * an all-reduced maxDiff for a sharded iteration. */
+int ppr_grank_plan_active_list(ppr_plan* p, int32_t it, int32_t* out);
+int ppr_grank_plan_fold_maxdiff(ppr_plan* p, int32_t it, double maxdiff);
 
 /* Downloads: final top-K (n*K) and the current L-slab (n*L, rows sorted, len per node). */
 int ppr_grank_plan_fetch(ppr_plan* p, int32_t* out_ids, double* out_scores, int32_t* out_len);

@@ -257,3 +257,55 @@ int oracle_grank(int64_t n, const int64_t* rp, const int32_t* col, const uint8_t
   acc_free(&a);
   return 0;
 }
+
+/* ---- stepping interface (tests of the source-sharded driver): the same maths as oracle_grank,
+ * split into init + one Jacobi step over an explicit list of sources ---- */
+int oracle_init_state(int64_t n, const int64_t* rp, const int32_t* col, int32_t L, double damping,
+                      int32_t* ids, double* sc, int32_t* len) {
+  acc_t a; memset(&a, 0, sizeof(a));
+  ent_t* buf = NULL; int64_t bufcap = 0;
+  for (int64_t v = 0; v < n; v++) {
+    int64_t deg = rp[v + 1] - rp[v];
+    double factor = damping / (double)deg;
+    acc_init(&a, deg + 1);
+    *acc_find(&a, (int32_t)v) = 1.0 - damping;
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) { double* p = acc_find(&a, col[e]); *p = *p + factor; }
+    len[v] = acc_top(&a, L, &buf, &bufcap, ids + v * L, sc + v * L);
+    acc_reset(&a);
+  }
+  free(buf); acc_free(&a);
+  return 0;
+}
+
+int oracle_step(int64_t n, const int64_t* rp, const int32_t* col, int32_t L, double damping,
+                const int32_t* ids, const double* sc, const int32_t* len, const int32_t* list,
+                int64_t count, int32_t* nids, double* nsc, int32_t* nlen, double* maxdiff) {
+  acc_t a; memset(&a, 0, sizeof(a));
+  ent_t* buf = NULL; int64_t bufcap = 0;
+  double md = 0.0;
+  (void)n;
+  for (int64_t q = 0; q < count; q++) {
+    int32_t v = list[q];
+    int64_t deg = rp[v + 1] - rp[v];
+    double factor = damping / (double)deg;
+    int64_t cand = 1;
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) cand += len[col[e]];
+    acc_init(&a, cand);
+    *acc_find(&a, v) = 1.0 - damping;
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
+      int32_t u = col[e];
+      for (int32_t j = 0; j < len[u]; j++) {
+        double* p = acc_find(&a, ids[(int64_t)u * L + j]);
+        *p = fma(sc[(int64_t)u * L + j], factor, *p);
+      }
+    }
+    nlen[v] = acc_top(&a, L, &buf, &bufcap, nids + (int64_t)v * L, nsc + (int64_t)v * L);
+    acc_reset(&a);
+    double d1 = norm1_rows(nids + (int64_t)v * L, nsc + (int64_t)v * L, nlen[v], ids + (int64_t)v * L,
+                           sc + (int64_t)v * L, len[v]);
+    if (d1 > md) md = d1;
+  }
+  free(buf); acc_free(&a);
+  *maxdiff = md;
+  return 0;
+}

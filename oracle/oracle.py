@@ -37,6 +37,11 @@ def lib():
                                    ctypes.c_int32, ctypes.c_double, ctypes.c_double, vp, vp, vp, vp,
                                    vp, vp, vp, vp]
         L.oracle_grank.restype = ctypes.c_int
+        L.oracle_init_state.argtypes = [ctypes.c_int64, vp, vp, ctypes.c_int32, ctypes.c_double, vp, vp, vp]
+        L.oracle_init_state.restype = ctypes.c_int
+        L.oracle_step.argtypes = [ctypes.c_int64, vp, vp, ctypes.c_int32, ctypes.c_double, vp, vp, vp, vp,
+                                  ctypes.c_int64, vp, vp, vp, ctypes.POINTER(ctypes.c_double)]
+        L.oracle_step.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -85,3 +90,89 @@ def grank(row_ptr, col, part, K, L, iterations, damping, tolerance, want_slab=Fa
 
 def ref_available() -> bool:
     return os.path.exists(REF_DRIVER)
+
+
+class OracleEngine:
+    """CPU stand-in for GrankPlan's step-level interface (test infrastructure): lets the
+    source-sharded driver (approximated_personalized_pagerank_amd/shard.py) run under gloo on
+    CPU with the oracle as the per-rank compute."""
+
+    def __init__(self, row_ptr, col, part, K, L, damping):
+        self.rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        self.col = np.ascontiguousarray(col, dtype=np.int32)
+        self.part = np.ascontiguousarray(part, dtype=np.uint8)
+        self.n = len(self.rp) - 1
+        self.K, self.L, self.d = K, L, damping
+        deg = np.diff(self.rp)
+        self.act = [np.nonzero((self.part == p) & (deg > 0))[0].astype(np.int32) for p in (0, 1)]
+        self.ids = np.full((self.n, L), -1, dtype=np.int32)
+        self.sc = np.zeros((self.n, L), dtype=np.float64)
+        self.len = np.zeros(self.n, dtype=np.int32)
+        self.nids, self.nsc, self.nlen = self.ids.copy(), self.sc.copy(), self.len.copy()
+        self.md = {}
+        Le = (L + 1) & ~1
+        self.row_bytes = 8 + 4 * Le + 8 * L
+        self.Le = Le
+
+    def init(self):
+        lib().oracle_init_state(self.n, _p(self.rp), _p(self.col) if len(self.col) else None, self.L, self.d,
+                                _p(self.ids), _p(self.sc), _p(self.len))
+
+    def active_list(self, it):
+        return self.act[it & 1]
+
+    def active_count(self, it):
+        return len(self.act[it & 1])
+
+    def iterate(self, it, b, e):
+        lst = np.ascontiguousarray(self.act[it & 1][b:e])
+        md = ctypes.c_double(0.0)
+        if len(lst):
+            lib().oracle_step(self.n, _p(self.rp), _p(self.col) if len(self.col) else None, self.L, self.d,
+                              _p(self.ids), _p(self.sc), _p(self.len), _p(lst), len(lst), _p(self.nids),
+                              _p(self.nsc), _p(self.nlen), ctypes.byref(md))
+        self.md[it] = max(self.md.get(it, 0.0), md.value)
+
+    def pack(self, it, b, e):
+        lst = self.act[it & 1][b:e]
+        out = np.zeros((len(lst), self.row_bytes), dtype=np.uint8)
+        for r, v in enumerate(lst):
+            out[r, :4] = np.frombuffer(np.int32(self.nlen[v]).tobytes(), dtype=np.uint8)
+            out[r, 8:8 + 4 * self.L] = self.nids[v].view(np.uint8)
+            out[r, 8 + 4 * self.Le:] = self.nsc[v].view(np.uint8)
+        return out.reshape(-1)
+
+    def pack_into(self, it, b, e, send):
+        rows = self.pack(it, b, e)
+        send.numpy()[: len(rows)] = rows
+
+    def unpack(self, it, b, e, buf):
+        lst = self.act[it & 1][b:e]
+        rows = np.asarray(buf, dtype=np.uint8)[: len(lst) * self.row_bytes].reshape(len(lst), self.row_bytes)
+        for r, v in enumerate(lst):
+            ln = int(rows[r, :4].view(np.int32)[0])
+            self.nlen[v] = ln
+            self.nids[v] = rows[r, 8:8 + 4 * self.L].view(np.int32)
+            self.nsc[v] = rows[r, 8 + 4 * self.Le:].view(np.float64)
+
+    def commit(self, it):
+        lst = self.act[it & 1]
+        self.ids[lst], self.sc[lst], self.len[lst] = self.nids[lst], self.nsc[lst], self.nlen[lst]
+
+    def read_maxdiff(self, it):
+        return self.md.get(it, 0.0)
+
+    def fold_maxdiff(self, it, d):
+        self.md[it] = d
+
+    def finish(self, iterations_run):
+        self.iterations_run = iterations_run
+
+    def fetch(self):
+        k = np.minimum(self.len, self.K)
+        ids = np.full((self.n, self.K), -1, dtype=np.int32)
+        sc = np.zeros((self.n, self.K), dtype=np.float64)
+        for v in range(self.n):
+            ids[v, :k[v]] = self.ids[v, :k[v]]
+            sc[v, :k[v]] = self.sc[v, :k[v]]
+        return ids, sc, k.astype(np.int32)
