@@ -96,6 +96,15 @@ def lib() -> ctypes.CDLL:
         "ppr_grank_plan_fetch": (ctypes.c_int, [vp, vp, vp, vp]),
         "ppr_grank_plan_fetch_slab": (ctypes.c_int, [vp, i32, vp, vp, vp]),
         "ppr_grank_plan_stream": (vp, [vp]),
+        "ppr_grank_plan_active_list": (ctypes.c_int, [vp, i32, vp]),
+        "ppr_grank_plan_fold_maxdiff": (ctypes.c_int, [vp, i32, f64]),
+        "ppr_device_count": (ctypes.c_int, [ctypes.POINTER(i32)]),
+        "ppr_comm_unique_id": (ctypes.c_int, [vp]),
+        "ppr_grank_plan_comm_init": (ctypes.c_int, [vp, vp, i32, i32]),
+        "ppr_grank_plan_shard_bounds": (ctypes.c_int, [vp, i32, i32, vp]),
+        "ppr_grank_plan_run_sharded": (ctypes.c_int, [vp, u32, f64, vp]),
+        "ppr_grank_plan_pack_host": (ctypes.c_int, [vp, i32, i64, i64, vp]),
+        "ppr_grank_plan_unpack_host": (ctypes.c_int, [vp, i32, i64, i64, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

@@ -29,7 +29,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result", "-Wno-unused-value",
-           "-o", LIB_PATH + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-lpthread"]
+           "-o", LIB_PATH + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-lrccl", "-lpthread"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -24,6 +24,7 @@
 // Init (include/grank.h:64-83) runs the same kernels in UNIT mode: every successor contributes
 // the basket {u: 1.0}, and fma(1.0, f, acc) == acc + f reproduces `scores[v][s] += factor`.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -101,6 +102,13 @@ struct ppr_plan {
   std::vector<int64_t> h_rp;       // host row pointers (hub planning)
   size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0, hub_lds_wave = 0;
   int hub_bucket = 512, hub_wave_t = 1024;
+  // source sharding (ppr_grank_plan_comm_init / ppr_grank_plan_run_sharded)
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  std::vector<double> work[2];        // per active source: merge work estimate (list order)
+  unsigned char* d_xsend = nullptr;   // packed rows of this rank
+  unsigned char* d_xrecv = nullptr;   // all-gathered rows
+  size_t xsend_bytes = 0, xrecv_bytes = 0;
   int64_t merge_launches = 0;
   double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_m0 = nullptr, ev_m1 = nullptr;
@@ -118,6 +126,8 @@ static void plan_free(ppr_plan* p) {
   if (p->ev_b) hipEventDestroy(p->ev_b);
   if (p->ev_m0) hipEventDestroy(p->ev_m0);
   if (p->ev_m1) hipEventDestroy(p->ev_m1);
+  if (p->comm) ncclCommDestroy(p->comm);
+  hipFree(p->d_xsend); hipFree(p->d_xrecv);
   if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
   delete p;
 }
@@ -212,6 +222,20 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
     if (g->row_ptr[v + 1] > g->row_ptr[v]) act[part[v]].push_back((int32_t)v);
   }
   p->h_rp.assign(g->row_ptr, g->row_ptr + n + 1);
+  // merge work estimate per active source (balanced source shards): sum over successors of the
+  // initial basket bound min(L, deg(u) + 1)
+  for (int q = 0; q < 2; q++) {
+    p->work[q].resize(act[q].size());
+    for (size_t i = 0; i < act[q].size(); i++) {
+      const int v = act[q][i];
+      double w = 1.0;
+      for (int64_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; e++) {
+        const int u = g->col[e];
+        w += (double)std::min<int64_t>(L, g->row_ptr[u + 1] - g->row_ptr[u] + 1);
+      }
+      p->work[q][i] = w;
+    }
+  }
   p->nact[0] = (int64_t)act[0].size();
   p->nact[1] = (int64_t)act[1].size();
 
@@ -780,6 +804,181 @@ extern "C" int ppr_grank_plan_active_list(ppr_plan* p, int32_t it, int32_t* out)
   const int part = it & 1;
   if (p->nact[part])
     HIP_OK(hipMemcpy(out, p->d_act[part], 4 * (size_t)p->nact[part], hipMemcpyDeviceToHost));
+  return PPR_OK;
+}
+
+#define NCCL_OK(expr)                                                                        \
+  do {                                                                                       \
+    ncclResult_t _r = (expr);                                                                \
+    if (_r != ncclSuccess) {                                                                 \
+      fprintf(stderr, "ppr_hip: %s failed: %s\n", #expr, ncclGetErrorString(_r));           \
+      return PPR_ERR_HIP;                                                                    \
+    }                                                                                        \
+  } while (0)
+
+extern "C" int ppr_device_count(int32_t* count) {
+  if (!count) return PPR_ERR_ARG;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *count = c;
+  return PPR_OK;
+}
+
+extern "C" int ppr_comm_unique_id(void* id_out) {
+  if (!id_out) return PPR_ERR_ARG;
+  ncclUniqueId id;
+  NCCL_OK(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, sizeof(id));
+  return PPR_OK;
+}
+
+extern "C" int ppr_grank_plan_comm_init(ppr_plan* p, const void* id, int32_t nranks, int32_t rank) {
+  if (!p || !id || nranks < 1 || rank < 0 || rank >= nranks) return PPR_ERR_ARG;
+  HIP_OK(hipSetDevice(p->device));
+  if (p->comm) { ncclCommDestroy(p->comm); p->comm = nullptr; }
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  NCCL_OK(ncclCommInitRank(&p->comm, nranks, uid, rank));
+  p->nranks = nranks;
+  p->rank = rank;
+  return PPR_OK;
+}
+
+// contiguous ranges of the active list with balanced estimated work
+static void shard_bounds(const std::vector<double>& w, int world, std::vector<int64_t>& b) {
+  const int64_t n = (int64_t)w.size();
+  b.assign(world + 1, 0);
+  double tot = 0;
+  for (double x : w) tot += x;
+  double run = 0;
+  int64_t i = 0;
+  for (int r = 1; r < world; r++) {
+    const double target = tot * r / world;
+    while (i < n && run + w[i] <= target) run += w[i++];
+    b[r] = i;
+  }
+  b[world] = n;
+}
+
+extern "C" int ppr_grank_plan_shard_bounds(ppr_plan* p, int32_t it, int32_t world, int64_t* bounds) {
+  if (!p || !bounds || world < 1 || it < 0) return PPR_ERR_ARG;
+  std::vector<int64_t> b;
+  shard_bounds(p->work[it & 1], world, b);
+  std::memcpy(bounds, b.data(), sizeof(int64_t) * (world + 1));
+  return PPR_OK;
+}
+
+static int ensure_dev(unsigned char** ptr, size_t* cap, size_t need) {
+  if (need <= *cap) return PPR_OK;
+  hipFree(*ptr);
+  *ptr = nullptr;
+  *cap = 0;
+  if (hipMalloc((void**)ptr, need) != hipSuccess) return PPR_ERR_OOM;
+  *cap = need;
+  return PPR_OK;
+}
+
+extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance,
+                                          ppr_stats* st) {
+  if (!p) return PPR_ERR_ARG;
+  if (iterations == 0) return PPR_ERR_ITERS;
+  if (p->nranks > 1 && !p->comm) return PPR_ERR_ARG;
+  HIP_OK(hipSetDevice(p->device));
+  hipStream_t s = p->stream;
+  HIP_OK(hipMemsetAsync(p->d_maxdiff, 0, 8 * (PPR_MAX_ITER_STATS + 1), s));
+  HIP_OK(hipMemsetAsync(p->d_stats, 0, 16, s));
+  p->merge_launches = 0;
+  p->merge_ms = 0.0;
+  HIP_OK(hipEventRecord(p->ev_a, s));
+  int rc = ppr_grank_plan_init(p);
+  if (rc) return rc;
+  std::vector<int64_t> bd[2];
+  shard_bounds(p->work[0], p->nranks, bd[0]);
+  shard_bounds(p->work[1], p->nranks, bd[1]);
+  int64_t rb = 0;
+  ppr_grank_plan_row_bytes(p, &rb);
+  double md[2] = {tolerance, tolerance};
+  uint32_t it = 0;
+  for (; it < iterations && std::max(md[0], md[1]) >= tolerance; it++) {
+    const std::vector<int64_t>& b = bd[it & 1];
+    rc = ppr_grank_plan_iterate(p, (int32_t)it, b[p->rank], b[p->rank + 1]);
+    if (rc) return rc;
+    unsigned long long* mdp = p->d_maxdiff + (it < PPR_MAX_ITER_STATS ? it : PPR_MAX_ITER_STATS);
+    if (p->nranks > 1) {
+      int64_t rows_max = 0;
+      for (int r = 0; r < p->nranks; r++) rows_max = std::max(rows_max, b[r + 1] - b[r]);
+      if (rows_max > 0) {
+        const size_t chunk = (size_t)rows_max * rb;
+        rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, chunk);
+        if (!rc) rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, chunk * p->nranks);
+        if (rc) return rc;
+        rc = ppr_grank_plan_pack(p, (int32_t)it, b[p->rank], b[p->rank + 1], p->d_xsend);
+        if (rc) return rc;
+        NCCL_OK(ncclAllGather(p->d_xsend, p->d_xrecv, chunk, ncclUint8, p->comm, s));
+        for (int r = 0; r < p->nranks; r++) {
+          if (r == p->rank || b[r + 1] == b[r]) continue;
+          rc = ppr_grank_plan_unpack(p, (int32_t)it, b[r], b[r + 1], p->d_xrecv + (size_t)r * chunk);
+          if (rc) return rc;
+        }
+      }
+      // maxDiff >= 0: the IEEE bit patterns order like the values, so an integer MAX is exact
+      NCCL_OK(ncclAllReduce(mdp, mdp, 1, ncclUint64, ncclMax, p->comm, s));
+    }
+    double d = 0.0;
+    rc = ppr_grank_plan_read_maxdiff(p, (int32_t)it, &d);
+    if (rc) return rc;
+    md[0] = d;
+    std::swap(md[0], md[1]);
+    if (st && it < PPR_MAX_ITER_STATS) st->max_diff[it] = d;
+  }
+  rc = ppr_grank_plan_finish(p, (int32_t)it);
+  if (rc) return rc;
+  HIP_OK(hipEventRecord(p->ev_b, s));
+  HIP_OK(hipEventSynchronize(p->ev_b));
+  if (st) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, p->ev_a, p->ev_b);
+    st->iterations_run = (int32_t)it;
+    st->device_ms = ms;
+    st->merge_ms = p->merge_ms;
+    unsigned long long sv[2];
+    HIP_OK(hipMemcpyAsync(sv, p->d_stats, 16, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    st->candidates = (int64_t)sv[0];
+    st->algo_bytes = (int64_t)sv[1];
+    st->merge_launches = p->merge_launches;
+  }
+  return PPR_OK;
+}
+
+// host-staged row exchange (gloo rehearsal on a single GPU; the RCCL path never uses these)
+extern "C" int ppr_grank_plan_pack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* host) {
+  if (!p || it < 0) return PPR_ERR_ARG;
+  int64_t rb = 0;
+  ppr_grank_plan_row_bytes(p, &rb);
+  const int64_t cnt = std::max<int64_t>(0, end - begin);
+  if (!cnt) return PPR_OK;
+  int rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, (size_t)cnt * rb);
+  if (rc) return rc;
+  rc = ppr_grank_plan_pack(p, it, begin, end, p->d_xsend);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(host, p->d_xsend, (size_t)cnt * rb, hipMemcpyDeviceToHost, p->stream));
+  HIP_OK(hipStreamSynchronize(p->stream));
+  return PPR_OK;
+}
+
+extern "C" int ppr_grank_plan_unpack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* host) {
+  if (!p || it < 0) return PPR_ERR_ARG;
+  int64_t rb = 0;
+  ppr_grank_plan_row_bytes(p, &rb);
+  const int64_t cnt = std::max<int64_t>(0, end - begin);
+  if (!cnt) return PPR_OK;
+  int rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, (size_t)cnt * rb);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(p->d_xrecv, host, (size_t)cnt * rb, hipMemcpyHostToDevice, p->stream));
+  rc = ppr_grank_plan_unpack(p, it, begin, end, p->d_xrecv);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(p->stream));
   return PPR_OK;
 }
 

@@ -44,7 +44,7 @@ def balanced_bounds(weights: np.ndarray, world: int) -> List[int]:
     return b
 
 
-class TorchComm:
+class TorchComm:  # collectives on torch tensors (tests; the GPU path never touches torch's HIP)
     """all_gather / all_reduce over torch.distributed (RCCL on GPUs, gloo on CPU)."""
 
     def __init__(self, device):
@@ -69,14 +69,16 @@ class TorchComm:
         self.dist.barrier()
 
 
-def run_sharded(engine, comm, iterations: int, tolerance: float, weights: Sequence[np.ndarray],
-                alloc_send, to_engine_buf) -> int:
+def run_sharded(engine, comm, iterations: int, tolerance: float, weights, alloc_send, to_engine_buf,
+                bounds=None) -> int:
     """GRank with the active sources of every iteration split over comm.world ranks.
-    weights[p]: work estimate of partition p's active list (engine.active_list order).
+    weights[p]: work estimate of partition p's active list (engine.active_list order), or
+    bounds[p]: explicit range boundaries per partition.
     alloc_send(nbytes) -> a send buffer the engine can pack into; to_engine_buf(t) -> what
     engine.unpack accepts. Returns the number of iterations run."""
     rank, world = comm.rank, comm.world
-    bounds = [balanced_bounds(weights[p], world) for p in (0, 1)]
+    if bounds is None:
+        bounds = [balanced_bounds(weights[p], world) for p in (0, 1)]
     rb = engine.row_bytes
     engine.init()
     md = [tolerance, tolerance]
@@ -104,16 +106,16 @@ def run_sharded(engine, comm, iterations: int, tolerance: float, weights: Sequen
 
 
 class GpuEngine:
-    """GrankPlan's step-level ABI with device row buffers from torch (plumbing only)."""
+    """GrankPlan's step-level ABI with host-staged row exchange (single-GPU rehearsal over gloo;
+    the production path is the native RCCL loop, ppr_grank_plan_run_sharded)."""
 
-    def __init__(self, plan, torch, device):
-        self.plan, self.torch, self.device = plan, torch, device
+    def __init__(self, plan):
         from . import _lib
         import ctypes
+        self.plan, self._lib, self._ct = plan, _lib, ctypes
         rb = ctypes.c_int64()
         _lib.check(_lib.lib().ppr_grank_plan_row_bytes(plan._p, ctypes.byref(rb)), "row_bytes")
         self.row_bytes = int(rb.value)
-        self._lib, self._ct = _lib, ctypes
 
     def init(self):
         self.plan.init()
@@ -131,10 +133,10 @@ class GpuEngine:
         self.plan.iterate(it, b, e)
 
     def pack_into(self, it, b, e, send):
-        self._lib.check(self._lib.lib().ppr_grank_plan_pack(self.plan._p, it, b, e, send.data_ptr()), "pack")
+        self._lib.check(self._lib.lib().ppr_grank_plan_pack_host(self.plan._p, it, b, e, send.data_ptr()), "pack")
 
-    def unpack(self, it, b, e, ptr):
-        self._lib.check(self._lib.lib().ppr_grank_plan_unpack(self.plan._p, it, b, e, ptr), "unpack")
+    def unpack(self, it, b, e, buf):
+        self._lib.check(self._lib.lib().ppr_grank_plan_unpack_host(self.plan._p, it, b, e, buf), "unpack")
 
     def commit(self, it):
         pass  # the slot flip is implicit on the device
@@ -149,82 +151,88 @@ class GpuEngine:
         self.plan.finish(iterations_run)
 
 
-def _setup(local):
-    """device for this rank (ranks beyond the visible GPUs share them: rehearsal on one GPU) and
-    the process group (PPR_DIST_BACKEND, default nccl = RCCL on ROCm)."""
-    import os
-    import torch
-    import torch.distributed as dist
-    ndev = max(1, torch.cuda.device_count())
-    dev = torch.device("cuda", local % ndev)
-    torch.cuda.set_device(dev)
-    if not dist.is_initialized():
-        backend = os.environ.get("PPR_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-    return dev
+class CpuComm:
+    """gloo collectives on host tensors (bootstrap and rehearsal)."""
+
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+
+    def all_gather_rows(self, send, nbytes_max):
+        out = self.torch.empty(self.world * nbytes_max, dtype=self.torch.uint8)
+        self.dist.all_gather_into_tensor(out, send)
+        return out
+
+    def all_reduce_max(self, x):
+        t = self.torch.tensor([x], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def barrier(self):
+        self.dist.barrier()
+
+
+def device_count() -> int:
+    import ctypes
+    from . import _lib
+    c = ctypes.c_int32(0)
+    _lib.lib().ppr_device_count(ctypes.byref(c))
+    return int(c.value)
 
 
 class ShardedGrank:
-    """Sharded GRank job on this rank's GPU (torch.distributed must be launched)."""
+    """Source-sharded GRank job of this rank. torch.distributed (gloo, host tensors only) is used
+    to bootstrap: torch's own HIP runtime is never initialised in this process, all device work
+    and the RCCL collectives run inside libppr_hip.so on the plan's stream.
+
+    PPR_DIST_BACKEND=nccl (default): native loop, RCCL all-gather of rows over xGMI.
+    PPR_DIST_BACKEND=gloo: Python loop, host-staged rows over gloo (lets several ranks share one
+    GPU, which RCCL refuses)."""
 
     def __init__(self, g, part, K, L, damping, local):
+        import os
+        import ctypes
         import torch
+        import torch.distributed as dist
+        from . import _lib
         from .grank import GrankPlan
-        self.torch = torch
-        self.dev = _setup(local)
-        self.comm = TorchComm(self.dev)
-        # one dedicated stream for the library's kernels and torch's collectives, so packing, the
-        # all-gather and unpacking are ordered (the legacy default stream would be handle 0, which
-        # the ABI reads as "library-owned stream")
-        self.stream = torch.cuda.Stream(device=self.dev)
-        self.plan = GrankPlan(g, K, L, damping, part=part, device=self.dev.index,
-                              stream=self.stream.cuda_stream)
-        self.eng = GpuEngine(self.plan, torch, self.dev)
-        w = work_estimate(g.row_ptr, g.col, L)
-        self.weights = [w[self.eng.active_list(p)] for p in (0, 1)]
-        self._bufs = {}
-        self.gloo = self.comm.dist.get_backend() == "gloo"
-
-    def _alloc(self, nbytes):
-        t = self._bufs.get(nbytes)
-        if t is None:
-            t = self._bufs[nbytes] = self.torch.empty(nbytes, dtype=self.torch.uint8, device=self.dev)
-        return t
+        self._lib, self._ct, self.torch, self.dist = _lib, ctypes, torch, dist
+        if not dist.is_initialized():
+            dist.init_process_group("gloo")
+        self.comm = CpuComm()
+        self.device = local % max(1, device_count())
+        self.mode = os.environ.get("PPR_DIST_BACKEND", "nccl")
+        self.plan = GrankPlan(g, K, L, damping, part=part, device=self.device, stats=True)
+        if self.mode == "nccl" and self.comm.world > 1:
+            uid = torch.zeros(128, dtype=torch.uint8)
+            if self.comm.rank == 0:
+                _lib.check(_lib.lib().ppr_comm_unique_id(uid.data_ptr()), "comm_unique_id")
+            dist.broadcast(uid, 0)
+            _lib.check(_lib.lib().ppr_grank_plan_comm_init(self.plan._p, uid.data_ptr(), self.comm.world,
+                                                           self.comm.rank), "comm_init")
+        self.eng = GpuEngine(self.plan)
+        self.last_stats = None
 
     def run(self, iterations, tolerance):
-        torch = self.torch
-
-        def to_buf(recv, off):
-            return recv.data_ptr() + off
-
-        comm = self.comm
-        if self.gloo:  # gloo: host staging of the row buffers
-            class HostComm:
-                rank, world = comm.rank, comm.world
-
-                def all_gather_rows(_, send, nb):
-                    torch.cuda.synchronize(self.dev)
-                    host = send.cpu()
-                    out = torch.empty(comm.world * nb, dtype=torch.uint8)
-                    comm.dist.all_gather_into_tensor(out, host)
-                    return out.to(self.dev)
-
-                def all_reduce_max(_, x):
-                    t = torch.tensor([x], dtype=torch.float64)
-                    comm.dist.all_reduce(t, op=comm.dist.ReduceOp.MAX)
-                    return float(t.item())
-
-                def barrier(_):
-                    comm.dist.barrier()
-            use = HostComm()
-        else:
-            use = comm
-        with torch.cuda.stream(self.stream):
-            its = run_sharded(self.eng, use, iterations, tolerance, self.weights, self._alloc, to_buf)
-        torch.cuda.synchronize(self.dev)
+        if self.mode == "nccl" or self.comm.world == 1:
+            st = self._lib.PprStats()
+            self._lib.check(self._lib.lib().ppr_grank_plan_run_sharded(self.plan._p, iterations, tolerance,
+                                                                       self._ct.byref(st)), "run_sharded")
+            self.plan.iterations_run = int(st.iterations_run)
+            self.last_stats = st
+            return int(st.iterations_run)
+        weights = []
+        for p in (0, 1):
+            b = np.zeros(self.comm.world + 1, dtype=np.int64)
+            self._lib.check(self._lib.lib().ppr_grank_plan_shard_bounds(self.plan._p, p, self.comm.world,
+                                                                        self._lib.ptr(b)), "bounds")
+            weights.append([int(x) for x in b])  # python ints: ctypes rejects numpy scalars
+        its = run_sharded(self.eng, self.comm, iterations, tolerance, None,
+                          lambda nb: self.torch.empty(nb, dtype=self.torch.uint8),
+                          lambda recv, off: int(recv.data_ptr() + off), bounds=weights)
+        self.plan.iterations_run = its
         return its
 
     def fetch(self):
@@ -235,31 +243,31 @@ class ShardedGrank:
 
 
 def run_distributed_bench(g, part, args, rank, world, local):
-    """bench.py N>1 path: source-sharded GRank job per step; returns (max elapsed, stats) on
-    rank 0. The graph is generated identically on every rank (same seed)."""
-    import torch
-    import torch.distributed as dist
+    """bench.py N>1 path: one source-sharded GRank job per step; (max elapsed, stats) on rank 0.
+    The graph is generated identically on every rank (same seed)."""
     job = ShardedGrank(g, part, args.K, args.L, args.damping, local)
-    dev = job.dev
     for _ in range(args.warmup):
         job.run(args.iters, args.tol)
-    torch.cuda.synchronize(dev)
     job.comm.barrier()
     t0 = time.perf_counter()
     its = 0
+    merge_ms = algo = 0.0
     for _ in range(args.steps):
         its = job.run(args.iters, args.tol)
-    torch.cuda.synchronize(dev)
+        if job.last_stats is not None:
+            merge_ms += job.last_stats.merge_ms
+            algo += job.last_stats.algo_bytes
+    el = time.perf_counter() - t0
     job.comm.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    if job.gloo:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    else:
-        el = el.to(dev)
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
+    elapsed = job.comm.all_reduce_max(el)
+    # algorithmic bytes are per rank: the job's total is their sum; merge time is the max
+    t = job.torch.tensor([algo], dtype=job.torch.float64)
+    job.dist.all_reduce(t)
+    algo_tot = float(t.item())
+    merge_max = job.comm.all_reduce_max(merge_ms)
     job.close()
-    dist.destroy_process_group()
+    job.dist.destroy_process_group()
     if rank != 0:
         return None
-    return elapsed, dict(merge_ms=0.0, algo_bytes=0, device_ms=elapsed * 1e3, iterations=its, launches=0)
+    return elapsed, dict(merge_ms=merge_max, algo_bytes=algo_tot, device_ms=elapsed * 1e3, iterations=its,
+                         launches=0)

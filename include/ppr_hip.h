@@ -129,6 +129,22 @@ int ppr_grank_plan_unpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, c
 int ppr_grank_plan_active_list(ppr_plan* p, int32_t it, int32_t* out);
 int ppr_grank_plan_fold_maxdiff(ppr_plan* p, int32_t it, double maxdiff);
 
+/* ---- source sharding over RCCL (one process per GPU) ----
+ * Rank 0 creates a 128-byte RCCL unique id, the caller broadcasts it (any channel), and every rank
+ * calls ppr_grank_plan_comm_init. ppr_grank_plan_run_sharded then runs the whole job like
+ * ppr_grank_plan_run, but each rank merges only its work-balanced range of every iteration's
+ * active list (ppr_grank_plan_shard_bounds) and the written rows are exchanged with
+ * ncclAllGather on the plan's stream; maxDiff is combined with ncclAllReduce(MAX) so every rank
+ * applies the reference's stopping rule to the same value. Results equal the 1-GPU run. */
+int ppr_device_count(int32_t* count);
+int ppr_comm_unique_id(void* id128);
+int ppr_grank_plan_comm_init(ppr_plan* p, const void* id128, int32_t nranks, int32_t rank);
+int ppr_grank_plan_shard_bounds(ppr_plan* p, int32_t it, int32_t nranks, int64_t* bounds);
+int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance, ppr_stats* st);
+/* host-staged variants of pack/unpack (rehearsal without RCCL; synchronous) */
+int ppr_grank_plan_pack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* host_buf);
+int ppr_grank_plan_unpack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* host_buf);
+
 /* Downloads: final top-K (n*K) and the current L-slab (n*L, rows sorted, len per node). */
 int ppr_grank_plan_fetch(ppr_plan* p, int32_t* out_ids, double* out_scores, int32_t* out_len);
 int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, int32_t* ids, double* scores,
