@@ -1,0 +1,79 @@
+// Drop-in check: code written against the reference's API (the README examples and the shape of
+// test/grankTest.cc) compiled unchanged against include/ppr/*.h and linked with libppr_hip.so.
+//   dropin_test bad <case>   parameter errors: same message + exit(EXIT_FAILURE), no device use
+//   dropin_test empty        empty graph -> empty result
+//   dropin_test ring         README ring of 100, K50 L100 30 it 1e-3: prints "src key score" rows
+//   dropin_test known        known answers of test/grankTest.cc (exit 0 when all hold)
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ppr/grank.h"
+#include "ppr/grankMulti.h"
+
+using namespace std;
+
+static int check(bool c, const char* what) {
+  if (!c) { fprintf(stderr, "FAILED: %s\n", what); return 1; }
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) return 2;
+  string mode = argv[1];
+  unordered_map<int, vector<int>> graph;
+  if (mode == "bad") {
+    int c = atoi(argv[2]);
+    switch (c) {  // test/grankTest.cc:20-29, test/grankMultiThreadTest.cc:22-32
+      case 0: ppr::grank(graph, 0, 3, 42, 0.5, 0.0001); break;
+      case 1: ppr::grank(graph, 2, 0, 32, 0.85, 0.0001); break;
+      case 2: ppr::grank(graph, 2, 1, 10, 0.5, 0.0001); break;
+      case 3: ppr::grank(graph, 2, 2, 0, 0.5, 0.0001); break;
+      case 4: ppr::grank(graph, 2, 2, 10, 1.5, 0.0001); break;
+      case 5: ppr::grank(graph, 2, 2, 10, -1.5, 0.0001); break;
+      case 6: ppr::grankMulti(graph, 2, 2, 10, 0.5, 0.0001, 0); break;
+    }
+    return 0;
+  }
+  if (mode == "empty") {
+    auto res = ppr::grank(graph, 10, 30, 100, 0.85, 0.0001);
+    return res.empty() ? 0 : 1;
+  }
+  if (mode == "ring") {  // README.md "GRank" example
+    for (int i = 0; i < 100; i++) graph[i].push_back((i + 1) % 100);
+    auto res = ppr::grank(graph, 50, 100, 30, 0.85, 0.001);
+    for (auto& kv : res)
+      for (auto& e : kv.second) printf("%d %d %.17g\n", kv.first, e.first, e.second);
+    return 0;
+  }
+  if (mode == "known") {
+    int bad = 0;
+    for (int i = 0; i < 10; i++) graph[i];
+    auto r = ppr::grank(graph, 10, 30, 100, 0.85, 0.0001);  // no edges (grankTest.cc:38-50)
+    for (int i = 0; i < 10; i++) bad += check(r[i].size() == 1 && fabs(r[i][i] - 0.15) < 1e-4, "no edges");
+    unordered_map<int, vector<int>> one;
+    one[0].push_back(0);
+    r = ppr::grank(one, 10, 30, 100, 0.85, 0.0001);  // self loop (:70-84)
+    bad += check(fabs(r[0][0] - 1.0) < 1e-4, "self loop");
+    unordered_map<int, vector<int>> star;
+    for (int i = 0; i < 6; i++) star[i];
+    for (int i = 1; i < 6; i++) star[i].push_back(0);
+    r = ppr::grankMulti(star, 10, 30, 100, 0.85, 0.0001, 4);  // star (:154-182)
+    bad += check(r[0].size() == 1 && fabs(r[0][0] - 0.15) < 1e-4, "star centre");
+    for (int i = 1; i < 6; i++) bad += check(r[i].size() == 2 && fabs(r[i][0] - 0.15 * 0.85) < 1e-4, "star leaf");
+    unordered_map<int, vector<int>> ring;
+    for (int i = 0; i < 100; i++) ring[i];
+    for (int i = 0; i < 99; i++) ring[i].push_back(i + 1);
+    ring[99].push_back(0);
+    r = ppr::grank(ring, 10, 10, 100, 0.85, 0.0001);  // testNodesGreaterThanK (:184-240)
+    for (int i = 0; i < 100; i++) {
+      bad += check(r[i].size() == 10, "ring size");
+      for (int u = 0; u < 9; u++) bad += check(r[i][(i + u) % 100] > r[i][(i + u + 1) % 100], "ring order");
+    }
+    return bad ? 1 : 0;
+  }
+  return 2;
+}
