@@ -3,13 +3,14 @@
 Drop-in surface of fruttasecca/approximated_personalized_pagerank:
   * C++: include/ppr/grank.h, include/ppr/grankMulti.h (same templates, same signatures)
   * C ABI: include/ppr_hip.h (libppr_hip.so, built in-tree for gfx950)
-  * Python: grank / grank_multi / GrankPlan below.
+  * Python: grank / grank_multi / GrankPlan / mccompletepathv2 / MccpPlan below.
 """
 from ._lib import PprError
 from .graph import Csr, read_edge_csv, rmat
 from .grank import GrankPlan, GrankResult, grank, grank_csr, grank_multi
+from .mccp2 import MccpPlan, McStats, mccompletepathv2, mccp2_csr
 
 __all__ = [
     "PprError", "Csr", "rmat", "read_edge_csv", "GrankPlan", "GrankResult", "grank", "grank_csr",
-    "grank_multi",
+    "grank_multi", "MccpPlan", "McStats", "mccompletepathv2", "mccp2_csr",
 ]

@@ -62,6 +62,20 @@ class PprStats(ctypes.Structure):
     ]
 
 
+class PprMcStats(ctypes.Structure):
+    _fields_ = [
+        ("device_ms", ctypes.c_double),
+        ("walk_ms", ctypes.c_double),
+        ("combine_ms", ctypes.c_double),
+        ("walk_nodes", ctypes.c_int64),
+        ("walks", ctypes.c_int64),
+        ("levels", ctypes.c_int64),
+        ("merge_launches", ctypes.c_int64),
+        ("candidates", ctypes.c_int64),
+        ("algo_bytes", ctypes.c_int64),
+    ]
+
+
 _lib = None
 
 
@@ -105,6 +119,13 @@ def lib() -> ctypes.CDLL:
         "ppr_grank_plan_run_sharded": (ctypes.c_int, [vp, u32, f64, vp]),
         "ppr_grank_plan_pack_host": (ctypes.c_int, [vp, i32, i64, i64, vp]),
         "ppr_grank_plan_unpack_host": (ctypes.c_int, [vp, i32, i64, i64, vp]),
+        "ppr_plan_fetch_slot": (ctypes.c_int, [vp, i32, vp, vp, vp]),
+        "ppr_mccp2_csr": (ctypes.c_int, [vp, u32, u32, u32, f64, ctypes.c_uint64, vp, vp, vp, vp, vp]),
+        "ppr_mccp2_plan_create": (ctypes.c_int, [vp, u32, u32, f64, vp, ctypes.POINTER(vp)]),
+        "ppr_mccp2_plan_info": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64)]),
+        "ppr_mccp2_plan_walk": (ctypes.c_int, [vp, u32, ctypes.c_uint64, i64, i64]),
+        "ppr_mccp2_plan_combine": (ctypes.c_int, [vp]),
+        "ppr_mccp2_plan_run": (ctypes.c_int, [vp, u32, ctypes.c_uint64, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

@@ -41,132 +41,11 @@
 
 using namespace pprk;
 
-#define HIP_OK(expr)                                  \
-  do {                                                \
-    hipError_t _e = (expr);                           \
-    if (_e != hipSuccess) {                           \
-      fprintf(stderr, "ppr_hip: %s failed: %s (%s:%d)\n", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
-      return PPR_ERR_HIP;                             \
-    }                                                 \
-  } while (0)
+#include "plan.h"
 
-namespace {
-constexpr int WG_TIER_PASSES = 3;
-
-int pow2_at_least(int64_t x) {
-  int p = 1;
-  while (p < x) p <<= 1;
-  return p;
-}
-}  // namespace
-
-
-// ================================================================================================
-// plan
-struct ppr_plan {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  bool own_stream = false;
-  int64_t n = 0, m = 0;
-  uint32_t K = 0, L = 0;
-  int Lp = 1;
-  double damping = 0.85;
-  int64_t* d_rp = nullptr;
-  int32_t* d_colx = nullptr;
-  uint8_t* d_part = nullptr;
-  int32_t* d_ids = nullptr;
-  double* d_sc = nullptr;
-  int32_t* d_len = nullptr;
-  int32_t* d_all = nullptr;       // 0..n-1 (init list)
-  int32_t* d_act[2] = {nullptr, nullptr};
-  int64_t nact[2] = {0, 0};
-  int32_t* d_cand = nullptr;
-  int32_t* d_tier_lists = nullptr;   // NLISTS * n
-  uint32_t* d_tier_cnt = nullptr;    // NLISTS (+1: workgroup overflow count)
-  int32_t* d_tier_cap = nullptr;     // NT + 1
-  int32_t* d_ovf = nullptr;          // sources the workgroup tier could not hold
-  int tierT[NT] = {0, 0, 0, 0};
-  int tierCap[NT + 1] = {0, 0, 0, 0, 0};
-  size_t wg_lds = 0;
-  bool hub_enabled = true;
-  unsigned long long* d_maxdiff = nullptr;  // PPR_MAX_ITER_STATS + 1
-  unsigned long long* d_stats = nullptr;    // 2
-  GlbWork* d_work = nullptr;
-  int64_t work_cap = 0;
-  void* d_scratch = nullptr;
-  size_t scratch_bytes = 0;
-  int32_t* d_out_ids = nullptr;
-  double* d_out_sc = nullptr;
-  int32_t* d_out_len = nullptr;
-  int flags = 0;
-  std::vector<int64_t> h_rp;       // host row pointers (hub planning)
-  size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0, hub_lds_wave = 0;
-  int hub_bucket = 512, hub_wave_t = 1024;
-  // source sharding (ppr_grank_plan_comm_init / ppr_grank_plan_run_sharded)
-  ncclComm_t comm = nullptr;
-  int nranks = 1, rank = 0;
-  std::vector<double> work[2];        // per active source: merge work estimate (list order)
-  unsigned char* d_xsend = nullptr;   // packed rows of this rank
-  unsigned char* d_xrecv = nullptr;   // all-gathered rows
-  size_t xsend_bytes = 0, xrecv_bytes = 0;
-  int64_t merge_launches = 0;
-  double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
-  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_m0 = nullptr, ev_m1 = nullptr;
-};
-
-static void plan_free(ppr_plan* p) {
-  if (!p) return;
-  hipFree(p->d_rp); hipFree(p->d_colx); hipFree(p->d_part); hipFree(p->d_ids); hipFree(p->d_sc);
-  hipFree(p->d_len); hipFree(p->d_all); hipFree(p->d_act[0]); hipFree(p->d_act[1]);
-  hipFree(p->d_cand); hipFree(p->d_tier_lists); hipFree(p->d_tier_cnt); hipFree(p->d_tier_cap);
-  hipFree(p->d_ovf);
-  hipFree(p->d_maxdiff); hipFree(p->d_stats); hipFree(p->d_work); hipFree(p->d_scratch);
-  hipFree(p->d_out_ids); hipFree(p->d_out_sc); hipFree(p->d_out_len);
-  if (p->ev_a) hipEventDestroy(p->ev_a);
-  if (p->ev_b) hipEventDestroy(p->ev_b);
-  if (p->ev_m0) hipEventDestroy(p->ev_m0);
-  if (p->ev_m1) hipEventDestroy(p->ev_m1);
-  if (p->comm) ncclCommDestroy(p->comm);
-  hipFree(p->d_xsend); hipFree(p->d_xrecv);
-  if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
-  delete p;
-}
-
-static int check_params(uint32_t K, uint32_t L, uint32_t iterations, double damping) {
-  if (K == 0) return PPR_ERR_K;
-  if (L == 0) return PPR_ERR_L;
-  if (K > L) return PPR_ERR_KL;
-  if (iterations == 0) return PPR_ERR_ITERS;
-  if (damping < 0 || damping > 1) return PPR_ERR_DAMPING;
-  return PPR_OK;
-}
-
-template <class T>
-static int dalloc(T** p, size_t count) {
-  if (count == 0) count = 1;
-  if (hipMalloc((void**)p, sizeof(T) * count) != hipSuccess) return PPR_ERR_OOM;
-  return PPR_OK;
-}
-
-#define TRY(x) do { int _r = (x); if (_r != PPR_OK) { plan_free(p); return _r; } } while (0)
-
-extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, uint32_t K,
-                                     uint32_t L, double damping, const ppr_opts* o,
-                                     ppr_plan** out) {
-  if (!g || !out || g->n < 0 || (g->n > 0 && !g->row_ptr)) return PPR_ERR_ARG;
-  if (g->n > 0 && g->row_ptr[g->n] > 0 && !g->col) return PPR_ERR_ARG;
-  int rc = check_params(K, L, 1, damping);
-  if (rc != PPR_OK) return rc;
-  if (L > (uint32_t)MAX_L) return PPR_ERR_RANGE;
-  if (g->n >= (1LL << 31) - 1) return PPR_ERR_RANGE;
-  const int64_t n = g->n;
-  const int64_t m = n ? g->row_ptr[n] : 0;
-  for (int64_t e = 0; e < m; e++)
-    if (g->col[e] < 0 || g->col[e] >= n) return PPR_ERR_GRAPH;
-  std::vector<uint8_t> part(n > 0 ? n : 1, 0);
-  if (part_in) std::memcpy(part.data(), part_in, n);
-  else if (n) { rc = ppr_find_partitions_csr(g, part.data()); if (rc) return rc; }
-
+int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t K, uint32_t L,
+               double damping, const ppr_opts* o, ppr_plan** out) {
+  const int64_t m = n ? row_ptr[n] : 0;
   ppr_plan* p = new (std::nothrow) ppr_plan();
   if (!p) return PPR_ERR_OOM;
   p->n = n; p->m = m; p->K = K; p->L = L; p->damping = damping;
@@ -212,32 +91,9 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
       else run = p->tierCap[t];
     }
   }
-
-  // host-side CSR with partition bit of the successor
-  std::vector<int32_t> colx(m > 0 ? m : 1);
-  for (int64_t e = 0; e < m; e++) colx[e] = g->col[e] | (part[g->col[e]] ? (int32_t)0x80000000 : 0);
-  std::vector<int32_t> all(n > 0 ? n : 1), act[2];
-  for (int64_t v = 0; v < n; v++) {
-    all[v] = (int32_t)v;
-    if (g->row_ptr[v + 1] > g->row_ptr[v]) act[part[v]].push_back((int32_t)v);
-  }
-  p->h_rp.assign(g->row_ptr, g->row_ptr + n + 1);
-  // merge work estimate per active source (balanced source shards): sum over successors of the
-  // initial basket bound min(L, deg(u) + 1)
-  for (int q = 0; q < 2; q++) {
-    p->work[q].resize(act[q].size());
-    for (size_t i = 0; i < act[q].size(); i++) {
-      const int v = act[q][i];
-      double w = 1.0;
-      for (int64_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; e++) {
-        const int u = g->col[e];
-        w += (double)std::min<int64_t>(L, g->row_ptr[u + 1] - g->row_ptr[u] + 1);
-      }
-      p->work[q][i] = w;
-    }
-  }
-  p->nact[0] = (int64_t)act[0].size();
-  p->nact[1] = (int64_t)act[1].size();
+  std::vector<int32_t> all(n > 0 ? n : 1);
+  for (int64_t v = 0; v < n; v++) all[v] = (int32_t)v;
+  p->h_rp.assign(row_ptr, row_ptr + n + 1);
 
   const size_t slab = (size_t)2 * n * L;
   TRY(dalloc(&p->d_rp, n + 1));
@@ -247,8 +103,6 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
   TRY(dalloc(&p->d_sc, slab));
   TRY(dalloc(&p->d_len, 2 * n));
   TRY(dalloc(&p->d_all, n));
-  TRY(dalloc(&p->d_act[0], p->nact[0]));
-  TRY(dalloc(&p->d_act[1], p->nact[1]));
   TRY(dalloc(&p->d_cand, n));
   TRY(dalloc(&p->d_tier_lists, (size_t)NLISTS * (n > 0 ? n : 1)));
   TRY(dalloc(&p->d_tier_cnt, NLISTS + 1));
@@ -261,12 +115,11 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
   TRY(dalloc(&p->d_out_len, n));
   hipStream_t st = p->stream;
   if (n) {
-    if (hipMemcpyAsync(p->d_rp, g->row_ptr, 8 * (n + 1), hipMemcpyHostToDevice, st) != hipSuccess ||
-        (m && hipMemcpyAsync(p->d_colx, colx.data(), 4 * m, hipMemcpyHostToDevice, st) != hipSuccess) ||
-        hipMemcpyAsync(p->d_part, part.data(), n, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(p->d_all, all.data(), 4 * n, hipMemcpyHostToDevice, st) != hipSuccess ||
-        (p->nact[0] && hipMemcpyAsync(p->d_act[0], act[0].data(), 4 * p->nact[0], hipMemcpyHostToDevice, st) != hipSuccess) ||
-        (p->nact[1] && hipMemcpyAsync(p->d_act[1], act[1].data(), 4 * p->nact[1], hipMemcpyHostToDevice, st) != hipSuccess)) {
+    if (hipMemcpyAsync(p->d_rp, row_ptr, 8 * (n + 1), hipMemcpyHostToDevice, st) != hipSuccess ||
+        (m && hipMemcpyAsync(p->d_colx, colx, 4 * m, hipMemcpyHostToDevice, st) != hipSuccess) ||
+        hipMemsetAsync(p->d_part, 0, n, st) != hipSuccess ||
+        hipMemsetAsync(p->d_len, 0, 8 * n, st) != hipSuccess ||
+        hipMemcpyAsync(p->d_all, all.data(), 4 * n, hipMemcpyHostToDevice, st) != hipSuccess) {
       plan_free(p); return PPR_ERR_HIP;
     }
   }
@@ -301,12 +154,71 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
   return PPR_OK;
 }
 
+extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, uint32_t K,
+                                     uint32_t L, double damping, const ppr_opts* o,
+                                     ppr_plan** out) {
+  if (!g || !out || g->n < 0 || (g->n > 0 && !g->row_ptr)) return PPR_ERR_ARG;
+  if (g->n > 0 && g->row_ptr[g->n] > 0 && !g->col) return PPR_ERR_ARG;
+  int rc = check_params(K, L, 1, damping);
+  if (rc != PPR_OK) return rc;
+  if (L > (uint32_t)MAX_L) return PPR_ERR_RANGE;
+  if (g->n >= (1LL << 31) - 1) return PPR_ERR_RANGE;
+  const int64_t n = g->n;
+  const int64_t m = n ? g->row_ptr[n] : 0;
+  for (int64_t e = 0; e < m; e++)
+    if (g->col[e] < 0 || g->col[e] >= n) return PPR_ERR_GRAPH;
+  std::vector<uint8_t> part(n > 0 ? n : 1, 0);
+  if (part_in) std::memcpy(part.data(), part_in, n);
+  else if (n) { rc = ppr_find_partitions_csr(g, part.data()); if (rc) return rc; }
+
+  // host-side CSR with partition bit of the successor
+  std::vector<int32_t> colx(m > 0 ? m : 1);
+  for (int64_t e = 0; e < m; e++) colx[e] = g->col[e] | (part[g->col[e]] ? (int32_t)0x80000000 : 0);
+  ppr_plan* p = nullptr;
+  rc = plan_alloc(n, g->row_ptr, colx.data(), K, L, damping, o, &p);
+  if (rc) return rc;
+  std::vector<int32_t> act[2];
+  for (int64_t v = 0; v < n; v++)
+    if (g->row_ptr[v + 1] > g->row_ptr[v]) act[part[v]].push_back((int32_t)v);
+  // merge work estimate per active source (balanced source shards): sum over successors of the
+  // initial basket bound min(L, deg(u) + 1)
+  for (int q = 0; q < 2; q++) {
+    p->work[q].resize(act[q].size());
+    for (size_t i = 0; i < act[q].size(); i++) {
+      const int v = act[q][i];
+      double w = 1.0;
+      for (int64_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; e++) {
+        const int u = g->col[e];
+        w += (double)std::min<int64_t>(L, g->row_ptr[u + 1] - g->row_ptr[u] + 1);
+      }
+      p->work[q][i] = w;
+    }
+  }
+  p->nact[0] = (int64_t)act[0].size();
+  p->nact[1] = (int64_t)act[1].size();
+  TRY(dalloc(&p->d_act[0], p->nact[0]));
+  TRY(dalloc(&p->d_act[1], p->nact[1]));
+  hipStream_t st = p->stream;
+  if (n) {
+    if (hipMemcpyAsync(p->d_part, part.data(), n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        (p->nact[0] && hipMemcpyAsync(p->d_act[0], act[0].data(), 4 * p->nact[0], hipMemcpyHostToDevice, st) != hipSuccess) ||
+        (p->nact[1] && hipMemcpyAsync(p->d_act[1], act[1].data(), 4 * p->nact[1], hipMemcpyHostToDevice, st) != hipSuccess) ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      plan_free(p); return PPR_ERR_HIP;
+    }
+  }
+  *out = p;
+  return PPR_OK;
+}
+
 extern "C" void ppr_grank_plan_destroy(ppr_plan* p) { plan_free(p); }
 extern "C" void* ppr_grank_plan_stream(ppr_plan* p) { return p ? (void*)p->stream : nullptr; }
 
 static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   IterArgs a;
   a.damping = p->damping;
+  a.mc = 0u;
+  a.rp = p->d_rp;
   a.unit = unit ? 1u : 0u;
   a.stats = (p->flags & PPR_FLAG_STATS) ? 1u : 0u;
   if (unit) { a.sA = 0; a.sB = 0; a.active = -1; return a; }
@@ -470,8 +382,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
 
 // classify + launch all tiers for `count` sources of `list`; the span is timed with events on
 // the plan's stream and added to merge_ms (iterations only, not init)
-static int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
-                     unsigned long long* maxdiff) {
+int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
+              unsigned long long* maxdiff) {
   if (count <= 0) return PPR_OK;
   HIP_OK(hipEventRecord(p->ev_m0, p->stream));
   int rc = run_merge_impl(p, a, list, count, maxdiff);
@@ -641,7 +553,11 @@ extern "C" int ppr_grank_plan_finish(ppr_plan* p, int32_t iterations_run) {
   if (!p || iterations_run < 0) return PPR_ERR_ARG;
   if (p->n == 0) return PPR_OK;
   HIP_OK(hipSetDevice(p->device));
-  const int sA = ((iterations_run + 1) / 2) & 1, sB = (iterations_run / 2) & 1;
+  return launch_topk(p, ((iterations_run + 1) / 2) & 1, (iterations_run / 2) & 1);
+}
+
+int launch_topk(ppr_plan* p, int sA, int sB) {
+  if (p->n == 0) return PPR_OK;
   DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
   const int64_t blocks = (p->n + 3) / 4;
   hipLaunchKernelGGL(k_topk, dim3((unsigned)blocks), dim3(256), 0, p->stream, s, p->d_part, sA, sB,

@@ -120,16 +120,18 @@ int ppr_execution_order_csr(const ppr_csr* g, int32_t* order) {
     for (int64_t v = 0; v < n; v++)
       for (int64_t e = rp[v]; e < rp[v + 1]; e++) pcol[fill[col[e]]++] = (int32_t)v;
   }
-  // sort by (indegree desc, outdegree asc) (include/mccompletepathv2.h:52-62); std::sort is not
-  // stable, so equal (in,out) pairs keep an implementation-defined order in the reference. We
-  // use a stable sort (graph order within equal pairs): a documented, deterministic choice.
-  std::vector<int32_t> sorted(n);
-  for (int64_t i = 0; i < n; i++) sorted[i] = (int32_t)i;
-  std::stable_sort(sorted.begin(), sorted.end(), [&](int32_t a, int32_t b) {
-    int64_t ia = prp[a + 1] - prp[a], ib = prp[b + 1] - prp[b];
-    if (ia != ib) return ia > ib;
-    return (rp[a + 1] - rp[a]) < (rp[b + 1] - rp[b]);
+  // sort by (indegree desc, outdegree asc) (include/mccompletepathv2.h:52-62). The reference uses
+  // the unstable std::sort on records in graph order; the order it leaves equal (in, out) pairs
+  // in is a function of the key sequence and the comparator only, so running the same library
+  // sort on (node, in, out) records in the same order reproduces it exactly.
+  struct Rec { int32_t node; int64_t in, out; };
+  std::vector<Rec> recs(n);
+  for (int64_t i = 0; i < n; i++) recs[i] = Rec{(int32_t)i, prp[i + 1] - prp[i], rp[i + 1] - rp[i]};
+  std::sort(recs.begin(), recs.end(), [](const Rec& a, const Rec& b) {
+    return a.in > b.in ? true : (a.in == b.in ? a.out < b.out : false);
   });
+  std::vector<int32_t> sorted(n);
+  for (int64_t i = 0; i < n; i++) sorted[i] = recs[i].node;
   // predecessor-release BFS (:64-111)
   std::vector<int64_t> wait(n);
   for (int64_t v = 0; v < n; v++) wait[v] = rp[v + 1] - rp[v];

@@ -9,12 +9,6 @@ namespace pprk {
 
 // ---------------------------------------------------------------------------------------------
 // big sources: one wave per source, table in HBM scratch (per-source region of T slots)
-struct GlbWork {
-  int32_t v;
-  int32_t pad;
-  int64_t off;   // slot offset into the scratch arrays
-  int64_t T;     // table slots (power of two)
-};
 
 __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArgs a,
                                                   const GlbWork* work, int64_t count,
@@ -40,7 +34,7 @@ __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArg
   for (int64_t i = lane_id(); i < wk.T; i += WAVE) keys[i] = EMPTY;
   __threadfence_block();
   const int64_t b = g.rp[v], e = g.rp[v + 1];
-  const double factor = a.damping / (double)(e - b);
+  const double factor = merge_factor(a, e - b);
 
   auto slot_of = [&](int key) -> uint64_t {
     uint64_t h = hash32((uint32_t)key) & mask;
@@ -56,7 +50,7 @@ __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArg
   };
   if (lane_id() == 0) {
     const uint64_t h = slot_of(v);
-    __hip_atomic_store(&acc[h], 1.0 - a.damping, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&acc[h], self_seed(a, e - b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __threadfence_block();
   // one successor basket per step: its keys are distinct, so lanes never collide within a step

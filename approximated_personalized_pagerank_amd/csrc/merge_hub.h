@@ -196,13 +196,14 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, Dev
   const int32_t* bk = bk_all + d.bk_off;
   const int64_t sb = d.st_off + bk[tk.x];
   const int nb = bk[tk.x + 1] - bk[tk.x];
-  const double factor = a.damping / (double)(g.rp[v + 1] - g.rp[v]);
+  const int64_t deg = g.rp[v + 1] - g.rp[v];
+  const double factor = merge_factor(a, deg);
   const int Lw = s.L;
   const int budget = T / 4 * 3;
   table_clear(t);
   int fill = 0;
   if ((int)hub_digit(v, d.logP) == tk.x) {
-    if (lane_id() == 0) { const uint32_t sl = table_slot(t, v); t.acc[sl] = 1.0 - a.damping; }
+    if (lane_id() == 0) { const uint32_t sl = table_slot(t, v); t.acc[sl] = self_seed(a, deg); }
     fill = 1;
   }
   wave_fence();
@@ -290,7 +291,8 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a
   const int32_t* bk = bk_all + d.bk_off;
   const int64_t sb = d.st_off + bk[tk.x], nb = bk[tk.x + 1] - bk[tk.x];
   const bool seed = (int)hub_digit(v, d.logP) == tk.x;
-  const double factor = a.damping / (double)(g.rp[v + 1] - g.rp[v]);
+  const int64_t deg = g.rp[v + 1] - g.rp[v];
+  const double factor = merge_factor(a, deg);
   const int Lw = s.L;
   // the bucket stream: staged (key, score) in successor order, next chunk loaded ahead
   auto each = [&](auto&& fn) {
@@ -318,7 +320,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a
   // optimistic single pass: a bucket dominated by a few hot keys holds few distinct keys
   int Pp = 1;
   for (;;) {
-    if (wg_accumulate(L, Pp, 0x51ed270bu, seed, v, 1.0 - a.damping, factor, Lw, each)) break;
+    if (wg_accumulate(L, Pp, 0x51ed270bu, seed, v, self_seed(a, deg), factor, Lw, each)) break;
     Pp *= 2;
     if (Pp > WG_MAX_PASSES) {
       if (threadIdx.x == 0) { const uint32_t pos = atomicAdd(ovf_cnt, 1u); ovf_list[pos] = -(tk.d + 1); }

@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
       while (t < NT + 1 && need > tier_cap[t]) t++;
       s_tier[slot] = t;
       s_src[slot] = v;
-      const int ownlen = a.unit ? 0 : s.len[s.lrow(a.active == 0 ? a.sA : a.sB, v)];
+      const int ownlen = (a.unit || a.mc) ? 0 : s.len[s.lrow(a.active == 0 ? a.sA : a.sB, v)];
       my_c += (unsigned long long)c;
       my_b += (unsigned long long)(8 + 8 * (e - b) + 12 * c + 12 * ownlen);
     }
@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
 __global__ void __launch_bounds__(256) k_stat_written(DevSlab s, IterArgs a, const int32_t* list,
                                                       int64_t count, unsigned long long* stats) {
   __shared__ unsigned long long red[WAVES_PER_BLOCK];
-  const int nxt = ((a.active == 1) ? a.sB : a.sA) ^ 1;
+  const int nxt = write_slot(a);
   unsigned long long b = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x)
     b += 12ull * (unsigned long long)s.len[s.lrow(nxt, list[i])] + 4ull;
@@ -153,10 +153,10 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
 
   const int v = list[w];
   const int64_t b = g.rp[v], e = g.rp[v + 1];
-  const double factor = a.damping / (double)(e - b);
+  const double factor = merge_factor(a, e - b);
 
   table_clear(t);
-  if (lane_id() == 0) { const uint32_t sl = table_slot(t, v); t.acc[sl] = 1.0 - a.damping; }
+  if (lane_id() == 0) { const uint32_t sl = table_slot(t, v); t.acc[sl] = self_seed(a, e - b); }
   wave_fence();
 
   if (a.unit) {

@@ -1,0 +1,142 @@
+// plan.h -- the device-resident state of one engine instance (ppr_plan, include/ppr_hip.h) and
+// the host-side helpers shared by the GRank (grank.hip) and MCCompletePathV2 (mccp2.hip) drivers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <vector>
+
+#include "../../include/ppr_hip.h"
+#include "ppr_common.h"
+
+using namespace pprk;
+
+#define HIP_OK(expr)                                  \
+  do {                                                \
+    hipError_t _e = (expr);                           \
+    if (_e != hipSuccess) {                           \
+      fprintf(stderr, "ppr_hip: %s failed: %s (%s:%d)\n", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+      return PPR_ERR_HIP;                             \
+    }                                                 \
+  } while (0)
+
+constexpr int WG_TIER_PASSES = 3;
+
+inline int pow2_at_least(int64_t x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+
+// ================================================================================================
+// plan
+struct ppr_plan {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int64_t n = 0, m = 0;
+  uint32_t K = 0, L = 0;
+  int Lp = 1;
+  double damping = 0.85;
+  int64_t* d_rp = nullptr;
+  int32_t* d_colx = nullptr;
+  uint8_t* d_part = nullptr;
+  int32_t* d_ids = nullptr;
+  double* d_sc = nullptr;
+  int32_t* d_len = nullptr;
+  int32_t* d_all = nullptr;       // 0..n-1 (init list)
+  int32_t* d_act[2] = {nullptr, nullptr};
+  int64_t nact[2] = {0, 0};
+  int32_t* d_cand = nullptr;
+  int32_t* d_tier_lists = nullptr;   // NLISTS * n
+  uint32_t* d_tier_cnt = nullptr;    // NLISTS (+1: workgroup overflow count)
+  int32_t* d_tier_cap = nullptr;     // NT + 1
+  int32_t* d_ovf = nullptr;          // sources the workgroup tier could not hold
+  int tierT[NT] = {0, 0, 0, 0};
+  int tierCap[NT + 1] = {0, 0, 0, 0, 0};
+  size_t wg_lds = 0;
+  bool hub_enabled = true;
+  unsigned long long* d_maxdiff = nullptr;  // PPR_MAX_ITER_STATS + 1
+  unsigned long long* d_stats = nullptr;    // 2
+  GlbWork* d_work = nullptr;
+  int64_t work_cap = 0;
+  void* d_scratch = nullptr;
+  size_t scratch_bytes = 0;
+  int32_t* d_out_ids = nullptr;
+  double* d_out_sc = nullptr;
+  int32_t* d_out_len = nullptr;
+  int flags = 0;
+  std::vector<int64_t> h_rp;       // host row pointers (hub planning)
+  size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0, hub_lds_wave = 0;
+  int hub_bucket = 512, hub_wave_t = 1024;
+  // source sharding (ppr_grank_plan_comm_init / ppr_grank_plan_run_sharded)
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  std::vector<double> work[2];        // per active source: merge work estimate (list order)
+  unsigned char* d_xsend = nullptr;   // packed rows of this rank
+  unsigned char* d_xrecv = nullptr;   // all-gathered rows
+  size_t xsend_bytes = 0, xrecv_bytes = 0;
+  int64_t merge_launches = 0;
+  double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
+  hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_m0 = nullptr, ev_m1 = nullptr;
+  // MCCompletePathV2 (mccp2.hip)
+  bool mc = false;
+  int32_t* d_mc_walk = nullptr;       // walk set W (nodes read before their final basket exists)
+  int64_t mc_nwalk = 0;
+  int32_t* d_mc_levels = nullptr;     // non-dangling nodes grouped by combine level
+  std::vector<int64_t> mc_level_off;  // level l = d_mc_levels[off[l] .. off[l+1])
+  int32_t* d_mc_dangling = nullptr;
+  int64_t mc_ndangling = 0;
+  int mc_T = 0;
+  double mc_walk_ms = 0.0;
+  int64_t mc_walks = 0;
+};
+
+inline void plan_free(ppr_plan* p) {
+  if (!p) return;
+  hipFree(p->d_rp); hipFree(p->d_colx); hipFree(p->d_part); hipFree(p->d_ids); hipFree(p->d_sc);
+  hipFree(p->d_len); hipFree(p->d_all); hipFree(p->d_act[0]); hipFree(p->d_act[1]);
+  hipFree(p->d_cand); hipFree(p->d_tier_lists); hipFree(p->d_tier_cnt); hipFree(p->d_tier_cap);
+  hipFree(p->d_ovf);
+  hipFree(p->d_maxdiff); hipFree(p->d_stats); hipFree(p->d_work); hipFree(p->d_scratch);
+  hipFree(p->d_out_ids); hipFree(p->d_out_sc); hipFree(p->d_out_len);
+  if (p->ev_a) hipEventDestroy(p->ev_a);
+  if (p->ev_b) hipEventDestroy(p->ev_b);
+  if (p->ev_m0) hipEventDestroy(p->ev_m0);
+  if (p->ev_m1) hipEventDestroy(p->ev_m1);
+  if (p->comm) ncclCommDestroy(p->comm);
+  hipFree(p->d_xsend); hipFree(p->d_xrecv);
+  hipFree(p->d_mc_walk); hipFree(p->d_mc_levels); hipFree(p->d_mc_dangling);
+  if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
+  delete p;
+}
+
+inline int check_params(uint32_t K, uint32_t L, uint32_t iterations, double damping) {
+  if (K == 0) return PPR_ERR_K;
+  if (L == 0) return PPR_ERR_L;
+  if (K > L) return PPR_ERR_KL;
+  if (iterations == 0) return PPR_ERR_ITERS;
+  if (damping < 0 || damping > 1) return PPR_ERR_DAMPING;
+  return PPR_OK;
+}
+
+template <class T>
+inline int dalloc(T** p, size_t count) {
+  if (count == 0) count = 1;
+  if (hipMalloc((void**)p, sizeof(T) * count) != hipSuccess) return PPR_ERR_OOM;
+  return PPR_OK;
+}
+
+#define TRY(x) do { int _r = (x); if (_r != PPR_OK) { plan_free(p); return _r; } } while (0)
+
+// plan buffers + merge tiers for a CSR whose colx (successor | read-slot bit << 31) is given;
+// no partitions, no active lists (grank.hip / mccp2.hip add their own)
+int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t K, uint32_t L,
+               double damping, const ppr_opts* o, ppr_plan** out);
+// final top-K: prefix K of the row in slot sA (partition 0 nodes) / sB (partition 1 nodes)
+int launch_topk(ppr_plan* p, int sA, int sB);
+// classify + every merge tier for `count` sources of the device list `list`
+int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
+              unsigned long long* maxdiff);

@@ -24,6 +24,14 @@ constexpr int NLISTS = NT + 2;
 constexpr int MAX_L = 4096;           // widest basket the kernels accept
 constexpr int WAVES_PER_BLOCK = 4;
 
+// one source of the HBM-table path (k_merge_glb)
+struct GlbWork {
+  int32_t v;
+  int32_t pad;
+  int64_t off;   // slot offset into the scratch arrays
+  int64_t T;     // table slots (power of two)
+};
+
 struct DevGraph {
   const int64_t* rp;
   const int32_t* colx;
@@ -41,14 +49,33 @@ struct DevSlab {
 };
 
 struct IterArgs {
-  int sA, sB;        // read slot of partition 0 / 1 nodes
+  int sA, sB;        // read slot of successors whose colx bit 31 is 0 / 1
   int active;        // partition updated in this iteration (-1 = init)
   double damping;
   uint32_t unit;     // init mode: every successor contributes {u: 1.0}
   uint32_t stats;
+  uint32_t mc;       // MCCompletePathV2 combine (include/mccompletepathv2.h:211-249)
+  const int64_t* rp; // row pointers (out-degree of the source in the epilogue)
 };
 
 __device__ __forceinline__ int read_slot(const IterArgs& a, int32_t cx) { return (cx < 0) ? a.sB : a.sA; }
+
+// Per-source constants of the two combines (deg > 0 for every merged source):
+//   GRank  acc = {v: 1-d};      acc[k] = fma(s, d/deg, acc[k]);      row = topL(acc)
+//          (include/grank.h:103-116)
+//   MC     acc = {v: 1/(d/deg)}; acc[k] = acc[k] + s (== fma(s, 1, acc[k]));
+//          row = topL(acc) * (d/deg)   (include/mccompletepathv2.h:214-247)
+__device__ __forceinline__ double merge_factor(const IterArgs& a, int64_t deg) {
+  return a.mc ? 1.0 : a.damping / (double)deg;
+}
+__device__ __forceinline__ double self_seed(const IterArgs& a, int64_t deg) {
+  return a.mc ? 1.0 / (a.damping / (double)deg) : 1.0 - a.damping;
+}
+// slot an active source writes: GRank ping-pongs per partition, MC writes its final basket to
+// slot 0 (slot 1 holds the random-walk baskets)
+__device__ __forceinline__ int write_slot(const IterArgs& a) {
+  return a.mc ? 0 : (((a.active == 1) ? a.sB : a.sA) ^ 1);
+}
 
 // Epilogue of one source, run by ONE wave: select the top-L of U candidates (keys/vals in LDS
 // or HBM), sort the row, write it to the next slot, norm1 against the old row, fold maxDiff.
@@ -88,6 +115,15 @@ __device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt v
       for (int i = lane_id(); i < cnt; i += WAVE) { s.ids[r + i] = rk[i]; s.sc[r + i] = bitsd(rv[i]); }
       if (lane_id() == 0) s.len[s.lrow(sl, v)] = cnt;
     }
+    return;
+  }
+  if (a.mc) {
+    // keepTop(L) first, then `*= factor` (include/mccompletepathv2.h:243-247); the row stays in
+    // the order of the unscaled scores, which scaling by factor > 0 does not invert
+    const double f = a.damping / (double)(a.rp[v + 1] - a.rp[v]);
+    const int64_t r = s.row(0, v);
+    for (int i = lane_id(); i < cnt; i += WAVE) { s.ids[r + i] = rk[i]; s.sc[r + i] = bitsd(rv[i]) * f; }
+    if (lane_id() == 0) s.len[s.lrow(0, v)] = cnt;
     return;
   }
   const int cur = (a.active == 1) ? a.sB : a.sA;

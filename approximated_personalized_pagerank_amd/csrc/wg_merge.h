@@ -400,10 +400,11 @@ __global__ void __launch_bounds__(WG_THREADS) k_merge_wg(DevGraph g, DevSlab s, 
   if (w >= count) return;
   const WgLds L = wg_carve(smem, WG_T, Lp, wg_pl(Lp));
   const int v = list[w];
-  const double factor = a.damping / (double)(g.rp[v + 1] - g.rp[v]);
+  const int64_t deg = g.rp[v + 1] - g.rp[v];
+  const double factor = merge_factor(a, deg);
   int P = (cand[v] + WG_PASS_CAP - 1) / WG_PASS_CAP;
   for (;;) {
-    const bool ok = wg_accumulate(L, P, 0x9e3779b9u, true, v, 1.0 - a.damping, factor, s.L,
+    const bool ok = wg_accumulate(L, P, 0x9e3779b9u, true, v, self_seed(a, deg), factor, s.L,
                                   [&](auto&& fn) { wg_slab_stream(L, g, s, a, v, fn); });
     if (ok) break;
     P *= 2;

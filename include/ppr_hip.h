@@ -77,7 +77,8 @@ const char* ppr_strerror(int code);
 /* BFS 2-colouring of include/internal/pprInternal.h:29-99; part[i] = 0 for partitions.first */
 int ppr_find_partitions_csr(const ppr_csr* g, uint8_t* part);
 
-/* MCCompletePathV2 node order, include/mccompletepathv2.h:36-113 (stable on ties) */
+/* MCCompletePathV2 node order, include/mccompletepathv2.h:36-113 (the same library sort on the
+ * same records, so ties come out in the reference's order) */
 int ppr_execution_order_csr(const ppr_csr* g, int32_t* order);
 
 /* Synthetic RMAT graph (Graph500 recursion, scrambled labels, deduped, successors ascending).
@@ -151,6 +152,40 @@ int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, int32_t* ids,
                               int32_t* len);
 /* Device stream the plan runs on (hipStream_t as void*), for event timing by the caller. */
 void* ppr_grank_plan_stream(ppr_plan* p);
+/* Raw basket slab slot (n*L ids / scores, n lengths; only the first len[v] entries of a row are
+ * meaningful). MC plans: slot 0 = final baskets, slot 1 = random-walk baskets of the walk set. */
+int ppr_plan_fetch_slot(ppr_plan* p, int32_t slot, int32_t* ids, double* scores, int32_t* len);
+
+/* ---- MCCompletePathV2 (ppr::mccompletepathv2, include/mccompletepathv2.h:182-258) ----
+ * `walks` is the reference's `iterations` (R): floor(R*d) walks per walk-set node. The walks use
+ * counter-based Philox4x32-10 keyed by `seed` (the reference seeds a global mt19937 from
+ * std::random_device, so runs are only statistically comparable); the combine is deterministic.
+ * Results: out_ids / out_scores n*K (rows score desc, id asc, unused id -1), out_len n. */
+typedef struct ppr_mc_stats {
+  double device_ms;        /* walks + combine + top-K, device events */
+  double walk_ms;          /* k_mc_walk */
+  double combine_ms;       /* level-synchronous merge kernels */
+  int64_t walk_nodes;      /* |W|: nodes whose random-walk basket some predecessor reads */
+  int64_t walks;           /* walks run (|W| * floor(R*d)) */
+  int64_t levels;          /* combine levels */
+  int64_t merge_launches;
+  int64_t candidates;      /* combine candidates (PPR_FLAG_STATS) */
+  int64_t algo_bytes;      /* combine algorithmic bytes (PPR_FLAG_STATS) */
+} ppr_mc_stats;
+
+int ppr_mccp2_csr(const ppr_csr* g, uint32_t K, uint32_t L, uint32_t walks, double damping,
+                  uint64_t seed, const ppr_opts* o, int32_t* out_ids, double* out_scores,
+                  int32_t* out_len, ppr_mc_stats* st);
+/* Plan form: executionOrder, walk set and combine levels are computed once and the graph stays
+ * resident. ppr_mccp2_plan_walk runs the walks of walk-set entries [begin, end) (walk-count
+ * sharding across GPUs needs no exchange); combine merges level by level and writes the top-K,
+ * fetched with ppr_grank_plan_fetch; destroy with ppr_grank_plan_destroy. */
+int ppr_mccp2_plan_create(const ppr_csr* g, uint32_t K, uint32_t L, double damping,
+                          const ppr_opts* o, ppr_plan** out);
+int ppr_mccp2_plan_info(ppr_plan* p, int64_t* walk_nodes, int64_t* levels, int64_t* dangling);
+int ppr_mccp2_plan_walk(ppr_plan* p, uint32_t walks, uint64_t seed, int64_t begin, int64_t end);
+int ppr_mccp2_plan_combine(ppr_plan* p);
+int ppr_mccp2_plan_run(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_stats* st);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,8 @@
 """oracle/oracle.py -- TEST INFRASTRUCTURE ONLY (tests/, __graft_entry__.smoke(), bench.py cpu_baseline).
 
-ctypes wrapper of the plain-C restatement oracle/grank_oracle.c (see its header for the
-reference file:line each piece follows and how it is pinned against the compiled reference).
+ctypes wrapper of the plain-C restatements oracle/grank_oracle.c (GRank) and oracle/mc_oracle.c
+(MCCompletePathV2); see their headers for the reference file:line each piece follows and how it
+is pinned against the compiled reference.
 The product path (approximated_personalized_pagerank_amd) never imports this module.
 """
 from __future__ import annotations
@@ -42,6 +43,11 @@ def lib():
         L.oracle_step.argtypes = [ctypes.c_int64, vp, vp, ctypes.c_int32, ctypes.c_double, vp, vp, vp, vp,
                                   ctypes.c_int64, vp, vp, vp, ctypes.POINTER(ctypes.c_double)]
         L.oracle_step.restype = ctypes.c_int
+        L.oracle_execution_order.argtypes = [ctypes.c_int64, vp, vp, vp]
+        L.oracle_execution_order.restype = ctypes.c_int
+        L.oracle_mccp2.argtypes = [ctypes.c_int64, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
+                                   ctypes.c_double, ctypes.c_uint64, vp, vp, vp, vp, vp, vp]
+        L.oracle_mccp2.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -85,6 +91,40 @@ def grank(row_ptr, col, part, K, L, iterations, damping, tolerance, want_slab=Fa
             s_ids[v, s_len[v]:] = -1
             s_sc[v, s_len[v]:] = 0.0
         out.update(slab_ids=s_ids, slab_scores=s_sc, slab_lens=s_len)
+    return out
+
+
+def execution_order(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:
+    """MCCompletePathV2 executionOrder (include/mccompletepathv2.h:36-113), dense ids."""
+    n = len(row_ptr) - 1
+    order = np.zeros(n, dtype=np.int32)
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+    cl = np.ascontiguousarray(col, dtype=np.int32)
+    if n:
+        assert lib().oracle_execution_order(n, _p(rp), _p(cl) if len(cl) else None, _p(order)) == 0
+    return order
+
+
+def mccp2(row_ptr, col, K, L, walks, damping, seed, want_walks=False):
+    """MCCompletePathV2 with the engine's Philox walks. Returns dict(ids [n,K], scores [n,K],
+    lens [n][, walk_ids [n,L], walk_scores [n,L], walk_lens [n]])."""
+    n = len(row_ptr) - 1
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+    cl = np.ascontiguousarray(col, dtype=np.int32)
+    ids = np.full((n, K), -1, dtype=np.int32)
+    sc = np.zeros((n, K), dtype=np.float64)
+    lens = np.zeros(n, dtype=np.int32)
+    w_ids = np.full((n, L), -1, dtype=np.int32) if want_walks else None
+    w_sc = np.zeros((n, L), dtype=np.float64) if want_walks else None
+    w_len = np.zeros(n, dtype=np.int32) if want_walks else None
+    if n:
+        rc = lib().oracle_mccp2(n, _p(rp), _p(cl) if len(cl) else None, K, L, walks, damping,
+                                seed & 0xFFFFFFFFFFFFFFFF, _p(ids), _p(sc), _p(lens), _p(w_ids), _p(w_sc),
+                                _p(w_len))
+        assert rc == 0, rc
+    out = dict(ids=ids, scores=sc, lens=lens)
+    if want_walks:
+        out.update(walk_ids=w_ids, walk_scores=w_sc, walk_lens=w_len)
     return out
 
 

@@ -4,6 +4,7 @@
 //   dropin_test empty        empty graph -> empty result
 //   dropin_test ring         README ring of 100, K50 L100 30 it 1e-3: prints "src key score" rows
 //   dropin_test known        known answers of test/grankTest.cc (exit 0 when all hold)
+//   dropin_test mcbad <case> / mcknown   the same for mccompletepathv2 (test/mccompletepathv2Test.cc)
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -13,6 +14,7 @@
 
 #include "ppr/grank.h"
 #include "ppr/grankMulti.h"
+#include "ppr/mccompletepathv2.h"
 
 using namespace std;
 
@@ -37,6 +39,48 @@ int main(int argc, char** argv) {
       case 6: ppr::grankMulti(graph, 2, 2, 10, 0.5, 0.0001, 0); break;
     }
     return 0;
+  }
+  if (mode == "mcbad") {
+    int c = atoi(argv[2]);
+    switch (c) {  // test/mccompletepathv2Test.cc:20-29
+      case 0: ppr::mccompletepathv2(graph, 0, 3, 42, 0.5); break;
+      case 1: ppr::mccompletepathv2(graph, 2, 0, 32, 0.85); break;
+      case 2: ppr::mccompletepathv2(graph, 2, 1, 10, 0.5); break;
+      case 3: ppr::mccompletepathv2(graph, 2, 2, 0, 0.5); break;
+      case 4: ppr::mccompletepathv2(graph, 2, 2, 10, 1.5); break;
+      case 5: ppr::mccompletepathv2(graph, 2, 2, 10, -1.5); break;
+    }
+    return 0;
+  }
+  if (mode == "mcknown") {
+    int bad = 0;
+    bad += check(ppr::mccompletepathv2(graph, 10, 30, 100, 0.85).empty(), "mc empty");
+    for (int i = 0; i < 10; i++) graph[i];
+    auto r = ppr::mccompletepathv2(graph, 10, 30, 100, 0.85);  // :38-50
+    for (int i = 0; i < 10; i++) bad += check(r[i].size() == 1 && fabs(r[i][i] - 1.0) < 1e-4, "mc no edges");
+    unordered_map<int, vector<int>> star;
+    for (int i = 0; i < 6; i++) star[i];
+    for (int i = 1; i < 6; i++) star[i].push_back(0);
+    r = ppr::mccompletepathv2(star, 10, 30, 100, 0.85);  // :154-172
+    bad += check(r[0].size() == 1 && fabs(r[0][0] - 1.0) < 1e-4, "mc star centre");
+    for (int i = 1; i < 6; i++) bad += check(r[i].size() == 2 && fabs(r[i][0] - 0.85) < 1e-4, "mc star leaf");
+    unordered_map<int, vector<int>> rev;
+    for (int i = 0; i < 6; i++) rev[i];
+    for (int i = 1; i < 6; i++) rev[0].push_back(i);
+    r = ppr::mccompletepathv2(rev, 10, 30, 100, 0.85);  // :184-205
+    bad += check(r[0].size() == 6 && fabs(r[0][0] - 1.0) < 1e-4, "mc reversed star centre");
+    for (int i = 1; i < 6; i++)
+      bad += check(r[i].size() == 1 && fabs(r[0][i] - 0.85 / 5) < 1e-4, "mc reversed star leaf");
+    unordered_map<int, vector<int>> ring;
+    for (int i = 0; i < 100; i++) ring[i];
+    for (int i = 0; i < 99; i++) ring[i].push_back(i + 1);
+    ring[99].push_back(0);
+    r = ppr::mccompletepathv2(ring, 10, 20, 100, 0.85);  // :221-255
+    for (int i = 0; i < 100; i++) {
+      bad += check(r[i].size() == 10, "mc ring size");
+      for (int u = 0; u < 9; u++) bad += check(r[i][(i + u) % 100] >= r[i][(i + u + 1) % 100], "mc ring order");
+    }
+    return bad ? 1 : 0;
   }
   if (mode == "empty") {
     auto res = ppr::grank(graph, 10, 30, 100, 0.85, 0.0001);

@@ -1,5 +1,5 @@
-"""The C++ drop-in headers (include/ppr/grank.h, grankMulti.h) compiled unchanged from code
-written against the reference's API, linked with libppr_hip.so."""
+"""The C++ drop-in headers (include/ppr/grank.h, grankMulti.h, mccompletepathv2.h) compiled
+unchanged from code written against the reference's API, linked with libppr_hip.so."""
 import os
 import subprocess
 
@@ -27,6 +27,20 @@ def dropin():
 def test_bad_parameters_exit_like_reference(dropin, case, msg):
     p = subprocess.run([dropin, "bad", str(case)], capture_output=True, text=True)
     assert p.returncode == 1 and msg in p.stderr
+
+
+@pytest.mark.parametrize("case,msg", [(0, "K must be positive"), (1, "L must be positive"), (2, "K must be <= L"),
+                                      (3, "iterations must be positive"), (4, "damping must be [0,1]"),
+                                      (5, "damping must be [0,1]")])
+def test_mc_bad_parameters_exit_like_reference(dropin, case, msg):
+    p = subprocess.run([dropin, "mcbad", str(case)], capture_output=True, text=True)
+    assert p.returncode == 1 and msg in p.stderr
+
+
+@pytest.mark.gpu
+def test_mc_known_answers_cpp(dropin):
+    p = subprocess.run([dropin, "mcknown"], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
 
 
 def test_empty_graph(dropin):

@@ -1,0 +1,115 @@
+"""GPU parity of MCCompletePathV2 (k_mc_walk + the merge tiers in MC mode) through the C ABI.
+
+Contract (DESIGN.md "MCCompletePathV2"): for a given seed the HIP path equals the restatement
+oracle/mc_oracle.c bit for bit -- every walk basket (as a key -> score set) and every final top-K
+row -- on every merge path; against the reference it is statistical (tests/test_mc_oracle.py pins
+the oracle) and the known answers of test/mccompletepathv2Test.cc hold.
+"""
+import numpy as np
+import pytest
+
+import approximated_personalized_pagerank_amd as ppr
+import oracle
+from helpers import jaccard_rows, load
+
+pytestmark = pytest.mark.gpu
+
+SEED = 1
+
+
+def walk_sets(ids, sc, lens):
+    return [dict(zip(ids[v, : lens[v]].tolist(), sc[v, : lens[v]].tolist())) for v in range(len(lens))]
+
+
+def check_vs_oracle(g, K, L, R, d, seed=SEED, walks=True):
+    plan = ppr.MccpPlan(g, K, L, d, device=0)
+    plan.run(R, seed)
+    r = plan.fetch()
+    o = oracle.mccp2(g.row_ptr, g.col, K, L, R, d, seed, want_walks=walks)
+    assert np.array_equal(r.lens, o["lens"])
+    assert np.array_equal(r.ids, o["ids"])
+    assert np.array_equal(r.scores.view(np.int64), o["scores"].view(np.int64))
+    if walks:
+        wi, ws, wl = plan.fetch_slot(1)
+        assert np.array_equal(wl, o["walk_lens"])
+        assert walk_sets(wi, ws, wl) == walk_sets(o["walk_ids"], o["walk_scores"], o["walk_lens"])
+    plan.close()
+    return r
+
+
+MC_FIXTURES = ["m1_noedges10", "m1_single_loop", "m1_two_linked", "m1_ring6", "m1_star", "m1_star_loop",
+               "m1_star_rev", "m1_star_rev_loops", "m1_ring100_k10_l20", "m2_random100_full",
+               "m3_rmat10_k16_l64"]
+
+
+@pytest.mark.parametrize("name", MC_FIXTURES)
+def test_gpu_mc_bit_exact_vs_oracle_fixtures(name):
+    f = load(name)
+    check_vs_oracle(ppr.Csr(f["rp"], f["col"]), f["K"], f["L"], min(f["iters"], 5000), f["damping"])
+
+
+def test_gpu_mc_eat_vs_oracle_and_reference():
+    f = load("m4_eat_k50_l200")
+    r = check_vs_oracle(ppr.Csr(f["rp"], f["col"]), f["K"], f["L"], f["iters"], f["damping"], walks=False)
+    z = f["z"]
+    s = z["sample"]
+    assert jaccard_rows(r.ids[s], r.lens[s], z["ids"], np.minimum(z["cnt"], f["K"])).mean() >= 0.98
+
+
+@pytest.mark.parametrize("scale,K,L,R", [(9, 8, 16, 200), (11, 16, 64, 300), (12, 32, 200, 100), (8, 4, 1000, 50)])
+def test_gpu_mc_bit_exact_vs_oracle_rmat(scale, K, L, R):
+    check_vs_oracle(ppr.rmat(scale, seed=scale * 7 + L), K, L, R, 0.85)
+
+
+@pytest.mark.parametrize("mask", ["0x20", "0x10", "0x0", "0x1", "0x21"])
+def test_gpu_mc_merge_paths_bit_exact(mask, monkeypatch):
+    """the level combine through each merge path alone (hub pipeline, workgroup tier, HBM table,
+    smallest wave tier + fallbacks) equals the oracle"""
+    monkeypatch.setenv("PPR_TIER_MASK", mask)
+    check_vs_oracle(ppr.rmat(10, seed=91), 16, 48, 100, 0.85, walks=False)
+
+
+@pytest.mark.parametrize("d", [0.5, 1.0])
+def test_gpu_mc_damping_edges(d):
+    # d = 1: walks end only at dangling nodes or the step cap (the reference loops forever)
+    ring = ppr.Csr(np.arange(21, dtype=np.int64), np.array([(i + 1) % 20 for i in range(20)], dtype=np.int32))
+    check_vs_oracle(ring, 5, 10, 8 if d == 1.0 else 300, d)
+    check_vs_oracle(ppr.rmat(8, seed=3), 8, 32, 20, d)
+
+
+def test_gpu_mc_known_answers_dict_api():
+    star = {i: ([0] if i else []) for i in range(6)}
+    res = ppr.mccompletepathv2(star, 10, 30, 100, 0.85)
+    assert res[0] == {0: 1.0}
+    assert all(len(res[i]) == 2 and abs(res[i][0] - 0.85) < 1e-4 for i in range(1, 6))
+    rev = {0: [1, 2, 3, 4, 5], 1: [], 2: [], 3: [], 4: [], 5: []}
+    res = ppr.mccompletepathv2(rev, 10, 30, 100, 0.85)
+    assert abs(res[0][0] - 1.0) < 1e-4
+    assert all(abs(res[0][i] - 0.85 / 5) < 1e-4 and res[i] == {i: 1.0} for i in range(1, 6))
+    assert ppr.mccompletepathv2({}, 10, 30, 100, 0.85) == {}
+    with pytest.raises(ppr.PprError, match="iterations must be positive"):
+        ppr.mccompletepathv2(star, 2, 2, 0, 0.5)
+
+
+def test_gpu_mc_deterministic_and_seeded():
+    g = ppr.rmat(11, seed=5)
+    a = ppr.mccp2_csr(g, 16, 64, 200, 0.85, seed=7, device=0)
+    b = ppr.mccp2_csr(g, 16, 64, 200, 0.85, seed=7, device=0)
+    c = ppr.mccp2_csr(g, 16, 64, 200, 0.85, seed=8, device=0)
+    assert np.array_equal(a.ids, b.ids) and np.array_equal(a.scores, b.scores)
+    assert not np.array_equal(a.scores, c.scores)
+
+
+def test_gpu_mc_walk_shards_compose():
+    """walk-count sharding: walks of disjoint walk-set ranges (one per GPU) + one combine equal the
+    single run"""
+    g = ppr.rmat(11, seed=13)
+    full = ppr.mccp2_csr(g, 16, 64, 200, 0.85, seed=3, device=0)
+    plan = ppr.MccpPlan(g, 16, 64, 0.85, device=0)
+    w = plan.walk_nodes
+    cuts = [0, w // 3, (2 * w) // 3, w]
+    for b, e in zip(cuts[:-1], cuts[1:]):
+        plan.walk(200, 3, b, e)
+    plan.combine()
+    r = plan.fetch()
+    assert np.array_equal(r.ids, full.ids) and np.array_equal(r.scores, full.scores)

@@ -89,6 +89,8 @@ def run_ref(mode, graph_path, K, L, iters, d, tol, threads=1):
 def save(name, res, params, sample=None, extra=None):
     d = dict(order=res["order"], rp=res["rp"], col=res["col"], part=res["part"],
              params=np.array(params, dtype=np.float64))
+    if res["exec_order"].size and res["exec_order"][0] >= 0:
+        d["exec_order"] = res["exec_order"]
     if sample is None:
         d.update(ids=res["ids"], scores=res["scores"], cnt=res["cnt"])
     else:
@@ -123,7 +125,66 @@ def rmat_lists(scale, seed=42):
     return keys, succ
 
 
+def main_mc():
+    """MCCompletePathV2 fixtures (mode mc): the reference's executionOrder (exact target) and one
+    sample of its random-walk result (statistical target), plus exact PPR where cheap."""
+    rng = np.random.default_rng(2017)
+
+    def mg(name, n, edges, K, L, R, pprss=False, sample=None, pprss_topk=False):
+        succ = [[] for _ in range(n)]
+        for a, b in edges:
+            succ[a].append(b)
+        extra = [("pprss", n, 0, 100, -1.0)] if pprss else ()
+        res = gen_graph(name, list(range(n)), succ, K, L, R, 0.85, -1.0, mode="mc", extra_modes=extra,
+                        sample=sample)
+        if pprss_topk:
+            # exact PPR of every source, kept to the top-K (quality reference for the MC rows)
+            with tempfile.TemporaryDirectory() as td:
+                gp = os.path.join(td, "g.bin")
+                write_graph_bin(gp, list(range(n)), succ)
+                ex = run_ref("pprss", gp, n, 0, 100, 0.85, -1.0)
+            assert np.array_equal(ex["order"], res["order"])
+            path = os.path.join(GOLDEN, name + ".npz")
+            z = dict(np.load(path))
+            z.update(pprss_ids=ex["ids"][:, :K], pprss_scores=ex["scores"][:, :K],
+                     pprss_cnt=np.minimum(ex["cnt"], K))
+            np.savez_compressed(path, **z)
+
+    # test/mccompletepathv2Test.cc graphs
+    mg("m1_noedges10", 10, [], 10, 30, 100)
+    mg("m1_single_loop", 1, [(0, 0)], 10, 30, 1000)
+    mg("m1_two_linked", 2, [(0, 1), (1, 0)], 10, 30, 1000, pprss=True)
+    mg("m1_ring6", 6, [(i, (i + 1) % 6) for i in range(6)], 10, 30, 20000, pprss=True)
+    mg("m1_star", 6, [(i, 0) for i in range(1, 6)], 10, 30, 100)
+    mg("m1_star_loop", 6, [(i, 0) for i in range(1, 6)] + [(0, 0)], 10, 30, 1000)
+    mg("m1_star_rev", 6, [(0, i) for i in range(1, 6)], 10, 30, 100)
+    mg("m1_star_rev_loops", 6, [(0, i) for i in range(1, 6)] + [(i, i) for i in range(1, 6)], 10, 30, 200)
+    ring100 = [(i, i + 1) for i in range(99)] + [(99, 0)]
+    mg("m1_ring100_k10_l20", 100, ring100, 10, 20, 1000)
+    # no truncation: statistical comparison against exact PPR
+    rnd = [(int(a), int(b)) for a, b in rng.integers(0, 100, size=(400, 2))]
+    mg("m2_random100_full", 100, rnd, 100, 100, 20000, pprss=True)
+    # RMAT: execution order (exact) and a truncating MC run
+    keys, succ = rmat_lists(10)
+    edges = [(a, b) for a in range(len(succ)) for b in succ[a]]
+    mg("m3_rmat10_k16_l64", len(keys), edges, 16, 64, 1000, pprss_topk=True)
+    keys, succ = rmat_lists(14)
+    edges = [(a, b) for a in range(len(succ)) for b in succ[a]]
+    mg("m3_rmat14_order", len(keys), edges, 1, 1, 1, sample=np.arange(0, dtype=np.int64))
+    # EAT, the reference CLI's call mccompletepathv2(50, 200, 1000, .85) (src/main.cc:48)
+    if os.path.exists(EAT):
+        with tempfile.TemporaryDirectory() as td:
+            out = os.path.join(td, "out.bin")
+            subprocess.run([DRIVER, "mc", EAT, out, "50", "200", "1000", "0.85", "-1", "1"], check=True)
+            res = read_out(out, 50)
+        n = len(res["order"])
+        sample = np.sort(rng.choice(n, 3000, replace=False)).astype(np.int64)
+        save("m4_eat_k50_l200", res, [50, 200, 1000, 0.85, -1.0], sample)
+
+
 def main():
+    if "--mc" in sys.argv:
+        return main_mc()
     os.makedirs(GOLDEN, exist_ok=True)
     if not os.path.exists(DRIVER):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
