@@ -25,6 +25,7 @@
 // the basket {u: 1.0}, and fma(1.0, f, acc) == acc + f reproduces `scores[v][s] += factor`.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -258,7 +259,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
   while (i0 < big.size()) {
     std::vector<HubDesc> desc;
     std::vector<HubTask> tiles, buckets;
-    int64_t cm = 0, stg = 0, pt = 0, bkn = 0;
+    int64_t cm = 0, stg = 0, pt = 0;
     int maxP = 1;
     size_t i = i0;
     while (i < big.size()) {
@@ -271,30 +272,37 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
       const int P = 1 << logP;
       const int T = (int)((deg + HUB_TILE - 1) / HUB_TILE);
       const int idx = (int)desc.size();
-      desc.push_back(HubDesc{v, logP, T, (int32_t)need, cm, stg, pt, bkn});
+      // staging offsets are cumulative candidate counts in descriptor order, the same order the
+      // device scan walks the concatenated count matrices in: scanned cm = absolute offsets
+      desc.push_back(HubDesc{v, logP, T, (int32_t)need, cm, stg, pt, 0});
       for (int t = 0; t < T; t++) tiles.push_back(HubTask{idx, t});
       for (int b = 0; b < P; b++) buckets.push_back(HubTask{idx, b});
       cm += (int64_t)P * T;
       stg += need - 1;
       pt += (int64_t)P * L;
-      bkn += 2 * P + 1;
       maxP = std::max(maxP, P);
       i++;
     }
+    const size_t nd = desc.size();
+    size_t scan_tmp = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (const int32_t*)nullptr, (int32_t*)nullptr, (int)cm, st);
     // scratch layout
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t off = 0;
-    const size_t o_desc = off; off = al(off + sizeof(HubDesc) * desc.size());
+    const size_t o_desc = off; off = al(off + sizeof(HubDesc) * nd);
     const size_t o_tile = off; off = al(off + sizeof(HubTask) * tiles.size());
     const size_t o_buck = off; off = al(off + sizeof(HubTask) * buckets.size());
     const size_t o_cm = off;   off = al(off + 4 * (size_t)cm);
-    const size_t o_bk = off;   off = al(off + 4 * (size_t)bkn);
+    const size_t o_cmx = off;  off = al(off + 4 * (size_t)cm);
+    const size_t o_tmp = off;  off = al(off + scan_tmp);
     const size_t o_sk = off;   off = al(off + 4 * (size_t)stg);
     const size_t o_ss = off;   off = al(off + 8 * (size_t)stg);
     const size_t o_pk = off;   off = al(off + 4 * (size_t)pt);
     const size_t o_ps = off;   off = al(off + 8 * (size_t)pt);
+    const size_t o_pc = off;   off = al(off + 4 * nd);
+    const size_t o_tau = off;  off = al(off + 8 * nd);
+    const size_t o_idx = off;  off = al(off + 4 * nd);
     const size_t o_ovf = off;  off = al(off + 4 * (buckets.size() + 1));
-    const size_t o_wl = off;   off = al(off + sizeof(HubTask) * (buckets.size() + 1));
     const size_t o_gl = off;   off = al(off + sizeof(HubTask) * (buckets.size() + 1));
     const size_t o_cnt = off;  off = al(off + 16);
     int rc = ensure_scratch(p, off);
@@ -304,73 +312,77 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     HubTask* d_tile = (HubTask*)(base + o_tile);
     HubTask* d_buck = (HubTask*)(base + o_buck);
     int32_t* d_cm = (int32_t*)(base + o_cm);
-    int32_t* d_bk = (int32_t*)(base + o_bk);
+    int32_t* d_cmx = (int32_t*)(base + o_cmx);
+    void* d_tmp = (void*)(base + o_tmp);
     int32_t* d_sk = (int32_t*)(base + o_sk);
     double* d_ss = (double*)(base + o_ss);
     int32_t* d_pk = (int32_t*)(base + o_pk);
     double* d_ps = (double*)(base + o_ps);
+    uint32_t* d_pc = (uint32_t*)(base + o_pc);
+    unsigned long long* d_tau = (unsigned long long*)(base + o_tau);
+    int32_t* d_idx = (int32_t*)(base + o_idx);
     int32_t* d_ovf = (int32_t*)(base + o_ovf);
     uint32_t* d_ovf_cnt = (uint32_t*)(d_ovf + buckets.size());
-    HubTask* d_wl = (HubTask*)(base + o_wl);
     HubTask* d_gl = (HubTask*)(base + o_gl);
-    uint32_t* d_lc = (uint32_t*)(base + o_cnt);  // [0] wave list, [1] workgroup list
-    HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * desc.size(), hipMemcpyHostToDevice, st));
+    uint32_t* d_lc = (uint32_t*)(base + o_cnt);  // [0] unused, [1] workgroup list
+    HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * nd, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_tile, tiles.data(), sizeof(HubTask) * tiles.size(), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_buck, buckets.data(), sizeof(HubTask) * buckets.size(), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(d_pc, 0, 4 * nd, st));
+    HIP_OK(hipMemsetAsync(d_tau, 0, 8 * nd, st));
     HIP_OK(hipMemsetAsync(d_ovf_cnt, 0, 4, st));
     HIP_OK(hipMemsetAsync(d_lc, 0, 8, st));
     const int64_t ntiles = (int64_t)tiles.size();
     const size_t lds_tile = (size_t)WAVES_PER_BLOCK * maxP * 4;
     const unsigned tb = (unsigned)((ntiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm);
+    hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm,
+                       d_tau);
     HIP_OK(hipGetLastError());
-    hipLaunchKernelGGL(k_hub_scan, dim3((unsigned)desc.size()), dim3(1024), 0, st, d_desc, d_cm, d_bk);
-    HIP_OK(hipGetLastError());
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, scan_tmp, d_cm, d_cmx, (int)cm, st));
     hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
-                       d_cm, d_sk, d_ss);
+                       d_cmx, d_sk, d_ss);
     HIP_OK(hipGetLastError());
     const int64_t nbuck = (int64_t)buckets.size();
     // every bucket goes to a single wave first: a bucket made long by one hot key (a core node
     // present in most successor baskets) still has few distinct keys, and its sequential fma
     // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
-    uint32_t lc[2] = {(uint32_t)nbuck, 0u};
-    (void)d_wl;
-    if (lc[0]) {
-      hipLaunchKernelGGL(k_hub_bucket_w, dim3((lc[0] + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK), dim3(256),
-                         p->hub_lds_wave, st, s, a, g, d_desc, d_buck, (int64_t)lc[0], d_bk, d_sk, d_ss, d_pk, d_ps,
-                         d_bk, p->Lp, d_gl, d_lc + 1, p->hub_wave_t);
-      HIP_OK(hipGetLastError());
-      HIP_OK(hipMemcpyAsync(&lc[1], d_lc + 1, 4, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-    }
-    if (lc[1]) {
-      hipLaunchKernelGGL(k_hub_bucket, dim3(lc[1]), dim3(WG_THREADS), p->hub_lds_wg, st, s, a, g,
-                         d_desc, d_gl, (int64_t)lc[1], d_bk, d_sk, d_ss, d_pk, d_ps, d_bk, p->Lp, d_ovf, d_ovf_cnt);
+    uint32_t nspill = 0;
+    hipLaunchKernelGGL(k_hub_bucket_w, dim3((unsigned)((nbuck + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)), dim3(256),
+                       p->hub_lds_wave, st, s, a, g, d_desc, d_buck, nbuck, d_cmx, d_sk, d_ss, d_pk, d_ps, d_pc,
+                       d_tau, p->Lp, d_gl, d_lc + 1, p->hub_wave_t);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(&nspill, d_lc + 1, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (nspill) {
+      hipLaunchKernelGGL(k_hub_bucket, dim3(nspill), dim3(WG_THREADS), p->hub_lds_wg, st, s, a, g,
+                         d_desc, d_gl, (int64_t)nspill, d_cmx, d_sk, d_ss, d_pk, d_ps, d_pc, d_tau, p->Lp, d_ovf,
+                         d_ovf_cnt);
       HIP_OK(hipGetLastError());
     }
     uint32_t novf = 0;
     HIP_OK(hipMemcpyAsync(&novf, d_ovf_cnt, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    const int32_t* didx = nullptr;
+    size_t nfinal = nd;
     if (novf) {
-      // sources with an overflowing bucket skip the final merge and take the HBM-table path:
-      // give them an empty descriptor range (logP stays, but their final is not launched)
+      // sources with an overflowing bucket skip the final merge and take the HBM-table path
       std::vector<int32_t> ov(novf);
       HIP_OK(hipMemcpyAsync(ov.data(), d_ovf, 4 * (size_t)novf, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
-      std::vector<char> bad(desc.size(), 0);
+      std::vector<char> bad(nd, 0);
       for (int32_t x : ov) bad[-x - 1] = 1;
-      std::vector<HubDesc> keep;
-      for (size_t k = 0; k < desc.size(); k++) {
+      std::vector<int32_t> keep;
+      for (size_t k = 0; k < nd; k++) {
         if (bad[k]) fallback.push_back(desc[k].v);
-        else keep.push_back(desc[k]);
+        else keep.push_back((int32_t)k);
       }
-      desc.swap(keep);
-      if (!desc.empty())
-        HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * desc.size(), hipMemcpyHostToDevice, st));
+      nfinal = keep.size();
+      if (nfinal) HIP_OK(hipMemcpyAsync(d_idx, keep.data(), 4 * nfinal, hipMemcpyHostToDevice, st));
+      didx = d_idx;
     }
-    if (!desc.empty()) {
-      hipLaunchKernelGGL(k_hub_final, dim3((unsigned)desc.size()), dim3(WG_THREADS), p->hub_lds_final, st, s, a,
-                         d_desc, d_bk, d_pk, d_ps, p->Lp, maxdiff, p->d_stats);
+    if (nfinal) {
+      hipLaunchKernelGGL(k_hub_final, dim3((unsigned)nfinal), dim3(WG_THREADS), p->hub_lds_final, st, s, a,
+                         d_desc, didx, d_pc, d_pk, d_ps, p->Lp, maxdiff, p->d_stats);
       HIP_OK(hipGetLastError());
     }
     p->merge_launches += 7;

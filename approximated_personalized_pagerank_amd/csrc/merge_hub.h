@@ -8,16 +8,24 @@ namespace pprk {
 // ---------------------------------------------------------------------------------------------
 // Hub pipeline (sources beyond the workgroup tier). A source's candidate stream (successor order)
 // is split by key into P = 2^logP buckets with a STABLE partition, so each key's contributions
-// keep their successor order inside its bucket; every bucket is then accumulated by the
-// workgroup kernel (one key set per bucket, disjoint across buckets) and the per-bucket top-L
-// lists are merged by one workgroup per source.
-//   k_hub_count    wave per tile (64 successors): per-bucket counts -> cm[b][t]
-//   k_hub_scan     block per source: exclusive scan of cm in (b, t) order -> scatter offsets
+// keep their successor order inside its bucket; every bucket is then accumulated on its own (one
+// key set per bucket, disjoint across buckets) and the bucket results that can still be in the
+// top-L are appended to one list per source, merged by one workgroup per source.
+//   k_hub_count    wave per tile (64 successors): per-bucket counts -> cm[b][t], and the pruning
+//                  bound tau (below)
+//   (device scan)  exclusive scan of every source's cm in (b, t) order, sources concatenated ->
+//                  absolute staging offsets (hipcub, host side)
 //   k_hub_scatter  wave per tile: ballot ranks inside a group + running per-bucket counters
 //   k_hub_bucket_w wave per bucket, private LDS table, no barriers: a hot key's long fma chain
 //                  occupies one wave while the CU's other waves keep working
 //   k_hub_bucket   workgroup per bucket whose distinct keys overflow the wave table
-//   k_hub_final    workgroup per source: top-L of the bucket lists, row, norm1
+//   k_hub_final    workgroup per source: top-L of the appended bucket results, row, norm1
+// Pruning bound: every contribution is >= 0, so a key's final value is at least any single
+// contribution, fma(s, f, acc) >= round(s * f) (monotone rounding). A successor u with a full
+// sorted row (len = L) thus puts L distinct keys at >= round(min(row u) * f), and
+//     tau = round(f * max_{u: len[u] = L} min(row u))
+// is a lower bound of the L-th largest final value: a bucket never needs to emit a key below tau
+// (ties at tau are kept, the (score desc, id asc) order decides them in k_hub_final).
 constexpr int HUB_TILE = 64;          // successors per tile (one wave)
 constexpr int HUB_BUCKET = 768;       // default target candidates per bucket (PPR_HUB_BUCKET)
 constexpr int HUB_MAX_LOGP = 12;      // per-wave LDS counters of the partition: 16 KB
@@ -31,11 +39,21 @@ struct HubDesc {
   int32_t logP;
   int32_t T;       // tiles
   int32_t need;    // candidates + 1
-  int64_t cm_off;  // count matrix (P*T ints)
+  int64_t cm_off;  // count matrix (P*T ints; after the scan: absolute staging offsets)
   int64_t st_off;  // staging (need-1 keys / scores)
-  int64_t pt_off;  // bucket top-L lists (P*L)
-  int64_t bk_off;  // bucket starts [P+1] then list lengths [P]
+  int64_t pt_off;  // appended bucket results (<= P*L entries, pt_cnt[desc] of them used)
+  int64_t pad;
 };
+
+// staging range of bucket x of source d (cm holds the scanned, absolute offsets)
+__device__ __forceinline__ void hub_bucket_range(const HubDesc& d, const int32_t* cm, int x,
+                                                 int64_t& start, int64_t& nb) {
+  const int P = 1 << d.logP;
+  if (d.T == 0) { start = d.st_off; nb = 0; return; }  // no successors (init of a dangling node)
+  start = cm[d.cm_off + (int64_t)x * d.T];
+  const int64_t end = (x + 1 < P) ? (int64_t)cm[d.cm_off + (int64_t)(x + 1) * d.T] : d.st_off + d.need - 1;
+  nb = end - start;
+}
 struct HubTask { int32_t d; int32_t x; };   // (descriptor, tile or bucket)
 
 __device__ __forceinline__ uint32_t hub_digit(int key, int logP) {
@@ -89,7 +107,8 @@ __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& 
 
 __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterArgs a,
                                                    const HubDesc* desc, const HubTask* tasks,
-                                                   int64_t ntasks, int maxP, int32_t* cm) {
+                                                   int64_t ntasks, int maxP, int32_t* cm,
+                                                   unsigned long long* tau) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
@@ -97,6 +116,22 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
   const HubTask tk = tasks[w];
   const HubDesc d = desc[tk.d];
   const int P = 1 << d.logP;
+  if (!a.unit) {  // max over this tile's full-row successors of their row minimum (unscaled)
+    const int64_t e = g.rp[d.v + 1];
+    const int64_t i = g.rp[d.v] + (int64_t)tk.x * HUB_TILE + lane_id();
+    unsigned long long mb = 0;
+    if (i < e) {
+      const int32_t cx = g.colx[i];
+      const int u = cx & 0x7fffffff;
+      const int sl = read_slot(a, cx);
+      // the last entry is the row minimum only for sorted rows: MC random-walk baskets (colx
+      // bit 31 in MC mode) are stored unsorted and are skipped
+      if (!(a.mc && cx < 0) && s.len[s.lrow(sl, u)] == s.L) mb = dbits(s.sc[s.row(sl, u) + s.L - 1]);
+    }
+#pragma unroll
+    for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
+    if (lane_id() == 0 && mb) atomicMax(&tau[tk.d], mb);
+  }
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * maxP;
   for (int i = lane_id(); i < P; i += WAVE) hist[i] = 0;
   wave_fence();
@@ -105,33 +140,6 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
   });
   wave_fence();
   for (int i = lane_id(); i < P; i += WAVE) cm[d.cm_off + (int64_t)i * d.T + tk.x] = (int32_t)hist[i];
-}
-
-__global__ void __launch_bounds__(1024) k_hub_scan(const HubDesc* desc, int32_t* cm, int32_t* bk) {
-  __shared__ int wsum[16];
-  __shared__ int carry;
-  const HubDesc d = desc[blockIdx.x];
-  const int P = 1 << d.logP;
-  const int64_t n = (int64_t)P * d.T;
-  int32_t* c = cm + d.cm_off;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int64_t base = 0; base < n; base += 1024) {
-    const int64_t i = base + threadIdx.x;
-    const int x = i < n ? c[i] : 0;
-    const int incl = wave_incl_scan(x);
-    if (lane_id() == WAVE - 1) wsum[threadIdx.x >> 6] = incl;
-    __syncthreads();
-    int add = carry;
-    for (int k = 0; k < (int)(threadIdx.x >> 6); k++) add += wsum[k];
-    if (i < n) c[i] = add + incl - x;   // exclusive
-    __syncthreads();
-    if (threadIdx.x == 1023) carry = add + incl;
-    __syncthreads();
-  }
-  int32_t* b = bk + d.bk_off;
-  for (int i = threadIdx.x; i < P; i += 1024) b[i] = d.T ? c[(int64_t)i * d.T] : 0;
-  if (threadIdx.x == 0) b[P] = carry;
 }
 
 __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, IterArgs a,
@@ -162,7 +170,7 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
     wave_fence();
     if (valid) {
       if (rank == 0) run[dg] = base + (uint32_t)__popcll(match);
-      const int64_t pos = d.st_off + cm[d.cm_off + (int64_t)dg * d.T + tk.x] + base + rank;
+      const int64_t pos = (int64_t)cm[d.cm_off + (int64_t)dg * d.T + tk.x] + base + rank;
       st_key[pos] = key;
       st_sc[pos] = sv;
     }
@@ -172,11 +180,11 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
 
 __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, DevGraph g,
                                                       const HubDesc* desc, const HubTask* tasks,
-                                                      int64_t ntasks, const int32_t* bk_all,
+                                                      int64_t ntasks, const int32_t* cm,
                                                       const int32_t* st_key, const double* st_sc,
-                                                      int32_t* pt_key, double* pt_sc,
-                                                      int32_t* bk_len_all, int Lp, HubTask* spill,
-                                                      uint32_t* spill_cnt, int T) {
+                                                      int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
+                                                      const unsigned long long* tau_b, int Lp,
+                                                      HubTask* spill, uint32_t* spill_cnt, int T) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
@@ -192,12 +200,12 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, Dev
   const HubTask tk = tasks[w];
   const HubDesc d = desc[tk.d];
   const int v = d.v;
-  const int P = 1 << d.logP;
-  const int32_t* bk = bk_all + d.bk_off;
-  const int64_t sb = d.st_off + bk[tk.x];
-  const int nb = bk[tk.x + 1] - bk[tk.x];
+  int64_t sb, nb64;
+  hub_bucket_range(d, cm, tk.x, sb, nb64);
+  const int nb = (int)nb64;
   const int64_t deg = g.rp[v + 1] - g.rp[v];
   const double factor = merge_factor(a, deg);
+  const double tau = tau_b[tk.d] ? bitsd(tau_b[tk.d]) * factor : 0.0;  // no bound: keep all (deg 0: factor inf)
   const int Lw = s.L;
   const int budget = T / 4 * 3;
   table_clear(t);
@@ -247,10 +255,30 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, Dev
     if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = tk; }
     return;
   }
-  const int U = table_compact(t);
-  int32_t* ok = pt_key + d.pt_off + (int64_t)tk.x * Lw;
-  double* os = pt_sc + d.pt_off + (int64_t)tk.x * Lw;
-  int cnt = U;
+  int U = table_compact(t);
+  // keep what can still reach the top-L: value >= tau (in place, order irrelevant)
+  {
+    int U2 = 0;
+    for (int i0 = 0; i0 < U; i0 += WAVE) {
+      const int i = i0 + l;
+      const int k = i < U ? t.keys[i] : 0;
+      const double x = i < U ? t.acc[i] : 0.0;
+      const bool keep = i < U && x >= tau;
+      const uint64_t m = __ballot(keep);
+      wave_fence();
+      if (keep) { const int pos = U2 + __popcll(m & lanemask_lt()); t.keys[pos] = k; t.acc[pos] = x; }
+      U2 += __popcll(m);
+      wave_fence();
+    }
+    U = U2;
+  }
+  const int cnt = U <= Lw ? U : Lw;
+  if (cnt == 0) return;
+  int at = 0;
+  if (l == 0) at = (int)atomicAdd(&pt_cnt[tk.d], (uint32_t)cnt);
+  at = __shfl(at, 0);
+  int32_t* ok = pt_key + d.pt_off + at;
+  double* os = pt_sc + d.pt_off + at;
   if (U <= Lw) {
     for (int i = l; i < U; i += WAVE) { ok[i] = t.keys[i]; os[i] = t.acc[i]; }
   } else {
@@ -266,18 +294,16 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, Dev
       if (sel) { const int pos = pos0 + __popcll(m & lanemask_lt()); ok[pos] = keys[i]; os[pos] = acc[i]; }
       pos0 += __popcll(m);
     }
-    cnt = Lw;
   }
-  if (l == 0) bk_len_all[d.bk_off + P + 1 + tk.x] = cnt;
 }
 
 __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a,
                                                            const DevGraph g, const HubDesc* desc,
                                                            const HubTask* tasks, int64_t ntasks,
-                                                           const int32_t* bk_all,
+                                                           const int32_t* cm,
                                                            const int32_t* st_key, const double* st_sc,
-                                                           int32_t* pt_key, double* pt_sc,
-                                                           int32_t* bk_len_all, int Lp,
+                                                           int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
+                                                           const unsigned long long* tau_b, int Lp,
                                                            int32_t* ovf_list, uint32_t* ovf_cnt) {
   extern __shared__ __align__(16) unsigned char smem[];
   if ((int64_t)blockIdx.x >= ntasks) return;
@@ -287,9 +313,8 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a
   const int wv = threadIdx.x >> 6;
   const int l = lane_id();
   const int v = d.v;
-  const int P = 1 << d.logP;
-  const int32_t* bk = bk_all + d.bk_off;
-  const int64_t sb = d.st_off + bk[tk.x], nb = bk[tk.x + 1] - bk[tk.x];
+  int64_t sb, nb;
+  hub_bucket_range(d, cm, tk.x, sb, nb);
   const bool seed = (int)hub_digit(v, d.logP) == tk.x;
   const int64_t deg = g.rp[v + 1] - g.rp[v];
   const double factor = merge_factor(a, deg);
@@ -327,38 +352,47 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a
       return;
     }
   }
-  if (wv == 0) {
+  if (wv == 0) {  // append the bucket's top-L entries >= tau
+    const double tau = tau_b[tk.d] ? bitsd(tau_b[tk.d]) * factor : 0.0;  // no bound: keep all (deg 0: factor inf)
     const int n = L.misc[M_PLEN];
-    int32_t* ok = pt_key + d.pt_off + (int64_t)tk.x * Lw;
-    double* os = pt_sc + d.pt_off + (int64_t)tk.x * Lw;
-    for (int i = l; i < n; i += WAVE) { ok[i] = L.pk[i]; os[i] = L.pv[i]; }
-    if (l == 0) bk_len_all[d.bk_off + P + 1 + tk.x] = n;
+    int cnt = 0;
+    for (int i = l; i < n; i += WAVE) cnt += L.pv[i] >= tau;
+    cnt = wave_sum(cnt);
+    if (cnt == 0) return;
+    int at = 0;
+    if (l == 0) at = (int)atomicAdd(&pt_cnt[tk.d], (uint32_t)cnt);
+    at = __shfl(at, 0);
+    int pos0 = 0;
+    for (int i0 = 0; i0 < n; i0 += WAVE) {
+      const int i = i0 + l;
+      const bool keep = i < n && L.pv[i] >= tau;
+      const uint64_t m = __ballot(keep);
+      if (keep) {
+        const int64_t q = d.pt_off + at + pos0 + __popcll(m & lanemask_lt());
+        pt_key[q] = L.pk[i];
+        pt_sc[q] = L.pv[i];
+      }
+      pos0 += __popcll(m);
+    }
   }
 }
 
 __global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a, const HubDesc* desc,
-                                                          const int32_t* bk_all, const int32_t* pt_key,
-                                                          const double* pt_sc, int Lp,
+                                                          const int32_t* didx, const uint32_t* pt_cnt,
+                                                          const int32_t* pt_key, const double* pt_sc, int Lp,
                                                           unsigned long long* maxdiff,
                                                           unsigned long long* stats) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const HubDesc d = desc[blockIdx.x];
+  const int di = didx ? didx[blockIdx.x] : (int)blockIdx.x;
+  const HubDesc d = desc[di];
   const WgLds L = wg_carve(smem, 0, Lp, 0);
-  const int P = 1 << d.logP;
   const int Lw = s.L;
-  const int32_t* blen = bk_all + d.bk_off + P + 1;
   const int32_t* pk = pt_key + d.pt_off;
   const double* pv = pt_sc + d.pt_off;
-  const int n = P * Lw;  // flattened (bucket, slot) index; slot < blen[bucket] is valid
-  auto occ = [&](int i) { return (i % Lw) < blen[i / Lw]; };
-  int total = 0;
-  for (int b = threadIdx.x; b < P; b += WG_THREADS) total += blen[b];
-  total = wave_sum(total);
-  if (lane_id() == 0) L.misc[16 + (threadIdx.x >> 6)] = total;
+  const int n = (int)pt_cnt[di];  // appended bucket results, any order
+  auto occ = [&](int) { return true; };
+  const int total = n;
   if (threadIdx.x == 0) L.misc[M_PLEN] = 0;
-  __syncthreads();
-  total = 0;
-  for (int i = 0; i < WG_WAVES; i++) total += L.misc[16 + i];
   __syncthreads();
   if (total <= Lw) {
     for (int i = threadIdx.x; i < n; i += WG_THREADS)

@@ -121,6 +121,82 @@ def cpu_baseline(g, part, slab, L, damping, iters, threads, budget, seed=0):
     }
 
 
+def main_mc(args):
+    """MCCompletePathV2 on RMAT (configs[4]): one step = walks of the whole walk set + the
+    level-synchronous combine + top-K, graph and plan resident. N > 1: each rank walks a contiguous
+    range of the walk set (walk-count shard, no exchange) and the value counts the walks of all
+    ranks; the combine needs every walk basket and runs on one GPU (N = 1 only)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    K = args.K if args.K != 64 else 50
+    L = args.L if args.L != 128 else 200
+    import approximated_personalized_pagerank_amd as ppr
+    from approximated_personalized_pagerank_amd import build as _build
+    if rank == 0:
+        _build.build()
+    t = time.time()
+    g = ppr.rmat(args.scale, seed=args.seed)
+    plan = ppr.MccpPlan(g, K, L, args.damping, device=local)
+    log(f"[rank {rank}] RMAT-{args.scale}: n={g.n} m={g.m} walk set={plan.walk_nodes} levels={plan.levels} "
+        f"dangling={plan.dangling} prep {time.time() - t:.1f}s")
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        w = plan.walk_nodes
+        b, e = w * rank // world, w * (rank + 1) // world
+        for _ in range(args.warmup):
+            plan.walk(args.walks, 1, b, e)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            plan.walk(args.walks, 1 + s, b, e)  # synchronous (event sync)
+        elapsed = time.perf_counter() - t0
+        tt = [0.0] * world
+        dist.all_gather_object(tt, elapsed)
+        dist.barrier()
+        if rank != 0:
+            return
+        elapsed = max(tt)
+        nw = int(args.walks * args.damping)
+        value = w * nw * args.steps / elapsed
+        line = {
+            "metric": "random walks/sec mccompletepathv2 walk phase on RMAT-22 (walk-count shard)",
+            "value": value, "unit": "walks/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic RMAT (Graph500 a=.57 b=.19 c=.19, edge factor 16, seed %d, dedup)" % args.seed,
+            "config": {"workload": f"mccompletepathv2 walks RMAT-{args.scale} L={L} R={args.walks} d={args.damping}",
+                       "walk_nodes": w, "parallelism": f"walk-shard x{world}"},
+        }
+        print(json.dumps(line), flush=True)
+        return
+    for _ in range(args.warmup):
+        plan.run(args.walks, 1)
+    walk_ms = comb_ms = 0.0
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        st = plan.run(args.walks, 1 + s)
+        walk_ms += st.walk_ms
+        comb_ms += st.combine_ms
+    elapsed = time.perf_counter() - t0
+    steps = args.steps
+    line = {
+        "metric": "source-nodes/sec mccompletepathv2 K=50 L=200 R=1000 on RMAT-22",
+        "value": g.n * steps / elapsed, "unit": "source-nodes/s", "n_gpus": 1, "steps": steps,
+        "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / steps, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic RMAT (Graph500 a=.57 b=.19 c=.19, edge factor 16, seed %d, dedup)" % args.seed,
+        "config": {"workload": f"mccompletepathv2 RMAT-{args.scale} K={K} L={L} R={args.walks} d={args.damping}",
+                   "nodes": g.n, "edges": g.m, "walk_nodes": st.walk_nodes, "walks_per_step": st.walks,
+                   "levels": st.levels, "parallelism": "1 GPU"},
+        "phases": {"walk_ms_per_step": walk_ms / steps, "combine_ms_per_step": comb_ms / steps,
+                   "walks_per_sec": st.walks * steps / (walk_ms / 1e3) if walk_ms > 0 else 0.0,
+                   "merge_launches_per_step": st.merge_launches},
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -136,7 +212,12 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-budget", type=float, default=1.5e9, help="sampled candidates for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["grank", "mc"], default="grank",
+                    help="mc: MCCompletePathV2 (configs[4]) with --K 50 --L 200 --walks 1000 defaults")
+    ap.add_argument("--walks", type=int, default=1000, help="mc: random walks per node (R)")
     args = ap.parse_args()
+    if args.workload == "mc":
+        return main_mc(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
