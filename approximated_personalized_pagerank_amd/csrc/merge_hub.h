@@ -124,9 +124,7 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
       const int32_t cx = g.colx[i];
       const int u = cx & 0x7fffffff;
       const int sl = read_slot(a, cx);
-      // the last entry is the row minimum only for sorted rows: MC random-walk baskets (colx
-      // bit 31 in MC mode) are stored unsorted and are skipped
-      if (!(a.mc && cx < 0) && s.len[s.lrow(sl, u)] == s.L) mb = dbits(s.sc[s.row(sl, u) + s.L - 1]);
+      if (s.len[s.lrow(sl, u)] == s.L) mb = dbits(s.sc[s.row(sl, u) + s.L - 1]);  // row minimum
     }
 #pragma unroll
     for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }

@@ -209,8 +209,11 @@ __global__ void __launch_bounds__(64) k_mc_walk(DevGraph g, DevSlab s, McArgs m,
     cslot = mc_apply(t, stepping, key, L, size, frozen, held);
   }
 
-  // basket: held keys, count / R (include/mccompletepathv2.h:159-160)
+  // basket: held keys, count / R (include/mccompletepathv2.h:159-160), compacted in place to the
+  // front of the table and sorted (score desc, id asc) like every other basket row, so its last
+  // entry is its minimum (the hub pipeline's pruning bound reads it)
   const double R = (double)m.R;
+  uint64_t* rv = reinterpret_cast<uint64_t*>(t.cnt);
   int U = 0;
   for (int base = 0; base < m.T; base += WAVE) {
     const int i = base + l;
@@ -218,13 +221,18 @@ __global__ void __launch_bounds__(64) k_mc_walk(DevGraph g, DevSlab s, McArgs m,
     const unsigned long long c = t.cnt[i];
     const bool occ = k != EMPTY && c != MC_REJ;
     const uint64_t mb = __ballot(occ);
+    wave_fence();
     if (occ) {
       const int pos = U + __popcll(mb & lanemask_lt());
-      s.ids[rs + pos] = k;
-      s.sc[rs + pos] = (double)c / R;
+      t.keys[pos] = k;
+      rv[pos] = dbits((double)c / R);
     }
     U += __popcll(mb);
+    wave_fence();
   }
+  const int Lp = L <= 1 ? 1 : (1 << (32 - __clz(L - 1)));
+  row_sort(rv, t.keys, U, Lp);
+  for (int i = l; i < U; i += WAVE) { s.ids[rs + i] = t.keys[i]; s.sc[rs + i] = bitsd(rv[i]); }
   if (l == 0) s.len[s.lrow(m.slot, src)] = U;
 }
 
