@@ -146,7 +146,9 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
                                                      int32_t* st_key, double* st_sc) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
-  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
+  // consecutive tiles of a source append to the same bucket runs: keep them on one XCD so the
+  // partial staging lines merge in its L2 instead of being written back piecemeal
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x) * WAVES_PER_BLOCK + wv;
   if (w >= ntasks) return;
   const HubTask tk = tasks[w];
   const HubDesc d = desc[tk.d];

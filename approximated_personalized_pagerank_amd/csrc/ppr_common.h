@@ -32,6 +32,14 @@ struct GlbWork {
   int64_t T;     // table slots (power of two)
 };
 
+// XCD-aware block remap (cdna_hip_programming.md T1): blocks with the same blockIdx % 8 share
+// an XCD (and its L2); give each such group a contiguous range of logical blocks, so neighbouring
+// work (adjacent tiles, adjacent output lines) lands in one L2. Bijective for any grid size.
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+  const int64_t q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 struct DevGraph {
   const int64_t* rp;
   const int32_t* colx;
