@@ -254,7 +254,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
   DevGraph g{p->d_rp, p->d_colx, p->n};
   DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
   const int64_t L = p->L;
-  const int64_t budget = 1LL << 28;  // staged candidates per batch (3 GiB of keys + scores)
+  const int64_t budget = 1LL << 28;  // staged candidates per batch (4 GiB of 16-B records)
   size_t i0 = 0;
   while (i0 < big.size()) {
     std::vector<HubDesc> desc;
@@ -295,8 +295,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     const size_t o_cm = off;   off = al(off + 4 * (size_t)cm);
     const size_t o_cmx = off;  off = al(off + 4 * (size_t)cm);
     const size_t o_tmp = off;  off = al(off + scan_tmp);
-    const size_t o_sk = off;   off = al(off + 4 * (size_t)stg);
-    const size_t o_ss = off;   off = al(off + 8 * (size_t)stg);
+    const size_t o_st = off;   off = al(off + sizeof(HubRec) * (size_t)stg);
     const size_t o_pk = off;   off = al(off + 4 * (size_t)pt);
     const size_t o_ps = off;   off = al(off + 8 * (size_t)pt);
     const size_t o_pc = off;   off = al(off + 4 * nd);
@@ -314,8 +313,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     int32_t* d_cm = (int32_t*)(base + o_cm);
     int32_t* d_cmx = (int32_t*)(base + o_cmx);
     void* d_tmp = (void*)(base + o_tmp);
-    int32_t* d_sk = (int32_t*)(base + o_sk);
-    double* d_ss = (double*)(base + o_ss);
+    HubRec* d_st = (HubRec*)(base + o_st);
     int32_t* d_pk = (int32_t*)(base + o_pk);
     double* d_ps = (double*)(base + o_ps);
     uint32_t* d_pc = (uint32_t*)(base + o_pc);
@@ -340,7 +338,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     HIP_OK(hipGetLastError());
     HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, scan_tmp, d_cm, d_cmx, (int)cm, st));
     hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
-                       d_cmx, d_sk, d_ss);
+                       d_cmx, d_st);
     HIP_OK(hipGetLastError());
     const int64_t nbuck = (int64_t)buckets.size();
     // every bucket goes to a single wave first: a bucket made long by one hot key (a core node
@@ -348,14 +346,14 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
     uint32_t nspill = 0;
     hipLaunchKernelGGL(k_hub_bucket_w, dim3((unsigned)((nbuck + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)), dim3(256),
-                       p->hub_lds_wave, st, s, a, g, d_desc, d_buck, nbuck, d_cmx, d_sk, d_ss, d_pk, d_ps, d_pc,
+                       p->hub_lds_wave, st, s, a, g, d_desc, d_buck, nbuck, d_cmx, d_st, d_pk, d_ps, d_pc,
                        d_tau, p->Lp, d_gl, d_lc + 1, p->hub_wave_t);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(&nspill, d_lc + 1, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (nspill) {
       hipLaunchKernelGGL(k_hub_bucket, dim3(nspill), dim3(WG_THREADS), p->hub_lds_wg, st, s, a, g,
-                         d_desc, d_gl, (int64_t)nspill, d_cmx, d_sk, d_ss, d_pk, d_ps, d_pc, d_tau, p->Lp, d_ovf,
+                         d_desc, d_gl, (int64_t)nspill, d_cmx, d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_ovf,
                          d_ovf_cnt);
       HIP_OK(hipGetLastError());
     }

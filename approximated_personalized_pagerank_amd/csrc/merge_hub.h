@@ -56,6 +56,14 @@ __device__ __forceinline__ void hub_bucket_range(const HubDesc& d, const int32_t
 }
 struct HubTask { int32_t d; int32_t x; };   // (descriptor, tile or bucket)
 
+// one staged candidate: key and score in one 16-B record, so a scattered store touches one
+// partial line instead of two (separate key / score arrays)
+struct alignas(16) HubRec {
+  int32_t key;
+  int32_t pad;
+  double sc;
+};
+
 __device__ __forceinline__ uint32_t hub_digit(int key, int logP) {
   return logP == 0 ? 0u : (hash_b((uint32_t)key) >> (32 - logP));
 }
@@ -143,7 +151,7 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
 __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, IterArgs a,
                                                      const HubDesc* desc, const HubTask* tasks,
                                                      int64_t ntasks, int maxP, const int32_t* cm,
-                                                     int32_t* st_key, double* st_sc) {
+                                                     HubRec* st) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   // consecutive tiles of a source append to the same bucket runs: keep them on one XCD so the
@@ -171,8 +179,7 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
     if (valid) {
       if (rank == 0) run[dg] = base + (uint32_t)__popcll(match);
       const int64_t pos = (int64_t)cm[d.cm_off + (int64_t)dg * d.T + tk.x] + base + rank;
-      st_key[pos] = key;
-      st_sc[pos] = sv;
+      st[pos] = HubRec{key, 0, sv};
     }
     wave_fence();
   });
@@ -181,7 +188,7 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
 __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, DevGraph g,
                                                       const HubDesc* desc, const HubTask* tasks,
                                                       int64_t ntasks, const int32_t* cm,
-                                                      const int32_t* st_key, const double* st_sc,
+                                                      const HubRec* st,
                                                       int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
                                                       const unsigned long long* tau_b, int Lp,
                                                       HubTask* spill, uint32_t* spill_cnt, int T) {
@@ -217,8 +224,9 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, Dev
   wave_fence();
   const int l = lane_id();
   bool nv = l < nb;
-  int nk = nv ? st_key[sb + l] : 0;
-  double ns = nv ? st_sc[sb + l] : 0.0;
+  HubRec nr = nv ? st[sb + l] : HubRec{0, 0, 0.0};
+  int nk = nr.key;
+  double ns = nr.sc;
   bool overflow = false;
   for (int g0 = 0; g0 < nb; g0 += WAVE) {
     const bool cv = nv;
@@ -227,8 +235,9 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, Dev
     if (g0 + WAVE < nb) {
       const int q = g0 + WAVE + l;
       nv = q < nb;
-      nk = nv ? st_key[sb + q] : 0;
-      ns = nv ? st_sc[sb + q] : 0.0;
+      const HubRec r = nv ? st[sb + q] : HubRec{0, 0, 0.0};
+      nk = r.key;
+      ns = r.sc;
     }
     if (fill + WAVE > budget) { overflow = true; break; }  // uniform
     uint32_t slot = 0;
@@ -301,7 +310,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a
                                                            const DevGraph g, const HubDesc* desc,
                                                            const HubTask* tasks, int64_t ntasks,
                                                            const int32_t* cm,
-                                                           const int32_t* st_key, const double* st_sc,
+                                                           const HubRec* st,
                                                            int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
                                                            const unsigned long long* tau_b, int Lp,
                                                            int32_t* ovf_list, uint32_t* ovf_cnt) {
@@ -323,8 +332,9 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a
   auto each = [&](auto&& fn) {
     auto ld = [&](int64_t q, bool& vv, int& kk, double& ss) {
       vv = q < nb;
-      kk = vv ? st_key[sb + q] : 0;
-      ss = vv ? st_sc[sb + q] : 0.0;
+      const HubRec r = vv ? st[sb + q] : HubRec{0, 0, 0.0};
+      kk = r.key;
+      ss = r.sc;
     };
     bool nv0, nv1;
     int nk0, nk1;
