@@ -114,6 +114,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   TRY(dalloc(&p->d_out_ids, (size_t)n * K));
   TRY(dalloc(&p->d_out_sc, (size_t)n * K));
   TRY(dalloc(&p->d_out_len, n));
+  if (getenv("PPR_DIAG")) {
+    TRY(dalloc(&p->d_diag, 160));
+    if (hipMemset(p->d_diag, 0, 160 * 8) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
+  }
   hipStream_t st = p->stream;
   if (n) {
     if (hipMemcpyAsync(p->d_rp, row_ptr, 8 * (n + 1), hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -145,8 +149,17 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_wave_t = e2 ? pow2_at_least(std::max(256, atoi(e2))) : HUB_WAVE_T;
     p->hub_wave_t = std::min(p->hub_wave_t, 8192);
   }
-  p->hub_lds_wave = hub_wave_lds(p->hub_wave_t) * WAVES_PER_BLOCK;
-  hipFuncSetAttribute((const void*)k_hub_bucket_w, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  {
+    const char* e3 = getenv("PPR_BW_MODE");
+    const char* e4 = getenv("PPR_BW_NG");
+    const char* e5 = getenv("PPR_BW_WAVES");
+    p->hub_bw_mode = e3 ? atoi(e3) : 1;
+    p->hub_bw_ng = (e4 && atoi(e4) == 8) ? 8 : 4;
+    p->hub_bw_waves = e5 ? std::max(1, std::min(4, atoi(e5))) : 1;
+  }
+  p->hub_lds_wave = hub_wave_lds(p->hub_wave_t, p->hub_bw_mode, p->hub_bw_ng) * p->hub_bw_waves;
+  hipFuncSetAttribute((const void*)k_hub_bucket_w<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_bucket_w<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_count, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -220,6 +233,7 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   a.damping = p->damping;
   a.mc = 0u;
   a.rp = p->d_rp;
+  a.diag = p->d_diag;
   a.unit = unit ? 1u : 0u;
   a.stats = (p->flags & PPR_FLAG_STATS) ? 1u : 0u;
   if (unit) { a.sA = 0; a.sB = 0; a.active = -1; return a; }
@@ -345,9 +359,16 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     // present in most successor baskets) still has few distinct keys, and its sequential fma
     // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
     uint32_t nspill = 0;
-    hipLaunchKernelGGL(k_hub_bucket_w, dim3((unsigned)((nbuck + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)), dim3(256),
-                       p->hub_lds_wave, st, s, a, g, d_desc, d_buck, nbuck, d_cmx, d_st, d_pk, d_ps, d_pc,
-                       d_tau, p->Lp, d_gl, d_lc + 1, p->hub_wave_t);
+    {
+      const int wpb = p->hub_bw_waves;
+      const dim3 grid((unsigned)((nbuck + wpb - 1) / wpb)), blk(64 * wpb);
+      if (p->hub_bw_ng == 8)
+        hipLaunchKernelGGL(k_hub_bucket_w<8>, grid, blk, p->hub_lds_wave, st, s, a, g, d_desc, d_buck, nbuck, d_cmx,
+                           d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_mode);
+      else
+        hipLaunchKernelGGL(k_hub_bucket_w<4>, grid, blk, p->hub_lds_wave, st, s, a, g, d_desc, d_buck, nbuck, d_cmx,
+                           d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_mode);
+    }
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(&nspill, d_lc + 1, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));

@@ -27,12 +27,19 @@ namespace pprk {
 // is a lower bound of the L-th largest final value: a bucket never needs to emit a key below tau
 // (ties at tau are kept, the (score desc, id asc) order decides them in k_hub_final).
 constexpr int HUB_TILE = 64;          // successors per tile (one wave)
-constexpr int HUB_BUCKET = 768;       // default target candidates per bucket (PPR_HUB_BUCKET)
+constexpr int HUB_BUCKET = 384;       // default target candidates per bucket (PPR_HUB_BUCKET)
 constexpr int HUB_MAX_LOGP = 12;      // per-wave LDS counters of the partition: 16 KB
-constexpr int HUB_WAVE_T = 1024;      // default wave bucket table slots, 12 B each (PPR_HUB_WAVE_T)
+constexpr int HUB_WAVE_T = 512;       // default wave bucket table slots (PPR_HUB_WAVE_T): 13 KB of LDS per wave
+constexpr int HUB_BW_BATCH = 8;       // staged groups a bucket wave keeps in flight
+constexpr int HUB_TW_BATCH = 4;       // candidate groups a tile wave gathers before using them
 
-// wave bucket LDS: table + radix histogram only (12 waves per CU at T = 1024)
-__host__ __device__ constexpr size_t hub_wave_lds(int T) { return (size_t)T * 12 + 1024; }
+
+// wave bucket LDS: acc f64[T] | keys i32[T] | cnt u16[T] | (mode 1: vals f64[CHUNK] |
+// touched u16[CHUNK] | tof u16[CHUNK + 2]); the radix histogram of the final select (1 KB)
+// follows cnt (aliasing vals in mode 1)
+__host__ __device__ constexpr size_t hub_wave_lds(int T, int mode, int ng) {
+  return (size_t)T * 14 + (mode == 1 ? (size_t)(ng * WAVE) * 12 + 4 : (size_t)1024);
+}
 
 struct HubDesc {
   int32_t v;
@@ -88,28 +95,39 @@ __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& 
   }
   const int incl = wave_incl_scan(ln);
   const int total = __shfl(incl, WAVE - 1);
-  for (int g0 = 0; g0 < total; g0 += WAVE) {
-    const int c = g0 + lane_id();
-    const bool valid = c < total;
-    int j = 0;
+  // HUB_TW_BATCH groups of 64 candidates are gathered before any is handed to f (one memory
+  // latency per batch); f still sees them in stream order
+  for (int g0 = 0; g0 < total; g0 += WAVE * HUB_TW_BATCH) {
+    int key[HUB_TW_BATCH];
+    double sv[HUB_TW_BATCH];
 #pragma unroll
-    for (int step = 32; step; step >>= 1) {
-      const int pv = __shfl(incl, j + step - 1);
-      if (pv <= c) j += step;
+    for (int k = 0; k < HUB_TW_BATCH; k++) {
+      const int c = g0 + k * WAVE + lane_id();
+      const bool valid = c < total;
+      int j = 0;
+#pragma unroll
+      for (int step = 32; step; step >>= 1) {
+        const int pv = __shfl(incl, j + step - 1);
+        if (pv <= c) j += step;
+      }
+      const int jj = j < WAVE ? j : WAVE - 1;
+      const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
+      const int ex = jj > 0 ? exv : 0;
+      const int uj = __shfl(u, jj);
+      const int sj = __shfl(sl, jj);
+      key[k] = 0;
+      sv[k] = 0.0;
+      if (valid) {
+        const int64_t r = s.row(sj, uj) + (c - ex);
+        key[k] = s.ids[r];
+        sv[k] = s.sc[r];
+      }
     }
-    const int jj = j < WAVE ? j : WAVE - 1;
-    const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
-    const int ex = jj > 0 ? exv : 0;
-    const int uj = __shfl(u, jj);
-    const int sj = __shfl(sl, jj);
-    int key = 0;
-    double sv = 0.0;
-    if (valid) {
-      const int64_t r = s.row(sj, uj) + (c - ex);
-      key = s.ids[r];
-      sv = s.sc[r];
+#pragma unroll
+    for (int k = 0; k < HUB_TW_BATCH; k++) {
+      if (g0 + k * WAVE >= total) break;  // uniform
+      f(g0 + k * WAVE + lane_id() < total, key[k], sv[k]);
     }
-    f(valid, key, sv);
   }
 }
 
@@ -185,25 +203,33 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   });
 }
 
+template <int NG>
 __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, DevGraph g,
                                                       const HubDesc* desc, const HubTask* tasks,
                                                       int64_t ntasks, const int32_t* cm,
                                                       const HubRec* st,
                                                       int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
                                                       const unsigned long long* tau_b, int Lp,
-                                                      HubTask* spill, uint32_t* spill_cnt, int T) {
+                                                      HubTask* spill, uint32_t* spill_cnt, int T,
+                                                      int mode) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
-  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (w >= ntasks) return;
-  unsigned char* base = smem + (size_t)wv * hub_wave_lds(T);
+  unsigned char* base = smem + (size_t)wv * hub_wave_lds(T, mode, NG);
   LdsTable t;
   t.acc = reinterpret_cast<double*>(base);
   t.keys = reinterpret_cast<int*>(base + (size_t)T * 8);
   t.mask = (uint32_t)T - 1;
   t.nbits = 31 - __clz(T);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 12);
+  ChunkLds ck;
+  ck.cnt = reinterpret_cast<uint16_t*>(base + (size_t)T * 12);
+  ck.vals = reinterpret_cast<double*>(base + (size_t)T * 14);
+  ck.touched = reinterpret_cast<uint16_t*>(base + (size_t)T * 14 + (size_t)(NG * WAVE) * 8);
+  ck.tof = ck.touched + NG * WAVE;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(ck.vals);  // final select only (after accumulation)
   (void)Lp;
+  const long long t_start = a.diag ? (long long)clock64() : 0;
   const HubTask tk = tasks[w];
   const HubDesc d = desc[tk.d];
   const int v = d.v;
@@ -215,7 +241,8 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, Dev
   const double tau = tau_b[tk.d] ? bitsd(tau_b[tk.d]) * factor : 0.0;  // no bound: keep all (deg 0: factor inf)
   const int Lw = s.L;
   const int budget = T / 4 * 3;
-  table_clear(t);
+  for (int i = lane_id(); i < T; i += WAVE) { t.keys[i] = EMPTY; ck.cnt[i] = 0; }
+  wave_fence();
   int fill = 0;
   if ((int)hub_digit(v, d.logP) == tk.x) {
     if (lane_id() == 0) { const uint32_t sl = table_slot(t, v); t.acc[sl] = self_seed(a, deg); }
@@ -223,46 +250,64 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, Dev
   }
   wave_fence();
   const int l = lane_id();
-  bool nv = l < nb;
-  HubRec nr = nv ? st[sb + l] : HubRec{0, 0, 0.0};
-  int nk = nr.key;
-  double ns = nr.sc;
   bool overflow = false;
-  for (int g0 = 0; g0 < nb; g0 += WAVE) {
-    const bool cv = nv;
-    const int ck = nk;
-    const double cs = ns;
-    if (g0 + WAVE < nb) {
-      const int q = g0 + WAVE + l;
-      nv = q < nb;
-      const HubRec r = nv ? st[sb + q] : HubRec{0, 0, 0.0};
-      nk = r.key;
-      ns = r.sc;
+  // chunks of HUB_BW_BATCH groups: all records of a chunk are loaded at once (one memory
+  // latency per chunk), their keys inserted group by group, then accumulated per key
+  // (chunk_accumulate) in stream order
+  for (int g0 = 0; g0 < nb; g0 += NG * WAVE) {
+    bool cv[NG];
+    uint32_t sl[NG];
+    double cs[NG];
+    int kk[NG];
+#pragma unroll
+    for (int k = 0; k < NG; k++) {
+      const int q = g0 + k * WAVE + l;
+      cv[k] = q < nb;
+      const HubRec r = cv[k] ? st[sb + q] : HubRec{0, 0, 0.0};
+      kk[k] = r.key;
+      cs[k] = r.sc;
     }
-    if (fill + WAVE > budget) { overflow = true; break; }  // uniform
-    uint32_t slot = 0;
-    bool ins = false;
-    if (cv) {
-      uint32_t h = hash32((uint32_t)ck) & t.mask;
-      for (;;) {
-        const int cur = t.keys[h];
-        if (cur == ck) break;
-        if (cur == EMPTY) {
-          const int prev = atomicCAS(&t.keys[h], EMPTY, ck);
-          if (prev == EMPTY) { t.acc[h] = 0.0; ins = true; break; }
-          if (prev == ck) break;
+#pragma unroll
+    for (int k = 0; k < NG; k++) {
+      if (fill + WAVE > budget) overflow = true;  // uniform: a group may bring 64 new keys
+      bool ins = false;
+      uint32_t h = 0;
+      if (cv[k] && !overflow) {
+        h = hash32((uint32_t)kk[k]) & t.mask;
+        for (;;) {
+          const int cur = t.keys[h];
+          if (cur == kk[k]) break;
+          if (cur == EMPTY) {
+            const int prev = atomicCAS(&t.keys[h], EMPTY, kk[k]);
+            if (prev == EMPTY) { t.acc[h] = 0.0; ins = true; break; }
+            if (prev == kk[k]) break;
+          }
+          h = (h + 1) & t.mask;
         }
-        h = (h + 1) & t.mask;
       }
-      slot = h;
+      sl[k] = h;
+      fill += __popcll(__ballot(ins));
+      wave_fence();
     }
-    fill += __popcll(__ballot(ins));
-    wave_fence();
-    apply_group(t.acc, cv, slot, cs, factor, t.nbits);
+    if (overflow) break;
+    if (mode == 1) {
+      chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NG; k++) {
+        if (g0 + k * WAVE >= nb) break;  // uniform
+        apply_group(t.acc, cv[k], sl[k], cs[k], factor, t.nbits);
+      }
+    }
   }
   if (overflow) {
     if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = tk; }
     return;
+  }
+  if (a.diag && l == 0) {  // bucket length histogram: count and cycles per log2(length) bin
+    const int bin = 31 - __clz(nb | 1);
+    atomicAdd(&a.diag[bin], 1ull);
+    atomicAdd(&a.diag[32 + bin], (unsigned long long)((long long)clock64() - t_start));
   }
   int U = table_compact(t);
   // keep what can still reach the top-L: value >= tau (in place, order irrelevant)
@@ -278,6 +323,10 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, Dev
       if (keep) { const int pos = U2 + __popcll(m & lanemask_lt()); t.keys[pos] = k; t.acc[pos] = x; }
       U2 += __popcll(m);
       wave_fence();
+    }
+    if (a.diag && l == 0) {  // distinct keys / kept keys per bucket
+      atomicAdd(&a.diag[64 + (31 - __clz(U | 1))], 1ull);
+      atomicAdd(&a.diag[96 + (31 - __clz(U2 | 1))], 1ull);
     }
     U = U2;
   }

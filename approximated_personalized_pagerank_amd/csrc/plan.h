@@ -71,6 +71,9 @@ struct ppr_plan {
   std::vector<int64_t> h_rp;       // host row pointers (hub planning)
   size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0, hub_lds_wave = 0;
   int hub_bucket = 512, hub_wave_t = 1024;
+  int hub_bw_mode = 1;             // PPR_BW_MODE: 0 apply_group per group, 1 chunk_accumulate
+  int hub_bw_ng = 4;               // PPR_BW_NG: groups per chunk (4 or 8)
+  int hub_bw_waves = 1;            // PPR_BW_WAVES: waves per block of k_hub_bucket_w
   // source sharding (ppr_grank_plan_comm_init / ppr_grank_plan_run_sharded)
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -81,6 +84,7 @@ struct ppr_plan {
   int64_t merge_launches = 0;
   double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_m0 = nullptr, ev_m1 = nullptr;
+  unsigned long long* d_diag = nullptr;  // PPR_DIAG=1: kernel histograms, printed at destroy
   // MCCompletePathV2 (mccp2.hip)
   bool mc = false;
   int32_t* d_mc_walk = nullptr;       // walk set W (nodes read before their final basket exists)
@@ -108,6 +112,17 @@ inline void plan_free(ppr_plan* p) {
   if (p->ev_m1) hipEventDestroy(p->ev_m1);
   if (p->comm) ncclCommDestroy(p->comm);
   hipFree(p->d_xsend); hipFree(p->d_xrecv);
+  if (p->d_diag) {
+    unsigned long long h[160];
+    if (hipMemcpy(h, p->d_diag, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+      fprintf(stderr, "ppr_diag bucket_w: log2(x) | buckets by len, Mcycles | by distinct keys | by kept keys\n");
+      for (int b = 0; b < 32; b++)
+        if (h[b] || h[64 + b] || h[96 + b] || h[128 + b])
+          fprintf(stderr, "ppr_diag %2d %12llu %12.1f | %12llu | %12llu | chain %12llu\n", b, h[b], h[32 + b] / 1e6,
+                  h[64 + b], h[96 + b], h[128 + b]);
+    }
+    hipFree(p->d_diag);
+  }
   hipFree(p->d_mc_walk); hipFree(p->d_mc_levels); hipFree(p->d_mc_dangling);
   if (p->own_stream && p->stream) hipStreamDestroy(p->stream);
   delete p;

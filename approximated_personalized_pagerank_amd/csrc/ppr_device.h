@@ -145,6 +145,91 @@ __device__ __forceinline__ void table_apply(const LdsTable& t, bool valid, int k
   apply_group(t.acc, valid, slot, s, factor, t.nbits);
 }
 
+// Grouped accumulation of one chunk of up to NG * 64 ordered records (record q = lane q % 64 of
+// group q / 64), an alternative to apply_group for streams with many repeated keys:
+//   A  per group, in order: find-or-insert every key (`slotfn`), rank the lanes sharing a slot
+//      (ballots over the slot bits), and give each record its occurrence index within the
+//      chunk for its slot; slots first seen in the chunk go to a `touched` list;
+//   B  exclusive scan of the per-slot counts over the touched list -> per-slot offsets;
+//   C  every record's value goes to vals[offset(slot) + occurrence];
+//   D  one lane per touched slot runs that slot's fma chain over vals in stream order.
+// A key's contributions therefore still meet acc in stream order (bit-exact with apply_group),
+// but a hot key costs one dependent fma per occurrence instead of a cross-lane round per
+// occurrence. cnt must be all-zero on entry and is left all-zero.
+struct ChunkLds {
+  uint16_t* cnt;      // [T] per-slot occurrences in the chunk, then offsets
+  double* vals;       // [NG * 64]
+  uint16_t* touched;  // [NG * 64]
+  uint16_t* tof;      // [NG * 64 + 1]
+};
+
+template <int NG>
+__device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c, int nbits,
+                                                 const bool (&valid)[NG], const uint32_t (&slot)[NG],
+                                                 const double (&val)[NG], double factor) {
+  const uint64_t lt = lanemask_lt();
+  uint32_t occ[NG];
+  int nt = 0;
+#pragma unroll
+  for (int k = 0; k < NG; k++) {
+    uint64_t mm = __ballot(valid[k]);
+    for (int b = 0; b < nbits; b++) {
+      const bool bit = (slot[k] >> b) & 1u;
+      const uint64_t bb = __ballot(valid[k] && bit);
+      mm &= bit ? bb : ~bb;
+    }
+    if (!valid[k]) mm = 0;
+    const bool leader = valid[k] && (mm & lt) == 0;
+    uint32_t base = 0;
+    if (leader) {
+      base = c.cnt[slot[k]];
+      c.cnt[slot[k]] = (uint16_t)(base + __popcll(mm));
+    }
+    const bool fresh = leader && base == 0;
+    const uint64_t fm = __ballot(fresh);
+    if (fresh) c.touched[nt + __popcll(fm & lt)] = (uint16_t)slot[k];
+    nt += __popcll(fm);
+    const int lead = mm ? (__ffsll((long long)mm) - 1) : lane_id();
+    base = (uint32_t)__shfl((int)base, lead);
+    occ[k] = base + (uint32_t)__popcll(mm & lt);
+    wave_fence();
+  }
+  // B: offsets of the touched slots (touched order), written over their counts
+  int run = 0;
+  for (int i0 = 0; i0 < nt; i0 += WAVE) {
+    const int i = i0 + lane_id();
+    const int n = i < nt ? c.cnt[c.touched[i]] : 0;
+    const int incl = wave_incl_scan(n);
+    if (i < nt) { c.tof[i] = (uint16_t)(run + incl - n); c.cnt[c.touched[i]] = (uint16_t)(run + incl - n); }
+    run += __shfl(incl, WAVE - 1);
+  }
+  if (lane_id() == 0) c.tof[nt] = (uint16_t)run;
+  wave_fence();
+  // C: values grouped by slot, stream order inside a slot
+#pragma unroll
+  for (int k = 0; k < NG; k++)
+    if (valid[k]) c.vals[c.cnt[slot[k]] + occ[k]] = val[k];
+  wave_fence();
+  // D: one lane per touched slot
+  for (int i = lane_id(); i < nt; i += WAVE) {
+    const uint32_t sl = c.touched[i];
+    const int b = c.tof[i], e = c.tof[i + 1];
+    double x = acc[sl];
+    int j = b;
+    for (; j + 4 <= e; j += 4) {
+      const double v0 = c.vals[j], v1 = c.vals[j + 1], v2 = c.vals[j + 2], v3 = c.vals[j + 3];
+      x = fma(v0, factor, x);
+      x = fma(v1, factor, x);
+      x = fma(v2, factor, x);
+      x = fma(v3, factor, x);
+    }
+    for (; j < e; j++) x = fma(c.vals[j], factor, x);
+    acc[sl] = x;
+    c.cnt[sl] = 0;
+  }
+  wave_fence();
+}
+
 // In-place compaction of occupied slots to the front (keys[0..U), acc[0..U)); returns U.
 __device__ __forceinline__ int table_compact(const LdsTable& t) {
   int U = 0;

@@ -35,6 +35,45 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+PROFILES = os.path.join(ROOT, "profiles")
+
+
+def pmc_traffic(tag):
+    """HBM bytes per step of the merge phase from the committed rocprofv3 PMC summary of this
+    workload (tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, separate passes), or None."""
+    import glob
+    hits = sorted(glob.glob(os.path.join(PROFILES, f"*_{tag}_pmc.json")))
+    if not hits:
+        return None, None
+    with open(hits[-1]) as f:
+        d = json.load(f)
+    return d.get("merge_phase_traffic_bytes"), os.path.relpath(hits[-1], ROOT)
+
+
+def mc_cpu_baseline(scale, K, L, walks, damping, seed):
+    """The reference's own mccompletepathv2 (single-threaded by design, include/mccompletepathv2.h)
+    compiled from /root/reference (oracle/_ref/ref_driver), timed on a bounded RMAT sample."""
+    drv = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+    if not os.path.exists(drv):
+        return None
+    import approximated_personalized_pagerank_amd as ppr
+    g = ppr.rmat(scale, seed=seed)
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "g.bin")
+        with open(path, "wb") as f:
+            np.array([g.n, g.m], dtype=np.int64).tofile(f)
+            np.arange(g.n, dtype=np.int32).tofile(f)
+            g.row_ptr.astype(np.int64).tofile(f)
+            g.col.astype(np.int32).tofile(f)
+        t0 = time.time()
+        subprocess.run([drv, "mc", path, os.path.join(td, "o.bin"), str(K), str(L), str(walks), repr(damping),
+                        "-1", "1"], check=True, capture_output=True)
+        wall = time.time() - t0
+    return {"value": g.n / wall, "unit": "source-nodes/s", "cores": 1, "kind": "reference",
+            "sample": (f"reference ppr::mccompletepathv2 (include/mccompletepathv2.h, -O3 -march=x86-64-v3, "
+                       f"sequential by design) whole job on RMAT-{scale} ({g.n} nodes, {g.m} edges, same K/L/R/d), "
+                       f"{wall:.1f} s incl. graph load; its per-node cost grows with scale (1.5x per 2 scales "
+                       f"measured at RMAT-14..18), so this overstates the RMAT-22 rate")}
 
 
 def log(*a):
@@ -181,6 +220,13 @@ def main_mc(args):
         comb_ms += st.combine_ms
     elapsed = time.perf_counter() - t0
     steps = args.steps
+    cpu = None
+    if not args.no_cpu_baseline:
+        try:
+            plan.close()
+            cpu = mc_cpu_baseline(max(8, args.scale - 8), K, L, args.walks, args.damping, args.seed)
+        except Exception as exc:  # reported, never fatal
+            log(f"mc cpu_baseline failed: {exc!r}")
     line = {
         "metric": "source-nodes/sec mccompletepathv2 K=50 L=200 R=1000 on RMAT-22",
         "value": g.n * steps / elapsed, "unit": "source-nodes/s", "n_gpus": 1, "steps": steps,
@@ -193,6 +239,7 @@ def main_mc(args):
         "phases": {"walk_ms_per_step": walk_ms / steps, "combine_ms_per_step": comb_ms / steps,
                    "walks_per_sec": st.walks * steps / (walk_ms / 1e3) if walk_ms > 0 else 0.0,
                    "merge_launches_per_step": st.merge_launches},
+        "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
 
@@ -272,6 +319,9 @@ def main():
     steps = args.steps
     value = g.n * steps / elapsed
     achieved = stats["algo_bytes"] / 1e9 / (stats["merge_ms"] / 1e3) if stats["merge_ms"] > 0 else 0.0
+    traffic, traffic_src = (None, None)
+    if (args.scale, args.K, args.L, args.iters) == (22, 64, 128, 30):
+        traffic, traffic_src = pmc_traffic(f"grank_rmat22_k64_l128")
     line = {
         "metric": "source-nodes/sec grank K=64 L=128 on RMAT-22; 1/2/4/8 MI355X + HBM GB/s",
         "value": value,
@@ -289,13 +339,15 @@ def main():
                                f"damping={args.damping} tol={args.tol}",
                    "nodes": g.n, "edges": g.m, "iterations_run": stats["iterations"],
                    "parallelism": f"source-shard x{world}" if world > 1 else "1 GPU"},
-        "roofline": {"bound": "hbm", "kernel": "merge phase (k_classify + k_merge_lds + k_merge_glb)",
+        "roofline": {"bound": "hbm",
+                     "kernel": ("basket-merge phase: k_classify + k_merge_lds (wave tiers) + hub pipeline "
+                                "(k_hub_count, device scan, k_hub_scatter, k_hub_bucket_w, k_hub_final)"),
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "algo_bytes_per_step": stats["algo_bytes"] / steps,
                      "merge_ms_per_step": stats["merge_ms"] / steps,
                      "merge_launches_per_step": stats["launches"] / steps,
-                     "traffic": None},
+                     "traffic": traffic, "traffic_source": traffic_src},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
