@@ -95,6 +95,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   std::vector<int32_t> all(n > 0 ? n : 1);
   for (int64_t v = 0; v < n; v++) all[v] = (int32_t)v;
   p->h_rp.assign(row_ptr, row_ptr + n + 1);
+  for (int64_t v = 0; v < n; v++) p->max_deg = std::max<int64_t>(p->max_deg, row_ptr[v + 1] - row_ptr[v]);
 
   const size_t slab = (size_t)2 * n * L;
   TRY(dalloc(&p->d_rp, n + 1));
@@ -106,7 +107,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   TRY(dalloc(&p->d_all, n));
   TRY(dalloc(&p->d_cand, n));
   TRY(dalloc(&p->d_tier_lists, (size_t)NLISTS * (n > 0 ? n : 1)));
-  TRY(dalloc(&p->d_tier_cnt, NLISTS + 1));
+  TRY(dalloc(&p->d_tier_cnt, NLISTS + 2));
+  TRY(dalloc(&p->d_big, n));
   TRY(dalloc(&p->d_tier_cap, NT + 1));
   TRY(dalloc(&p->d_ovf, n));
   TRY(dalloc(&p->d_maxdiff, PPR_MAX_ITER_STATS + 1));
@@ -156,6 +158,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_bw_mode = e3 ? atoi(e3) : 1;
     p->hub_bw_ng = (e4 && atoi(e4) == 8) ? 8 : 4;
     p->hub_bw_waves = e5 ? std::max(1, std::min(4, atoi(e5))) : 1;
+    const char* e6 = getenv("PPR_HUB_SLICE");
+    p->hub_slice = std::max<int>(std::max<int>(64, (int)L), e6 ? atoi(e6) : HUB_SLICE);
   }
   p->hub_lds_wave = hub_wave_lds(p->hub_wave_t, p->hub_bw_mode, p->hub_bw_ng) * p->hub_bw_waves;
   hipFuncSetAttribute((const void*)k_hub_bucket_w<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -257,6 +261,8 @@ static int ensure_scratch(ppr_plan* p, size_t need) {
   return PPR_OK;
 }
 
+static int ensure_dev(unsigned char** ptr, size_t* cap, size_t need);
+
 static int ceil_log2(int64_t x) { int k = 0; while ((1LL << k) < x) k++; return k; }
 
 // Hub pipeline over `big` (sources beyond the workgroup tier). Sources whose buckets overflow
@@ -288,7 +294,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
       const int idx = (int)desc.size();
       // staging offsets are cumulative candidate counts in descriptor order, the same order the
       // device scan walks the concatenated count matrices in: scanned cm = absolute offsets
-      desc.push_back(HubDesc{v, logP, T, (int32_t)need, cm, stg, pt, 0});
+      desc.push_back(HubDesc{v, logP, T, (int32_t)need, cm, stg, pt, 0});  // red: set after the buckets
       for (int t = 0; t < T; t++) tiles.push_back(HubTask{idx, t});
       for (int b = 0; b < P; b++) buckets.push_back(HubTask{idx, b});
       cm += (int64_t)P * T;
@@ -337,6 +343,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     uint32_t* d_ovf_cnt = (uint32_t*)(d_ovf + buckets.size());
     HubTask* d_gl = (HubTask*)(base + o_gl);
     uint32_t* d_lc = (uint32_t*)(base + o_cnt);  // [0] unused, [1] workgroup list
+    int32_t* d_rk = nullptr;                       // sliced reductions of long appended lists
+    double* d_rs = nullptr;
     HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * nd, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_tile, tiles.data(), sizeof(HubTask) * tiles.size(), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(d_buck, buckets.data(), sizeof(HubTask) * buckets.size(), hipMemcpyHostToDevice, st));
@@ -381,6 +389,40 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     uint32_t novf = 0;
     HIP_OK(hipMemcpyAsync(&novf, d_ovf_cnt, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    // cut long appended lists (k_hub_reduce) so no k_hub_final workgroup selects from more than
+    // a few slices' worth of entries
+    std::vector<uint32_t> pcnt(nd);
+    HIP_OK(hipMemcpyAsync(pcnt.data(), d_pc, 4 * nd, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    {
+      std::vector<HubTask> rt;
+      int64_t roff = 0;
+      for (size_t k = 0; k < nd; k++) {
+        if (pcnt[k] <= (uint32_t)(2 * p->hub_slice)) { desc[k].red = 0; continue; }
+        const int ns = (int)((pcnt[k] + p->hub_slice - 1) / p->hub_slice);
+        desc[k].red = 1 + roff;
+        roff += (int64_t)ns * L;
+        for (int x = 0; x < ns; x++) rt.push_back(HubTask{(int32_t)k, x});
+      }
+      if (!rt.empty()) {
+        // separate buffer: the staging in d_scratch is still live
+        size_t ro = 0;
+        const size_t o_rt = ro;  ro = al(ro + sizeof(HubTask) * rt.size());
+        const size_t o_rk = ro;  ro = al(ro + 4 * (size_t)roff);
+        const size_t o_rs = ro;  ro = al(ro + 8 * (size_t)roff);
+        rc = ensure_dev(&p->d_red, &p->red_bytes, ro);
+        if (rc) return rc;
+        HubTask* d_rt = (HubTask*)(p->d_red + o_rt);
+        d_rk = (int32_t*)(p->d_red + o_rk);
+        d_rs = (double*)(p->d_red + o_rs);
+        HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * nd, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(d_rt, rt.data(), sizeof(HubTask) * rt.size(), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_hub_reduce, dim3((unsigned)rt.size()), dim3(WG_THREADS), p->hub_lds_final, st, s, d_desc,
+                           d_rt, d_pc, d_pk, d_ps, d_rk, d_rs, p->Lp, p->hub_slice);
+        HIP_OK(hipGetLastError());
+        p->merge_launches++;
+      }
+    }
     const int32_t* didx = nullptr;
     size_t nfinal = nd;
     if (novf) {
@@ -401,7 +443,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     }
     if (nfinal) {
       hipLaunchKernelGGL(k_hub_final, dim3((unsigned)nfinal), dim3(WG_THREADS), p->hub_lds_final, st, s, a,
-                         d_desc, didx, d_pc, d_pk, d_ps, p->Lp, maxdiff, p->d_stats);
+                         d_desc, didx, d_pc, d_pk, d_ps, d_rk, d_rs, p->hub_slice, p->Lp, maxdiff,
+                         p->d_stats);
       HIP_OK(hipGetLastError());
     }
     p->merge_launches += 7;
@@ -432,10 +475,15 @@ static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, i
   hipStream_t st = p->stream;
   DevGraph g{p->d_rp, p->d_colx, p->n};
   DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
-  HIP_OK(hipMemsetAsync(p->d_tier_cnt, 0, sizeof(uint32_t) * (NLISTS + 1), st));
+  HIP_OK(hipMemsetAsync(p->d_tier_cnt, 0, sizeof(uint32_t) * (NLISTS + 2), st));
   const int64_t nb = (count + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(256), 0, st, g, s, a, list, count,
-                     p->d_tier_cap, p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats);
+                     p->d_tier_cap, p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big);
+  HIP_OK(hipGetLastError());
+  if (!a.unit && p->max_deg > CLS_BIG_DEG) {
+    hipLaunchKernelGGL(k_classify_big, dim3(256), dim3(CLS_BIG_THREADS), 0, st, g, s, a, p->d_tier_cap,
+                       p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big);
+  }
   HIP_OK(hipGetLastError());
   uint32_t cnt[NLISTS + 1];
   HIP_OK(hipMemcpyAsync(cnt, p->d_tier_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));

@@ -32,6 +32,7 @@ constexpr int HUB_MAX_LOGP = 12;      // per-wave LDS counters of the partition:
 constexpr int HUB_WAVE_T = 512;       // default wave bucket table slots (PPR_HUB_WAVE_T): 13 KB of LDS per wave
 constexpr int HUB_BW_BATCH = 8;       // staged groups a bucket wave keeps in flight
 constexpr int HUB_TW_BATCH = 4;       // candidate groups a tile wave gathers before using them
+constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per reducing workgroup (PPR_HUB_SLICE)
 
 
 // wave bucket LDS: acc f64[T] | keys i32[T] | cnt u16[T] | (mode 1: vals f64[CHUNK] |
@@ -49,7 +50,7 @@ struct HubDesc {
   int64_t cm_off;  // count matrix (P*T ints; after the scan: absolute staging offsets)
   int64_t st_off;  // staging (need-1 keys / scores)
   int64_t pt_off;  // appended bucket results (<= P*L entries, pt_cnt[desc] of them used)
-  int64_t pad;
+  int64_t red;     // 0, or 1 + offset of the sliced reduction of the appended list (k_hub_reduce)
 };
 
 // staging range of bucket x of source d (cm holds the scanned, absolute offsets)
@@ -436,9 +437,47 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a
   }
 }
 
+// Long appended lists (a hub with thousands of buckets) are cut before k_hub_final: one
+// workgroup per HUB_SLICE entries keeps the slice's top-L (the top-L of a union lies in the union
+// of its parts' top-Ls); every full slice then contributes exactly L entries at red + slice * L.
+__global__ void __launch_bounds__(WG_THREADS) k_hub_reduce(DevSlab s, const HubDesc* desc, const HubTask* tasks,
+                                                           const uint32_t* pt_cnt, const int32_t* pt_key,
+                                                           const double* pt_sc, int32_t* red_key, double* red_sc,
+                                                           int Lp, int slice) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const HubTask tk = tasks[blockIdx.x];
+  const HubDesc d = desc[tk.d];
+  const WgLds L = wg_carve(smem, 0, Lp, 0);
+  const int Lw = s.L;
+  const int n_all = (int)pt_cnt[tk.d];
+  const int b = tk.x * slice;
+  const int n = min(slice, n_all - b);
+  const int32_t* pk = pt_key + d.pt_off + b;
+  const double* pv = pt_sc + d.pt_off + b;
+  int32_t* ok = red_key + (d.red - 1) + (int64_t)tk.x * Lw;
+  double* os = red_sc + (d.red - 1) + (int64_t)tk.x * Lw;
+  if (n <= Lw) {
+    for (int i = threadIdx.x; i < n; i += WG_THREADS) { ok[i] = pk[i]; os[i] = pv[i]; }
+    return;
+  }
+  if (threadIdx.x == 0) L.misc[M_PLEN] = 0;
+  __syncthreads();
+  const SelCrit c = wg_select_top(L, n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; },
+                                  [&](int) { return true; });
+  for (int i = threadIdx.x; i < n; i += WG_THREADS) {
+    if (sel_test(c, dbits(pv[i]), (uint32_t)~pk[i])) {
+      const int pos = atomicAdd(&L.misc[M_PLEN], 1);
+      ok[pos] = pk[i];
+      os[pos] = pv[i];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a, const HubDesc* desc,
                                                           const int32_t* didx, const uint32_t* pt_cnt,
-                                                          const int32_t* pt_key, const double* pt_sc, int Lp,
+                                                          const int32_t* pt_key, const double* pt_sc,
+                                                          const int32_t* red_key, const double* red_sc, int slice,
+                                                          int Lp,
                                                           unsigned long long* maxdiff,
                                                           unsigned long long* stats) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -446,9 +485,15 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a,
   const HubDesc d = desc[di];
   const WgLds L = wg_carve(smem, 0, Lp, 0);
   const int Lw = s.L;
+  int n = (int)pt_cnt[di];  // appended bucket results, any order
   const int32_t* pk = pt_key + d.pt_off;
   const double* pv = pt_sc + d.pt_off;
-  const int n = (int)pt_cnt[di];  // appended bucket results, any order
+  if (d.red) {  // the list was cut to the top-L of every HUB_SLICE entries by k_hub_reduce
+    const int ns = (n + slice - 1) / slice, last = n - (ns - 1) * slice;
+    n = (ns - 1) * Lw + (last < Lw ? last : Lw);
+    pk = red_key + (d.red - 1);
+    pv = red_sc + (d.red - 1);
+  }
   auto occ = [&](int) { return true; };
   const int total = n;
   if (threadIdx.x == 0) L.misc[M_PLEN] = 0;

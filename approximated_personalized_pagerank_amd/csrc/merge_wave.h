@@ -15,12 +15,15 @@ namespace pprk {
 
 constexpr int CLS_PER_WAVE = 16;
 constexpr int CLS_PER_BLOCK = CLS_PER_WAVE * WAVES_PER_BLOCK;
+constexpr int CLS_BIG_DEG = 2048;     // sources with more successors are summed by k_classify_big
+constexpr int CLS_BIG_THREADS = 1024;
 
 __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArgs a,
                                                   const int32_t* list, int64_t count,
                                                   const int32_t* tier_cap, int32_t* tier_lists,
                                                   uint32_t* tier_cnt, int64_t list_cap,
-                                                  int32_t* cand, unsigned long long* stats) {
+                                                  int32_t* cand, unsigned long long* stats,
+                                                  int32_t* big_list) {
   __shared__ int s_tier[CLS_PER_BLOCK];
   __shared__ int s_src[CLS_PER_BLOCK];
   __shared__ uint32_t s_base[NLISTS];
@@ -33,6 +36,14 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
     if (idx >= count) { if (lane_id() == 0) s_tier[slot] = -1; continue; }
     const int v = list[idx];
     const int64_t b = g.rp[v], e = g.rp[v + 1];
+    if (!a.unit && e - b > CLS_BIG_DEG) {
+      // a long successor list would serialise this wave's 16 sources: hand it to k_classify_big
+      if (lane_id() == 0) {
+        s_tier[slot] = -1;
+        big_list[atomicAdd(&tier_cnt[NLISTS + 1], 1u)] = v;
+      }
+      continue;
+    }
     long long c = 0;
     if (a.unit) {
       c = e - b;
@@ -77,6 +88,45 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
     for (int i = 0; i < WAVES_PER_BLOCK; i++) { sc += s_red[0][i]; sb += s_red[1][i]; }
     if (sc) atomicAdd(&stats[0], sc);
     if (sb) atomicAdd(&stats[1], sb);
+  }
+}
+
+// k_classify's long-list sources: one block per source (grid-stride over the list), the
+// successor sum split over the block; same tier rule and statistics as k_classify
+__global__ void __launch_bounds__(CLS_BIG_THREADS) k_classify_big(DevGraph g, DevSlab s, IterArgs a,
+                                                                  const int32_t* tier_cap, int32_t* tier_lists,
+                                                                  uint32_t* tier_cnt, int64_t list_cap,
+                                                                  int32_t* cand, unsigned long long* stats,
+                                                                  const int32_t* big_list) {
+  __shared__ long long red[CLS_BIG_THREADS / WAVE];
+  const uint32_t nbig = __hip_atomic_load(&tier_cnt[NLISTS + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
+    const int v = big_list[i];
+    const int64_t b = g.rp[v], e = g.rp[v + 1];
+    long long c = 0;
+    for (int64_t k = b + threadIdx.x; k < e; k += CLS_BIG_THREADS) {
+      const int32_t cx = g.colx[k];
+      c += s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)];
+    }
+#pragma unroll
+    for (int o = 32; o; o >>= 1) c += __shfl_xor(c, o);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      c = 0;
+      for (int k = 0; k < CLS_BIG_THREADS / WAVE; k++) c += red[k];
+      const int64_t need = c + 1;
+      cand[v] = (int32_t)(need > 0x7fffffff ? 0x7fffffff : need);
+      int t = 0;
+      while (t < NT + 1 && need > tier_cap[t]) t++;
+      tier_lists[(int64_t)t * list_cap + atomicAdd(&tier_cnt[t], 1u)] = v;
+      if (a.stats) {
+        const int ownlen = a.mc ? 0 : s.len[s.lrow(a.active == 0 ? a.sA : a.sB, v)];
+        atomicAdd(&stats[0], (unsigned long long)c);
+        atomicAdd(&stats[1], (unsigned long long)(8 + 8 * (e - b) + 12 * c + 12 * ownlen));
+      }
+    }
+    __syncthreads();
   }
 }
 

@@ -51,7 +51,11 @@ struct ppr_plan {
   int64_t nact[2] = {0, 0};
   int32_t* d_cand = nullptr;
   int32_t* d_tier_lists = nullptr;   // NLISTS * n
-  uint32_t* d_tier_cnt = nullptr;    // NLISTS (+1: workgroup overflow count)
+  uint32_t* d_tier_cnt = nullptr;    // NLISTS, +1 workgroup overflow count, +1 k_classify_big list length
+  int32_t* d_big = nullptr;          // sources k_classify hands to k_classify_big
+  unsigned char* d_red = nullptr;    // k_hub_reduce output when the hub scratch has no room left
+  size_t red_bytes = 0;
+  int64_t max_deg = 0;
   int32_t* d_tier_cap = nullptr;     // NT + 1
   int32_t* d_ovf = nullptr;          // sources the workgroup tier could not hold
   int tierT[NT] = {0, 0, 0, 0};
@@ -74,6 +78,7 @@ struct ppr_plan {
   int hub_bw_mode = 1;             // PPR_BW_MODE: 0 apply_group per group, 1 chunk_accumulate
   int hub_bw_ng = 4;               // PPR_BW_NG: groups per chunk (4 or 8)
   int hub_bw_waves = 1;            // PPR_BW_WAVES: waves per block of k_hub_bucket_w
+  int hub_slice = 8192;            // PPR_HUB_SLICE: k_hub_reduce slice (>= L)
   // source sharding (ppr_grank_plan_comm_init / ppr_grank_plan_run_sharded)
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -102,7 +107,7 @@ inline void plan_free(ppr_plan* p) {
   if (!p) return;
   hipFree(p->d_rp); hipFree(p->d_colx); hipFree(p->d_part); hipFree(p->d_ids); hipFree(p->d_sc);
   hipFree(p->d_len); hipFree(p->d_all); hipFree(p->d_act[0]); hipFree(p->d_act[1]);
-  hipFree(p->d_cand); hipFree(p->d_tier_lists); hipFree(p->d_tier_cnt); hipFree(p->d_tier_cap);
+  hipFree(p->d_cand); hipFree(p->d_tier_lists); hipFree(p->d_tier_cnt); hipFree(p->d_tier_cap); hipFree(p->d_big); hipFree(p->d_red);
   hipFree(p->d_ovf);
   hipFree(p->d_maxdiff); hipFree(p->d_stats); hipFree(p->d_work); hipFree(p->d_scratch);
   hipFree(p->d_out_ids); hipFree(p->d_out_sc); hipFree(p->d_out_len);

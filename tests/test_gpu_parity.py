@@ -100,6 +100,21 @@ def test_gpu_deterministic_and_multi_equal():
     assert m1 == m2
 
 
+def test_gpu_hub_reduce_and_classify_big_bit_exact(monkeypatch):
+    """long appended hub lists cut by k_hub_reduce (slice forced small) and long successor lists
+    summed by k_classify_big (RMAT-14 hubs exceed 2048 successors) match the oracle"""
+    monkeypatch.setenv("PPR_HUB_SLICE", "64")
+    monkeypatch.setenv("PPR_TIER_MASK", "0x21")
+    g = ppr.rmat(14, seed=5)
+    assert g.degrees().max() > 2048
+    part = g.partitions()
+    r = ppr.grank_csr(g, 8, 32, 3, 0.85, -1.0, part=part, device=0)
+    o = oracle.grank(g.row_ptr, g.col, part, 8, 32, 3, 0.85, -1.0)
+    assert np.array_equal(r.max_diff, o["max_diff"])
+    assert np.array_equal(r.ids, o["ids"])
+    assert np.array_equal(r.scores, o["scores"])
+
+
 @pytest.mark.parametrize("mask", ["0x10", "0x0", "0x11", "0x3", "0x20", "0x21", "0x30"])
 def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
     """every merge path alone (wave tiers 0x1-0x8, workgroup tier 0x10, hub pipeline 0x20, HBM-table
