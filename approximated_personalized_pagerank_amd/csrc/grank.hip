@@ -155,13 +155,20 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     const char* e3 = getenv("PPR_BW_MODE");
     const char* e4 = getenv("PPR_BW_NG");
     const char* e5 = getenv("PPR_BW_WAVES");
-    p->hub_bw_mode = e3 ? atoi(e3) : 1;
+    (void)e3;
     p->hub_bw_ng = (e4 && atoi(e4) == 8) ? 8 : 4;
     p->hub_bw_waves = e5 ? std::max(1, std::min(4, atoi(e5))) : 1;
     const char* e6 = getenv("PPR_HUB_SLICE");
     p->hub_slice = std::max<int>(std::max<int>(64, (int)L), e6 ? atoi(e6) : HUB_SLICE);
   }
-  p->hub_lds_wave = hub_wave_lds(p->hub_wave_t, p->hub_bw_mode, p->hub_bw_ng) * p->hub_bw_waves;
+  p->hub_lds_wave = hub_wave_lds(p->hub_wave_t, p->hub_bw_ng) * p->hub_bw_waves;
+  {
+    hipDeviceProp_t prop;
+    p->num_cus = hipGetDeviceProperties(&prop, p->device) == hipSuccess ? prop.multiProcessorCount : 256;
+    // persistent bucket waves: as many blocks as fit on every CU at once (LDS-bound)
+    const int per_cu = std::max<int>(1, std::min<int>(32 / p->hub_bw_waves, (int)((160 * 1024) / p->hub_lds_wave)));
+    p->hub_bw_blocks = p->num_cus * per_cu;
+  }
   hipFuncSetAttribute((const void*)k_hub_bucket_w<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket_w<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -324,6 +331,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     const size_t o_ovf = off;  off = al(off + 4 * (buckets.size() + 1));
     const size_t o_gl = off;   off = al(off + sizeof(HubTask) * (buckets.size() + 1));
     const size_t o_cnt = off;  off = al(off + 16);
+    const size_t o_bw = off;   off = al(off + sizeof(BucketWork) * buckets.size());
     int rc = ensure_scratch(p, off);
     if (rc) return rc;
     char* base = (char*)p->d_scratch;
@@ -342,7 +350,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     int32_t* d_ovf = (int32_t*)(base + o_ovf);
     uint32_t* d_ovf_cnt = (uint32_t*)(d_ovf + buckets.size());
     HubTask* d_gl = (HubTask*)(base + o_gl);
-    uint32_t* d_lc = (uint32_t*)(base + o_cnt);  // [0] unused, [1] workgroup list
+    uint32_t* d_lc = (uint32_t*)(base + o_cnt);  // [0] bucket-wave work counter, [1] workgroup list
+    BucketWork* d_bw = (BucketWork*)(base + o_bw);
     int32_t* d_rk = nullptr;                       // sliced reductions of long appended lists
     double* d_rs = nullptr;
     HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * nd, hipMemcpyHostToDevice, st));
@@ -367,17 +376,21 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     // present in most successor baskets) still has few distinct keys, and its sequential fma
     // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
     uint32_t nspill = 0;
+    hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, a, d_desc, d_buck, nbuck,
+                       d_cmx, d_tau, d_bw);
+    HIP_OK(hipGetLastError());
     {
       const int wpb = p->hub_bw_waves;
-      const dim3 grid((unsigned)((nbuck + wpb - 1) / wpb)), blk(64 * wpb);
+      const int64_t blocks = (nbuck + wpb - 1) / wpb;
+      const dim3 grid((unsigned)blocks), blk(64 * wpb);
       if (p->hub_bw_ng == 8)
-        hipLaunchKernelGGL(k_hub_bucket_w<8>, grid, blk, p->hub_lds_wave, st, s, a, g, d_desc, d_buck, nbuck, d_cmx,
-                           d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_mode);
+        hipLaunchKernelGGL(k_hub_bucket_w<8>, grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_lc, d_st, d_pk, d_ps,
+                           d_pc, d_gl, d_lc + 1, p->hub_wave_t);
       else
-        hipLaunchKernelGGL(k_hub_bucket_w<4>, grid, blk, p->hub_lds_wave, st, s, a, g, d_desc, d_buck, nbuck, d_cmx,
-                           d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_mode);
+        hipLaunchKernelGGL(k_hub_bucket_w<4>, grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_lc, d_st, d_pk, d_ps,
+                           d_pc, d_gl, d_lc + 1, p->hub_wave_t);
+      HIP_OK(hipGetLastError());
     }
-    HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(&nspill, d_lc + 1, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (nspill) {

@@ -35,11 +35,10 @@ constexpr int HUB_TW_BATCH = 4;       // candidate groups a tile wave gathers be
 constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per reducing workgroup (PPR_HUB_SLICE)
 
 
-// wave bucket LDS: acc f64[T] | keys i32[T] | cnt u16[T] | (mode 1: vals f64[CHUNK] |
-// touched u16[CHUNK] | tof u16[CHUNK + 2]); the radix histogram of the final select (1 KB)
-// follows cnt (aliasing vals in mode 1)
-__host__ __device__ constexpr size_t hub_wave_lds(int T, int mode, int ng) {
-  return (size_t)T * 14 + (mode == 1 ? (size_t)(ng * WAVE) * 12 + 4 : (size_t)1024);
+// wave bucket LDS: acc f64[T] | keys i32[T] | cnt u16[T] | vals f64[CHUNK] | touched u16[CHUNK] |
+// tof u16[CHUNK + 2]; the radix histogram of the final select (1 KB) aliases vals
+__host__ __device__ constexpr size_t hub_wave_lds(int T, int ng) {
+  return (size_t)T * 14 + (size_t)(ng * WAVE) * 12 + 4;
 }
 
 struct HubDesc {
@@ -204,20 +203,51 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   });
 }
 
+// one bucket of the wave kernel, resolved once by k_hub_prep (thread per bucket) so the
+// persistent bucket waves start each bucket with a single 64-B load
+struct BucketWork {
+  int64_t start;    // staging index of the bucket's first record
+  int64_t pt_off;   // the source's appended-results list
+  int32_t nb;       // records
+  int32_t d;        // descriptor
+  int32_t x;        // bucket (digit)
+  int32_t seed;     // the source id when this bucket holds the source's own key, else -1
+  double factor, tau, selfval;
+};
+
+__global__ void __launch_bounds__(256) k_hub_prep(DevGraph g, IterArgs a, const HubDesc* desc,
+                                                  const HubTask* tasks, int64_t ntasks, const int32_t* cm,
+                                                  const unsigned long long* tau_b, BucketWork* bw) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ntasks) return;
+  const HubTask tk = tasks[i];
+  const HubDesc d = desc[tk.d];
+  BucketWork w;
+  int64_t nb;
+  hub_bucket_range(d, cm, tk.x, w.start, nb);
+  w.nb = (int32_t)nb;
+  w.pt_off = d.pt_off;
+  w.d = tk.d;
+  w.x = tk.x;
+  w.seed = (int)hub_digit(d.v, d.logP) == tk.x ? d.v : -1;
+  const int64_t deg = g.rp[d.v + 1] - g.rp[d.v];
+  w.factor = merge_factor(a, deg);
+  w.tau = tau_b[tk.d] ? bitsd(tau_b[tk.d]) * w.factor : 0.0;  // no bound: keep all (deg 0: factor inf)
+  w.selfval = self_seed(a, deg);
+  bw[i] = w;
+}
+
+// Bucket waves: one wave per bucket, its work record resolved by k_hub_prep. Per bucket: private LDS table (T slots, 3/4 usable; a bucket with more distinct
+// keys spills to k_hub_bucket), chunks of NG groups loaded at once and accumulated with
+// chunk_accumulate, then the keys >= tau, at most L of them, appended to the source's list.
 template <int NG>
-__global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, DevGraph g,
-                                                      const HubDesc* desc, const HubTask* tasks,
-                                                      int64_t ntasks, const int32_t* cm,
-                                                      const HubRec* st,
+__global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, const BucketWork* bw,
+                                                      int64_t nbuck, uint32_t* next, const HubRec* st,
                                                       int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
-                                                      const unsigned long long* tau_b, int Lp,
-                                                      HubTask* spill, uint32_t* spill_cnt, int T,
-                                                      int mode) {
+                                                      HubTask* spill, uint32_t* spill_cnt, int T) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
-  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-  if (w >= ntasks) return;
-  unsigned char* base = smem + (size_t)wv * hub_wave_lds(T, mode, NG);
+  unsigned char* base = smem + (size_t)wv * hub_wave_lds(T, NG);
   LdsTable t;
   t.acc = reinterpret_cast<double*>(base);
   t.keys = reinterpret_cast<int*>(base + (size_t)T * 8);
@@ -229,129 +259,118 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, Dev
   ck.touched = reinterpret_cast<uint16_t*>(base + (size_t)T * 14 + (size_t)(NG * WAVE) * 8);
   ck.tof = ck.touched + NG * WAVE;
   uint32_t* hist = reinterpret_cast<uint32_t*>(ck.vals);  // final select only (after accumulation)
-  (void)Lp;
-  const long long t_start = a.diag ? (long long)clock64() : 0;
-  const HubTask tk = tasks[w];
-  const HubDesc d = desc[tk.d];
-  const int v = d.v;
-  int64_t sb, nb64;
-  hub_bucket_range(d, cm, tk.x, sb, nb64);
-  const int nb = (int)nb64;
-  const int64_t deg = g.rp[v + 1] - g.rp[v];
-  const double factor = merge_factor(a, deg);
-  const double tau = tau_b[tk.d] ? bitsd(tau_b[tk.d]) * factor : 0.0;  // no bound: keep all (deg 0: factor inf)
+  const int l = lane_id();
   const int Lw = s.L;
   const int budget = T / 4 * 3;
-  for (int i = lane_id(); i < T; i += WAVE) { t.keys[i] = EMPTY; ck.cnt[i] = 0; }
-  wave_fence();
-  int fill = 0;
-  if ((int)hub_digit(v, d.logP) == tk.x) {
-    if (lane_id() == 0) { const uint32_t sl = table_slot(t, v); t.acc[sl] = self_seed(a, deg); }
-    fill = 1;
-  }
-  wave_fence();
-  const int l = lane_id();
-  bool overflow = false;
-  // chunks of HUB_BW_BATCH groups: all records of a chunk are loaded at once (one memory
-  // latency per chunk), their keys inserted group by group, then accumulated per key
-  // (chunk_accumulate) in stream order
-  for (int g0 = 0; g0 < nb; g0 += NG * WAVE) {
-    bool cv[NG];
-    uint32_t sl[NG];
-    double cs[NG];
-    int kk[NG];
-#pragma unroll
-    for (int k = 0; k < NG; k++) {
-      const int q = g0 + k * WAVE + l;
-      cv[k] = q < nb;
-      const HubRec r = cv[k] ? st[sb + q] : HubRec{0, 0, 0.0};
-      kk[k] = r.key;
-      cs[k] = r.sc;
+  // one bucket per wave (persistent waves with a static stride or a shared work counter measured
+  // slower: the hardware refills CUs better than a fixed grid balances hot buckets)
+  const int64_t cur = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (cur >= nbuck) return;
+  (void)next;
+  const BucketWork W = bw[cur];
+  {
+    const long long t_start = a.diag ? (long long)clock64() : 0;
+    const int nb = W.nb;
+    for (int i = l; i < T; i += WAVE) { t.keys[i] = EMPTY; ck.cnt[i] = 0; }
+    wave_fence();
+    int fill = 0;
+    if (W.seed >= 0) {
+      if (l == 0) { const uint32_t sl = table_slot(t, W.seed); t.acc[sl] = W.selfval; }
+      fill = 1;
     }
-#pragma unroll
-    for (int k = 0; k < NG; k++) {
-      if (fill + WAVE > budget) overflow = true;  // uniform: a group may bring 64 new keys
-      bool ins = false;
-      uint32_t h = 0;
-      if (cv[k] && !overflow) {
-        h = hash32((uint32_t)kk[k]) & t.mask;
-        for (;;) {
-          const int cur = t.keys[h];
-          if (cur == kk[k]) break;
-          if (cur == EMPTY) {
-            const int prev = atomicCAS(&t.keys[h], EMPTY, kk[k]);
-            if (prev == EMPTY) { t.acc[h] = 0.0; ins = true; break; }
-            if (prev == kk[k]) break;
-          }
-          h = (h + 1) & t.mask;
-        }
-      }
-      sl[k] = h;
-      fill += __popcll(__ballot(ins));
-      wave_fence();
-    }
-    if (overflow) break;
-    if (mode == 1) {
-      chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor);
-    } else {
+    wave_fence();
+    bool overflow = false;
+    for (int g0 = 0; g0 < nb; g0 += NG * WAVE) {
+      bool cv[NG];
+      uint32_t sl[NG];
+      double cs[NG];
+      int kk[NG];
 #pragma unroll
       for (int k = 0; k < NG; k++) {
-        if (g0 + k * WAVE >= nb) break;  // uniform
-        apply_group(t.acc, cv[k], sl[k], cs[k], factor, t.nbits);
+        const int q = g0 + k * WAVE + l;
+        cv[k] = q < nb;
+        const HubRec r = cv[k] ? st[W.start + q] : HubRec{0, 0, 0.0};
+        kk[k] = r.key;
+        cs[k] = r.sc;
       }
+#pragma unroll
+      for (int k = 0; k < NG; k++) {
+        if (fill + WAVE > budget) overflow = true;  // uniform: a group may bring 64 new keys
+        bool ins = false;
+        uint32_t h = 0;
+        if (cv[k] && !overflow) {
+          h = hash32((uint32_t)kk[k]) & t.mask;
+          for (;;) {
+            const int c = t.keys[h];
+            if (c == kk[k]) break;
+            if (c == EMPTY) {
+              const int prev = atomicCAS(&t.keys[h], EMPTY, kk[k]);
+              if (prev == EMPTY) { t.acc[h] = 0.0; ins = true; break; }
+              if (prev == kk[k]) break;
+            }
+            h = (h + 1) & t.mask;
+          }
+        }
+        sl[k] = h;
+        fill += __popcll(__ballot(ins));
+        wave_fence();
+      }
+      if (overflow) break;
+      chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, W.factor);
     }
-  }
-  if (overflow) {
-    if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = tk; }
-    return;
-  }
-  if (a.diag && l == 0) {  // bucket length histogram: count and cycles per log2(length) bin
-    const int bin = 31 - __clz(nb | 1);
-    atomicAdd(&a.diag[bin], 1ull);
-    atomicAdd(&a.diag[32 + bin], (unsigned long long)((long long)clock64() - t_start));
-  }
-  int U = table_compact(t);
-  // keep what can still reach the top-L: value >= tau (in place, order irrelevant)
-  {
-    int U2 = 0;
-    for (int i0 = 0; i0 < U; i0 += WAVE) {
-      const int i = i0 + l;
-      const int k = i < U ? t.keys[i] : 0;
-      const double x = i < U ? t.acc[i] : 0.0;
-      const bool keep = i < U && x >= tau;
-      const uint64_t m = __ballot(keep);
-      wave_fence();
-      if (keep) { const int pos = U2 + __popcll(m & lanemask_lt()); t.keys[pos] = k; t.acc[pos] = x; }
-      U2 += __popcll(m);
-      wave_fence();
-    }
-    if (a.diag && l == 0) {  // distinct keys / kept keys per bucket
-      atomicAdd(&a.diag[64 + (31 - __clz(U | 1))], 1ull);
-      atomicAdd(&a.diag[96 + (31 - __clz(U2 | 1))], 1ull);
-    }
-    U = U2;
-  }
-  const int cnt = U <= Lw ? U : Lw;
-  if (cnt == 0) return;
-  int at = 0;
-  if (l == 0) at = (int)atomicAdd(&pt_cnt[tk.d], (uint32_t)cnt);
-  at = __shfl(at, 0);
-  int32_t* ok = pt_key + d.pt_off + at;
-  double* os = pt_sc + d.pt_off + at;
-  if (U <= Lw) {
-    for (int i = l; i < U; i += WAVE) { ok[i] = t.keys[i]; os[i] = t.acc[i]; }
-  } else {
-    const int* keys = t.keys;
-    const double* acc = t.acc;
-    const SelCrit c = select_top(U, Lw, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, hist);
-    int pos0 = 0;
-    for (int i0 = 0; i0 < U; i0 += WAVE) {
-      const int i = i0 + l;
-      bool sel = false;
-      if (i < U) sel = sel_test(c, dbits(acc[i]), (uint32_t)~keys[i]);
-      const uint64_t m = __ballot(sel);
-      if (sel) { const int pos = pos0 + __popcll(m & lanemask_lt()); ok[pos] = keys[i]; os[pos] = acc[i]; }
-      pos0 += __popcll(m);
+    if (overflow) {
+      if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = HubTask{W.d, W.x}; }
+    } else {
+      if (a.diag && l == 0) {  // bucket length histogram: count and cycles per log2(length) bin
+        const int bin = 31 - __clz(nb | 1);
+        atomicAdd(&a.diag[bin], 1ull);
+        atomicAdd(&a.diag[32 + bin], (unsigned long long)((long long)clock64() - t_start));
+      }
+      int U = table_compact(t);
+      // keep what can still reach the top-L: value >= tau (in place, order irrelevant)
+      {
+        int U2 = 0;
+        for (int i0 = 0; i0 < U; i0 += WAVE) {
+          const int i = i0 + l;
+          const int k = i < U ? t.keys[i] : 0;
+          const double x = i < U ? t.acc[i] : 0.0;
+          const bool keep = i < U && x >= W.tau;
+          const uint64_t m = __ballot(keep);
+          wave_fence();
+          if (keep) { const int pos = U2 + __popcll(m & lanemask_lt()); t.keys[pos] = k; t.acc[pos] = x; }
+          U2 += __popcll(m);
+          wave_fence();
+        }
+        if (a.diag && l == 0) {  // distinct keys / kept keys per bucket
+          atomicAdd(&a.diag[64 + (31 - __clz(U | 1))], 1ull);
+          atomicAdd(&a.diag[96 + (31 - __clz(U2 | 1))], 1ull);
+        }
+        U = U2;
+      }
+      const int cnt = U <= Lw ? U : Lw;
+      if (cnt > 0) {
+        int at = 0;
+        if (l == 0) at = (int)atomicAdd(&pt_cnt[W.d], (uint32_t)cnt);
+        at = __shfl(at, 0);
+        int32_t* ok = pt_key + W.pt_off + at;
+        double* os = pt_sc + W.pt_off + at;
+        if (U <= Lw) {
+          for (int i = l; i < U; i += WAVE) { ok[i] = t.keys[i]; os[i] = t.acc[i]; }
+        } else {
+          const int* keys = t.keys;
+          const double* acc = t.acc;
+          const SelCrit c = select_top(U, Lw, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, hist);
+          int pos0 = 0;
+          for (int i0 = 0; i0 < U; i0 += WAVE) {
+            const int i = i0 + l;
+            bool sel = false;
+            if (i < U) sel = sel_test(c, dbits(acc[i]), (uint32_t)~keys[i]);
+            const uint64_t m = __ballot(sel);
+            if (sel) { const int pos = pos0 + __popcll(m & lanemask_lt()); ok[pos] = keys[i]; os[pos] = acc[i]; }
+            pos0 += __popcll(m);
+          }
+        }
+      }
     }
   }
 }

@@ -75,7 +75,8 @@ struct ppr_plan {
   std::vector<int64_t> h_rp;       // host row pointers (hub planning)
   size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0, hub_lds_wave = 0;
   int hub_bucket = 512, hub_wave_t = 1024;
-  int hub_bw_mode = 1;             // PPR_BW_MODE: 0 apply_group per group, 1 chunk_accumulate
+  int num_cus = 256;
+  int hub_bw_blocks = 0;           // persistent k_hub_bucket_w grid
   int hub_bw_ng = 4;               // PPR_BW_NG: groups per chunk (4 or 8)
   int hub_bw_waves = 1;            // PPR_BW_WAVES: waves per block of k_hub_bucket_w
   int hub_slice = 8192;            // PPR_HUB_SLICE: k_hub_reduce slice (>= L)
