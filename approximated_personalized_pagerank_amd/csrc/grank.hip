@@ -275,7 +275,7 @@ static int ceil_log2(int64_t x) { int k = 0; while ((1LL << k) < x) k++; return 
 // Hub pipeline over `big` (sources beyond the workgroup tier). Sources whose buckets overflow
 // the workgroup accumulator are appended to `fallback` (HBM-table path).
 static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& big,
-                    const std::vector<int32_t>& cand, unsigned long long* maxdiff,
+                    const std::vector<int32_t>& cand /* parallel to big */, unsigned long long* maxdiff,
                     std::vector<int32_t>& fallback) {
   hipStream_t st = p->stream;
   DevGraph g{p->d_rp, p->d_colx, p->n};
@@ -291,17 +291,18 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
     size_t i = i0;
     while (i < big.size()) {
       const int v = big[i];
-      const int64_t need = cand[v];
+      const int64_t need = cand[i];
       const int64_t deg = p->h_rp[v + 1] - p->h_rp[v];
       if (!desc.empty() && stg + need > budget) break;
       int logP = ceil_log2((need + p->hub_bucket - 1) / p->hub_bucket);
       logP = std::max(1, std::min(HUB_MAX_LOGP, logP));
       const int P = 1 << logP;
-      const int T = (int)((deg + HUB_TILE - 1) / HUB_TILE);
+      const int tw = (int)std::max<int64_t>(1, std::min<int64_t>(HUB_TILE, HUB_TILE_CAND / L));
+      const int T = (int)((deg + tw - 1) / tw);
       const int idx = (int)desc.size();
       // staging offsets are cumulative candidate counts in descriptor order, the same order the
       // device scan walks the concatenated count matrices in: scanned cm = absolute offsets
-      desc.push_back(HubDesc{v, logP, T, (int32_t)need, cm, stg, pt, 0});  // red: set after the buckets
+      desc.push_back(HubDesc{v, logP, T, (int32_t)need, tw, 0, cm, stg, pt, 0});  // red: set after the buckets
       for (int t = 0; t < T; t++) tiles.push_back(HubTask{idx, t});
       for (int b = 0; b < P; b++) buckets.push_back(HubTask{idx, b});
       cm += (int64_t)P * T;
@@ -537,8 +538,12 @@ static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, i
     std::vector<int32_t> hubs(cnt[TIER_BIG]);
     HIP_OK(hipMemcpyAsync(hubs.data(), p->d_tier_lists + (int64_t)TIER_BIG * p->n, 4 * (size_t)cnt[TIER_BIG],
                           hipMemcpyDeviceToHost, st));
-    std::vector<int32_t> hcand(p->n);
-    HIP_OK(hipMemcpyAsync(hcand.data(), p->d_cand, 4 * (size_t)p->n, hipMemcpyDeviceToHost, st));
+    // candidate counts of the hub sources only (gathered on the device: the whole array is 4 n B)
+    std::vector<int32_t> hcand(cnt[TIER_BIG]);
+    hipLaunchKernelGGL(k_gather_i32, dim3((cnt[TIER_BIG] + 255) / 256), dim3(256), 0, st,
+                       p->d_tier_lists + (int64_t)TIER_BIG * p->n, (int64_t)cnt[TIER_BIG], p->d_cand, p->d_ovf);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(hcand.data(), p->d_ovf, 4 * (size_t)cnt[TIER_BIG], hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (p->hub_enabled) {
       int r = run_hubs(p, a, hubs, hcand, maxdiff, big);

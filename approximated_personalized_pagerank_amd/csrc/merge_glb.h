@@ -10,6 +10,13 @@ namespace pprk {
 // ---------------------------------------------------------------------------------------------
 // big sources: one wave per source, table in HBM scratch (per-source region of T slots)
 
+// out[i] = src[list[i]]
+__global__ void __launch_bounds__(256) k_gather_i32(const int32_t* list, int64_t count, const int32_t* src,
+                                                    int32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) out[i] = src[list[i]];
+}
+
 __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArgs a,
                                                   const GlbWork* work, int64_t count,
                                                   int32_t* gkeys, double* gacc, int32_t* ckeys,

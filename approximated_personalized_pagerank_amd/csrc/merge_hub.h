@@ -26,7 +26,8 @@ namespace pprk {
 //     tau = round(f * max_{u: len[u] = L} min(row u))
 // is a lower bound of the L-th largest final value: a bucket never needs to emit a key below tau
 // (ties at tau are kept, the (score desc, id asc) order decides them in k_hub_final).
-constexpr int HUB_TILE = 64;          // successors per tile (one wave)
+constexpr int HUB_TILE = 64;          // max successors per tile (one wave); HubDesc.tw is the actual width
+constexpr int HUB_TILE_CAND = 4096;   // target candidates per tile: tw = clamp(4096 / L, 1, 64)
 constexpr int HUB_BUCKET = 384;       // default target candidates per bucket (PPR_HUB_BUCKET)
 constexpr int HUB_MAX_LOGP = 12;      // per-wave LDS counters of the partition: 16 KB
 constexpr int HUB_WAVE_T = 512;       // default wave bucket table slots (PPR_HUB_WAVE_T): 13 KB of LDS per wave
@@ -46,6 +47,8 @@ struct HubDesc {
   int32_t logP;
   int32_t T;       // tiles
   int32_t need;    // candidates + 1
+  int32_t tw;      // successors per tile (<= 64; about 4096 candidates per tile)
+  int32_t pad;
   int64_t cm_off;  // count matrix (P*T ints; after the scan: absolute staging offsets)
   int64_t st_off;  // staging (need-1 keys / scores)
   int64_t pt_off;  // appended bucket results (<= P*L entries, pt_cnt[desc] of them used)
@@ -78,16 +81,17 @@ __device__ __forceinline__ uint32_t hub_digit(int key, int logP) {
 // walk the candidates of tile t of source d in successor order, 64 per step
 template <class F>
 __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
-                                              int v, int t, F f) {
-  const int64_t b = g.rp[v], e = g.rp[v + 1];
-  const int64_t i = b + (int64_t)t * HUB_TILE + lane_id();
+                                              int v, int t, int tw, F f) {
+  const int64_t b = g.rp[v];
+  const int64_t e = min(g.rp[v + 1], b + (int64_t)(t + 1) * tw);
+  const int64_t i = b + (int64_t)t * tw + lane_id();
   if (a.unit) {  // init: every successor contributes {u: 1.0}
-    const bool valid = i < e;
+    const bool valid = lane_id() < tw && i < e;
     f(valid, valid ? (g.colx[i] & 0x7fffffff) : 0, 1.0);
     return;
   }
   int u = 0, sl = 0, ln = 0;
-  if (i < e) {
+  if (lane_id() < tw && i < e) {
     const int32_t cx = g.colx[i];
     u = cx & 0x7fffffff;
     sl = read_slot(a, cx);
@@ -144,9 +148,9 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
   const int P = 1 << d.logP;
   if (!a.unit) {  // max over this tile's full-row successors of their row minimum (unscaled)
     const int64_t e = g.rp[d.v + 1];
-    const int64_t i = g.rp[d.v] + (int64_t)tk.x * HUB_TILE + lane_id();
+    const int64_t i = g.rp[d.v] + (int64_t)tk.x * d.tw + lane_id();
     unsigned long long mb = 0;
-    if (i < e) {
+    if (lane_id() < d.tw && i < e) {
       const int32_t cx = g.colx[i];
       const int u = cx & 0x7fffffff;
       const int sl = read_slot(a, cx);
@@ -159,7 +163,7 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * maxP;
   for (int i = lane_id(); i < P; i += WAVE) hist[i] = 0;
   wave_fence();
-  hub_tile_walk(g, s, a, d.v, tk.x, [&](bool valid, int key, double) {
+  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, [&](bool valid, int key, double) {
     if (valid) atomicAdd(&hist[hub_digit(key, d.logP)], 1u);
   });
   wave_fence();
@@ -183,7 +187,7 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   for (int i = lane_id(); i < P; i += WAVE) run[i] = 0;
   wave_fence();
   const uint64_t lt = lanemask_lt();
-  hub_tile_walk(g, s, a, d.v, tk.x, [&](bool valid, int key, double sv) {
+  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, [&](bool valid, int key, double sv) {
     const uint32_t dg = valid ? hub_digit(key, d.logP) : 0u;
     // lanes holding the same digit: AND of per-bit ballots (stable rank = lower lanes first)
     uint64_t match = __ballot(valid);
