@@ -15,7 +15,7 @@ namespace pprk {
 
 constexpr int CLS_PER_WAVE = 16;
 constexpr int CLS_PER_BLOCK = CLS_PER_WAVE * WAVES_PER_BLOCK;
-constexpr int CLS_BIG_DEG = 2048;     // sources with more successors are summed by k_classify_big
+constexpr int CLS_BIG_DEG = 512;      // sources with more successors are summed by k_classify_big
 constexpr int CLS_BIG_THREADS = 1024;
 
 __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArgs a,
