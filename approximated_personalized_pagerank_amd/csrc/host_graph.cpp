@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -58,49 +59,132 @@ int hw_threads() {
   return (int)std::min<unsigned>(h, 16);
 }
 
+// PPR_HOST_THREADS, else OMP_NUM_THREADS (the CPU share on shared hosts), else hw_threads()
+int host_threads() {
+  const char* e = getenv("PPR_HOST_THREADS");
+  if (!e || !*e) e = getenv("OMP_NUM_THREADS");
+  if (e && *e && atoi(e) > 0) return std::min(atoi(e), 64);
+  return hw_threads();
+}
+
 }  // namespace
 
 extern "C" {
 
 int ppr_find_partitions_csr(const ppr_csr* g, uint8_t* part) {
+  // The reference's BFS (pprInternal.h:29-99) takes roots in graph order, puts a root in
+  // partitions.first and every newly reached successor / predecessor in the partition opposite
+  // to the node that reached it. In a FIFO BFS all nodes that can reach a node first sit at the
+  // same depth, so partition(v) = parity of the undirected BFS distance from the root of v's weakly
+  // connected component, and that root is the component's first node in graph order (earlier
+  // components are exhausted before the next root is taken). Both are order-free, so they are
+  // computed in parallel: union-find for the roots, a level-synchronous multi-source BFS for the
+  // depths -- same partitions as the sequential sweep, on all host threads.
   if (!g || !part || g->n < 0) return PPR_ERR_ARG;
   const int64_t n = g->n;
   if (n == 0) return PPR_OK;
   const int64_t* rp = g->row_ptr;
   const int32_t* col = g->col;
   const int64_t m = rp[n];
-  // predecessor lists in graph-iteration order (pprInternal.h:38-47)
+  const int nth = host_threads();
+  std::atomic<bool> bad(false);
+  // predecessor lists: per-thread destination counts over contiguous source ranges, then each
+  // thread fills its own offsets (no atomics; lists end up in source order)
+  const int tt = (int64_t)n * nth * 4 <= (int64_t)512 << 20 ? nth : 1;
+  std::vector<std::vector<int32_t>> cnt(tt);
   std::vector<int64_t> prp(n + 1, 0);
-  for (int64_t e = 0; e < m; e++) {
-    if (col[e] < 0 || col[e] >= n) return PPR_ERR_GRAPH;
-    prp[col[e] + 1]++;
-  }
-  for (int64_t i = 0; i < n; i++) prp[i + 1] += prp[i];
-  std::vector<int32_t> pcol(m > 0 ? m : 1);
-  {
-    std::vector<int64_t> fill(prp.begin(), prp.end() - 1);
-    for (int64_t v = 0; v < n; v++)
-      for (int64_t e = rp[v]; e < rp[v + 1]; e++) pcol[fill[col[e]]++] = (int32_t)v;
-  }
-  std::vector<uint8_t> vis(n, 0);
-  std::vector<int32_t> q(n);
-  for (int64_t r = 0; r < n; r++) {
-    if (vis[r]) continue;
-    int64_t qh = 0, qt = 0;
-    vis[r] = 1; part[r] = 0; q[qt++] = (int32_t)r;   // root joins partitions.first (:57-63)
-    while (qh < qt) {
-      const int32_t x = q[qh++];
-      const uint8_t c = part[x] ^ 1;                  // opposite colour (:69-70)
-      for (int64_t e = rp[x]; e < rp[x + 1]; e++) {
-        const int32_t s = col[e];
-        if (!vis[s]) { vis[s] = 1; part[s] = c; q[qt++] = s; }
+  parallel_for(n, tt, [&](int64_t b, int64_t e, int t) {
+    std::vector<int32_t>& c = cnt[t];
+    c.assign(n, 0);
+    for (int64_t v = b; v < e; v++)
+      for (int64_t k = rp[v]; k < rp[v + 1]; k++) {
+        const int32_t s = col[k];
+        if (s < 0 || s >= n) { bad = true; return; }
+        c[s]++;
       }
-      for (int64_t e = prp[x]; e < prp[x + 1]; e++) {
-        const int32_t s = pcol[e];
-        if (!vis[s]) { vis[s] = 1; part[s] = c; q[qt++] = s; }
+  });
+  if (bad) return PPR_ERR_GRAPH;
+  parallel_for(n, nth, [&](int64_t b, int64_t e, int) {
+    for (int64_t s = b; s < e; s++) {
+      int64_t x = 0;
+      for (int t = 0; t < tt; t++) x += cnt[t].empty() ? 0 : cnt[t][s];
+      prp[s + 1] = x;
+    }
+  });
+  for (int64_t i = 0; i < n; i++) prp[i + 1] += prp[i];
+  parallel_for(n, nth, [&](int64_t b, int64_t e, int) {  // counts -> each thread's write offsets
+    for (int64_t s = b; s < e; s++) {
+      int64_t o = prp[s];
+      for (int t = 0; t < tt; t++) {
+        if (cnt[t].empty()) continue;
+        const int32_t c = cnt[t][s];
+        cnt[t][s] = (int32_t)(o - prp[s]);
+        o += c;
       }
     }
+  });
+  std::vector<int32_t> pcol(m > 0 ? m : 1);
+  parallel_for(n, tt, [&](int64_t b, int64_t e, int t) {
+    std::vector<int32_t>& c = cnt[t];
+    for (int64_t v = b; v < e; v++)
+      for (int64_t k = rp[v]; k < rp[v + 1]; k++) pcol[prp[col[k]] + c[col[k]]++] = (int32_t)v;
+  });
+  cnt.clear();
+  // weakly connected components, representative = smallest id (lock-free union by index)
+  std::vector<int32_t> parent(n);
+  for (int64_t v = 0; v < n; v++) parent[v] = (int32_t)v;
+  auto find = [&](int32_t x) {
+    for (;;) {
+      const int32_t p = __atomic_load_n(&parent[x], __ATOMIC_RELAXED);
+      if (p == x) return x;
+      const int32_t gp = __atomic_load_n(&parent[p], __ATOMIC_RELAXED);
+      if (gp != p) __atomic_compare_exchange_n(&parent[x], const_cast<int32_t*>(&p), gp, false, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED);
+      x = p;
+    }
+  };
+  parallel_for(n, nth, [&](int64_t b, int64_t e, int) {
+    for (int64_t v = b; v < e; v++)
+      for (int64_t k = rp[v]; k < rp[v + 1]; k++) {
+        int32_t x = (int32_t)v, y = col[k];
+        for (;;) {
+          x = find(x);
+          y = find(y);
+          if (x == y) break;
+          if (x > y) std::swap(x, y);
+          int32_t expect = y;  // hang the larger root under the smaller one
+          if (__atomic_compare_exchange_n(&parent[y], &expect, x, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) break;
+        }
+      }
+  });
+  // multi-source BFS from every component's smallest node
+  std::vector<int32_t> depth(n, -1);
+  std::vector<int32_t> front;
+  for (int64_t v = 0; v < n; v++)
+    if (find((int32_t)v) == (int32_t)v) { depth[v] = 0; front.push_back((int32_t)v); }
+  std::vector<std::vector<int32_t>> next(nth);
+  for (int32_t d = 0; !front.empty(); d++) {
+    for (auto& x : next) x.clear();
+    parallel_for((int64_t)front.size(), nth, [&](int64_t b, int64_t e, int t) {
+      std::vector<int32_t>& out = next[t];
+      auto visit = [&](int32_t s) {
+        int32_t expect = -1;
+        if (__atomic_load_n(&depth[s], __ATOMIC_RELAXED) == -1 &&
+            __atomic_compare_exchange_n(&depth[s], &expect, d + 1, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED))
+          out.push_back(s);
+      };
+      for (int64_t i = b; i < e; i++) {
+        const int32_t x = front[i];
+        for (int64_t k = rp[x]; k < rp[x + 1]; k++) visit(col[k]);
+        for (int64_t k = prp[x]; k < prp[x + 1]; k++) visit(pcol[k]);
+      }
+    });
+    front.clear();
+    for (auto& x : next) front.insert(front.end(), x.begin(), x.end());
   }
+  parallel_for(n, nth, [&](int64_t b, int64_t e, int) {
+    for (int64_t v = b; v < e; v++) part[v] = (uint8_t)(depth[v] & 1);
+  });
   return PPR_OK;
 }
 

@@ -18,7 +18,11 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <iostream>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -27,6 +31,28 @@
 
 namespace ppr {
 namespace hipdetail {
+
+// run f(begin, end) over [0, n) on the host's hardware threads (the map <-> CSR conversions
+// dominate end-to-end time once the device phase takes seconds)
+// host threads: PPR_HOST_THREADS, else OMP_NUM_THREADS (set to the CPU share on shared hosts,
+// where hardware_concurrency() reports every CPU of the machine), else hardware_concurrency()
+inline size_t host_threads() {
+  const char* e = getenv("PPR_HOST_THREADS");
+  if (!e || !*e) e = getenv("OMP_NUM_THREADS");
+  if (e && *e && atoi(e) > 0) return (size_t)atoi(e);
+  return std::max<size_t>(1, std::thread::hardware_concurrency());
+}
+
+template <class F>
+inline void parallel_ranges(size_t n, F f) {
+  size_t nt = host_threads();
+  nt = std::min<size_t>(nt, std::max<size_t>(1, n / 4096));
+  if (nt <= 1) { f((size_t)0, n); return; }
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (size_t t = 0; t < nt; t++) th.emplace_back(f, n * t / nt, n * (t + 1) / nt);
+  for (auto& x : th) x.join();
+}
 
 template <typename Key>
 struct Flat {
@@ -45,17 +71,31 @@ inline Flat<Key> flatten(const std::unordered_map<Key, std::vector<Key>>& graph)
     idx.emplace(kv.first, (int32_t)f.keys.size());
     f.keys.push_back(&kv.first);
   }
-  f.rp.reserve(graph.size() + 1);
-  f.rp.push_back(0);
-  for (const Key* k : f.keys) {
-    for (const Key& s : graph.find(*k)->second) {
-      auto it = idx.find(s);
-      // every successor must be a key (README.md:69-73); the reference's behaviour is undefined
-      if (it == idx.end()) { std::cerr << ppr_strerror(PPR_ERR_GRAPH) << std::endl; exit(EXIT_FAILURE); }
-      f.col.push_back(it->second);
+  const size_t n = f.keys.size();
+  std::vector<const std::vector<Key>*> succ(n);
+  f.rp.assign(n + 1, 0);
+  {
+    size_t v = 0;
+    for (const auto& kv : graph) {  // same iteration order as above
+      succ[v] = &kv.second;
+      f.rp[v + 1] = f.rp[v] + (int64_t)kv.second.size();
+      v++;
     }
-    f.rp.push_back((int64_t)f.col.size());
   }
+  f.col.resize((size_t)f.rp[n]);
+  std::atomic<bool> bad(false);
+  parallel_ranges(n, [&](size_t b, size_t e) {
+    for (size_t v = b; v < e; v++) {
+      int64_t o = f.rp[v];
+      for (const Key& s : *succ[v]) {
+        auto it = idx.find(s);
+        // every successor must be a key (README.md:69-73); the reference's behaviour is undefined
+        if (it == idx.end()) { bad = true; return; }
+        f.col[(size_t)o++] = it->second;
+      }
+    }
+  });
+  if (bad) { std::cerr << ppr_strerror(PPR_ERR_GRAPH) << std::endl; exit(EXIT_FAILURE); }
   return f;
 }
 
@@ -78,12 +118,17 @@ inline std::unordered_map<Key, std::unordered_map<Key, double>> materialize(
     const Flat<Key>& f, size_t K, const std::vector<int32_t>& ids, const std::vector<double>& sc,
     const std::vector<int32_t>& len) {
   std::unordered_map<Key, std::unordered_map<Key, double>> out;
-  out.reserve(f.keys.size());
-  for (size_t v = 0; v < f.keys.size(); v++) {
-    std::unordered_map<Key, double>& m = out[*f.keys[v]];
-    m.reserve((size_t)len[v]);
-    for (int32_t i = 0; i < len[v]; i++) m.emplace(*f.keys[ids[v * K + i]], sc[v * K + i]);
-  }
+  const size_t n = f.keys.size();
+  out.reserve(n);
+  std::vector<std::unordered_map<Key, double>*> row(n);
+  for (size_t v = 0; v < n; v++) row[v] = &out[*f.keys[v]];  // outer inserts: one thread
+  parallel_ranges(n, [&](size_t b, size_t e) {               // inner maps are independent
+    for (size_t v = b; v < e; v++) {
+      std::unordered_map<Key, double>& m = *row[v];
+      m.reserve((size_t)len[v]);
+      for (int32_t i = 0; i < len[v]; i++) m.emplace(*f.keys[ids[v * K + i]], sc[v * K + i]);
+    }
+  });
   return out;
 }
 
@@ -93,15 +138,28 @@ inline std::unordered_map<Key, std::unordered_map<Key, double>> grank_device(
     double damping, double tolerance) {
   if (graph.empty()) return {};
   if (K > 0xffffffffu || L > 0xffffffffu || iterations > 0xffffffffu) fail(PPR_ERR_RANGE);
+  const auto t0 = std::chrono::steady_clock::now();
   Flat<Key> f = flatten(graph);
   const size_t n = f.keys.size();
   ppr_csr g{(int64_t)n, f.rp.data(), f.col.empty() ? nullptr : f.col.data()};
   std::vector<int32_t> ids(n * K), len(n);
   std::vector<double> sc(n * K);
+  ppr_stats st;
+  const auto t1 = std::chrono::steady_clock::now();
   const int rc = ppr_grank_csr(&g, nullptr, (uint32_t)K, (uint32_t)L, (uint32_t)iterations, damping,
-                               tolerance, nullptr, ids.data(), sc.data(), len.data(), nullptr);
+                               tolerance, nullptr, ids.data(), sc.data(), len.data(), &st);
   if (rc != PPR_OK) fail(rc);
-  return materialize(f, K, ids, sc, len);
+  const auto t2 = std::chrono::steady_clock::now();
+  auto out = materialize(f, K, ids, sc, len);
+  if (getenv("PPR_TIMING")) {  // phase breakdown of one call (stderr)
+    const auto t3 = std::chrono::steady_clock::now();
+    auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double>(b - a).count();
+    };
+    std::cerr << "ppr_timing flatten_s " << sec(t0, t1) << " csr_call_s " << sec(t1, t2) << " device_s "
+              << st.device_ms / 1e3 << " materialize_s " << sec(t2, t3) << std::endl;
+  }
+  return out;
 }
 
 }  // namespace hipdetail

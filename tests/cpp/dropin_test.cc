@@ -5,6 +5,8 @@
 //   dropin_test ring         README ring of 100, K50 L100 30 it 1e-3: prints "src key score" rows
 //   dropin_test known        known answers of test/grankTest.cc (exit 0 when all hold)
 //   dropin_test mcbad <case> / mcknown   the same for mccompletepathv2 (test/mccompletepathv2Test.cc)
+//   dropin_test e2e <scale>  RMAT graph as unordered_map, ppr::grank(K64, L128, 10 it) end to end
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -81,6 +83,28 @@ int main(int argc, char** argv) {
       for (int u = 0; u < 9; u++) bad += check(r[i][(i + u) % 100] >= r[i][(i + u + 1) % 100], "mc ring order");
     }
     return bad ? 1 : 0;
+  }
+  if (mode == "e2e") {
+    const int scale = atoi(argv[2]);
+    const int64_t n = 1LL << scale;
+    std::vector<int64_t> rp(n + 1);
+    const int64_t m = ppr_rmat_generate(scale, 16, 0.57, 0.19, 0.19, 42, rp.data(), nullptr, 0);
+    std::vector<int32_t> col(m);
+    ppr_rmat_generate(scale, 16, 0.57, 0.19, 0.19, 42, rp.data(), col.data(), m);
+    auto t0 = std::chrono::steady_clock::now();
+    for (int64_t v = 0; v < n; v++) {
+      std::vector<int>& s = graph[(int)v];
+      s.assign(col.begin() + rp[v], col.begin() + rp[v + 1]);
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    auto res = ppr::grank(graph, 64, 128, 10, 0.85, -1.0);
+    auto t2 = std::chrono::steady_clock::now();
+    size_t entries = 0;
+    for (auto& kv : res) entries += kv.second.size();
+    printf("{\"nodes\": %lld, \"edges\": %lld, \"rows\": %zu, \"entries\": %zu, \"build_s\": %.3f, \"total_s\": %.3f}\n",
+           (long long)n, (long long)m, res.size(), entries,
+           std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count());
+    return 0;
   }
   if (mode == "empty") {
     auto res = ppr::grank(graph, 10, 30, 100, 0.85, 0.0001);

@@ -16,7 +16,7 @@ BIN = os.path.join(ROOT, "tests", "cpp", "_dropin_test")
 @pytest.fixture(scope="module")
 def dropin():
     subprocess.run(["g++", "-std=c++11", "-O2", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "cpp", "dropin_test.cc"), "-o", BIN, "-L", PKG, "-lppr_hip",
+                    os.path.join(ROOT, "tests", "cpp", "dropin_test.cc"), "-o", BIN, "-pthread", "-L", PKG, "-lppr_hip",
                     f"-Wl,-rpath,{PKG}"], check=True)
     return BIN
 
@@ -66,3 +66,12 @@ def test_readme_ring_bit_exact_vs_reference(dropin):
     for v in range(len(order)):
         row = {int(order[z["ids"][v, i]]): float(z["scores"][v, i]) for i in range(int(min(z["cnt"][v], f["K"])))}
         assert got[int(order[v])] == row  # exact float equality
+
+
+@pytest.mark.gpu
+def test_end_to_end_timing_rmat(dropin):
+    """reference-API call on an unordered_map RMAT-16 graph: flatten + device + materialise"""
+    out = subprocess.run([dropin, "e2e", "16"], capture_output=True, text=True, check=True).stdout
+    import json
+    d = json.loads(out.strip().splitlines()[-1])
+    assert d["nodes"] == 1 << 16 and d["rows"] == 1 << 16 and d["total_s"] > 0
