@@ -6,11 +6,11 @@ Drop-in surface of fruttasecca/approximated_personalized_pagerank:
   * Python: grank / grank_multi / GrankPlan / mccompletepathv2 / MccpPlan below.
 """
 from ._lib import PprError
-from .graph import Csr, read_edge_csv, rmat
+from .graph import Csr, import_edge_csv, read_edge_csv, rmat
 from .grank import GrankPlan, GrankResult, grank, grank_csr, grank_multi
 from .mccp2 import MccpPlan, McStats, mccompletepathv2, mccp2_csr
 
 __all__ = [
-    "PprError", "Csr", "rmat", "read_edge_csv", "GrankPlan", "GrankResult", "grank", "grank_csr",
+    "PprError", "Csr", "rmat", "read_edge_csv", "import_edge_csv", "GrankPlan", "GrankResult", "grank", "grank_csr",
     "grank_multi", "MccpPlan", "McStats", "mccompletepathv2", "mccp2_csr",
 ]

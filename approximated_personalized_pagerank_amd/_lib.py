@@ -120,6 +120,7 @@ def lib() -> ctypes.CDLL:
         "ppr_grank_plan_pack_host": (ctypes.c_int, [vp, i32, i64, i64, vp]),
         "ppr_grank_plan_unpack_host": (ctypes.c_int, [vp, i32, i64, i64, vp]),
         "ppr_plan_fetch_slot": (ctypes.c_int, [vp, i32, vp, vp, vp]),
+        "ppr_import_edge_csv": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(i64), ctypes.POINTER(i64), vp, vp, vp]),
         "ppr_mccp2_csr": (ctypes.c_int, [vp, u32, u32, u32, f64, ctypes.c_uint64, vp, vp, vp, vp, vp]),
         "ppr_mccp2_plan_create": (ctypes.c_int, [vp, u32, u32, f64, vp, ctypes.POINTER(vp)]),
         "ppr_mccp2_plan_info": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(i64)]),

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/ppr_hip.h"
+#include "../../include/ppr/importGraph.h"
 
 namespace {
 
@@ -301,3 +302,38 @@ int64_t ppr_rmat_generate(int32_t scale, int32_t edge_factor, double a, double b
 }
 
 }  // extern "C"
+
+extern "C" int ppr_import_edge_csv(const char* path, int64_t* n_out, int64_t* m_out, int32_t* keys,
+                                   int64_t* row_ptr, int32_t* col) {
+  // src/main.cc:78-112 through ppr::importGraph; dense ids = the map's iteration order. Call
+  // with keys/row_ptr/col NULL for the sizes, then again with buffers of n, n+1 and m entries.
+  if (!path || !n_out || !m_out) return PPR_ERR_ARG;
+  std::ifstream probe(path);
+  if (!probe) return PPR_ERR_ARG;
+  probe.close();
+  std::unordered_map<int, std::vector<int>> g;
+  try {
+    g = ppr::importGraph(path, false);
+  } catch (...) {
+    return PPR_ERR_ARG;  // a line std::stoi rejects (the reference throws)
+  }
+  const int64_t n = (int64_t)g.size();
+  int64_t m = 0;
+  for (const auto& kv : g) m += (int64_t)kv.second.size();
+  *n_out = n;
+  *m_out = m;
+  if (!keys && !row_ptr && !col) return PPR_OK;
+  if (!keys || !row_ptr || (m > 0 && !col)) return PPR_ERR_ARG;
+  std::unordered_map<int, int32_t> idx;
+  idx.reserve(g.size());
+  int32_t i = 0;
+  for (const auto& kv : g) { keys[i] = kv.first; idx[kv.first] = i; i++; }
+  row_ptr[0] = 0;
+  int64_t o = 0;
+  i = 0;
+  for (const auto& kv : g) {
+    for (int s : kv.second) col[o++] = idx.at(s);
+    row_ptr[++i] = o;
+  }
+  return PPR_OK;
+}

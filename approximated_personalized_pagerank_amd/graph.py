@@ -100,6 +100,22 @@ def rmat(scale: int, edge_factor: int = 16, a: float = 0.57, b: float = 0.19, c:
     return Csr(rp, col[:m])
 
 
+def import_edge_csv(path: str) -> Csr:
+    """The reference CLI's importer (src/main.cc:78-112) run natively (ppr::importGraph), so the
+    dense ids follow the reference's own unordered_map iteration order: same partitions, same
+    executionOrder, same results as the reference run on the file."""
+    import ctypes
+    n, m = ctypes.c_int64(), ctypes.c_int64()
+    L = _lib.lib()
+    _lib.check(L.ppr_import_edge_csv(path.encode(), ctypes.byref(n), ctypes.byref(m), None, None, None), "import")
+    keys = np.zeros(n.value, dtype=np.int32)
+    rp = np.zeros(n.value + 1, dtype=np.int64)
+    col = np.zeros(max(m.value, 1), dtype=np.int32)
+    _lib.check(L.ppr_import_edge_csv(path.encode(), ctypes.byref(n), ctypes.byref(m), keys.ctypes.data, rp.ctypes.data,
+                                     col.ctypes.data), "import")
+    return Csr(rp, col[: m.value], [int(k) for k in keys])
+
+
 def read_edge_csv(path: str) -> Dict[int, List[int]]:
     """Edge list `a,b` per line with the observable behaviour of the reference's importer
     (src/main.cc:78-112): the target is inserted first, repeated edges are skipped, first

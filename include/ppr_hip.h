@@ -81,6 +81,12 @@ int ppr_find_partitions_csr(const ppr_csr* g, uint8_t* part);
  * same records, so ties come out in the reference's order) */
 int ppr_execution_order_csr(const ppr_csr* g, int32_t* order);
 
+/* Edge-list importer of the reference CLI (src/main.cc:78-112): "a,b" per line, targets inserted
+ * first, repeated edges kept once; dense ids follow the resulting unordered_map's iteration order
+ * (the reference's). Call with keys/row_ptr/col NULL for n and m, then with buffers. */
+int ppr_import_edge_csv(const char* path, int64_t* n, int64_t* m, int32_t* keys, int64_t* row_ptr,
+                        int32_t* col);
+
 /* Synthetic RMAT graph (Graph500 recursion, scrambled labels, deduped, successors ascending).
  * Call with col = NULL to get m (row_ptr[n+1] is filled either way); returns m or -error. */
 int64_t ppr_rmat_generate(int32_t scale, int32_t edge_factor, double a, double b, double c,

@@ -87,3 +87,22 @@ def test_execution_order_is_permutation():
 def test_from_dict_rejects_unknown_successor():
     with pytest.raises(ppr.PprError):
         ppr.Csr.from_dict({0: [1]})
+
+
+def test_import_edge_csv_semantics(tmp_path):
+    # src/main.cc:78-112: targets inserted, repeated edges kept once, successor order kept, \r dropped
+    p = tmp_path / "g.csv"
+    p.write_bytes(b"1,2\r\n1,3\n2,1\n1,2\n4,4\n3,5\n")
+    g = ppr.import_edge_csv(str(p))
+    succ = {g.key(i): [g.key(int(c)) for c in g.col[g.row_ptr[i]:g.row_ptr[i + 1]]] for i in range(g.n)}
+    assert succ == {1: [2, 3], 2: [1], 3: [5], 4: [4], 5: []}
+    assert g.m == 5
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/example.txt"), reason="reference tree absent")
+def test_import_edge_csv_reference_order_eat():
+    # the reference's own iteration order of example.txt (recorded in the g4 fixture by ref_driver)
+    g = ppr.import_edge_csv("/root/reference/example.txt")
+    f = load("g4_eat_k50_l100")
+    assert np.array_equal(np.array(g.keys), f["z"]["order"])
+    assert np.array_equal(g.row_ptr, f["rp"]) and np.array_equal(g.col, f["col"])
