@@ -270,113 +270,144 @@ static int ensure_scratch(ppr_plan* p, size_t need) {
 
 static int ensure_dev(unsigned char** ptr, size_t* cap, size_t need);
 
-static int ceil_log2(int64_t x) { int k = 0; while ((1LL << k) < x) k++; return k; }
+static int ceil_log2(int64_t x) { return x <= 1 ? 0 : 64 - __builtin_clzll((unsigned long long)(x - 1)); }
 
-// Hub pipeline over `big` (sources beyond the workgroup tier). Sources whose buckets overflow
-// the workgroup accumulator are appended to `fallback` (HBM-table path).
-static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& big,
-                    const std::vector<int32_t>& cand /* parallel to big */, unsigned long long* maxdiff,
+// Hub pipeline over `big` (sources beyond the workgroup tier), in batches bounded by the staging
+// budget. Everything is planned on the host up front from the candidate counts (O(#hubs)); the
+// per-batch task lists are expanded on the device and no step of a batch waits for the host, so
+// the batches run back to back. Sources with a bucket that overflows every LDS table are appended
+// to `fallback` (HBM-table path) after the last batch (the only host sync here).
+static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
+                    const int32_t* cand /* parallel to big, then the out-degrees */, size_t nbig, unsigned long long* maxdiff,
                     std::vector<int32_t>& fallback) {
   hipStream_t st = p->stream;
   DevGraph g{p->d_rp, p->d_colx, p->n};
   DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
   const int64_t L = p->L;
   const int64_t budget = 1LL << 28;  // staged candidates per batch (4 GiB of 16-B records)
-  size_t i0 = 0;
-  while (i0 < big.size()) {
-    std::vector<HubDesc> desc;
-    std::vector<HubTask> tiles, buckets;
-    int64_t cm = 0, stg = 0, pt = 0;
-    int maxP = 1;
-    size_t i = i0;
-    while (i < big.size()) {
-      const int v = big[i];
-      const int64_t need = cand[i];
-      const int64_t deg = p->h_rp[v + 1] - p->h_rp[v];
-      if (!desc.empty() && stg + need > budget) break;
-      int logP = ceil_log2((need + p->hub_bucket - 1) / p->hub_bucket);
-      logP = std::max(1, std::min(HUB_MAX_LOGP, logP));
-      const int P = 1 << logP;
-      const int tw = (int)std::max<int64_t>(1, std::min<int64_t>(HUB_TILE, HUB_TILE_CAND / L));
-      const int T = (int)((deg + tw - 1) / tw);
-      const int idx = (int)desc.size();
-      // staging offsets are cumulative candidate counts in descriptor order, the same order the
-      // device scan walks the concatenated count matrices in: scanned cm = absolute offsets
-      desc.push_back(HubDesc{v, logP, T, (int32_t)need, tw, 0, cm, stg, pt, 0});  // red: set after the buckets
-      for (int t = 0; t < T; t++) tiles.push_back(HubTask{idx, t});
-      for (int b = 0; b < P; b++) buckets.push_back(HubTask{idx, b});
-      cm += (int64_t)P * T;
-      stg += need - 1;
-      pt += (int64_t)P * L;
-      maxP = std::max(maxP, P);
-      i++;
+  const int slice = p->hub_slice;
+  using Batch = HubBatch;
+  std::vector<Batch>& batches = p->hub_batches;
+  batches.clear();
+  {
+    int rc0 = ensure_pinned(&p->h_desc_pin, &p->h_desc_bytes, sizeof(HubDesc) * (nbig + 1));
+    if (rc0) return rc0;
+  }
+  HubDesc* desc = (HubDesc*)p->h_desc_pin;
+  size_t nd_all = 0;
+  {
+    size_t i = 0;
+    while (i < nbig) {
+      Batch b{nd_all, 0, 0, 0, 0, 0, 0, 0, 0, 1};
+      while (i < nbig) {
+        const int v = big[i];
+        const int64_t need = cand[i];
+        const int64_t deg = cand[nbig + i];
+        if (nd_all > b.d0 && b.stg + need > budget) break;
+        int logP = ceil_log2((need + p->hub_bucket - 1) / p->hub_bucket);
+        logP = std::max(1, std::min(HUB_MAX_LOGP, logP));
+        const int P = 1 << logP;
+        const int tw = (int)std::max<int64_t>(1, std::min<int64_t>(HUB_TILE, HUB_TILE_CAND / L));
+        const int T = (int)((deg + tw - 1) / tw);
+        const int64_t ptc = (int64_t)P * L;
+        const int nsl = ptc > 2 * slice ? (int)((ptc + slice - 1) / slice) : 0;
+        // staging offsets are cumulative candidate counts in descriptor order, the same order the
+        // device scan walks the concatenated count matrices in: scanned cm = absolute offsets
+        desc[nd_all++] = HubDesc{v, logP, T, (int32_t)need, tw, nsl, b.cm, b.stg, b.pt, b.red, b.ntiles, b.nbuck, b.nrt};
+        b.cm += (int64_t)P * T;
+        b.stg += need - 1;
+        b.pt += ptc;
+        b.red += (int64_t)nsl * L;
+        b.ntiles += T;
+        b.nbuck += P;
+        b.nrt += nsl;
+        b.maxP = std::max(b.maxP, P);
+        i++;
+      }
+      b.d1 = nd_all;
+      batches.push_back(b);
     }
-    const size_t nd = desc.size();
-    size_t scan_tmp = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (const int32_t*)nullptr, (int32_t*)nullptr, (int)cm, st);
-    // scratch layout
-    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    size_t off = 0;
-    const size_t o_desc = off; off = al(off + sizeof(HubDesc) * nd);
-    const size_t o_tile = off; off = al(off + sizeof(HubTask) * tiles.size());
-    const size_t o_buck = off; off = al(off + sizeof(HubTask) * buckets.size());
-    const size_t o_cm = off;   off = al(off + 4 * (size_t)cm);
-    const size_t o_cmx = off;  off = al(off + 4 * (size_t)cm);
-    const size_t o_tmp = off;  off = al(off + scan_tmp);
-    const size_t o_st = off;   off = al(off + sizeof(HubRec) * (size_t)stg);
-    const size_t o_pk = off;   off = al(off + 4 * (size_t)pt);
-    const size_t o_ps = off;   off = al(off + 8 * (size_t)pt);
-    const size_t o_pc = off;   off = al(off + 4 * nd);
-    const size_t o_tau = off;  off = al(off + 8 * nd);
-    const size_t o_idx = off;  off = al(off + 4 * nd);
-    const size_t o_ovf = off;  off = al(off + 4 * (buckets.size() + 1));
-    const size_t o_gl = off;   off = al(off + sizeof(HubTask) * (buckets.size() + 1));
-    const size_t o_cnt = off;  off = al(off + 16);
-    const size_t o_bw = off;   off = al(off + sizeof(BucketWork) * buckets.size());
-    int rc = ensure_scratch(p, off);
-    if (rc) return rc;
-    char* base = (char*)p->d_scratch;
-    HubDesc* d_desc = (HubDesc*)(base + o_desc);
-    HubTask* d_tile = (HubTask*)(base + o_tile);
-    HubTask* d_buck = (HubTask*)(base + o_buck);
-    int32_t* d_cm = (int32_t*)(base + o_cm);
-    int32_t* d_cmx = (int32_t*)(base + o_cmx);
-    void* d_tmp = (void*)(base + o_tmp);
-    HubRec* d_st = (HubRec*)(base + o_st);
-    int32_t* d_pk = (int32_t*)(base + o_pk);
-    double* d_ps = (double*)(base + o_ps);
-    uint32_t* d_pc = (uint32_t*)(base + o_pc);
-    unsigned long long* d_tau = (unsigned long long*)(base + o_tau);
-    int32_t* d_idx = (int32_t*)(base + o_idx);
-    int32_t* d_ovf = (int32_t*)(base + o_ovf);
-    uint32_t* d_ovf_cnt = (uint32_t*)(d_ovf + buckets.size());
-    HubTask* d_gl = (HubTask*)(base + o_gl);
-    uint32_t* d_lc = (uint32_t*)(base + o_cnt);  // [0] bucket-wave work counter, [1] workgroup list
-    BucketWork* d_bw = (BucketWork*)(base + o_bw);
-    int32_t* d_rk = nullptr;                       // sliced reductions of long appended lists
-    double* d_rs = nullptr;
-    HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * nd, hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(d_tile, tiles.data(), sizeof(HubTask) * tiles.size(), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(d_buck, buckets.data(), sizeof(HubTask) * buckets.size(), hipMemcpyHostToDevice, st));
+  }
+  // one scratch layout for every batch (maxima), so no batch reallocates under a running one
+  Batch mx{0, 0, 0, 0, 0, 0, 0, 0, 0, 1};
+  size_t maxnd = 0;
+  for (const Batch& b : batches) {
+    mx.cm = std::max(mx.cm, b.cm); mx.stg = std::max(mx.stg, b.stg); mx.pt = std::max(mx.pt, b.pt);
+    mx.ntiles = std::max(mx.ntiles, b.ntiles); mx.nbuck = std::max(mx.nbuck, b.nbuck);
+    mx.nrt = std::max(mx.nrt, b.nrt); mx.red = std::max(mx.red, b.red);
+    maxnd = std::max(maxnd, b.d1 - b.d0);
+  }
+  size_t scan_tmp = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (const int32_t*)nullptr, (int32_t*)nullptr, (int)mx.cm, st);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t off = 0;
+  const size_t o_desc = off; off = al(off + sizeof(HubDesc) * nd_all);
+  const size_t o_tile = off; off = al(off + sizeof(HubTask) * mx.ntiles);
+  const size_t o_buck = off; off = al(off + sizeof(HubTask) * mx.nbuck);
+  const size_t o_rt = off;   off = al(off + sizeof(HubTask) * (mx.nrt + 1));
+  const size_t o_cm = off;   off = al(off + 4 * (size_t)mx.cm);
+  const size_t o_cmx = off;  off = al(off + 4 * (size_t)mx.cm);
+  const size_t o_tmp = off;  off = al(off + scan_tmp);
+  const size_t o_st = off;   off = al(off + sizeof(HubRec) * (size_t)mx.stg);
+  const size_t o_pk = off;   off = al(off + 4 * (size_t)mx.pt);
+  const size_t o_ps = off;   off = al(off + 8 * (size_t)mx.pt);
+  const size_t o_rk = off;   off = al(off + 4 * (size_t)(mx.red + 1));
+  const size_t o_rs = off;   off = al(off + 8 * (size_t)(mx.red + 1));
+  const size_t o_pc = off;   off = al(off + 4 * maxnd);
+  const size_t o_tau = off;  off = al(off + 8 * maxnd);
+  const size_t o_of = off;   off = al(off + 4 * maxnd);
+  const size_t o_ovl = off;  off = al(off + 4 * (nd_all + 1));
+  const size_t o_gl = off;   off = al(off + sizeof(HubTask) * (mx.nbuck + 1));
+  const size_t o_cnt = off;  off = al(off + 16);
+  const size_t o_bw = off;   off = al(off + sizeof(BucketWork) * mx.nbuck);
+  int rc = ensure_scratch(p, off);
+  if (rc) return rc;
+  char* base = (char*)p->d_scratch;
+  HubDesc* d_desc_all = (HubDesc*)(base + o_desc);
+  HubTask* d_tile = (HubTask*)(base + o_tile);
+  HubTask* d_buck = (HubTask*)(base + o_buck);
+  HubTask* d_rt = (HubTask*)(base + o_rt);
+  int32_t* d_cm = (int32_t*)(base + o_cm);
+  int32_t* d_cmx = (int32_t*)(base + o_cmx);
+  void* d_tmp = (void*)(base + o_tmp);
+  HubRec* d_st = (HubRec*)(base + o_st);
+  int32_t* d_pk = (int32_t*)(base + o_pk);
+  double* d_ps = (double*)(base + o_ps);
+  int32_t* d_rk = (int32_t*)(base + o_rk);
+  double* d_rs = (double*)(base + o_rs);
+  uint32_t* d_pc = (uint32_t*)(base + o_pc);
+  unsigned long long* d_tau = (unsigned long long*)(base + o_tau);
+  int32_t* d_oflag = (int32_t*)(base + o_of);
+  int32_t* d_ovl = (int32_t*)(base + o_ovl);     // [0] count, [1..] sources for the HBM-table path
+  HubTask* d_gl = (HubTask*)(base + o_gl);
+  uint32_t* d_lc = (uint32_t*)(base + o_cnt);    // [1] spill list length
+  BucketWork* d_bw = (BucketWork*)(base + o_bw);
+  HIP_OK(hipMemcpyAsync(d_desc_all, desc, sizeof(HubDesc) * nd_all, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemsetAsync(d_ovl, 0, 4, st));
+  for (const Batch& b : batches) {
+    const size_t nd = b.d1 - b.d0;
+    HubDesc* d_desc = d_desc_all + b.d0;
+    const int maxP = b.maxP;
     HIP_OK(hipMemsetAsync(d_pc, 0, 4 * nd, st));
     HIP_OK(hipMemsetAsync(d_tau, 0, 8 * nd, st));
-    HIP_OK(hipMemsetAsync(d_ovf_cnt, 0, 4, st));
+    HIP_OK(hipMemsetAsync(d_oflag, 0, 4 * nd, st));
     HIP_OK(hipMemsetAsync(d_lc, 0, 8, st));
-    const int64_t ntiles = (int64_t)tiles.size();
+    hipLaunchKernelGGL(k_hub_expand, dim3((unsigned)nd), dim3(256), 0, st, d_desc, d_tile, d_buck, d_rt);
+    HIP_OK(hipGetLastError());
+    const int64_t ntiles = b.ntiles;
     const size_t lds_tile = (size_t)WAVES_PER_BLOCK * maxP * 4;
     const unsigned tb = (unsigned)((ntiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm,
                        d_tau);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, scan_tmp, d_cm, d_cmx, (int)cm, st));
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, scan_tmp, d_cm, d_cmx, (int)b.cm, st));
     hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
                        d_cmx, d_st);
     HIP_OK(hipGetLastError());
-    const int64_t nbuck = (int64_t)buckets.size();
+    const int64_t nbuck = b.nbuck;
     // every bucket goes to a single wave first: a bucket made long by one hot key (a core node
     // present in most successor baskets) still has few distinct keys, and its sequential fma
     // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
-    uint32_t nspill = 0;
     hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, a, d_desc, d_buck, nbuck,
                        d_cmx, d_tau, d_bw);
     HIP_OK(hipGetLastError());
@@ -392,78 +423,32 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& 
                            d_pc, d_gl, d_lc + 1, p->hub_wave_t);
       HIP_OK(hipGetLastError());
     }
-    HIP_OK(hipMemcpyAsync(&nspill, d_lc + 1, 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (nspill) {
-      hipLaunchKernelGGL(k_hub_bucket, dim3(nspill), dim3(WG_THREADS), p->hub_lds_wg, st, s, a, g,
-                         d_desc, d_gl, (int64_t)nspill, d_cmx, d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_ovf,
-                         d_ovf_cnt);
+    // spilled buckets (distinct keys beyond the wave table): persistent workgroups over the spill
+    // list, whose length only the device knows
+    hipLaunchKernelGGL(k_hub_bucket, dim3((unsigned)p->num_cus), dim3(WG_THREADS), p->hub_lds_wg, st, s, a, g,
+                       d_desc, d_gl, d_lc + 1, d_cmx, d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_oflag, d_ovl);
+    HIP_OK(hipGetLastError());
+    // long appended lists are cut (k_hub_reduce) so no k_hub_final workgroup selects from more
+    // than a few slices' worth of entries; slices are reserved for the worst case, idle ones exit
+    if (b.nrt) {
+      hipLaunchKernelGGL(k_hub_reduce, dim3((unsigned)b.nrt), dim3(WG_THREADS), p->hub_lds_final, st, s, d_desc,
+                         d_rt, d_pc, d_pk, d_ps, d_rk, d_rs, p->Lp, slice);
       HIP_OK(hipGetLastError());
+      p->merge_launches++;
     }
-    uint32_t novf = 0;
-    HIP_OK(hipMemcpyAsync(&novf, d_ovf_cnt, 4, hipMemcpyDeviceToHost, st));
+    hipLaunchKernelGGL(k_hub_final, dim3((unsigned)nd), dim3(WG_THREADS), p->hub_lds_final, st, s, a, d_desc,
+                       d_oflag, d_pc, d_pk, d_ps, d_rk, d_rs, slice, p->Lp, maxdiff, p->d_stats);
+    HIP_OK(hipGetLastError());
+    p->merge_launches += 9;
+  }
+  int32_t novf = 0;
+  HIP_OK(hipMemcpyAsync(&novf, d_ovl, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (novf) {
+    std::vector<int32_t> ov(novf);
+    HIP_OK(hipMemcpyAsync(ov.data(), d_ovl + 1, 4 * (size_t)novf, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    // cut long appended lists (k_hub_reduce) so no k_hub_final workgroup selects from more than
-    // a few slices' worth of entries
-    std::vector<uint32_t> pcnt(nd);
-    HIP_OK(hipMemcpyAsync(pcnt.data(), d_pc, 4 * nd, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    {
-      std::vector<HubTask> rt;
-      int64_t roff = 0;
-      for (size_t k = 0; k < nd; k++) {
-        if (pcnt[k] <= (uint32_t)(2 * p->hub_slice)) { desc[k].red = 0; continue; }
-        const int ns = (int)((pcnt[k] + p->hub_slice - 1) / p->hub_slice);
-        desc[k].red = 1 + roff;
-        roff += (int64_t)ns * L;
-        for (int x = 0; x < ns; x++) rt.push_back(HubTask{(int32_t)k, x});
-      }
-      if (!rt.empty()) {
-        // separate buffer: the staging in d_scratch is still live
-        size_t ro = 0;
-        const size_t o_rt = ro;  ro = al(ro + sizeof(HubTask) * rt.size());
-        const size_t o_rk = ro;  ro = al(ro + 4 * (size_t)roff);
-        const size_t o_rs = ro;  ro = al(ro + 8 * (size_t)roff);
-        rc = ensure_dev(&p->d_red, &p->red_bytes, ro);
-        if (rc) return rc;
-        HubTask* d_rt = (HubTask*)(p->d_red + o_rt);
-        d_rk = (int32_t*)(p->d_red + o_rk);
-        d_rs = (double*)(p->d_red + o_rs);
-        HIP_OK(hipMemcpyAsync(d_desc, desc.data(), sizeof(HubDesc) * nd, hipMemcpyHostToDevice, st));
-        HIP_OK(hipMemcpyAsync(d_rt, rt.data(), sizeof(HubTask) * rt.size(), hipMemcpyHostToDevice, st));
-        hipLaunchKernelGGL(k_hub_reduce, dim3((unsigned)rt.size()), dim3(WG_THREADS), p->hub_lds_final, st, s, d_desc,
-                           d_rt, d_pc, d_pk, d_ps, d_rk, d_rs, p->Lp, p->hub_slice);
-        HIP_OK(hipGetLastError());
-        p->merge_launches++;
-      }
-    }
-    const int32_t* didx = nullptr;
-    size_t nfinal = nd;
-    if (novf) {
-      // sources with an overflowing bucket skip the final merge and take the HBM-table path
-      std::vector<int32_t> ov(novf);
-      HIP_OK(hipMemcpyAsync(ov.data(), d_ovf, 4 * (size_t)novf, hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-      std::vector<char> bad(nd, 0);
-      for (int32_t x : ov) bad[-x - 1] = 1;
-      std::vector<int32_t> keep;
-      for (size_t k = 0; k < nd; k++) {
-        if (bad[k]) fallback.push_back(desc[k].v);
-        else keep.push_back((int32_t)k);
-      }
-      nfinal = keep.size();
-      if (nfinal) HIP_OK(hipMemcpyAsync(d_idx, keep.data(), 4 * nfinal, hipMemcpyHostToDevice, st));
-      didx = d_idx;
-    }
-    if (nfinal) {
-      hipLaunchKernelGGL(k_hub_final, dim3((unsigned)nfinal), dim3(WG_THREADS), p->hub_lds_final, st, s, a,
-                         d_desc, didx, d_pc, d_pk, d_ps, d_rk, d_rs, p->hub_slice, p->Lp, maxdiff,
-                         p->d_stats);
-      HIP_OK(hipGetLastError());
-    }
-    p->merge_launches += 7;
-    HIP_OK(hipStreamSynchronize(st));  // scratch is reused by the next batch
-    i0 = i;
+    fallback.insert(fallback.end(), ov.begin(), ov.end());
   }
   return PPR_OK;
 }
@@ -535,21 +520,32 @@ static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, i
     if (cnt[t] && !p->tierT[t]) { int r = pull(p->d_tier_lists + (int64_t)t * p->n, cnt[t]); if (r) return r; }
   { int r = pull(p->d_ovf, cnt[NLISTS]); if (r) return r; }
   if (cnt[TIER_BIG]) {
-    std::vector<int32_t> hubs(cnt[TIER_BIG]);
-    HIP_OK(hipMemcpyAsync(hubs.data(), p->d_tier_lists + (int64_t)TIER_BIG * p->n, 4 * (size_t)cnt[TIER_BIG],
-                          hipMemcpyDeviceToHost, st));
-    // candidate counts of the hub sources only (gathered on the device: the whole array is 4 n B)
-    std::vector<int32_t> hcand(cnt[TIER_BIG]);
-    hipLaunchKernelGGL(k_gather_i32, dim3((cnt[TIER_BIG] + 255) / 256), dim3(256), 0, st,
-                       p->d_tier_lists + (int64_t)TIER_BIG * p->n, (int64_t)cnt[TIER_BIG], p->d_cand, p->d_ovf);
+    const size_t nh = cnt[TIER_BIG];
+    {
+      size_t capb = p->h_hub_cap * 12;
+      void* ptr = p->h_hub_pin;
+      int r = ensure_pinned(&ptr, &capb, 12 * nh);
+      if (r) return r;
+      p->h_hub_pin = (int32_t*)ptr;
+      p->h_hub_cap = capb / 12;
+    }
+    int32_t* hubs = p->h_hub_pin;
+    int32_t* hcand = p->h_hub_pin + nh;  // | out-degrees at hcand + nh
+    HIP_OK(hipMemcpyAsync(hubs, p->d_tier_lists + (int64_t)TIER_BIG * p->n, 4 * nh, hipMemcpyDeviceToHost, st));
+    // candidate counts and degrees of the hub sources only (gathered on the device, so the host
+    // planning loop reads them sequentially)
+    if (2 * nh > (size_t)p->n) { int r = ensure_dev((unsigned char**)&p->d_gath, &p->gath_bytes, 8 * nh); if (r) return r; }
+    int32_t* d_g = 2 * nh > (size_t)p->n ? p->d_gath : p->d_ovf;
+    hipLaunchKernelGGL(k_gather_cand_deg, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st,
+                       p->d_tier_lists + (int64_t)TIER_BIG * p->n, (int64_t)nh, p->d_cand, p->d_rp, d_g);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(hcand.data(), p->d_ovf, 4 * (size_t)cnt[TIER_BIG], hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(hcand, d_g, 8 * nh, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (p->hub_enabled) {
-      int r = run_hubs(p, a, hubs, hcand, maxdiff, big);
+      int r = run_hubs(p, a, hubs, hcand, nh, maxdiff, big);
       if (r) return r;
     } else {
-      big.insert(big.end(), hubs.begin(), hubs.end());
+      big.insert(big.end(), hubs, hubs + nh);
     }
   }
   if (big.empty()) return PPR_OK;

@@ -17,6 +17,17 @@ __global__ void __launch_bounds__(256) k_gather_i32(const int32_t* list, int64_t
   if (i < count) out[i] = src[list[i]];
 }
 
+// hub planning inputs, gathered so the host walks them sequentially: candidate counts and
+// out-degrees of the listed sources (out[0..count) | out[count..2 count))
+__global__ void __launch_bounds__(256) k_gather_cand_deg(const int32_t* list, int64_t count, const int32_t* cand,
+                                                         const int64_t* rp, int32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int v = list[i];
+  out[i] = cand[v];
+  out[count + i] = (int32_t)(rp[v + 1] - rp[v]);
+}
+
 __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArgs a,
                                                   const GlbWork* work, int64_t count,
                                                   int32_t* gkeys, double* gacc, int32_t* ckeys,

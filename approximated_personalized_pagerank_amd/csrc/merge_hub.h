@@ -48,12 +48,17 @@ struct HubDesc {
   int32_t T;       // tiles
   int32_t need;    // candidates + 1
   int32_t tw;      // successors per tile (<= 64; about 4096 candidates per tile)
-  int32_t pad;
+  int32_t nsl;     // k_hub_reduce slices reserved (upper bound from P * L appended entries)
   int64_t cm_off;  // count matrix (P*T ints; after the scan: absolute staging offsets)
   int64_t st_off;  // staging (need-1 keys / scores)
   int64_t pt_off;  // appended bucket results (<= P*L entries, pt_cnt[desc] of them used)
-  int64_t red;     // 0, or 1 + offset of the sliced reduction of the appended list (k_hub_reduce)
+  int64_t red;     // offset of the sliced reduction (k_hub_reduce), used iff pt_cnt > 2 * slice
+  int64_t tile_off, buck_off, rt_off;  // first tile / bucket / reduce task of this source in its batch
 };
+
+// the batch's task lists, expanded on the device from the descriptors (one block per source):
+// tiles (d, t) for k_hub_count / k_hub_scatter, buckets (d, b) for k_hub_prep, reduce slices (d, x)
+struct HubTask;
 
 // staging range of bucket x of source d (cm holds the scanned, absolute offsets)
 __device__ __forceinline__ void hub_bucket_range(const HubDesc& d, const int32_t* cm, int x,
@@ -65,6 +70,16 @@ __device__ __forceinline__ void hub_bucket_range(const HubDesc& d, const int32_t
   nb = end - start;
 }
 struct HubTask { int32_t d; int32_t x; };   // (descriptor, tile or bucket)
+
+__global__ void __launch_bounds__(256) k_hub_expand(const HubDesc* desc, HubTask* tiles, HubTask* buckets,
+                                                    HubTask* rts) {
+  const int d = blockIdx.x;
+  const HubDesc D = desc[d];
+  const int P = 1 << D.logP;
+  for (int t = threadIdx.x; t < D.T; t += blockDim.x) tiles[D.tile_off + t] = HubTask{d, t};
+  for (int b = threadIdx.x; b < P; b += blockDim.x) buckets[D.buck_off + b] = HubTask{d, b};
+  for (int x = threadIdx.x; x < D.nsl; x += blockDim.x) rts[D.rt_off + x] = HubTask{d, x};
+}
 
 // one staged candidate: key and score in one 16-B record, so a scattered store touches one
 // partial line instead of two (separate key / score arrays)
@@ -379,18 +394,14 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
   }
 }
 
-__global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a,
-                                                           const DevGraph g, const HubDesc* desc,
-                                                           const HubTask* tasks, int64_t ntasks,
-                                                           const int32_t* cm,
-                                                           const HubRec* st,
-                                                           int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
-                                                           const unsigned long long* tau_b, int Lp,
-                                                           int32_t* ovf_list, uint32_t* ovf_cnt) {
+__device__ __forceinline__ void hub_bucket_one(const DevSlab& s, const IterArgs& a, const DevGraph& g,
+                                               const HubDesc* desc, const HubTask tk, const int32_t* cm,
+                                               const HubRec* st, int32_t* pt_key, double* pt_sc,
+                                               uint32_t* pt_cnt, const unsigned long long* tau_b, int Lp,
+                                               int32_t* ovf_flag, int32_t* ovf_list) {
   extern __shared__ __align__(16) unsigned char smem[];
-  if ((int64_t)blockIdx.x >= ntasks) return;
-  const HubTask tk = tasks[blockIdx.x];
   const HubDesc d = desc[tk.d];
+
   const WgLds L = wg_carve(smem, WG_T, Lp, wg_pl(Lp));
   const int wv = threadIdx.x >> 6;
   const int l = lane_id();
@@ -431,7 +442,10 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a
     if (wg_accumulate(L, Pp, 0x51ed270bu, seed, v, self_seed(a, deg), factor, Lw, each)) break;
     Pp *= 2;
     if (Pp > WG_MAX_PASSES) {
-      if (threadIdx.x == 0) { const uint32_t pos = atomicAdd(ovf_cnt, 1u); ovf_list[pos] = -(tk.d + 1); }
+      if (threadIdx.x == 0 && atomicExch(&ovf_flag[tk.d], 1) == 0) {
+        const int pos = atomicAdd(&ovf_list[0], 1);
+        ovf_list[1 + pos] = d.v;
+      }
       return;
     }
   }
@@ -460,6 +474,23 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a
   }
 }
 
+// persistent grid over the spill list of k_hub_bucket_w (its length is read on the device, so
+// the host never waits for it); a bucket that overflows here too flags its source for the
+// HBM-table path (ovf_flag[d], source id appended to ovf_list[1..], count in ovf_list[0])
+__global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a,
+                                                           const DevGraph g, const HubDesc* desc,
+                                                           const HubTask* tasks, const uint32_t* ntasks_p,
+                                                           const int32_t* cm,
+                                                           const HubRec* st,
+                                                           int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
+                                                           const unsigned long long* tau_b, int Lp,
+                                                           int32_t* ovf_flag, int32_t* ovf_list) {
+  const uint32_t ntasks = *ntasks_p;
+  for (uint32_t task = blockIdx.x; task < ntasks; task += gridDim.x) {
+    __syncthreads();  // LDS of the previous task fully consumed
+    hub_bucket_one(s, a, g, desc, tasks[task], cm, st, pt_key, pt_sc, pt_cnt, tau_b, Lp, ovf_flag, ovf_list);
+  }
+}
 // Long appended lists (a hub with thousands of buckets) are cut before k_hub_final: one
 // workgroup per HUB_SLICE entries keeps the slice's top-L (the top-L of a union lies in the union
 // of its parts' top-Ls); every full slice then contributes exactly L entries at red + slice * L.
@@ -473,12 +504,14 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_reduce(DevSlab s, const HubD
   const WgLds L = wg_carve(smem, 0, Lp, 0);
   const int Lw = s.L;
   const int n_all = (int)pt_cnt[tk.d];
+  if (n_all <= 2 * slice) return;  // short list: k_hub_final selects from it directly
   const int b = tk.x * slice;
+  if (b >= n_all) return;          // slices are reserved for the worst case P * L
   const int n = min(slice, n_all - b);
   const int32_t* pk = pt_key + d.pt_off + b;
   const double* pv = pt_sc + d.pt_off + b;
-  int32_t* ok = red_key + (d.red - 1) + (int64_t)tk.x * Lw;
-  double* os = red_sc + (d.red - 1) + (int64_t)tk.x * Lw;
+  int32_t* ok = red_key + d.red + (int64_t)tk.x * Lw;
+  double* os = red_sc + d.red + (int64_t)tk.x * Lw;
   if (n <= Lw) {
     for (int i = threadIdx.x; i < n; i += WG_THREADS) { ok[i] = pk[i]; os[i] = pv[i]; }
     return;
@@ -497,25 +530,26 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_reduce(DevSlab s, const HubD
 }
 
 __global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a, const HubDesc* desc,
-                                                          const int32_t* didx, const uint32_t* pt_cnt,
+                                                          const int32_t* ovf_flag, const uint32_t* pt_cnt,
                                                           const int32_t* pt_key, const double* pt_sc,
                                                           const int32_t* red_key, const double* red_sc, int slice,
                                                           int Lp,
                                                           unsigned long long* maxdiff,
                                                           unsigned long long* stats) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int di = didx ? didx[blockIdx.x] : (int)blockIdx.x;
+  const int di = (int)blockIdx.x;
+  if (ovf_flag[di]) return;  // a bucket overflowed every LDS table: the HBM-table path redoes the source
   const HubDesc d = desc[di];
   const WgLds L = wg_carve(smem, 0, Lp, 0);
   const int Lw = s.L;
   int n = (int)pt_cnt[di];  // appended bucket results, any order
   const int32_t* pk = pt_key + d.pt_off;
   const double* pv = pt_sc + d.pt_off;
-  if (d.red) {  // the list was cut to the top-L of every HUB_SLICE entries by k_hub_reduce
+  if (n > 2 * slice) {  // the list was cut to the top-L of every HUB_SLICE entries by k_hub_reduce
     const int ns = (n + slice - 1) / slice, last = n - (ns - 1) * slice;
     n = (ns - 1) * Lw + (last < Lw ? last : Lw);
-    pk = red_key + (d.red - 1);
-    pv = red_sc + (d.red - 1);
+    pk = red_key + d.red;
+    pv = red_sc + d.red;
   }
   auto occ = [&](int) { return true; };
   const int total = n;

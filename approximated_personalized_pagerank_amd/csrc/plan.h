@@ -53,8 +53,6 @@ struct ppr_plan {
   int32_t* d_tier_lists = nullptr;   // NLISTS * n
   uint32_t* d_tier_cnt = nullptr;    // NLISTS, +1 workgroup overflow count, +1 k_classify_big list length
   int32_t* d_big = nullptr;          // sources k_classify hands to k_classify_big
-  unsigned char* d_red = nullptr;    // k_hub_reduce output when the hub scratch has no room left
-  size_t red_bytes = 0;
   int64_t max_deg = 0;
   int32_t* d_tier_cap = nullptr;     // NT + 1
   int32_t* d_ovf = nullptr;          // sources the workgroup tier could not hold
@@ -75,6 +73,15 @@ struct ppr_plan {
   std::vector<int64_t> h_rp;       // host row pointers (hub planning)
   size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0, hub_lds_wave = 0;
   int hub_bucket = 512, hub_wave_t = 1024;
+  // pinned host staging of the hub planning (hub list + candidate counts down, descriptors up):
+  // pageable copies of these (tens of MB per iteration) stalled the stream for milliseconds
+  int32_t* h_hub_pin = nullptr;    // [2 * cap]: hub ids | candidate counts
+  size_t h_hub_cap = 0;
+  void* h_desc_pin = nullptr;
+  size_t h_desc_bytes = 0;
+  std::vector<HubBatch> hub_batches;
+  int32_t* d_gath = nullptr;       // hub planning gather when 2 * hubs > n (d_ovf is n ints)
+  size_t gath_bytes = 0;
   int num_cus = 256;
   int hub_bw_blocks = 0;           // persistent k_hub_bucket_w grid
   int hub_bw_ng = 4;               // PPR_BW_NG: groups per chunk (4 or 8)
@@ -108,8 +115,8 @@ inline void plan_free(ppr_plan* p) {
   if (!p) return;
   hipFree(p->d_rp); hipFree(p->d_colx); hipFree(p->d_part); hipFree(p->d_ids); hipFree(p->d_sc);
   hipFree(p->d_len); hipFree(p->d_all); hipFree(p->d_act[0]); hipFree(p->d_act[1]);
-  hipFree(p->d_cand); hipFree(p->d_tier_lists); hipFree(p->d_tier_cnt); hipFree(p->d_tier_cap); hipFree(p->d_big); hipFree(p->d_red);
-  hipFree(p->d_ovf);
+  hipFree(p->d_cand); hipFree(p->d_tier_lists); hipFree(p->d_tier_cnt); hipFree(p->d_tier_cap); hipFree(p->d_big);
+  hipFree(p->d_ovf); hipFree(p->d_gath);
   hipFree(p->d_maxdiff); hipFree(p->d_stats); hipFree(p->d_work); hipFree(p->d_scratch);
   hipFree(p->d_out_ids); hipFree(p->d_out_sc); hipFree(p->d_out_len);
   if (p->ev_a) hipEventDestroy(p->ev_a);
@@ -118,6 +125,8 @@ inline void plan_free(ppr_plan* p) {
   if (p->ev_m1) hipEventDestroy(p->ev_m1);
   if (p->comm) ncclCommDestroy(p->comm);
   hipFree(p->d_xsend); hipFree(p->d_xrecv);
+  if (p->h_hub_pin) hipHostFree(p->h_hub_pin);
+  if (p->h_desc_pin) hipHostFree(p->h_desc_pin);
   if (p->d_diag) {
     unsigned long long h[160];
     if (hipMemcpy(h, p->d_diag, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
@@ -140,6 +149,18 @@ inline int check_params(uint32_t K, uint32_t L, uint32_t iterations, double damp
   if (K > L) return PPR_ERR_KL;
   if (iterations == 0) return PPR_ERR_ITERS;
   if (damping < 0 || damping > 1) return PPR_ERR_DAMPING;
+  return PPR_OK;
+}
+
+// grow-only pinned host buffer
+inline int ensure_pinned(void** ptr, size_t* cap, size_t need) {
+  if (need <= *cap) return PPR_OK;
+  if (*ptr) hipHostFree(*ptr);
+  *ptr = nullptr;
+  *cap = 0;
+  need = need + need / 4 + 4096;
+  if (hipHostMalloc(ptr, need, hipHostMallocDefault) != hipSuccess) return PPR_ERR_OOM;
+  *cap = need;
   return PPR_OK;
 }
 
