@@ -155,7 +155,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     const char* e3 = getenv("PPR_BW_MODE");
     const char* e4 = getenv("PPR_BW_NG");
     const char* e5 = getenv("PPR_BW_WAVES");
-    (void)e3;
+    p->hub_bw_owner = e3 ? atoi(e3) != 0 : false;  // PPR_BW_MODE=1: owner-slot accumulation (measured 6 % slower)
     p->hub_bw_ng = (e4 && atoi(e4) == 8) ? 8 : 4;
     p->hub_bw_waves = e5 ? std::max(1, std::min(4, atoi(e5))) : 1;
     const char* e6 = getenv("PPR_HUB_SLICE");
@@ -169,8 +169,9 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     const int per_cu = std::max<int>(1, std::min<int>(32 / p->hub_bw_waves, (int)((160 * 1024) / p->hub_lds_wave)));
     p->hub_bw_blocks = p->num_cus * per_cu;
   }
-  hipFuncSetAttribute((const void*)k_hub_bucket_w<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_bucket_w<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_bucket_w<4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_bucket_w<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_bucket_w<4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_count, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -295,17 +296,22 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   }
   HubDesc* desc = (HubDesc*)p->h_desc_pin;
   size_t nd_all = 0;
+  auto logp_of = [&](int64_t need) {
+    return std::max(1, std::min(HUB_MAX_LOGP, ceil_log2((need + p->hub_bucket - 1) / p->hub_bucket)));
+  };
+  // hubs stay in list order: batches mixing large and small sources hide the long hot-key
+  // buckets of the large ones (grouping them by size measured 10 % slower)
   {
-    size_t i = 0;
-    while (i < nbig) {
+    size_t oi = 0;
+    while (oi < nbig) {
       Batch b{nd_all, 0, 0, 0, 0, 0, 0, 0, 0, 1};
-      while (i < nbig) {
+      while (oi < nbig) {
+        const size_t i = oi;
         const int v = big[i];
         const int64_t need = cand[i];
         const int64_t deg = cand[nbig + i];
         if (nd_all > b.d0 && b.stg + need > budget) break;
-        int logP = ceil_log2((need + p->hub_bucket - 1) / p->hub_bucket);
-        logP = std::max(1, std::min(HUB_MAX_LOGP, logP));
+        const int logP = logp_of(need);
         const int P = 1 << logP;
         const int tw = (int)std::max<int64_t>(1, std::min<int64_t>(HUB_TILE, HUB_TILE_CAND / L));
         const int T = (int)((deg + tw - 1) / tw);
@@ -322,7 +328,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
         b.nbuck += P;
         b.nrt += nsl;
         b.maxP = std::max(b.maxP, P);
-        i++;
+        oi++;
       }
       b.d1 = nd_all;
       batches.push_back(b);
@@ -415,12 +421,15 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       const int wpb = p->hub_bw_waves;
       const int64_t blocks = (nbuck + wpb - 1) / wpb;
       const dim3 grid((unsigned)blocks), blk(64 * wpb);
-      if (p->hub_bw_ng == 8)
-        hipLaunchKernelGGL(k_hub_bucket_w<8>, grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_lc, d_st, d_pk, d_ps,
-                           d_pc, d_gl, d_lc + 1, p->hub_wave_t);
+      if (p->hub_bw_owner)
+        hipLaunchKernelGGL((k_hub_bucket_w<4, true>), grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_lc, d_st, d_pk,
+                           d_ps, d_pc, d_gl, d_lc + 1, p->hub_wave_t);
+      else if (p->hub_bw_ng == 8)
+        hipLaunchKernelGGL((k_hub_bucket_w<8, false>), grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_lc, d_st, d_pk,
+                           d_ps, d_pc, d_gl, d_lc + 1, p->hub_wave_t);
       else
-        hipLaunchKernelGGL(k_hub_bucket_w<4>, grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_lc, d_st, d_pk, d_ps,
-                           d_pc, d_gl, d_lc + 1, p->hub_wave_t);
+        hipLaunchKernelGGL((k_hub_bucket_w<4, false>), grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_lc, d_st, d_pk,
+                           d_ps, d_pc, d_gl, d_lc + 1, p->hub_wave_t);
       HIP_OK(hipGetLastError());
     }
     // spilled buckets (distinct keys beyond the wave table): persistent workgroups over the spill

@@ -39,7 +39,10 @@ constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per redu
 // wave bucket LDS: acc f64[T] | keys i32[T] | cnt u16[T] | vals f64[CHUNK] | touched u16[CHUNK] |
 // tof u16[CHUNK + 2]; the radix histogram of the final select (1 KB) aliases vals
 __host__ __device__ constexpr size_t hub_wave_lds(int T, int ng) {
-  return (size_t)T * 14 + (size_t)(ng * WAVE) * 12 + 4;
+  // chunk mode: acc | keys | cnt u16 | vals | touched | tof;  owner mode: acc | keys | own u32 | hist
+  return ((size_t)T * 14 + (size_t)(ng * WAVE) * 12 + 4) > ((size_t)T * 16 + 1024)
+             ? ((size_t)T * 14 + (size_t)(ng * WAVE) * 12 + 4)
+             : ((size_t)T * 16 + 1024);
 }
 
 struct HubDesc {
@@ -114,11 +117,10 @@ __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& 
   }
   const int incl = wave_incl_scan(ln);
   const int total = __shfl(incl, WAVE - 1);
-  // HUB_TW_BATCH groups of 64 candidates are gathered before any is handed to f (one memory
-  // latency per batch); f still sees them in stream order
-  for (int g0 = 0; g0 < total; g0 += WAVE * HUB_TW_BATCH) {
-    int key[HUB_TW_BATCH];
-    double sv[HUB_TW_BATCH];
+  // HUB_TW_BATCH groups of 64 candidates are gathered together (one memory latency per batch),
+  // and the next batch is in flight while f consumes the current one; f still sees the
+  // candidates in stream order
+  auto load = [&](int g0, int (&key)[HUB_TW_BATCH], double (&sv)[HUB_TW_BATCH]) {
 #pragma unroll
     for (int k = 0; k < HUB_TW_BATCH; k++) {
       const int c = g0 + k * WAVE + lane_id();
@@ -142,6 +144,14 @@ __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& 
         sv[k] = s.sc[r];
       }
     }
+  };
+  int key[HUB_TW_BATCH], nkey[HUB_TW_BATCH];
+  double sv[HUB_TW_BATCH], nsv[HUB_TW_BATCH];
+  if (total > 0) load(0, nkey, nsv);
+  for (int g0 = 0; g0 < total; g0 += WAVE * HUB_TW_BATCH) {
+#pragma unroll
+    for (int k = 0; k < HUB_TW_BATCH; k++) { key[k] = nkey[k]; sv[k] = nsv[k]; }
+    if (g0 + WAVE * HUB_TW_BATCH < total) load(g0 + WAVE * HUB_TW_BATCH, nkey, nsv);
 #pragma unroll
     for (int k = 0; k < HUB_TW_BATCH; k++) {
       if (g0 + k * WAVE >= total) break;  // uniform
@@ -198,10 +208,15 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   const HubTask tk = tasks[w];
   const HubDesc d = desc[tk.d];
   const int P = 1 << d.logP;
+  // running staging position of every bucket for this tile, seeded from the scanned count
+  // matrix once (one strided gather), so the per-group scatter never waits on global memory
+  // (offsets are relative to the source's staging start: they fit 32 bits)
   uint32_t* run = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * maxP;
-  for (int i = lane_id(); i < P; i += WAVE) run[i] = 0;
+  const int64_t base0 = d.st_off;
+  for (int i = lane_id(); i < P; i += WAVE) run[i] = (uint32_t)(cm[d.cm_off + (int64_t)i * d.T + tk.x] - base0);
   wave_fence();
   const uint64_t lt = lanemask_lt();
+  HubRec* stv = st + base0;
   hub_tile_walk(g, s, a, d.v, tk.x, d.tw, [&](bool valid, int key, double sv) {
     const uint32_t dg = valid ? hub_digit(key, d.logP) : 0u;
     // lanes holding the same digit: AND of per-bit ballots (stable rank = lower lanes first)
@@ -215,8 +230,7 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
     wave_fence();
     if (valid) {
       if (rank == 0) run[dg] = base + (uint32_t)__popcll(match);
-      const int64_t pos = (int64_t)cm[d.cm_off + (int64_t)dg * d.T + tk.x] + base + rank;
-      st[pos] = HubRec{key, 0, sv};
+      stv[base + rank] = HubRec{key, 0, sv};
     }
     wave_fence();
   });
@@ -259,7 +273,7 @@ __global__ void __launch_bounds__(256) k_hub_prep(DevGraph g, IterArgs a, const 
 // Bucket waves: one wave per bucket, its work record resolved by k_hub_prep. Per bucket: private LDS table (T slots, 3/4 usable; a bucket with more distinct
 // keys spills to k_hub_bucket), chunks of NG groups loaded at once and accumulated with
 // chunk_accumulate, then the keys >= tau, at most L of them, appended to the source's list.
-template <int NG>
+template <int NG, bool OWNER>
 __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, const BucketWork* bw,
                                                       int64_t nbuck, uint32_t* next, const HubRec* st,
                                                       int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
@@ -277,7 +291,9 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
   ck.vals = reinterpret_cast<double*>(base + (size_t)T * 14);
   ck.touched = reinterpret_cast<uint16_t*>(base + (size_t)T * 14 + (size_t)(NG * WAVE) * 8);
   ck.tof = ck.touched + NG * WAVE;
-  uint32_t* hist = reinterpret_cast<uint32_t*>(ck.vals);  // final select only (after accumulation)
+  uint32_t* own = reinterpret_cast<uint32_t*>(base + (size_t)T * 12);  // OWNER mode (aliases cnt/vals)
+  uint32_t* hist = OWNER ? reinterpret_cast<uint32_t*>(base + (size_t)T * 16)
+                         : reinterpret_cast<uint32_t*>(ck.vals);  // final select only (after accumulation)
   const int l = lane_id();
   const int Lw = s.L;
   const int budget = T / 4 * 3;
@@ -290,7 +306,8 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
   {
     const long long t_start = a.diag ? (long long)clock64() : 0;
     const int nb = W.nb;
-    for (int i = l; i < T; i += WAVE) { t.keys[i] = EMPTY; ck.cnt[i] = 0; }
+    if (OWNER) { for (int i = l; i < T; i += WAVE) { t.keys[i] = EMPTY; own[i] = 0xffu; } }
+    else { for (int i = l; i < T; i += WAVE) { t.keys[i] = EMPTY; ck.cnt[i] = 0; } }
     wave_fence();
     int fill = 0;
     if (W.seed >= 0) {
@@ -335,7 +352,12 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
         wave_fence();
       }
       if (overflow) break;
-      chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, W.factor);
+      if (OWNER) {
+#pragma unroll
+        for (int k = 0; k < NG; k++) apply_group_owner(t.acc, own, cv[k], sl[k], cs[k], W.factor);
+      } else {
+        chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, W.factor);
+      }
     }
     if (overflow) {
       if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = HubTask{W.d, W.x}; }
@@ -345,26 +367,25 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
         atomicAdd(&a.diag[bin], 1ull);
         atomicAdd(&a.diag[32 + bin], (unsigned long long)((long long)clock64() - t_start));
       }
-      int U = table_compact(t);
-      // keep what can still reach the top-L: value >= tau (in place, order irrelevant)
-      {
-        int U2 = 0;
-        for (int i0 = 0; i0 < U; i0 += WAVE) {
-          const int i = i0 + l;
-          const int k = i < U ? t.keys[i] : 0;
-          const double x = i < U ? t.acc[i] : 0.0;
-          const bool keep = i < U && x >= W.tau;
-          const uint64_t m = __ballot(keep);
-          wave_fence();
-          if (keep) { const int pos = U2 + __popcll(m & lanemask_lt()); t.keys[pos] = k; t.acc[pos] = x; }
-          U2 += __popcll(m);
-          wave_fence();
-        }
-        if (a.diag && l == 0) {  // distinct keys / kept keys per bucket
-          atomicAdd(&a.diag[64 + (31 - __clz(U | 1))], 1ull);
-          atomicAdd(&a.diag[96 + (31 - __clz(U2 | 1))], 1ull);
-        }
-        U = U2;
+      // compact the occupied slots that can still reach the top-L (value >= tau) to the front, in
+      // one pass (writes land at or below the slots already read)
+      int U = 0, Uall = 0;
+      for (int i0 = 0; i0 < T; i0 += WAVE) {
+        const int i = i0 + l;
+        const int k = t.keys[i];
+        const double x = t.acc[i];
+        const bool occ = k != EMPTY;
+        const bool keep = occ && x >= W.tau;
+        const uint64_t m = __ballot(keep);
+        if (a.diag) Uall += __popcll(__ballot(occ));
+        wave_fence();
+        if (keep) { const int pos = U + __popcll(m & lanemask_lt()); t.keys[pos] = k; t.acc[pos] = x; }
+        U += __popcll(m);
+        wave_fence();
+      }
+      if (a.diag && l == 0) {  // distinct keys / kept keys per bucket
+        atomicAdd(&a.diag[64 + (31 - __clz(Uall | 1))], 1ull);
+        atomicAdd(&a.diag[96 + (31 - __clz(U | 1))], 1ull);
       }
       const int cnt = U <= Lw ? U : Lw;
       if (cnt > 0) {

@@ -84,6 +84,7 @@ struct ppr_plan {
   size_t gath_bytes = 0;
   int num_cus = 256;
   int hub_bw_blocks = 0;           // persistent k_hub_bucket_w grid
+  bool hub_bw_owner = false;       // PPR_BW_MODE: 1 owner-slot accumulation, 0 ballot chunks (default)
   int hub_bw_ng = 4;               // PPR_BW_NG: groups per chunk (4 or 8)
   int hub_bw_waves = 1;            // PPR_BW_WAVES: waves per block of k_hub_bucket_w
   int hub_slice = 8192;            // PPR_HUB_SLICE: k_hub_reduce slice (>= L)
