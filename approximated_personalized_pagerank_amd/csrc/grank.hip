@@ -104,6 +104,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   TRY(dalloc(&p->d_ids, slab));
   TRY(dalloc(&p->d_sc, slab));
   TRY(dalloc(&p->d_len, 2 * n));
+  TRY(dalloc(&p->d_rix, (size_t)2 * n * NRANGE));
+  TRY(dalloc(&p->d_rmin, 2 * n));
   TRY(dalloc(&p->d_all, n));
   TRY(dalloc(&p->d_cand, n));
   TRY(dalloc(&p->d_tier_lists, (size_t)NLISTS * (n > 0 ? n : 1)));
@@ -126,6 +128,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         (m && hipMemcpyAsync(p->d_colx, colx, 4 * m, hipMemcpyHostToDevice, st) != hipSuccess) ||
         hipMemsetAsync(p->d_part, 0, n, st) != hipSuccess ||
         hipMemsetAsync(p->d_len, 0, 8 * n, st) != hipSuccess ||
+        hipMemsetAsync(p->d_rix, 0, sizeof(uint16_t) * 2 * n * NRANGE, st) != hipSuccess ||
+        hipMemsetAsync(p->d_rmin, 0, 16 * n, st) != hipSuccess ||
         hipMemcpyAsync(p->d_all, all.data(), 4 * n, hipMemcpyHostToDevice, st) != hipSuccess) {
       plan_free(p); return PPR_ERR_HIP;
     }
@@ -174,6 +178,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   hipFuncSetAttribute((const void*)k_hub_bucket_w<4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_topk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_count, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   *out = p;
@@ -283,7 +288,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
                     std::vector<int32_t>& fallback) {
   hipStream_t st = p->stream;
   DevGraph g{p->d_rp, p->d_colx, p->n};
-  DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
+  const DevSlab s = dev_slab(p);
   const int64_t L = p->L;
   const int64_t budget = 1LL << 28;  // staged candidates per batch (4 GiB of 16-B records)
   const int slice = p->hub_slice;
@@ -482,7 +487,7 @@ static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, i
                           unsigned long long* maxdiff) {
   hipStream_t st = p->stream;
   DevGraph g{p->d_rp, p->d_colx, p->n};
-  DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
+  const DevSlab s = dev_slab(p);
   HIP_OK(hipMemsetAsync(p->d_tier_cnt, 0, sizeof(uint32_t) * (NLISTS + 2), st));
   const int64_t nb = (count + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(256), 0, st, g, s, a, list, count,
@@ -629,7 +634,7 @@ extern "C" int ppr_grank_plan_iterate(ppr_plan* p, int32_t it, int64_t begin, in
   int rc = run_merge(p, a, p->d_act[part] + begin, end - begin, md);
   if (rc) return rc;
   if (a.stats) {  // bytes of the rows this iteration wrote (outside the timed merge span)
-    DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
+    const DevSlab s = dev_slab(p);
     const int64_t cnt = end - begin;
     const unsigned blocks = (unsigned)std::min<int64_t>((cnt + 255) / 256, 1024);
     hipLaunchKernelGGL(k_stat_written, dim3(blocks), dim3(256), 0, p->stream, s, a,
@@ -660,10 +665,11 @@ extern "C" int ppr_grank_plan_finish(ppr_plan* p, int32_t iterations_run) {
 
 int launch_topk(ppr_plan* p, int sA, int sB) {
   if (p->n == 0) return PPR_OK;
-  DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
-  const int64_t blocks = (p->n + 3) / 4;
-  hipLaunchKernelGGL(k_topk, dim3((unsigned)blocks), dim3(256), 0, p->stream, s, p->d_part, sA, sB,
-                     (int)p->K, p->d_out_ids, p->d_out_sc, p->d_out_len);
+  const DevSlab s = dev_slab(p);
+  const int wpb = p->Lp <= 1024 ? 4 : 1;  // one wave per row, Lp * 12 B of LDS each
+  const int64_t blocks = (p->n + wpb - 1) / wpb;
+  hipLaunchKernelGGL(k_topk, dim3((unsigned)blocks), dim3(64 * wpb), (size_t)wpb * p->Lp * 12, p->stream, s,
+                     p->d_part, sA, sB, (int)p->K, p->Lp, p->d_out_ids, p->d_out_sc, p->d_out_len);
   HIP_OK(hipGetLastError());
   return PPR_OK;
 }
@@ -751,14 +757,21 @@ extern "C" int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, in
       HIP_OK(hipMemcpyAsync(tl.data(), p->d_len + (size_t)sl * p->n, 4 * p->n, hipMemcpyDeviceToHost, st));
       HIP_OK(hipStreamSynchronize(st));
     }
+    // rows are stored in hash order: hand them out sorted by (score desc, id asc)
+    std::vector<std::pair<double, int32_t>> row(L);
     for (int64_t v = 0; v < p->n; v++) {
       const int want = part[v] ? sB : sA;
       if (want != sl) continue;
-      if (len) len[v] = tl[v];
+      const int ln = tl[v];
+      if (len) len[v] = ln;
+      for (int i = 0; i < ln; i++) row[i] = {ts[v * L + i], ti[v * L + i]};
+      std::sort(row.begin(), row.begin() + ln, [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
+        return x.first > y.first || (x.first == y.first && x.second < y.second);
+      });
       for (size_t i = 0; i < L; i++) {
-        const bool in = (int)i < tl[v];
-        if (ids) ids[v * L + i] = in ? ti[v * L + i] : -1;
-        if (scores) scores[v * L + i] = in ? ts[v * L + i] : 0.0;
+        const bool in = (int)i < ln;
+        if (ids) ids[v * L + i] = in ? row[i].second : -1;
+        if (scores) scores[v * L + i] = in ? row[i].first : 0.0;
       }
     }
   }
@@ -768,7 +781,7 @@ extern "C" int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, in
 extern "C" int ppr_grank_plan_row_bytes(ppr_plan* p, int64_t* bytes) {
   if (!p || !bytes) return PPR_ERR_ARG;
   const int64_t Le = ((int64_t)p->L + 1) & ~1LL;
-  *bytes = 8 + 4 * Le + 8 * (int64_t)p->L;
+  *bytes = 8 + 4 * Le + 8 * (int64_t)p->L + 8 + 2 * NRANGE;
   return PPR_OK;
 }
 
@@ -781,7 +794,7 @@ static int pack_common(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void
   HIP_OK(hipSetDevice(p->device));
   const IterArgs a = iter_args(p, it, false);
   const int nxt = ((a.active == 1) ? a.sB : a.sA) ^ 1;
-  DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
+  const DevSlab s = dev_slab(p);
   int64_t rb = 0;
   ppr_grank_plan_row_bytes(p, &rb);
   const int Le = (int)(((int64_t)p->L + 1) & ~1LL);

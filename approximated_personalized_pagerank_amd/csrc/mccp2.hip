@@ -139,7 +139,7 @@ extern "C" int ppr_mccp2_plan_walk(ppr_plan* p, uint32_t walks, uint64_t seed, i
   m.T = p->mc_T;
   m.slot = 1;
   DevGraph g{p->d_rp, p->d_colx, p->n};
-  DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
+  const DevSlab s = dev_slab(p);
   HIP_OK(hipEventRecord(p->ev_m0, p->stream));
   hipLaunchKernelGGL(k_mc_walk, dim3((unsigned)(end - begin)), dim3(64), mc_wave_lds(p->mc_T), p->stream, g, s, m,
                      p->d_mc_walk + begin, end - begin);
@@ -157,9 +157,9 @@ extern "C" int ppr_mccp2_plan_combine(ppr_plan* p) {
   if (!p || !p->mc) return PPR_ERR_ARG;
   if (p->n == 0) return PPR_OK;
   HIP_OK(hipSetDevice(p->device));
-  DevSlab s{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L};
+  const DevSlab s = dev_slab(p);
   if (p->mc_ndangling) {
-    hipLaunchKernelGGL(k_mc_selfrow, dim3((unsigned)((p->mc_ndangling + 255) / 256)), dim3(256), 0, p->stream, s,
+    hipLaunchKernelGGL(k_mc_selfrow, dim3((unsigned)((p->mc_ndangling + 3) / 4)), dim3(256), 0, p->stream, s,
                        p->d_mc_dangling, p->mc_ndangling, 0);
     HIP_OK(hipGetLastError());
   }

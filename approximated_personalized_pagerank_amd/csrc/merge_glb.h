@@ -110,26 +110,42 @@ __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArg
 }
 
 // ---------------------------------------------------------------------------------------------
-// final top-K (include/grank.h:143-147): rows are sorted, so top-K is the first min(K, len)
-__global__ void k_topk(DevSlab s, const uint8_t* part, int sA, int sB, int K, int32_t* oid,
-                       double* osc, int32_t* olen) {
-  const int64_t v = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
+// final top-K (include/grank.h:143-147): the stored row is in hash order, so each wave loads it
+// into LDS, sorts it by (score desc, id asc) and writes the first min(K, len) entries
+__global__ void __launch_bounds__(256) k_topk(DevSlab s, const uint8_t* part, int sA, int sB, int K, int Lp,
+                                              int32_t* oid, double* osc, int32_t* olen) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int wv = threadIdx.x >> 6;
+  const int64_t v = (int64_t)blockIdx.x * (blockDim.x / WAVE) + wv;
   if (v >= s.n) return;
+  uint64_t* rv = reinterpret_cast<uint64_t*>(smem) + (size_t)wv * Lp;
+  int* rk = reinterpret_cast<int*>(smem + (size_t)(blockDim.x / WAVE) * Lp * 8) + (size_t)wv * Lp;
   const int sl = part[v] ? sB : sA;
   const int len = s.len[s.lrow(sl, v)];
   const int k = len < K ? len : K;
   const int64_t r = s.row(sl, v);
+  for (int i = lane_id(); i < len; i += WAVE) { rv[i] = dbits(s.sc[r + i]); rk[i] = s.ids[r + i]; }
+  wave_fence();
+  row_sort(rv, rk, len, Lp);
   for (int i = lane_id(); i < K; i += WAVE) {
-    oid[v * K + i] = i < k ? s.ids[r + i] : -1;
-    osc[v * K + i] = i < k ? s.sc[r + i] : 0.0;
+    oid[v * K + i] = i < k ? rk[i] : -1;
+    osc[v * K + i] = i < k ? bitsd(rv[i]) : 0.0;
   }
   if (lane_id() == 0) olen[v] = k;
 }
 
 // Row exchange for source sharding. Packed row r (of sources list[0..count)) occupies
-// row_bytes = 8 + 4*Le + 8*L bytes: int32 len, int32 pad, int32 ids[Le] (Le = L rounded up to
-// even, so the f64 scores stay 8-byte aligned), f64 scores[L]. Rows are the next-slot baskets
-// the iteration wrote.
+// row_bytes = 8 + 4*Le + 8*L + 8 + 2*NRANGE bytes: int32 len, int32 pad, int32 ids[Le] (Le = L
+// rounded up to even, so the f64 scores stay 8-byte aligned), f64 scores[L], f64 row minimum,
+// u16 range index[NRANGE]. Rows are the next-slot baskets the iteration wrote (stored order).
+__device__ __forceinline__ void packed_row_parts(unsigned char* row, int Le, int L, int32_t*& rid, double*& rsc,
+                                                 double*& rmn, uint16_t*& rix) {
+  rid = reinterpret_cast<int32_t*>(row + 8);
+  rsc = reinterpret_cast<double*>(row + 8 + 4 * (int64_t)Le);
+  rmn = reinterpret_cast<double*>(row + 8 + 4 * (int64_t)Le + 8 * (int64_t)L);
+  rix = reinterpret_cast<uint16_t*>(row + 8 + 4 * (int64_t)Le + 8 * (int64_t)L + 8);
+}
+
 __global__ void k_pack_rows(DevSlab s, int nxt, const int32_t* list, int64_t count,
                             unsigned char* buf, int64_t row_bytes, int Le) {
   const int64_t r = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
@@ -137,11 +153,16 @@ __global__ void k_pack_rows(DevSlab s, int nxt, const int32_t* list, int64_t cou
   const int v = list[r];
   unsigned char* row = buf + r * row_bytes;
   const int len = s.len[s.lrow(nxt, v)];
-  int32_t* rid = reinterpret_cast<int32_t*>(row + 8);
-  double* rsc = reinterpret_cast<double*>(row + 8 + 4 * (int64_t)Le);
+  int32_t* rid; double* rsc; double* rmn; uint16_t* rix;
+  packed_row_parts(row, Le, s.L, rid, rsc, rmn, rix);
   const int64_t src = s.row(nxt, v);
   for (int i = lane_id(); i < len; i += WAVE) { rid[i] = s.ids[src + i]; rsc[i] = s.sc[src + i]; }
-  if (lane_id() == 0) { reinterpret_cast<int32_t*>(row)[0] = len; reinterpret_cast<int32_t*>(row)[1] = 0; }
+  rix[lane_id()] = s.rix[s.xrow(nxt, v) + lane_id()];
+  if (lane_id() == 0) {
+    reinterpret_cast<int32_t*>(row)[0] = len;
+    reinterpret_cast<int32_t*>(row)[1] = 0;
+    *rmn = s.rmin[s.lrow(nxt, v)];
+  }
 }
 
 __global__ void k_unpack_rows(DevSlab s, int nxt, const int32_t* list, int64_t count,
@@ -149,13 +170,14 @@ __global__ void k_unpack_rows(DevSlab s, int nxt, const int32_t* list, int64_t c
   const int64_t r = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
   if (r >= count) return;
   const int v = list[r];
-  const unsigned char* row = buf + r * row_bytes;
+  unsigned char* row = const_cast<unsigned char*>(buf) + r * row_bytes;
   const int len = reinterpret_cast<const int32_t*>(row)[0];
-  const int32_t* rid = reinterpret_cast<const int32_t*>(row + 8);
-  const double* rsc = reinterpret_cast<const double*>(row + 8 + 4 * (int64_t)Le);
+  int32_t* rid; double* rsc; double* rmn; uint16_t* rix;
+  packed_row_parts(row, Le, s.L, rid, rsc, rmn, rix);
   const int64_t dst = s.row(nxt, v);
   for (int i = lane_id(); i < len; i += WAVE) { s.ids[dst + i] = rid[i]; s.sc[dst + i] = rsc[i]; }
-  if (lane_id() == 0) s.len[s.lrow(nxt, v)] = len;
+  s.rix[s.xrow(nxt, v) + lane_id()] = rix[lane_id()];
+  if (lane_id() == 0) { s.len[s.lrow(nxt, v)] = len; s.rmin[s.lrow(nxt, v)] = *rmn; }
 }
 
 __global__ void k_zero_u64(unsigned long long* p, int n) {

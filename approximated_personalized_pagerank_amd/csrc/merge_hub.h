@@ -22,7 +22,7 @@ namespace pprk {
 //   k_hub_final    workgroup per source: top-L of the appended bucket results, row, norm1
 // Pruning bound: every contribution is >= 0, so a key's final value is at least any single
 // contribution, fma(s, f, acc) >= round(s * f) (monotone rounding). A successor u with a full
-// sorted row (len = L) thus puts L distinct keys at >= round(min(row u) * f), and
+// row (len = L) thus puts L distinct keys at >= round(rmin[u] * f), and
 //     tau = round(f * max_{u: len[u] = L} min(row u))
 // is a lower bound of the L-th largest final value: a bucket never needs to emit a key below tau
 // (ties at tau are kept, the (score desc, id asc) order decides them in k_hub_final).
@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
       const int32_t cx = g.colx[i];
       const int u = cx & 0x7fffffff;
       const int sl = read_slot(a, cx);
-      if (s.len[s.lrow(sl, u)] == s.L) mb = dbits(s.sc[s.row(sl, u) + s.L - 1]);  // row minimum
+      if (s.len[s.lrow(sl, u)] == s.L) mb = dbits(s.rmin[s.lrow(sl, u)]);  // row minimum
     }
 #pragma unroll
     for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }

@@ -141,7 +141,8 @@ __global__ void __launch_bounds__(64) k_mc_walk(DevGraph g, DevSlab s, McArgs m,
   const int L = s.L;
   const int64_t rs = s.row(m.slot, src);
   if (g.rp[src + 1] == g.rp[src]) {
-    if (l == 0) { s.ids[rs] = src; s.sc[rs] = 1.0; s.len[s.lrow(m.slot, src)] = 1; }
+    s.rix[s.xrow(m.slot, src) + l] = row_range(src) <= (uint32_t)l ? 1 : 0;
+    if (l == 0) { s.ids[rs] = src; s.sc[rs] = 1.0; s.len[s.lrow(m.slot, src)] = 1; s.rmin[s.lrow(m.slot, src)] = 1.0; }
     return;
   }
   for (int i = l; i < m.T; i += WAVE) t.keys[i] = EMPTY;
@@ -210,8 +211,7 @@ __global__ void __launch_bounds__(64) k_mc_walk(DevGraph g, DevSlab s, McArgs m,
   }
 
   // basket: held keys, count / R (include/mccompletepathv2.h:159-160), compacted in place to the
-  // front of the table and sorted (score desc, id asc) like every other basket row, so its last
-  // entry is its minimum (the hub pipeline's pruning bound reads it)
+  // front of the table and stored like every other basket row (hash order, range index, minimum)
   const double R = (double)m.R;
   uint64_t* rv = reinterpret_cast<uint64_t*>(t.cnt);
   int U = 0;
@@ -231,20 +231,25 @@ __global__ void __launch_bounds__(64) k_mc_walk(DevGraph g, DevSlab s, McArgs m,
     wave_fence();
   }
   const int Lp = L <= 1 ? 1 : (1 << (32 - __clz(L - 1)));
-  row_sort(rv, t.keys, U, Lp);
-  for (int i = l; i < U; i += WAVE) { s.ids[rs + i] = t.keys[i]; s.sc[rs + i] = bitsd(rv[i]); }
-  if (l == 0) s.len[s.lrow(m.slot, src)] = U;
+  (void)rs;
+  write_row(s, m.slot, src, rv, t.keys, U, Lp, false, 1.0);
 }
 
-// final basket of a dangling node: {v: 1.0} (include/mccompletepathv2.h:214, factor 1.0)
+// final basket of a dangling node: {v: 1.0} (include/mccompletepathv2.h:214, factor 1.0);
+// one wave per node (lane q writes range-index entry q)
 __global__ void __launch_bounds__(256) k_mc_selfrow(DevSlab s, const int32_t* list, int64_t count, int slot) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
   if (i >= count) return;
   const int v = list[i];
-  const int64_t r = s.row(slot, v);
-  s.ids[r] = v;
-  s.sc[r] = 1.0;
-  s.len[s.lrow(slot, v)] = 1;
+  const uint32_t q = (uint32_t)lane_id();
+  s.rix[s.xrow(slot, v) + q] = row_range(v) <= q ? 1 : 0;
+  if (q == 0) {
+    const int64_t r = s.row(slot, v);
+    s.ids[r] = v;
+    s.sc[r] = 1.0;
+    s.len[s.lrow(slot, v)] = 1;
+    s.rmin[s.lrow(slot, v)] = 1.0;
+  }
 }
 
 }  // namespace pprk

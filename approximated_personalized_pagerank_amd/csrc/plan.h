@@ -46,6 +46,8 @@ struct ppr_plan {
   int32_t* d_ids = nullptr;
   double* d_sc = nullptr;
   int32_t* d_len = nullptr;
+  uint16_t* d_rix = nullptr;      // [2][n][NRANGE] row range index
+  double* d_rmin = nullptr;       // [2][n] row minimum
   int32_t* d_all = nullptr;       // 0..n-1 (init list)
   int32_t* d_act[2] = {nullptr, nullptr};
   int64_t nact[2] = {0, 0};
@@ -114,7 +116,7 @@ struct ppr_plan {
 
 inline void plan_free(ppr_plan* p) {
   if (!p) return;
-  hipFree(p->d_rp); hipFree(p->d_colx); hipFree(p->d_part); hipFree(p->d_ids); hipFree(p->d_sc);
+  hipFree(p->d_rp); hipFree(p->d_colx); hipFree(p->d_part); hipFree(p->d_ids); hipFree(p->d_sc); hipFree(p->d_rix); hipFree(p->d_rmin);
   hipFree(p->d_len); hipFree(p->d_all); hipFree(p->d_act[0]); hipFree(p->d_act[1]);
   hipFree(p->d_cand); hipFree(p->d_tier_lists); hipFree(p->d_tier_cnt); hipFree(p->d_tier_cap); hipFree(p->d_big);
   hipFree(p->d_ovf); hipFree(p->d_gath);
@@ -151,6 +153,10 @@ inline int check_params(uint32_t K, uint32_t L, uint32_t iterations, double damp
   if (iterations == 0) return PPR_ERR_ITERS;
   if (damping < 0 || damping > 1) return PPR_ERR_DAMPING;
   return PPR_OK;
+}
+
+inline DevSlab dev_slab(const ppr_plan* p) {
+  return DevSlab{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L, p->d_rix, p->d_rmin};
 }
 
 // grow-only pinned host buffer

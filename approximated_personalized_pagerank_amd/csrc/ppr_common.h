@@ -49,15 +49,63 @@ struct DevGraph {
   int64_t n;
 };
 
+// Basket rows are stored in ascending hash_b(key) order, with a 64-entry range index per row:
+// rix[r] = number of entries whose key lies in hash range <= r (range = top 6 bits of hash_b),
+// so the entries of any hash-prefix bucket form one contiguous segment of every row (the
+// segmented hub merge reads them without a partition pass), and rmin = the row's smallest score
+// (the hubs' top-L pruning bound).
+constexpr int NRANGE = 64;
+constexpr int RANGE_BITS = 6;
+__device__ __forceinline__ uint32_t row_range(int key) { return hash_b((uint32_t)key) >> (32 - RANGE_BITS); }
+
 struct DevSlab {
   int32_t* ids;
   double* sc;
   int32_t* len;
   int64_t n;
   int32_t L;
+  uint16_t* rix;   // [2][n][NRANGE]
+  double* rmin;    // [2][n]
   __device__ __forceinline__ int64_t row(int slot, int64_t u) const { return ((int64_t)slot * n + u) * L; }
   __device__ __forceinline__ int64_t lrow(int slot, int64_t u) const { return (int64_t)slot * n + u; }
+  __device__ __forceinline__ int64_t xrow(int slot, int64_t u) const { return ((int64_t)slot * n + u) * NRANGE; }
 };
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) { const uint64_t y = (uint64_t)__shfl_xor((unsigned long long)x, o); x = y < x ? y : x; }
+  return x;
+}
+
+// Store a finished row of cnt entries held in LDS (rv = score bits, rk = ids) into slot `slot` of
+// node v: sorted in place by hash_b(key), scores multiplied by `scale` when `scaled` (MC), plus
+// the range index and the row minimum. One wave.
+__device__ __forceinline__ void write_row(const DevSlab& s, int slot, int v, uint64_t* rv, int* rk, int cnt,
+                                          int Lp, bool scaled, double scale) {
+  row_sort_hash(rv, rk, cnt, Lp);
+  const int64_t r = s.row(slot, v);
+  uint64_t mn = ~0ull;
+  for (int i = lane_id(); i < cnt; i += WAVE) {
+    double x = bitsd(rv[i]);
+    if (scaled) x *= scale;
+    s.ids[r + i] = rk[i];
+    s.sc[r + i] = x;
+    const uint64_t b = dbits(x);
+    mn = b < mn ? b : mn;
+  }
+  mn = wave_min_u64(mn);
+  // lane q: entries with range <= q (ranges ascend along the sorted row)
+  const uint32_t q = (uint32_t)lane_id();
+  int pos = 0;
+  for (int b = Lp; b; b >>= 1)
+    if (pos + b <= cnt && row_range(rk[pos + b - 1]) <= q) pos += b;
+  s.rix[s.xrow(slot, v) + q] = (uint16_t)pos;
+  if (lane_id() == 0) {
+    s.len[s.lrow(slot, v)] = cnt;
+    s.rmin[s.lrow(slot, v)] = cnt ? bitsd(mn) : 0.0;
+  }
+  wave_fence();
+}
 
 struct IterArgs {
   int sA, sB;        // read slot of successors whose colx bit 31 is 0 / 1
@@ -118,31 +166,23 @@ __device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt v
     cnt = L;
   }
   wave_fence();
-  row_sort(rv, rk, cnt, Lp);
   if (a.unit) {
     // init writes both slots: a dangling source never updates, so its basket must be valid in
     // whichever slot its partition reads
-    for (int sl = 0; sl < 2; sl++) {
-      const int64_t r = s.row(sl, v);
-      for (int i = lane_id(); i < cnt; i += WAVE) { s.ids[r + i] = rk[i]; s.sc[r + i] = bitsd(rv[i]); }
-      if (lane_id() == 0) s.len[s.lrow(sl, v)] = cnt;
-    }
+    write_row(s, 0, v, rv, rk, cnt, Lp, false, 1.0);
+    write_row(s, 1, v, rv, rk, cnt, Lp, false, 1.0);
     return;
   }
   if (a.mc) {
-    // keepTop(L) first, then `*= factor` (include/mccompletepathv2.h:243-247); the row stays in
-    // the order of the unscaled scores, which scaling by factor > 0 does not invert
+    // keepTop(L) first, then `*= factor` (include/mccompletepathv2.h:243-247)
     const double f = a.damping / (double)(a.rp[v + 1] - a.rp[v]);
-    const int64_t r = s.row(0, v);
-    for (int i = lane_id(); i < cnt; i += WAVE) { s.ids[r + i] = rk[i]; s.sc[r + i] = bitsd(rv[i]) * f; }
-    if (lane_id() == 0) s.len[s.lrow(0, v)] = cnt;
+    write_row(s, 0, v, rv, rk, cnt, Lp, true, f);
     return;
   }
   const int cur = (a.active == 1) ? a.sB : a.sA;
   const int nxt = cur ^ 1;
-  const int64_t r = s.row(nxt, v);
-  for (int i = lane_id(); i < cnt; i += WAVE) { s.ids[r + i] = rk[i]; s.sc[r + i] = bitsd(rv[i]); }
-  if (lane_id() == 0) s.len[s.lrow(nxt, v)] = cnt;
+  // rv/rk are left in the stored (hash) order: norm1 walks the new row in that order
+  write_row(s, nxt, v, rv, rk, cnt, Lp, false, 1.0);
   const int64_t ro = s.row(cur, v);
   const int olen = s.len[s.lrow(cur, v)];
   const double d1 = row_norm1(rv, rk, cnt, s.ids + ro, s.sc + ro, olen, hk, hv, mf, 2 * Lp);

@@ -38,6 +38,10 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   return x;
 }
 
+// the basket-row order and the hub key-bucket digit: rows are stored by ascending hash_b(key)
+// (a bijection of the 32-bit id space, so distinct keys never tie)
+__device__ __forceinline__ uint32_t hash_b(uint32_t x) { return hash32(x ^ 0x9e3779b9u); }
+
 __device__ __forceinline__ int wave_incl_scan(int x) {
 #pragma unroll
   for (int o = 1; o < WAVE; o <<= 1) {
@@ -400,6 +404,30 @@ __device__ __forceinline__ void row_sort(uint64_t* rv, int* rk, int cnt, int Lp)
         // descending overall: blocks with (i & k) == 0 descend
         const bool desc = (i & k) == 0;
         const bool swap = desc ? row_less(av, ak, bv, bk) : row_less(bv, bk, av, ak);
+        if (swap) { rv[i] = bv; rv[p] = av; rk[i] = bk; rk[p] = ak; }
+      }
+      wave_fence();
+    }
+  }
+}
+
+// Row buffer sorted by ascending hash_b(key) (the stored basket order); EMPTY keys sort last.
+__device__ __forceinline__ uint64_t hash_order(int key) {
+  return key == EMPTY ? ~0ull : (uint64_t)hash_b((uint32_t)key);
+}
+__device__ __forceinline__ void row_sort_hash(uint64_t* rv, int* rk, int cnt, int Lp) {
+  for (int i = cnt + lane_id(); i < Lp; i += WAVE) { rv[i] = 0; rk[i] = EMPTY; }  // sentinels last
+  wave_fence();
+  for (int k = 2; k <= Lp; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = lane_id(); t < (Lp >> 1); t += WAVE) {
+        const int i = ((t / j) * 2 * j) + (t % j);
+        const int p = i + j;
+        const uint64_t av = rv[i], bv = rv[p];
+        const int ak = rk[i], bk = rk[p];
+        const uint64_t ha = hash_order(ak), hb = hash_order(bk);
+        const bool asc = (i & k) == 0;
+        const bool swap = asc ? (ha > hb) : (ha < hb);
         if (swap) { rv[i] = bv; rv[p] = av; rk[i] = bk; rk[p] = ak; }
       }
       wave_fence();

@@ -22,7 +22,6 @@ constexpr int WG_THREADS = WG_WAVES * WAVE;      // 512
 constexpr int WG_CHUNK = 2 * WG_THREADS;         // candidates per routing step
 constexpr int WG_WIN = WG_THREADS;               // successors per window
 
-__device__ __forceinline__ uint32_t hash_b(uint32_t x) { return hash32(x ^ 0x9e3779b9u); }
 
 // shared-table variant of table_slot with an occupancy budget (returns 0xffffffff when full)
 __device__ __forceinline__ uint32_t wg_slot(int* keys, double* acc, uint32_t T, uint32_t h0,

@@ -26,7 +26,8 @@
  *                                             stores rows in that order
  *   norm1        include/internal/pprInternal.h:147-165  sum |new-old| over the key union; the
  *                                             summation order here is the HIP kernel's fixed
- *                                             64-lane pattern (see norm1_rows) so maxDiff is
+ *                                             64-lane pattern over rows in their stored (hash)
+ *                                             order (norm1_rows, norm1_stored) so maxDiff is
  *                                             bit-identical too
  *   stop rule    include/grank.h:90-94,140   maxDiff[2] = {tol, tol}; loop while
  *                                             i < iterations && max(maxDiff) >= tol
@@ -133,6 +134,31 @@ static double norm1_rows(const int32_t* nid, const double* nsc, int32_t nlen,
   return p[0];
 }
 
+/* The HIP path stores every basket row in ascending hash_b(key) order (the hub merge reads
+ * hash-range segments of rows), and norm1 walks the rows in that stored order: restate it by
+ * sorting copies of both rows by hash_b before the fixed lane pattern above. */
+static uint32_t hash_b(uint32_t x) { return mix32(x ^ 0x9e3779b9u); }
+
+static int cmp_hash(const void* a, const void* b) {
+  const uint32_t x = hash_b((uint32_t)((const ent_t*)a)->key), y = hash_b((uint32_t)((const ent_t*)b)->key);
+  return (x > y) - (x < y);
+}
+
+static double norm1_stored(const int32_t* nid, const double* nsc, int32_t nlen,
+                           const int32_t* oid, const double* osc, int32_t olen) {
+  ent_t* e = (ent_t*)malloc(sizeof(ent_t) * (size_t)(nlen + olen + 1));
+  int32_t* ni = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nlen + olen + 1));
+  double* ns = (double*)malloc(sizeof(double) * (size_t)(nlen + olen + 1));
+  for (int32_t i = 0; i < nlen; i++) { e[i].key = nid[i]; e[i].sc = nsc[i]; }
+  for (int32_t j = 0; j < olen; j++) { e[nlen + j].key = oid[j]; e[nlen + j].sc = osc[j]; }
+  qsort(e, (size_t)nlen, sizeof(ent_t), cmp_hash);
+  qsort(e + nlen, (size_t)olen, sizeof(ent_t), cmp_hash);
+  for (int32_t i = 0; i < nlen + olen; i++) { ni[i] = e[i].key; ns[i] = e[i].sc; }
+  const double d = norm1_rows(ni, ns, nlen, ni + nlen, ns + nlen, olen);
+  free(e); free(ni); free(ns);
+  return d;
+}
+
 /* ---- partitions: include/internal/pprInternal.h:29-99 in dense (graph-iteration) order ---- */
 int oracle_find_partitions(int64_t n, const int64_t* rp, const int32_t* col, uint8_t* part) {
   int64_t m = n ? rp[n] : 0;
@@ -228,7 +254,7 @@ int oracle_grank(int64_t n, const int64_t* rp, const int32_t* col, const uint8_t
       }
       nl[v] = acc_top(&a, L, &buf, &bufcap, ni + v * L, ns + v * L);
       acc_reset(&a);
-      double d1 = norm1_rows(ni + v * L, ns + v * L, nl[v], ci + v * L, cs + v * L, cl[v]);
+      double d1 = norm1_stored(ni + v * L, ns + v * L, nl[v], ci + v * L, cs + v * L, cl[v]);
       if (d1 > md[0]) md[0] = d1;
     }
     for (int64_t v = 0; v < n; v++) {
@@ -301,7 +327,7 @@ int oracle_step(int64_t n, const int64_t* rp, const int32_t* col, int32_t L, dou
     }
     nlen[v] = acc_top(&a, L, &buf, &bufcap, nids + (int64_t)v * L, nsc + (int64_t)v * L);
     acc_reset(&a);
-    double d1 = norm1_rows(nids + (int64_t)v * L, nsc + (int64_t)v * L, nlen[v], ids + (int64_t)v * L,
+    double d1 = norm1_stored(nids + (int64_t)v * L, nsc + (int64_t)v * L, nlen[v], ids + (int64_t)v * L,
                            sc + (int64_t)v * L, len[v]);
     if (d1 > md) md = d1;
   }

@@ -15,8 +15,8 @@
  *   mccompletepathv2 :182-258  nodes in that order; map = {v: 1/f} (f = d/deg, 1 for dangling);
  *                           for s in succ(v): map += (final basket of s if s came earlier, else
  *                           the walk basket of s, computed once); keepTop(L); map *= f; finally
- *                           keepTop(K). keepTop ties: (score desc, dense id asc), rows stored in
- *                           that order (the reference leaves ties to unordered_map order).
+ *                           keepTop(K) of the scaled map. keepTop ties: (score desc, dense id
+ *                           asc) (the reference leaves ties to unordered_map order).
  *   walkNode :115-165       {u: R}; floor(R*d) walks; a walk moves while the current node has
  *                           successors, counts the reached node if present or fewer than L keys
  *                           are held, continues while U <= d; counts / R. Dangling: {u: 1.0}.
@@ -362,11 +362,13 @@ int oracle_mccp2(int64_t n, const int64_t* rp, const int32_t* col, int32_t K, in
     }
     flen[v] = (int32_t)keep;
   }
-  for (int64_t v = 0; v < n; v++) {                   /* keepTop(K) (:252-256) */
+  for (int64_t v = 0; v < n; v++) {                   /* keepTop(K) (:252-256) on the scaled map */
     const int32_t k = flen[v] < K ? flen[v] : K;
+    for (int32_t t = 0; t < flen[v]; t++) { ent[t].key = fid[v * L + t]; ent[t].sc = fsc[v * L + t]; }
+    qsort(ent, (size_t)flen[v], sizeof(ment_t), cmp_ment);  /* scaling can tie two scores */
     for (int32_t t = 0; t < K; t++) {
-      out_ids[v * K + t] = t < k ? fid[v * L + t] : -1;
-      out_sc[v * K + t] = t < k ? fsc[v * L + t] : 0.0;
+      out_ids[v * K + t] = t < k ? ent[t].key : -1;
+      out_sc[v * K + t] = t < k ? ent[t].sc : 0.0;
     }
     out_len[v] = k;
   }
