@@ -156,10 +156,20 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_wave_t = std::min(p->hub_wave_t, 8192);
   }
   {
-    const char* e3 = getenv("PPR_BW_MODE");
     const char* e4 = getenv("PPR_BW_NG");
     const char* e5 = getenv("PPR_BW_WAVES");
-    p->hub_bw_owner = e3 ? atoi(e3) != 0 : false;  // PPR_BW_MODE=1: owner-slot accumulation (measured 6 % slower)
+    // segmented hub buckets (k_hub_seg): PPR_HUB_SEG=0 disables, PPR_SEG_BUCKET target candidates
+    // per bucket, PPR_SEG_T wave table slots, PPR_SEG_WPB waves per block
+    const char* s1 = getenv("PPR_HUB_SEG");
+    const char* s2 = getenv("PPR_SEG_BUCKET");
+    const char* s3 = getenv("PPR_SEG_T");
+    const char* s4 = getenv("PPR_SEG_WPB");
+    p->seg_enabled = s1 ? atoi(s1) != 0 : false;  // measured no faster than the staged partition
+
+    p->seg_bucket = s2 ? std::max(32, atoi(s2)) : 256;
+    p->seg_t = s3 ? pow2_at_least(std::max(256, atoi(s3))) : 512;
+    p->seg_t = std::min(p->seg_t, 4096);
+    p->seg_wpb = s4 ? std::max(1, std::min(4, atoi(s4))) : 1;
     p->hub_bw_ng = (e4 && atoi(e4) == 8) ? 8 : 4;
     p->hub_bw_waves = e5 ? std::max(1, std::min(4, atoi(e5))) : 1;
     const char* e6 = getenv("PPR_HUB_SLICE");
@@ -173,9 +183,9 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     const int per_cu = std::max<int>(1, std::min<int>(32 / p->hub_bw_waves, (int)((160 * 1024) / p->hub_lds_wave)));
     p->hub_bw_blocks = p->num_cus * per_cu;
   }
-  hipFuncSetAttribute((const void*)k_hub_bucket_w<4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_bucket_w<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_bucket_w<4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_bucket_w<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_bucket_w<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_seg<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_topk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -309,28 +319,35 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   {
     size_t oi = 0;
     while (oi < nbig) {
-      Batch b{nd_all, 0, 0, 0, 0, 0, 0, 0, 0, 1};
+      Batch b{nd_all, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1};
       while (oi < nbig) {
         const size_t i = oi;
         const int v = big[i];
         const int64_t need = cand[i];
         const int64_t deg = cand[nbig + i];
-        if (nd_all > b.d0 && b.stg + need > budget) break;
-        const int logP = logp_of(need);
+        // segmented path (no partition pass): iterations only (the init has no successor rows),
+        // and at most 2^RANGE_BITS buckets of about seg_bucket candidates
+        const int lseg = std::max(0, ceil_log2((need + p->seg_bucket - 1) / p->seg_bucket));
+        const bool seg = p->seg_enabled && !a.unit && lseg <= RANGE_BITS;
+        const int64_t ptc0 = (int64_t)(1 << (seg ? lseg : logp_of(need))) * L;
+        if (nd_all > b.d0 &&
+            (b.stg + (seg ? 0 : need) > budget || b.pt + ptc0 > budget || b.nseg + (1 << lseg) > (1 << 24))) break;
+        const int logP = seg ? lseg : logp_of(need);
         const int P = 1 << logP;
         const int tw = (int)std::max<int64_t>(1, std::min<int64_t>(HUB_TILE, HUB_TILE_CAND / L));
-        const int T = (int)((deg + tw - 1) / tw);
+        const int T = seg ? 0 : (int)((deg + tw - 1) / tw);
         const int64_t ptc = (int64_t)P * L;
         const int nsl = ptc > 2 * slice ? (int)((ptc + slice - 1) / slice) : 0;
         // staging offsets are cumulative candidate counts in descriptor order, the same order the
         // device scan walks the concatenated count matrices in: scanned cm = absolute offsets
-        desc[nd_all++] = HubDesc{v, logP, T, (int32_t)need, tw, nsl, b.cm, b.stg, b.pt, b.red, b.ntiles, b.nbuck, b.nrt};
+        desc[nd_all++] = HubDesc{v, logP, T, (int32_t)need, tw, nsl, b.cm, b.stg, b.pt, b.red, b.ntiles, b.nbuck, b.nrt,
+                                 seg ? b.nseg : -1};
         b.cm += (int64_t)P * T;
-        b.stg += need - 1;
+        b.stg += seg ? 0 : need - 1;
         b.pt += ptc;
         b.red += (int64_t)nsl * L;
         b.ntiles += T;
-        b.nbuck += P;
+        if (seg) b.nseg += P; else b.nbuck += P;
         b.nrt += nsl;
         b.maxP = std::max(b.maxP, P);
         oi++;
@@ -340,12 +357,12 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     }
   }
   // one scratch layout for every batch (maxima), so no batch reallocates under a running one
-  Batch mx{0, 0, 0, 0, 0, 0, 0, 0, 0, 1};
+  Batch mx{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1};
   size_t maxnd = 0;
   for (const Batch& b : batches) {
     mx.cm = std::max(mx.cm, b.cm); mx.stg = std::max(mx.stg, b.stg); mx.pt = std::max(mx.pt, b.pt);
     mx.ntiles = std::max(mx.ntiles, b.ntiles); mx.nbuck = std::max(mx.nbuck, b.nbuck);
-    mx.nrt = std::max(mx.nrt, b.nrt); mx.red = std::max(mx.red, b.red);
+    mx.nrt = std::max(mx.nrt, b.nrt); mx.red = std::max(mx.red, b.red); mx.nseg = std::max(mx.nseg, b.nseg);
     maxnd = std::max(maxnd, b.d1 - b.d0);
   }
   size_t scan_tmp = 0;
@@ -356,6 +373,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   const size_t o_tile = off; off = al(off + sizeof(HubTask) * mx.ntiles);
   const size_t o_buck = off; off = al(off + sizeof(HubTask) * mx.nbuck);
   const size_t o_rt = off;   off = al(off + sizeof(HubTask) * (mx.nrt + 1));
+  const size_t o_sg = off;   off = al(off + sizeof(HubTask) * (mx.nseg + 1));
   const size_t o_cm = off;   off = al(off + 4 * (size_t)mx.cm);
   const size_t o_cmx = off;  off = al(off + 4 * (size_t)mx.cm);
   const size_t o_tmp = off;  off = al(off + scan_tmp);
@@ -378,6 +396,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   HubTask* d_tile = (HubTask*)(base + o_tile);
   HubTask* d_buck = (HubTask*)(base + o_buck);
   HubTask* d_rt = (HubTask*)(base + o_rt);
+  HubTask* d_sg = (HubTask*)(base + o_sg);
   int32_t* d_cm = (int32_t*)(base + o_cm);
   int32_t* d_cmx = (int32_t*)(base + o_cmx);
   void* d_tmp = (void*)(base + o_tmp);
@@ -403,9 +422,17 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     HIP_OK(hipMemsetAsync(d_tau, 0, 8 * nd, st));
     HIP_OK(hipMemsetAsync(d_oflag, 0, 4 * nd, st));
     HIP_OK(hipMemsetAsync(d_lc, 0, 8, st));
-    hipLaunchKernelGGL(k_hub_expand, dim3((unsigned)nd), dim3(256), 0, st, d_desc, d_tile, d_buck, d_rt);
+    hipLaunchKernelGGL(k_hub_expand, dim3((unsigned)nd), dim3(256), 0, st, d_desc, d_tile, d_buck, d_rt, d_sg);
     HIP_OK(hipGetLastError());
+    if (b.nseg) {
+      hipLaunchKernelGGL(k_hub_seg<4>, dim3((unsigned)((b.nseg + p->seg_wpb - 1) / p->seg_wpb)), dim3(64 * p->seg_wpb),
+                         hub_wave_lds(p->seg_t, 4) * p->seg_wpb, st, g, s, a, d_desc, d_sg, b.nseg, d_pk, d_ps, d_pc,
+                         d_oflag, d_ovl, p->seg_t);
+      HIP_OK(hipGetLastError());
+      p->merge_launches++;
+    }
     const int64_t ntiles = b.ntiles;
+    if (ntiles) {
     const size_t lds_tile = (size_t)WAVES_PER_BLOCK * maxP * 4;
     const unsigned tb = (unsigned)((ntiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm,
@@ -426,15 +453,12 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       const int wpb = p->hub_bw_waves;
       const int64_t blocks = (nbuck + wpb - 1) / wpb;
       const dim3 grid((unsigned)blocks), blk(64 * wpb);
-      if (p->hub_bw_owner)
-        hipLaunchKernelGGL((k_hub_bucket_w<4, true>), grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_lc, d_st, d_pk,
-                           d_ps, d_pc, d_gl, d_lc + 1, p->hub_wave_t);
-      else if (p->hub_bw_ng == 8)
-        hipLaunchKernelGGL((k_hub_bucket_w<8, false>), grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_lc, d_st, d_pk,
-                           d_ps, d_pc, d_gl, d_lc + 1, p->hub_wave_t);
+      if (p->hub_bw_ng == 8)
+        hipLaunchKernelGGL(k_hub_bucket_w<8>, grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
+                           d_gl, d_lc + 1, p->hub_wave_t);
       else
-        hipLaunchKernelGGL((k_hub_bucket_w<4, false>), grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_lc, d_st, d_pk,
-                           d_ps, d_pc, d_gl, d_lc + 1, p->hub_wave_t);
+        hipLaunchKernelGGL(k_hub_bucket_w<4>, grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
+                           d_gl, d_lc + 1, p->hub_wave_t);
       HIP_OK(hipGetLastError());
     }
     // spilled buckets (distinct keys beyond the wave table): persistent workgroups over the spill
@@ -442,6 +466,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     hipLaunchKernelGGL(k_hub_bucket, dim3((unsigned)p->num_cus), dim3(WG_THREADS), p->hub_lds_wg, st, s, a, g,
                        d_desc, d_gl, d_lc + 1, d_cmx, d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_oflag, d_ovl);
     HIP_OK(hipGetLastError());
+    }  // staged partition
     // long appended lists are cut (k_hub_reduce) so no k_hub_final workgroup selects from more
     // than a few slices' worth of entries; slices are reserved for the worst case, idle ones exit
     if (b.nrt) {
@@ -936,19 +961,24 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
     if (rc) return rc;
     unsigned long long* mdp = p->d_maxdiff + (it < PPR_MAX_ITER_STATS ? it : PPR_MAX_ITER_STATS);
     if (p->nranks > 1) {
-      int64_t rows_max = 0;
-      for (int r = 0; r < p->nranks; r++) rows_max = std::max(rows_max, b[r + 1] - b[r]);
-      if (rows_max > 0) {
-        const size_t chunk = (size_t)rows_max * rb;
-        rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, chunk);
-        if (!rc) rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, chunk * p->nranks);
+      // variable-size all-gather: every rank broadcasts its own rows (grouped). Ranges are balanced
+      // by work, not rows, so padding every rank to the largest range would multiply the bytes;
+      // each rank packs its rows in place at its offset of the receive buffer.
+      std::vector<size_t> xo(p->nranks + 1, 0);
+      for (int r = 0; r < p->nranks; r++) xo[r + 1] = xo[r] + (size_t)(b[r + 1] - b[r]) * (size_t)rb;
+      if (xo[p->nranks]) {
+        rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, xo[p->nranks]);
         if (rc) return rc;
-        rc = ppr_grank_plan_pack(p, (int32_t)it, b[p->rank], b[p->rank + 1], p->d_xsend);
+        rc = ppr_grank_plan_pack(p, (int32_t)it, b[p->rank], b[p->rank + 1], p->d_xrecv + xo[p->rank]);
         if (rc) return rc;
-        NCCL_OK(ncclAllGather(p->d_xsend, p->d_xrecv, chunk, ncclUint8, p->comm, s));
+        NCCL_OK(ncclGroupStart());
+        for (int r = 0; r < p->nranks; r++)
+          if (xo[r + 1] > xo[r])
+            NCCL_OK(ncclBroadcast(p->d_xrecv + xo[r], p->d_xrecv + xo[r], xo[r + 1] - xo[r], ncclUint8, r, p->comm, s));
+        NCCL_OK(ncclGroupEnd());
         for (int r = 0; r < p->nranks; r++) {
           if (r == p->rank || b[r + 1] == b[r]) continue;
-          rc = ppr_grank_plan_unpack(p, (int32_t)it, b[r], b[r + 1], p->d_xrecv + (size_t)r * chunk);
+          rc = ppr_grank_plan_unpack(p, (int32_t)it, b[r], b[r + 1], p->d_xrecv + xo[r]);
           if (rc) return rc;
         }
       }

@@ -39,10 +39,7 @@ constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per redu
 // wave bucket LDS: acc f64[T] | keys i32[T] | cnt u16[T] | vals f64[CHUNK] | touched u16[CHUNK] |
 // tof u16[CHUNK + 2]; the radix histogram of the final select (1 KB) aliases vals
 __host__ __device__ constexpr size_t hub_wave_lds(int T, int ng) {
-  // chunk mode: acc | keys | cnt u16 | vals | touched | tof;  owner mode: acc | keys | own u32 | hist
-  return ((size_t)T * 14 + (size_t)(ng * WAVE) * 12 + 4) > ((size_t)T * 16 + 1024)
-             ? ((size_t)T * 14 + (size_t)(ng * WAVE) * 12 + 4)
-             : ((size_t)T * 16 + 1024);
+  return (size_t)T * 14 + (size_t)(ng * WAVE) * 12 + 4;
 }
 
 struct HubDesc {
@@ -57,6 +54,7 @@ struct HubDesc {
   int64_t pt_off;  // appended bucket results (<= P*L entries, pt_cnt[desc] of them used)
   int64_t red;     // offset of the sliced reduction (k_hub_reduce), used iff pt_cnt > 2 * slice
   int64_t tile_off, buck_off, rt_off;  // first tile / bucket / reduce task of this source in its batch
+  int64_t sg_off;  // >= 0: segmented source (k_hub_seg), first segment task; -1: staged partition
 };
 
 // the batch's task lists, expanded on the device from the descriptors (one block per source):
@@ -75,12 +73,16 @@ __device__ __forceinline__ void hub_bucket_range(const HubDesc& d, const int32_t
 struct HubTask { int32_t d; int32_t x; };   // (descriptor, tile or bucket)
 
 __global__ void __launch_bounds__(256) k_hub_expand(const HubDesc* desc, HubTask* tiles, HubTask* buckets,
-                                                    HubTask* rts) {
+                                                    HubTask* rts, HubTask* segs) {
   const int d = blockIdx.x;
   const HubDesc D = desc[d];
   const int P = 1 << D.logP;
   for (int t = threadIdx.x; t < D.T; t += blockDim.x) tiles[D.tile_off + t] = HubTask{d, t};
-  for (int b = threadIdx.x; b < P; b += blockDim.x) buckets[D.buck_off + b] = HubTask{d, b};
+  if (D.sg_off >= 0) {
+    for (int b = threadIdx.x; b < P; b += blockDim.x) segs[D.sg_off + b] = HubTask{d, b};
+  } else {
+    for (int b = threadIdx.x; b < P; b += blockDim.x) buckets[D.buck_off + b] = HubTask{d, b};
+  }
   for (int x = threadIdx.x; x < D.nsl; x += blockDim.x) rts[D.rt_off + x] = HubTask{d, x};
 }
 
@@ -273,144 +275,288 @@ __global__ void __launch_bounds__(256) k_hub_prep(DevGraph g, IterArgs a, const 
 // Bucket waves: one wave per bucket, its work record resolved by k_hub_prep. Per bucket: private LDS table (T slots, 3/4 usable; a bucket with more distinct
 // keys spills to k_hub_bucket), chunks of NG groups loaded at once and accumulated with
 // chunk_accumulate, then the keys >= tau, at most L of them, appended to the source's list.
-template <int NG, bool OWNER>
+// ---------------------------------------------------------------------------------------------
+// One bucket on one wave: private LDS table (T slots, 3/4 usable), chunks of NG groups of 64
+// ordered candidates accumulated with chunk_accumulate, then the keys >= tau, at most L of them,
+// appended to the source's result list. Shared by the staged buckets (k_hub_bucket_w) and the
+// segmented buckets (k_hub_seg).
+struct BucketWave {
+  LdsTable t;
+  ChunkLds ck;
+  uint32_t* hist;
+  int T, budget, fill;
+  bool overflow;
+
+  __device__ __forceinline__ void setup(unsigned char* base, int T_, int NG) {
+    T = T_;
+    t.acc = reinterpret_cast<double*>(base);
+    t.keys = reinterpret_cast<int*>(base + (size_t)T * 8);
+    t.mask = (uint32_t)T - 1;
+    t.nbits = 31 - __clz(T);
+    ck.cnt = reinterpret_cast<uint16_t*>(base + (size_t)T * 12);
+    ck.vals = reinterpret_cast<double*>(base + (size_t)T * 14);
+    ck.touched = reinterpret_cast<uint16_t*>(base + (size_t)T * 14 + (size_t)(NG * WAVE) * 8);
+    ck.tof = ck.touched + NG * WAVE;
+    hist = reinterpret_cast<uint32_t*>(ck.vals);  // final select only (after accumulation)
+    budget = T / 4 * 3;
+    fill = 0;
+    overflow = false;
+    for (int i = lane_id(); i < T; i += WAVE) { t.keys[i] = EMPTY; ck.cnt[i] = 0; }
+    wave_fence();
+  }
+
+  __device__ __forceinline__ void seed(int key, double val) {
+    if (lane_id() == 0) { const uint32_t sl = table_slot(t, key); t.acc[sl] = val; }
+    fill = 1;
+    wave_fence();
+  }
+
+  // find-or-insert the NG groups' keys, then accumulate them in stream order; sets overflow
+  // (uniform) instead when the table could run out of slots
+  template <int NG>
+  __device__ __forceinline__ void chunk(const bool (&cv)[NG], const int (&kk)[NG], const double (&cs)[NG],
+                                        double factor) {
+    uint32_t sl[NG];
+#pragma unroll
+    for (int k = 0; k < NG; k++) {
+      if (fill + WAVE > budget) overflow = true;  // uniform: a group may bring 64 new keys
+      bool ins = false;
+      uint32_t h = 0;
+      if (cv[k] && !overflow) {
+        h = hash32((uint32_t)kk[k]) & t.mask;
+        for (;;) {
+          const int c = t.keys[h];
+          if (c == kk[k]) break;
+          if (c == EMPTY) {
+            const int prev = atomicCAS(&t.keys[h], EMPTY, kk[k]);
+            if (prev == EMPTY) { t.acc[h] = 0.0; ins = true; break; }
+            if (prev == kk[k]) break;
+          }
+          h = (h + 1) & t.mask;
+        }
+      }
+      sl[k] = h;
+      fill += __popcll(__ballot(ins));
+      wave_fence();
+    }
+    if (overflow) return;
+    chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor);
+  }
+
+  // keys >= tau (at most L by (score desc, id asc)) appended to the source's list
+  __device__ __forceinline__ void emit(double tau, int Lw, uint32_t* pt_cnt_d, int32_t* pt_key, double* pt_sc,
+                                       const IterArgs& a) {
+    const int l = lane_id();
+    // compact the occupied slots that can still reach the top-L (value >= tau) to the front, in
+    // one pass (writes land at or below the slots already read)
+    int U = 0, Uall = 0;
+    for (int i0 = 0; i0 < T; i0 += WAVE) {
+      const int i = i0 + l;
+      const int k = t.keys[i];
+      const double x = t.acc[i];
+      const bool occ = k != EMPTY;
+      const bool keep = occ && x >= tau;
+      const uint64_t m = __ballot(keep);
+      if (a.diag) Uall += __popcll(__ballot(occ));
+      wave_fence();
+      if (keep) { const int pos = U + __popcll(m & lanemask_lt()); t.keys[pos] = k; t.acc[pos] = x; }
+      U += __popcll(m);
+      wave_fence();
+    }
+    if (a.diag && l == 0) {  // distinct keys / kept keys per bucket
+      atomicAdd(&a.diag[64 + (31 - __clz(Uall | 1))], 1ull);
+      atomicAdd(&a.diag[96 + (31 - __clz(U | 1))], 1ull);
+    }
+    const int cnt = U <= Lw ? U : Lw;
+    if (cnt == 0) return;
+    int at = 0;
+    if (l == 0) at = (int)atomicAdd(pt_cnt_d, (uint32_t)cnt);
+    at = __shfl(at, 0);
+    int32_t* ok = pt_key + at;
+    double* os = pt_sc + at;
+    if (U <= Lw) {
+      for (int i = l; i < U; i += WAVE) { ok[i] = t.keys[i]; os[i] = t.acc[i]; }
+      return;
+    }
+    const int* keys = t.keys;
+    const double* acc = t.acc;
+    const SelCrit c = select_top(U, Lw, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, hist);
+    int pos0 = 0;
+    for (int i0 = 0; i0 < U; i0 += WAVE) {
+      const int i = i0 + l;
+      bool sel = false;
+      if (i < U) sel = sel_test(c, dbits(acc[i]), (uint32_t)~keys[i]);
+      const uint64_t m = __ballot(sel);
+      if (sel) { const int pos = pos0 + __popcll(m & lanemask_lt()); ok[pos] = keys[i]; os[pos] = acc[i]; }
+      pos0 += __popcll(m);
+    }
+  }
+};
+
+// Bucket waves over the staged partition: one wave per bucket, its work record resolved by
+// k_hub_prep; a bucket with more distinct keys than the table holds spills to k_hub_bucket.
+template <int NG>
 __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, const BucketWork* bw,
-                                                      int64_t nbuck, uint32_t* next, const HubRec* st,
+                                                      int64_t nbuck, const HubRec* st,
                                                       int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
                                                       HubTask* spill, uint32_t* spill_cnt, int T) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
-  unsigned char* base = smem + (size_t)wv * hub_wave_lds(T, NG);
-  LdsTable t;
-  t.acc = reinterpret_cast<double*>(base);
-  t.keys = reinterpret_cast<int*>(base + (size_t)T * 8);
-  t.mask = (uint32_t)T - 1;
-  t.nbits = 31 - __clz(T);
-  ChunkLds ck;
-  ck.cnt = reinterpret_cast<uint16_t*>(base + (size_t)T * 12);
-  ck.vals = reinterpret_cast<double*>(base + (size_t)T * 14);
-  ck.touched = reinterpret_cast<uint16_t*>(base + (size_t)T * 14 + (size_t)(NG * WAVE) * 8);
-  ck.tof = ck.touched + NG * WAVE;
-  uint32_t* own = reinterpret_cast<uint32_t*>(base + (size_t)T * 12);  // OWNER mode (aliases cnt/vals)
-  uint32_t* hist = OWNER ? reinterpret_cast<uint32_t*>(base + (size_t)T * 16)
-                         : reinterpret_cast<uint32_t*>(ck.vals);  // final select only (after accumulation)
   const int l = lane_id();
-  const int Lw = s.L;
-  const int budget = T / 4 * 3;
   // one bucket per wave (persistent waves with a static stride or a shared work counter measured
   // slower: the hardware refills CUs better than a fixed grid balances hot buckets)
   const int64_t cur = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (cur >= nbuck) return;
-  (void)next;
   const BucketWork W = bw[cur];
-  {
-    const long long t_start = a.diag ? (long long)clock64() : 0;
-    const int nb = W.nb;
-    if (OWNER) { for (int i = l; i < T; i += WAVE) { t.keys[i] = EMPTY; own[i] = 0xffu; } }
-    else { for (int i = l; i < T; i += WAVE) { t.keys[i] = EMPTY; ck.cnt[i] = 0; } }
-    wave_fence();
-    int fill = 0;
-    if (W.seed >= 0) {
-      if (l == 0) { const uint32_t sl = table_slot(t, W.seed); t.acc[sl] = W.selfval; }
-      fill = 1;
+  const long long t_start = a.diag ? (long long)clock64() : 0;
+  BucketWave B;
+  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG);
+  if (W.seed >= 0) B.seed(W.seed, W.selfval);
+  const int nb = W.nb;
+  for (int g0 = 0; g0 < nb; g0 += NG * WAVE) {
+    bool cv[NG];
+    double cs[NG];
+    int kk[NG];
+#pragma unroll
+    for (int k = 0; k < NG; k++) {
+      const int q = g0 + k * WAVE + l;
+      cv[k] = q < nb;
+      const HubRec r = cv[k] ? st[W.start + q] : HubRec{0, 0, 0.0};
+      kk[k] = r.key;
+      cs[k] = r.sc;
     }
-    wave_fence();
-    bool overflow = false;
-    for (int g0 = 0; g0 < nb; g0 += NG * WAVE) {
+    B.chunk<NG>(cv, kk, cs, W.factor);
+    if (B.overflow) break;
+  }
+  if (B.overflow) {
+    if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = HubTask{W.d, W.x}; }
+    return;
+  }
+  if (a.diag && l == 0) {  // bucket length histogram: count and cycles per log2(length) bin
+    const int bin = 31 - __clz(nb | 1);
+    atomicAdd(&a.diag[bin], 1ull);
+    atomicAdd(&a.diag[32 + bin], (unsigned long long)((long long)clock64() - t_start));
+  }
+  B.emit(W.tau, s.L, &pt_cnt[W.d], pt_key + W.pt_off, pt_sc + W.pt_off, a);
+}
+
+// Segmented buckets (no partition pass): basket rows are stored in hash_b order with a range
+// index (DevSlab::rix), so bucket x of a source with logP <= RANGE_BITS buckets -- the keys whose
+// top logP hash bits equal x -- is ONE contiguous segment of every successor row. One wave per
+// (source, bucket) walks the successors in order, 64 at a time: per successor the segment bounds
+// (two u16 of one 128-B index line) and, for the pruning bound, the row minimum of full rows;
+// then the window's segments are gathered as one ordered candidate stream, NG groups per chunk.
+// Stream order is successor order, so every key's fma chain keeps the reference order.
+template <int NG>
+__global__ void __launch_bounds__(256) k_hub_seg(DevGraph g, DevSlab s, IterArgs a, const HubDesc* desc,
+                                                 const HubTask* tasks, int64_t ntasks, int32_t* pt_key,
+                                                 double* pt_sc, uint32_t* pt_cnt, int32_t* ovf_flag,
+                                                 int32_t* ovf_list, int T) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int wv = threadIdx.x >> 6;
+  const int l = lane_id();
+  const int64_t cur = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (cur >= ntasks) return;
+  const HubTask tk = tasks[cur];
+  const HubDesc d = desc[tk.d];
+  const int v = d.v;
+  const int64_t b = g.rp[v], e = g.rp[v + 1];
+  const double factor = merge_factor(a, e - b);
+  const int sh = RANGE_BITS - d.logP;                // ranges per bucket: 1 << sh
+  const int r0 = tk.x << sh, r1 = (tk.x + 1) << sh;  // ranges [r0, r1)
+  // PPR_DIAG: cycles per phase (setup, successor window, gather, accumulate, emit), waves, candidates
+  const bool dg = a.diag != nullptr;
+  long long tc = dg ? (long long)clock64() : 0;
+  unsigned long long ph[5] = {0, 0, 0, 0, 0}, ncand = 0;
+  auto lap = [&](int k) {
+    if (dg) { const long long t2 = (long long)clock64(); ph[k] += (unsigned long long)(t2 - tc); tc = t2; }
+  };
+  BucketWave B;
+  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG);
+  {
+    const int rg = (int)row_range(v);
+    if (rg >= r0 && rg < r1) B.seed(v, self_seed(a, e - b));
+  }
+  lap(0);
+  unsigned long long mb = 0;  // max row minimum over full successor rows (unscaled)
+  for (int64_t e0 = b; e0 < e; e0 += WAVE) {
+    const int64_t i = e0 + l;
+    int u = 0, sl = 0, lo = 0, ln = 0;
+    if (i < e) {
+      const int32_t cx = g.colx[i];
+      u = cx & 0x7fffffff;
+      sl = read_slot(a, cx);
+      const uint16_t* ix = s.rix + s.xrow(sl, u);
+      lo = r0 ? (int)ix[r0 - 1] : 0;
+      ln = (int)ix[r1 - 1] - lo;
+      if ((int)ix[NRANGE - 1] == s.L) {
+        const unsigned long long m = dbits(s.rmin[s.lrow(sl, u)]);
+        mb = m > mb ? m : mb;
+      }
+    }
+    const int incl = wave_incl_scan(ln);
+    const int total = __shfl(incl, WAVE - 1);
+    ncand += (unsigned long long)total;
+    lap(1);
+    for (int g0 = 0; g0 < total; g0 += NG * WAVE) {
       bool cv[NG];
-      uint32_t sl[NG];
       double cs[NG];
       int kk[NG];
 #pragma unroll
       for (int k = 0; k < NG; k++) {
-        const int q = g0 + k * WAVE + l;
-        cv[k] = q < nb;
-        const HubRec r = cv[k] ? st[W.start + q] : HubRec{0, 0, 0.0};
-        kk[k] = r.key;
-        cs[k] = r.sc;
-      }
+        const int c = g0 + k * WAVE + l;
+        int j = 0;
 #pragma unroll
-      for (int k = 0; k < NG; k++) {
-        if (fill + WAVE > budget) overflow = true;  // uniform: a group may bring 64 new keys
-        bool ins = false;
-        uint32_t h = 0;
-        if (cv[k] && !overflow) {
-          h = hash32((uint32_t)kk[k]) & t.mask;
-          for (;;) {
-            const int c = t.keys[h];
-            if (c == kk[k]) break;
-            if (c == EMPTY) {
-              const int prev = atomicCAS(&t.keys[h], EMPTY, kk[k]);
-              if (prev == EMPTY) { t.acc[h] = 0.0; ins = true; break; }
-              if (prev == kk[k]) break;
-            }
-            h = (h + 1) & t.mask;
-          }
+        for (int step = 32; step; step >>= 1) {
+          const int pv = __shfl(incl, j + step - 1);
+          if (pv <= c) j += step;
         }
-        sl[k] = h;
-        fill += __popcll(__ballot(ins));
-        wave_fence();
+        const int jj = j < WAVE ? j : WAVE - 1;
+        const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
+        const int ex = jj > 0 ? exv : 0;
+        const int uj = __shfl(u, jj);
+        const int sj = __shfl(sl, jj);
+        const int lj = __shfl(lo, jj);
+        cv[k] = c < total;
+        kk[k] = 0;
+        cs[k] = 0.0;
+        if (cv[k]) {
+          const int64_t r = s.row(sj, uj) + lj + (c - ex);
+          kk[k] = s.ids[r];
+          cs[k] = s.sc[r];
+        }
       }
-      if (overflow) break;
-      if (OWNER) {
+      if (dg) {  // wait for the gathers before timing them
+        int z = 0;
 #pragma unroll
-        for (int k = 0; k < NG; k++) apply_group_owner(t.acc, own, cv[k], sl[k], cs[k], W.factor);
-      } else {
-        chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, W.factor);
+        for (int k = 0; k < NG; k++) z += kk[k] + (int)(cs[k] > 2.0);
+        if (z == 0x7fffffff) wave_fence();
+        lap(2);
       }
+      B.chunk<NG>(cv, kk, cs, factor);
+      lap(3);
+      if (B.overflow) break;
     }
-    if (overflow) {
-      if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = HubTask{W.d, W.x}; }
-    } else {
-      if (a.diag && l == 0) {  // bucket length histogram: count and cycles per log2(length) bin
-        const int bin = 31 - __clz(nb | 1);
-        atomicAdd(&a.diag[bin], 1ull);
-        atomicAdd(&a.diag[32 + bin], (unsigned long long)((long long)clock64() - t_start));
-      }
-      // compact the occupied slots that can still reach the top-L (value >= tau) to the front, in
-      // one pass (writes land at or below the slots already read)
-      int U = 0, Uall = 0;
-      for (int i0 = 0; i0 < T; i0 += WAVE) {
-        const int i = i0 + l;
-        const int k = t.keys[i];
-        const double x = t.acc[i];
-        const bool occ = k != EMPTY;
-        const bool keep = occ && x >= W.tau;
-        const uint64_t m = __ballot(keep);
-        if (a.diag) Uall += __popcll(__ballot(occ));
-        wave_fence();
-        if (keep) { const int pos = U + __popcll(m & lanemask_lt()); t.keys[pos] = k; t.acc[pos] = x; }
-        U += __popcll(m);
-        wave_fence();
-      }
-      if (a.diag && l == 0) {  // distinct keys / kept keys per bucket
-        atomicAdd(&a.diag[64 + (31 - __clz(Uall | 1))], 1ull);
-        atomicAdd(&a.diag[96 + (31 - __clz(U | 1))], 1ull);
-      }
-      const int cnt = U <= Lw ? U : Lw;
-      if (cnt > 0) {
-        int at = 0;
-        if (l == 0) at = (int)atomicAdd(&pt_cnt[W.d], (uint32_t)cnt);
-        at = __shfl(at, 0);
-        int32_t* ok = pt_key + W.pt_off + at;
-        double* os = pt_sc + W.pt_off + at;
-        if (U <= Lw) {
-          for (int i = l; i < U; i += WAVE) { ok[i] = t.keys[i]; os[i] = t.acc[i]; }
-        } else {
-          const int* keys = t.keys;
-          const double* acc = t.acc;
-          const SelCrit c = select_top(U, Lw, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, hist);
-          int pos0 = 0;
-          for (int i0 = 0; i0 < U; i0 += WAVE) {
-            const int i = i0 + l;
-            bool sel = false;
-            if (i < U) sel = sel_test(c, dbits(acc[i]), (uint32_t)~keys[i]);
-            const uint64_t m = __ballot(sel);
-            if (sel) { const int pos = pos0 + __popcll(m & lanemask_lt()); ok[pos] = keys[i]; os[pos] = acc[i]; }
-            pos0 += __popcll(m);
-          }
-        }
-      }
+    if (B.overflow) break;
+  }
+  if (B.overflow) {
+    // more distinct keys than the wave table: the whole source takes the HBM-table path
+    if (l == 0 && atomicExch(&ovf_flag[tk.d], 1) == 0) {
+      const int pos = atomicAdd(&ovf_list[0], 1);
+      ovf_list[1 + pos] = v;
+    }
+    return;
+  }
+#pragma unroll
+  for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
+  const double tau = mb ? bitsd(mb) * factor : 0.0;
+  B.emit(tau, s.L, &pt_cnt[tk.d], pt_key + d.pt_off, pt_sc + d.pt_off, a);
+  if (dg) {
+    lap(4);
+    if (l == 0) {
+      for (int k = 0; k < 5; k++) atomicAdd(&a.diag[128 + k], ph[k]);
+      atomicAdd(&a.diag[133], 1ull);
+      atomicAdd(&a.diag[134], ncand);
     }
   }
 }

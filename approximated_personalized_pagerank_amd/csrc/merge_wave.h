@@ -206,6 +206,7 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
   const double factor = merge_factor(a, e - b);
 
   table_clear(t);
+  unsigned long long mb = 0;  // top-L pruning bound: max row minimum over full successor rows
   if (lane_id() == 0) { const uint32_t sl = table_slot(t, v); t.acc[sl] = self_seed(a, e - b); }
   wave_fence();
 
@@ -225,6 +226,8 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
         u = cx & 0x7fffffff;
         sl = read_slot(a, cx);
         ln = s.len[s.lrow(sl, u)];
+        const unsigned long long rm = dbits(s.rmin[s.lrow(sl, u)]);  // loaded beside len
+        if (ln == s.L && rm > mb) mb = rm;
       }
       const int incl = wave_incl_scan(ln);
       const int total = __shfl(incl, WAVE - 1);
@@ -242,7 +245,12 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
     }
   }
   wave_fence();
-  const int U = table_compact(t);
+  // keys below the bound cannot reach the top-L (a full successor row puts L distinct keys at
+  // >= round(rmin * factor), the hub pipeline's tau): dropped before the select
+#pragma unroll
+  for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
+  const double tau = (!a.unit && mb) ? bitsd(mb) * factor : 0.0;
+  const int U = table_compact_min(t, tau);
   const int* keys = t.keys;
   const double* acc = t.acc;
   finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, s, a, hist,

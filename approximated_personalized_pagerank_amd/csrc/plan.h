@@ -86,7 +86,8 @@ struct ppr_plan {
   size_t gath_bytes = 0;
   int num_cus = 256;
   int hub_bw_blocks = 0;           // persistent k_hub_bucket_w grid
-  bool hub_bw_owner = false;       // PPR_BW_MODE: 1 owner-slot accumulation, 0 ballot chunks (default)
+  bool seg_enabled = false;        // segmented hub buckets (k_hub_seg, PPR_HUB_SEG=1)
+  int seg_bucket = 256, seg_t = 512, seg_wpb = 1;
   int hub_bw_ng = 4;               // PPR_BW_NG: groups per chunk (4 or 8)
   int hub_bw_waves = 1;            // PPR_BW_WAVES: waves per block of k_hub_bucket_w
   int hub_slice = 8192;            // PPR_HUB_SLICE: k_hub_reduce slice (>= L)
@@ -135,9 +136,13 @@ inline void plan_free(ppr_plan* p) {
     if (hipMemcpy(h, p->d_diag, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
       fprintf(stderr, "ppr_diag bucket_w: log2(x) | buckets by len, Mcycles | by distinct keys | by kept keys\n");
       for (int b = 0; b < 32; b++)
-        if (h[b] || h[64 + b] || h[96 + b] || h[128 + b])
-          fprintf(stderr, "ppr_diag %2d %12llu %12.1f | %12llu | %12llu | chain %12llu\n", b, h[b], h[32 + b] / 1e6,
-                  h[64 + b], h[96 + b], h[128 + b]);
+        if (h[b] || h[64 + b] || h[96 + b])
+          fprintf(stderr, "ppr_diag %2d %12llu %12.1f | %12llu | %12llu\n", b, h[b], h[32 + b] / 1e6,
+                  h[64 + b], h[96 + b]);
+      if (h[133])
+        fprintf(stderr, "ppr_diag k_hub_seg: %llu waves, %.1f candidates/wave, Mcycles setup %.1f window %.1f "
+                "gather %.1f accumulate %.1f emit %.1f\n", h[133], (double)h[134] / (double)h[133], h[128] / 1e6,
+                h[129] / 1e6, h[130] / 1e6, h[131] / 1e6, h[132] / 1e6);
     }
     hipFree(p->d_diag);
   }

@@ -234,37 +234,6 @@ __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c,
   wave_fence();
 }
 
-// Apply one group of <= 64 ordered candidates (lane order == stream order) whose slots are
-// resolved, finding the lanes that share a slot through the LDS instead of ballots over the slot
-// bits: every valid lane posts its lane id to own[slot] with an atomic min, so a lane reading back
-// another id is a later occurrence of a key already present in the group ("dup"). The first
-// occurrences apply their fma directly (one read-modify-write per slot); the dups are then
-// chained per slot, lowest lane first, on top of it. own[] is all 0xff on entry and left so.
-__device__ __forceinline__ void apply_group_owner(double* acc, uint32_t* own, bool valid, uint32_t slot,
-                                                  double s, double factor) {
-  const uint32_t l = (uint32_t)lane_id();
-  if (valid) atomicMin(&own[slot], l);
-  wave_fence();
-  const uint32_t w = valid ? own[slot] : l;
-  const bool dup = w != l;
-  wave_fence();
-  if (valid && !dup) acc[slot] = fma(s, factor, acc[slot]);
-  wave_fence();
-  if (valid) own[slot] = 0xffu;
-  uint64_t dm = __ballot(dup);
-  while (dm) {
-    const int fl = __ffsll((long long)dm) - 1;
-    const uint32_t S = (uint32_t)__builtin_amdgcn_readlane((int)slot, fl);
-    const uint64_t m = __ballot(dup && slot == S);
-    double a = acc[S];
-    for (uint64_t r = m; r; r &= r - 1) a = fma(readlane_d(s, __ffsll((long long)r) - 1), factor, a);
-    if ((int)l == fl) acc[S] = a;
-    wave_fence();
-    dm &= ~m;
-  }
-  wave_fence();
-}
-
 // In-place compaction of occupied slots to the front (keys[0..U), acc[0..U)); returns U.
 __device__ __forceinline__ int table_compact(const LdsTable& t) {
   int U = 0;
@@ -276,6 +245,27 @@ __device__ __forceinline__ int table_compact(const LdsTable& t) {
     const uint64_t m = __ballot(occ);
     wave_fence();
     if (occ) {
+      const int pos = U + __popcll(m & lanemask_lt());
+      t.keys[pos] = k;
+      t.acc[pos] = a;
+    }
+    wave_fence();
+    U += __popcll(m);
+  }
+  return U;
+}
+
+// In-place compaction of the occupied slots whose value is >= lo (the top-L pruning bound).
+__device__ __forceinline__ int table_compact_min(const LdsTable& t, double lo) {
+  int U = 0;
+  for (uint32_t base = 0; base <= t.mask; base += WAVE) {
+    const uint32_t i = base + lane_id();
+    const int k = t.keys[i];
+    const double a = t.acc[i];
+    const bool keep = k != EMPTY && a >= lo;
+    const uint64_t m = __ballot(keep);
+    wave_fence();
+    if (keep) {
       const int pos = U + __popcll(m & lanemask_lt());
       t.keys[pos] = k;
       t.acc[pos] = a;

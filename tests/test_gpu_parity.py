@@ -129,3 +129,29 @@ def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
         assert np.array_equal(r.lens, o["lens"])
         assert np.array_equal(r.ids, o["ids"])
         assert np.array_equal(r.scores, o["scores"])
+
+
+@pytest.mark.parametrize("seg_env", [
+    {"PPR_HUB_SEG": "0"},                                                   # staged partition only
+    {"PPR_HUB_SEG": "0", "PPR_HUB_WAVE_T": "256", "PPR_HUB_BUCKET": "512"},  # spills to k_hub_bucket
+    {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "16"},                           # many segments, up to 64 buckets
+    {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "4096", "PPR_SEG_T": "4096"},    # one segment spanning all ranges
+    {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "2048", "PPR_SEG_T": "256"},     # table overflow -> HBM-table path
+    {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "64", "PPR_SEG_WPB": "4"},       # four segment waves per block
+])
+def test_gpu_hub_bucket_variants_bit_exact(seg_env, monkeypatch):
+    """every hub bucket engine -- staged buckets on one wave each (k_hub_bucket_w), spills to the
+    workgroup kernel (k_hub_bucket), hash-range segments of the successor rows (k_hub_seg) --
+    matches the oracle bit for bit, alone (hub tier only, 0x20) and mixed with the wave tiers"""
+    for k, v in seg_env.items():
+        monkeypatch.setenv(k, v)
+    for mask, (scale, K, L, it) in [("0x20", (10, 16, 32, 5)), ("0x21", (11, 8, 64, 4)), ("0x20", (12, 8, 128, 3))]:
+        monkeypatch.setenv("PPR_TIER_MASK", mask)
+        g = ppr.rmat(scale, seed=91 + scale)
+        part = g.partitions()
+        r = ppr.grank_csr(g, K, L, it, 0.85, -1.0, part=part, device=0)
+        o = oracle.grank(g.row_ptr, g.col, part, K, L, it, 0.85, -1.0)
+        assert np.array_equal(r.max_diff, o["max_diff"])
+        assert np.array_equal(r.lens, o["lens"])
+        assert np.array_equal(r.ids, o["ids"])
+        assert np.array_equal(r.scores, o["scores"])
