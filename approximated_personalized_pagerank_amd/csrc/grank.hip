@@ -44,6 +44,35 @@ using namespace pprk;
 
 #include "plan.h"
 
+namespace pprk {
+// Probe of the LDS atomic order chunk_accumulate's `ordered` mode relies on: every lane of a wave
+// adds 1 to a counter chosen with heavy collisions; the returned old value must equal the number
+// of lower lanes on the same counter, for every collision pattern tried. One block; *ok stays 1
+// only if no lane ever disagrees.
+__global__ void __launch_bounds__(256) k_probe_lds_rank(int* ok, int trials) {
+  __shared__ uint32_t cnt[4][512];
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  int bad = 0;
+  for (int t = 0; t < trials; t++) {
+    const uint32_t r = hash32(t * 104729u + wv * 31u + 7u);
+    const uint32_t S = 1u << (r % 10);
+    for (int i = l; i < 512; i += WAVE) cnt[wv][i] = 0;
+    wave_fence();
+    const uint32_t slot = hash32(r ^ (uint32_t)(l * 2654435761u)) & (S - 1);
+    const uint32_t got = atomicAdd(&cnt[wv][slot], 1u);
+    uint32_t want = 0;
+    for (int j = 0; j < WAVE; j++) {
+      const uint32_t sj = (uint32_t)__shfl((int)slot, j);
+      if (j < l && sj == slot) want++;
+    }
+    bad |= got != want;
+    wave_fence();
+  }
+  if (bad) atomicAnd(ok, 0);
+}
+
+}  // namespace pprk
+
 int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t K, uint32_t L,
                double damping, const ppr_opts* o, ppr_plan** out) {
   const int64_t m = n ? row_ptr[n] : 0;
@@ -183,6 +212,26 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     const int per_cu = std::max<int>(1, std::min<int>(32 / p->hub_bw_waves, (int)((160 * 1024) / p->hub_lds_wave)));
     p->hub_bw_blocks = p->num_cus * per_cu;
   }
+  {
+    // chunk_accumulate's occurrence ranks from returning LDS atomics need same-address lanes served
+    // in lane order: probe it once on this device, fall back to ballot ranks otherwise
+    const char* e = getenv("PPR_LDS_RANK");
+    int* d_ok = nullptr;
+    int ok = 0;
+    if ((!e || atoi(e) != 0) && hipMalloc(&d_ok, sizeof(int)) == hipSuccess) {
+      ok = 1;
+      if (hipMemcpy(d_ok, &ok, sizeof(int), hipMemcpyHostToDevice) == hipSuccess) {
+        hipLaunchKernelGGL(k_probe_lds_rank, dim3(1), dim3(256), 0, p->stream, d_ok, 4096);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p->stream) != hipSuccess ||
+            hipMemcpy(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+          ok = 0;
+      } else {
+        ok = 0;
+      }
+      hipFree(d_ok);
+    }
+    p->lds_rank = ok ? 1u : 0u;
+  }
   hipFuncSetAttribute((const void*)k_hub_bucket_w<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket_w<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_seg<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -263,6 +312,7 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   a.diag = p->d_diag;
   a.unit = unit ? 1u : 0u;
   a.stats = (p->flags & PPR_FLAG_STATS) ? 1u : 0u;
+  a.lds_rank = p->lds_rank;
   if (unit) { a.sA = 0; a.sB = 0; a.active = -1; return a; }
   a.sA = ((it + 1) / 2) & 1;
   a.sB = (it / 2) & 1;

@@ -173,6 +173,7 @@ extern "C" int ppr_mccp2_plan_combine(ppr_plan* p) {
   a.mc = 1u;
   a.rp = p->d_rp;
   a.diag = p->d_diag;
+  a.lds_rank = p->lds_rank;
   const int64_t nl = (int64_t)p->mc_level_off.size() - 1;
   for (int64_t l = 0; l < nl; l++) {
     const int64_t b = p->mc_level_off[l], e = p->mc_level_off[l + 1];

@@ -39,7 +39,7 @@ constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per redu
 // wave bucket LDS: acc f64[T] | keys i32[T] | cnt u16[T] | vals f64[CHUNK] | touched u16[CHUNK] |
 // tof u16[CHUNK + 2]; the radix histogram of the final select (1 KB) aliases vals
 __host__ __device__ constexpr size_t hub_wave_lds(int T, int ng) {
-  return (size_t)T * 14 + (size_t)(ng * WAVE) * 12 + 4;
+  return (size_t)T * 16 + (size_t)(ng * WAVE) * 12 + 4;
 }
 
 struct HubDesc {
@@ -286,16 +286,18 @@ struct BucketWave {
   uint32_t* hist;
   int T, budget, fill;
   bool overflow;
+  bool ordered;  // lane-ordered LDS atomics (IterArgs::lds_rank)
 
-  __device__ __forceinline__ void setup(unsigned char* base, int T_, int NG) {
+  __device__ __forceinline__ void setup(unsigned char* base, int T_, int NG, bool ordered_) {
     T = T_;
+    ordered = ordered_;
     t.acc = reinterpret_cast<double*>(base);
     t.keys = reinterpret_cast<int*>(base + (size_t)T * 8);
     t.mask = (uint32_t)T - 1;
     t.nbits = 31 - __clz(T);
-    ck.cnt = reinterpret_cast<uint16_t*>(base + (size_t)T * 12);
-    ck.vals = reinterpret_cast<double*>(base + (size_t)T * 14);
-    ck.touched = reinterpret_cast<uint16_t*>(base + (size_t)T * 14 + (size_t)(NG * WAVE) * 8);
+    ck.cnt = reinterpret_cast<uint32_t*>(base + (size_t)T * 12);
+    ck.vals = reinterpret_cast<double*>(base + (size_t)T * 16);
+    ck.touched = reinterpret_cast<uint16_t*>(base + (size_t)T * 16 + (size_t)(NG * WAVE) * 8);
     ck.tof = ck.touched + NG * WAVE;
     hist = reinterpret_cast<uint32_t*>(ck.vals);  // final select only (after accumulation)
     budget = T / 4 * 3;
@@ -340,7 +342,7 @@ struct BucketWave {
       wave_fence();
     }
     if (overflow) return;
-    chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor);
+    chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor, ordered);
   }
 
   // keys >= tau (at most L by (score desc, id asc)) appended to the source's list
@@ -410,7 +412,7 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
   const BucketWork W = bw[cur];
   const long long t_start = a.diag ? (long long)clock64() : 0;
   BucketWave B;
-  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG);
+  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0);
   if (W.seed >= 0) B.seed(W.seed, W.selfval);
   const int nb = W.nb;
   for (int g0 = 0; g0 < nb; g0 += NG * WAVE) {
@@ -472,7 +474,7 @@ __global__ void __launch_bounds__(256) k_hub_seg(DevGraph g, DevSlab s, IterArgs
     if (dg) { const long long t2 = (long long)clock64(); ph[k] += (unsigned long long)(t2 - tc); tc = t2; }
   };
   BucketWave B;
-  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG);
+  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0);
   {
     const int rg = (int)row_range(v);
     if (rg >= r0 && rg < r1) B.seed(v, self_seed(a, e - b));

@@ -86,6 +86,7 @@ struct ppr_plan {
   size_t gath_bytes = 0;
   int num_cus = 256;
   int hub_bw_blocks = 0;           // persistent k_hub_bucket_w grid
+  uint32_t lds_rank = 0;           // k_probe_lds_rank passed (PPR_LDS_RANK=0 forces the ballot path)
   bool seg_enabled = false;        // segmented hub buckets (k_hub_seg, PPR_HUB_SEG=1)
   int seg_bucket = 256, seg_t = 512, seg_wpb = 1;
   int hub_bw_ng = 4;               // PPR_BW_NG: groups per chunk (4 or 8)

@@ -116,6 +116,7 @@ struct IterArgs {
   uint32_t mc;       // MCCompletePathV2 combine (include/mccompletepathv2.h:211-249)
   const int64_t* rp; // row pointers (out-degree of the source in the epilogue)
   unsigned long long* diag;  // PPR_DIAG: per-kernel histograms (nullptr = off)
+  uint32_t lds_rank;         // LDS atomics return same-address lanes in lane order (probed per plan)
 };
 
 __device__ __forceinline__ int read_slot(const IterArgs& a, int32_t cx) { return (cx < 0) ? a.sB : a.sA; }

@@ -161,19 +161,35 @@ __device__ __forceinline__ void table_apply(const LdsTable& t, bool valid, int k
 // but a hot key costs one dependent fma per occurrence instead of a cross-lane round per
 // occurrence. cnt must be all-zero on entry and is left all-zero.
 struct ChunkLds {
-  uint16_t* cnt;      // [T] per-slot occurrences in the chunk, then offsets
+  uint32_t* cnt;      // [T] per-slot occurrences in the chunk, then offsets
   double* vals;       // [NG * 64]
   uint16_t* touched;  // [NG * 64]
   uint16_t* tof;      // [NG * 64 + 1]
 };
 
+// With `ordered` (lane-ordered LDS atomics, verified on the device at plan creation: see
+// k_probe_lds_rank), phase A takes each record's occurrence index straight from a returning LDS
+// atomic add on its slot's counter -- same-address lanes of one instruction receive the old
+// values in lane order, i.e. stream order -- instead of from ballots over the slot bits.
 template <int NG>
 __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c, int nbits,
                                                  const bool (&valid)[NG], const uint32_t (&slot)[NG],
-                                                 const double (&val)[NG], double factor) {
+                                                 const double (&val)[NG], double factor, bool ordered) {
   const uint64_t lt = lanemask_lt();
   uint32_t occ[NG];
   int nt = 0;
+  if (ordered) {
+#pragma unroll
+    for (int k = 0; k < NG; k++) {
+      const uint32_t o = valid[k] ? atomicAdd(&c.cnt[slot[k]], 1u) : 1u;
+      const bool fresh = valid[k] && o == 0;
+      const uint64_t fm = __ballot(fresh);
+      if (fresh) c.touched[nt + __popcll(fm & lt)] = (uint16_t)slot[k];
+      nt += __popcll(fm);
+      occ[k] = o;
+    }
+    wave_fence();
+  } else
 #pragma unroll
   for (int k = 0; k < NG; k++) {
     uint64_t mm = __ballot(valid[k]);
@@ -187,7 +203,7 @@ __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c,
     uint32_t base = 0;
     if (leader) {
       base = c.cnt[slot[k]];
-      c.cnt[slot[k]] = (uint16_t)(base + __popcll(mm));
+      c.cnt[slot[k]] = base + (uint32_t)__popcll(mm);
     }
     const bool fresh = leader && base == 0;
     const uint64_t fm = __ballot(fresh);
@@ -204,7 +220,7 @@ __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c,
     const int i = i0 + lane_id();
     const int n = i < nt ? c.cnt[c.touched[i]] : 0;
     const int incl = wave_incl_scan(n);
-    if (i < nt) { c.tof[i] = (uint16_t)(run + incl - n); c.cnt[c.touched[i]] = (uint16_t)(run + incl - n); }
+    if (i < nt) { c.tof[i] = (uint16_t)(run + incl - n); c.cnt[c.touched[i]] = (uint32_t)(run + incl - n); }
     run += __shfl(incl, WAVE - 1);
   }
   if (lane_id() == 0) c.tof[nt] = (uint16_t)run;
