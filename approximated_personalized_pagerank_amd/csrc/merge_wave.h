@@ -150,9 +150,9 @@ __global__ void __launch_bounds__(256) k_stat_written(DevSlab s, IterArgs a, con
 
 // per-wave LDS bytes for table size T and padded width Lp
 // layout: acc f64[T] | keys i32[T] | rv u64[Lp] | rk i32[Lp] | hist u32[256] | hk i32[2Lp] |
-//         hv i32[2Lp] | mf i32[Lp]
+//         hv i32[2Lp] | mf i32[Lp] | own u8[T]
 __host__ __device__ constexpr size_t lds_wave_bytes(int T, int Lp) {
-  return (size_t)T * 12 + (size_t)Lp * 12 + 1024 + (size_t)Lp * 20;
+  return (size_t)T * 13 + (size_t)Lp * 12 + 1024 + (size_t)Lp * 20;
 }
 
 // the candidate of stream position c inside the current successor window (all lanes execute:
@@ -200,6 +200,7 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
   int* hk = reinterpret_cast<int*>(base + (size_t)T * 12 + (size_t)Lp * 12 + 1024);
   int* hv = hk + 2 * Lp;
   int* mf = hv + 2 * Lp;
+  uint8_t* own = reinterpret_cast<uint8_t*>(mf + Lp);
 
   const int v = list[w];
   const int64_t b = g.rp[v], e = g.rp[v + 1];
@@ -215,7 +216,7 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
       const int64_t i = e0 + lane_id();
       const bool valid = i < e;
       const int key = valid ? (g.colx[i] & 0x7fffffff) : 0;
-      table_apply(t, valid, key, 1.0, factor);
+      table_apply_own(t, own, valid, key, 1.0, factor);
     }
   } else {
     for (int64_t e0 = b; e0 < e; e0 += WAVE) {
@@ -240,7 +241,7 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
         const int ck = nk;
         const double cs = ns;
         if (g0 + WAVE < total) window_fetch(s, incl, u, sl, total, g0 + WAVE + lane_id(), nv, nk, ns);
-        table_apply(t, cv, ck, cs, factor);
+        table_apply_own(t, own, cv, ck, cs, factor);
       }
     }
   }

@@ -149,6 +149,27 @@ __device__ __forceinline__ void table_apply(const LdsTable& t, bool valid, int k
   apply_group(t.acc, valid, slot, s, factor, t.nbits);
 }
 
+// table_apply with a cheap duplicate test first: every valid lane stores its lane id into own[slot]
+// (one byte per slot); when every lane reads its own id back, the group's slots are distinct (two
+// lanes sharing a slot cannot both win the store) and each lane applies its fma directly -- the
+// usual case in the wave tier, where a group mostly holds one successor's basket (distinct keys).
+// Groups with a repeated slot take apply_group's ordered chains.
+__device__ __forceinline__ void table_apply_own(const LdsTable& t, uint8_t* own, bool valid, int key, double s,
+                                                double factor) {
+  const uint32_t slot = valid ? table_slot(t, key) : 0u;
+  const uint8_t l = (uint8_t)lane_id();
+  if (valid) own[slot] = l;
+  wave_fence();
+  const bool dup = valid && own[slot] != l;
+  wave_fence();
+  if (!__ballot(dup)) {
+    if (valid) t.acc[slot] = fma(s, factor, t.acc[slot]);
+    wave_fence();
+    return;
+  }
+  apply_group(t.acc, valid, slot, s, factor, t.nbits);
+}
+
 // Grouped accumulation of one chunk of up to NG * 64 ordered records (record q = lane q % 64 of
 // group q / 64), an alternative to apply_group for streams with many repeated keys:
 //   A  per group, in order: find-or-insert every key (`slotfn`), rank the lanes sharing a slot
