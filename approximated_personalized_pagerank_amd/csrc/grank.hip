@@ -203,8 +203,18 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_bw_waves = e5 ? std::max(1, std::min(4, atoi(e5))) : 1;
     const char* e6 = getenv("PPR_HUB_SLICE");
     p->hub_slice = std::max<int>(std::max<int>(64, (int)L), e6 ? atoi(e6) : HUB_SLICE);
+    const char* e7 = getenv("PPR_HUB_STREAMS");
+    p->hub_streams = (e7 && atoi(e7) == 1) ? 1 : 2;
   }
   p->hub_lds_wave = hub_wave_lds(p->hub_wave_t, p->hub_bw_ng) * p->hub_bw_waves;
+  if (p->hub_streams == 2) {
+    if (hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&p->stream3, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&p->ev_wave, hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
+    for (int i = 0; i < 2; i++)
+      if (hipEventCreateWithFlags(&p->ev_part[i], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&p->ev_buck[i], hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
+  }
   {
     hipDeviceProp_t prop;
     p->num_cus = hipGetDeviceProperties(&prop, p->device) == hipSuccess ? prop.multiProcessorCount : 256;
@@ -418,8 +428,12 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   size_t scan_tmp = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (const int32_t*)nullptr, (int32_t*)nullptr, (int)mx.cm, st);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  // shared: descriptors + overflow list; then one (or two) per-batch regions
   size_t off = 0;
   const size_t o_desc = off; off = al(off + sizeof(HubDesc) * nd_all);
+  const size_t o_ovl = off;  off = al(off + 4 * (nd_all + 1));
+  const size_t shared = off;
+  off = 0;
   const size_t o_tile = off; off = al(off + sizeof(HubTask) * mx.ntiles);
   const size_t o_buck = off; off = al(off + sizeof(HubTask) * mx.nbuck);
   const size_t o_rt = off;   off = al(off + sizeof(HubTask) * (mx.nrt + 1));
@@ -435,101 +449,117 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   const size_t o_pc = off;   off = al(off + 4 * maxnd);
   const size_t o_tau = off;  off = al(off + 8 * maxnd);
   const size_t o_of = off;   off = al(off + 4 * maxnd);
-  const size_t o_ovl = off;  off = al(off + 4 * (nd_all + 1));
   const size_t o_gl = off;   off = al(off + sizeof(HubTask) * (mx.nbuck + 1));
   const size_t o_cnt = off;  off = al(off + 16);
   const size_t o_bw = off;   off = al(off + sizeof(BucketWork) * mx.nbuck);
-  int rc = ensure_scratch(p, off);
+  const size_t region = off;
+  // two streams only pay when there is a next batch to overlap with
+  const int nreg = (p->hub_streams == 2 && batches.size() > 1) ? 2 : 1;
+  int rc = ensure_scratch(p, shared + region * nreg);
   if (rc) return rc;
   char* base = (char*)p->d_scratch;
   HubDesc* d_desc_all = (HubDesc*)(base + o_desc);
-  HubTask* d_tile = (HubTask*)(base + o_tile);
-  HubTask* d_buck = (HubTask*)(base + o_buck);
-  HubTask* d_rt = (HubTask*)(base + o_rt);
-  HubTask* d_sg = (HubTask*)(base + o_sg);
-  int32_t* d_cm = (int32_t*)(base + o_cm);
-  int32_t* d_cmx = (int32_t*)(base + o_cmx);
-  void* d_tmp = (void*)(base + o_tmp);
-  HubRec* d_st = (HubRec*)(base + o_st);
-  int32_t* d_pk = (int32_t*)(base + o_pk);
-  double* d_ps = (double*)(base + o_ps);
-  int32_t* d_rk = (int32_t*)(base + o_rk);
-  double* d_rs = (double*)(base + o_rs);
-  uint32_t* d_pc = (uint32_t*)(base + o_pc);
-  unsigned long long* d_tau = (unsigned long long*)(base + o_tau);
-  int32_t* d_oflag = (int32_t*)(base + o_of);
   int32_t* d_ovl = (int32_t*)(base + o_ovl);     // [0] count, [1..] sources for the HBM-table path
-  HubTask* d_gl = (HubTask*)(base + o_gl);
-  uint32_t* d_lc = (uint32_t*)(base + o_cnt);    // [1] spill list length
-  BucketWork* d_bw = (BucketWork*)(base + o_bw);
   HIP_OK(hipMemcpyAsync(d_desc_all, desc, sizeof(HubDesc) * nd_all, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemsetAsync(d_ovl, 0, 4, st));
-  for (const Batch& b : batches) {
+  // partition stage (expand, count, scan, scatter, prep) of batch i on `st`, its bucket stage
+  // (bucket waves, spills, segments, reduce, final) on `sb`; batch i+2 reuses batch i's region
+  // once batch i's bucket stage has finished
+  hipStream_t sb = nreg == 2 ? p->stream2 : st;
+  for (size_t bi = 0; bi < batches.size(); bi++) {
+    const Batch& b = batches[bi];
+    const int r = (int)(bi % nreg);
+    char* rb = base + shared + region * r;
+    HubTask* d_tile = (HubTask*)(rb + o_tile);
+    HubTask* d_buck = (HubTask*)(rb + o_buck);
+    HubTask* d_rt = (HubTask*)(rb + o_rt);
+    HubTask* d_sg = (HubTask*)(rb + o_sg);
+    int32_t* d_cm = (int32_t*)(rb + o_cm);
+    int32_t* d_cmx = (int32_t*)(rb + o_cmx);
+    void* d_tmp = (void*)(rb + o_tmp);
+    HubRec* d_st = (HubRec*)(rb + o_st);
+    int32_t* d_pk = (int32_t*)(rb + o_pk);
+    double* d_ps = (double*)(rb + o_ps);
+    int32_t* d_rk = (int32_t*)(rb + o_rk);
+    double* d_rs = (double*)(rb + o_rs);
+    uint32_t* d_pc = (uint32_t*)(rb + o_pc);
+    unsigned long long* d_tau = (unsigned long long*)(rb + o_tau);
+    int32_t* d_oflag = (int32_t*)(rb + o_of);
+    HubTask* d_gl = (HubTask*)(rb + o_gl);
+    uint32_t* d_lc = (uint32_t*)(rb + o_cnt);    // [1] spill list length
+    BucketWork* d_bw = (BucketWork*)(rb + o_bw);
     const size_t nd = b.d1 - b.d0;
     HubDesc* d_desc = d_desc_all + b.d0;
     const int maxP = b.maxP;
+    if (nreg == 2 && bi >= 2) HIP_OK(hipStreamWaitEvent(st, p->ev_buck[r], 0));
     HIP_OK(hipMemsetAsync(d_pc, 0, 4 * nd, st));
     HIP_OK(hipMemsetAsync(d_tau, 0, 8 * nd, st));
     HIP_OK(hipMemsetAsync(d_oflag, 0, 4 * nd, st));
     HIP_OK(hipMemsetAsync(d_lc, 0, 8, st));
     hipLaunchKernelGGL(k_hub_expand, dim3((unsigned)nd), dim3(256), 0, st, d_desc, d_tile, d_buck, d_rt, d_sg);
     HIP_OK(hipGetLastError());
+    const int64_t ntiles = b.ntiles;
+    const int64_t nbuck = b.nbuck;
+    if (ntiles) {
+      const size_t lds_tile = (size_t)WAVES_PER_BLOCK * maxP * 4;
+      const unsigned tb = (unsigned)((ntiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+      hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm,
+                         d_tau);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, scan_tmp, d_cm, d_cmx, (int)b.cm, st));
+      hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
+                         d_cmx, d_st);
+      HIP_OK(hipGetLastError());
+      hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, a, d_desc, d_buck,
+                         nbuck, d_cmx, d_tau, d_bw);
+      HIP_OK(hipGetLastError());
+    }
+    if (nreg == 2) {
+      HIP_OK(hipEventRecord(p->ev_part[r], st));
+      HIP_OK(hipStreamWaitEvent(sb, p->ev_part[r], 0));
+    }
     if (b.nseg) {
       hipLaunchKernelGGL(k_hub_seg<4>, dim3((unsigned)((b.nseg + p->seg_wpb - 1) / p->seg_wpb)), dim3(64 * p->seg_wpb),
-                         hub_wave_lds(p->seg_t, 4) * p->seg_wpb, st, g, s, a, d_desc, d_sg, b.nseg, d_pk, d_ps, d_pc,
+                         hub_wave_lds(p->seg_t, 4) * p->seg_wpb, sb, g, s, a, d_desc, d_sg, b.nseg, d_pk, d_ps, d_pc,
                          d_oflag, d_ovl, p->seg_t);
       HIP_OK(hipGetLastError());
       p->merge_launches++;
     }
-    const int64_t ntiles = b.ntiles;
     if (ntiles) {
-    const size_t lds_tile = (size_t)WAVES_PER_BLOCK * maxP * 4;
-    const unsigned tb = (unsigned)((ntiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-    hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm,
-                       d_tau);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, scan_tmp, d_cm, d_cmx, (int)b.cm, st));
-    hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
-                       d_cmx, d_st);
-    HIP_OK(hipGetLastError());
-    const int64_t nbuck = b.nbuck;
-    // every bucket goes to a single wave first: a bucket made long by one hot key (a core node
-    // present in most successor baskets) still has few distinct keys, and its sequential fma
-    // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
-    hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, a, d_desc, d_buck, nbuck,
-                       d_cmx, d_tau, d_bw);
-    HIP_OK(hipGetLastError());
-    {
+      // every bucket goes to a single wave first: a bucket made long by one hot key (a core node
+      // present in most successor baskets) still has few distinct keys, and its sequential fma
+      // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
       const int wpb = p->hub_bw_waves;
       const int64_t blocks = (nbuck + wpb - 1) / wpb;
       const dim3 grid((unsigned)blocks), blk(64 * wpb);
       if (p->hub_bw_ng == 8)
-        hipLaunchKernelGGL(k_hub_bucket_w<8>, grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
+        hipLaunchKernelGGL(k_hub_bucket_w<8>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
                            d_gl, d_lc + 1, p->hub_wave_t);
       else
-        hipLaunchKernelGGL(k_hub_bucket_w<4>, grid, blk, p->hub_lds_wave, st, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
+        hipLaunchKernelGGL(k_hub_bucket_w<4>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
                            d_gl, d_lc + 1, p->hub_wave_t);
       HIP_OK(hipGetLastError());
+      // spilled buckets (distinct keys beyond the wave table): persistent workgroups over the spill
+      // list, whose length only the device knows
+      hipLaunchKernelGGL(k_hub_bucket, dim3((unsigned)p->num_cus), dim3(WG_THREADS), p->hub_lds_wg, sb, s, a, g,
+                         d_desc, d_gl, d_lc + 1, d_cmx, d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_oflag, d_ovl);
+      HIP_OK(hipGetLastError());
     }
-    // spilled buckets (distinct keys beyond the wave table): persistent workgroups over the spill
-    // list, whose length only the device knows
-    hipLaunchKernelGGL(k_hub_bucket, dim3((unsigned)p->num_cus), dim3(WG_THREADS), p->hub_lds_wg, st, s, a, g,
-                       d_desc, d_gl, d_lc + 1, d_cmx, d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_oflag, d_ovl);
-    HIP_OK(hipGetLastError());
-    }  // staged partition
     // long appended lists are cut (k_hub_reduce) so no k_hub_final workgroup selects from more
     // than a few slices' worth of entries; slices are reserved for the worst case, idle ones exit
     if (b.nrt) {
-      hipLaunchKernelGGL(k_hub_reduce, dim3((unsigned)b.nrt), dim3(WG_THREADS), p->hub_lds_final, st, s, d_desc,
+      hipLaunchKernelGGL(k_hub_reduce, dim3((unsigned)b.nrt), dim3(WG_THREADS), p->hub_lds_final, sb, s, d_desc,
                          d_rt, d_pc, d_pk, d_ps, d_rk, d_rs, p->Lp, slice);
       HIP_OK(hipGetLastError());
       p->merge_launches++;
     }
-    hipLaunchKernelGGL(k_hub_final, dim3((unsigned)nd), dim3(WG_THREADS), p->hub_lds_final, st, s, a, d_desc,
+    hipLaunchKernelGGL(k_hub_final, dim3((unsigned)nd), dim3(WG_THREADS), p->hub_lds_final, sb, s, a, d_desc,
                        d_oflag, d_pc, d_pk, d_ps, d_rk, d_rs, slice, p->Lp, maxdiff, p->d_stats);
     HIP_OK(hipGetLastError());
     p->merge_launches += 9;
+    if (nreg == 2) HIP_OK(hipEventRecord(p->ev_buck[r], sb));
   }
+  if (nreg == 2) HIP_OK(hipStreamWaitEvent(st, p->ev_buck[(batches.size() - 1) % 2], 0));
   int32_t novf = 0;
   HIP_OK(hipMemcpyAsync(&novf, d_ovl, 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
@@ -549,6 +579,10 @@ int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count
   if (count <= 0) return PPR_OK;
   HIP_OK(hipEventRecord(p->ev_m0, p->stream));
   int rc = run_merge_impl(p, a, list, count, maxdiff);
+  if (p->stream3) {  // the wave tiers ran on stream3
+    HIP_OK(hipEventRecord(p->ev_wave, p->stream3));
+    HIP_OK(hipStreamWaitEvent(p->stream, p->ev_wave, 0));
+  }
   if (rc) return rc;
   HIP_OK(hipEventRecord(p->ev_m1, p->stream));
   HIP_OK(hipEventSynchronize(p->ev_m1));
@@ -576,11 +610,13 @@ static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, i
   uint32_t cnt[NLISTS + 1];
   HIP_OK(hipMemcpyAsync(cnt, p->d_tier_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
+  // the classification is complete (host sync): the wave tiers need no event to start on stream3
+  hipStream_t sw = p->stream3 ? p->stream3 : st;
   for (int t = 0; t < NT; t++) {
     if (!cnt[t] || !p->tierT[t]) continue;
     const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * WAVES_PER_BLOCK;
     const int64_t blocks = ((int64_t)cnt[t] + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-    hipLaunchKernelGGL(k_merge_lds, dim3((unsigned)blocks), dim3(256), bytes, st, g, s, a,
+    hipLaunchKernelGGL(k_merge_lds, dim3((unsigned)blocks), dim3(256), bytes, sw, g, s, a,
                        p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], p->tierT[t], p->Lp,
                        maxdiff, p->d_stats);
     HIP_OK(hipGetLastError());

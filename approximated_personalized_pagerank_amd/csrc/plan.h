@@ -102,6 +102,12 @@ struct ppr_plan {
   int64_t merge_launches = 0;
   double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_m0 = nullptr, ev_m1 = nullptr;
+  // PPR_HUB_STREAMS=2 (default): the hub pipeline's bucket stage of batch i runs on stream2 while
+  // the partition stage of batch i+1 runs on the plan's stream (two scratch regions), and the wave
+  // tiers run on stream3 beside the whole hub pipeline (disjoint sources)
+  int hub_streams = 2;
+  hipStream_t stream2 = nullptr, stream3 = nullptr;
+  hipEvent_t ev_part[2] = {nullptr, nullptr}, ev_buck[2] = {nullptr, nullptr}, ev_wave = nullptr;
   unsigned long long* d_diag = nullptr;  // PPR_DIAG=1: kernel histograms, printed at destroy
   // MCCompletePathV2 (mccp2.hip)
   bool mc = false;
@@ -128,6 +134,13 @@ inline void plan_free(ppr_plan* p) {
   if (p->ev_b) hipEventDestroy(p->ev_b);
   if (p->ev_m0) hipEventDestroy(p->ev_m0);
   if (p->ev_m1) hipEventDestroy(p->ev_m1);
+  for (int i = 0; i < 2; i++) {
+    if (p->ev_part[i]) hipEventDestroy(p->ev_part[i]);
+    if (p->ev_buck[i]) hipEventDestroy(p->ev_buck[i]);
+  }
+  if (p->ev_wave) hipEventDestroy(p->ev_wave);
+  if (p->stream2) hipStreamDestroy(p->stream2);
+  if (p->stream3) hipStreamDestroy(p->stream3);
   if (p->comm) ncclCommDestroy(p->comm);
   hipFree(p->d_xsend); hipFree(p->d_xrecv);
   if (p->h_hub_pin) hipHostFree(p->h_hub_pin);
