@@ -12,6 +12,9 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libppr_hip.so")
+# A/B experiments only (tools/build_variant.py): load a variant build of the same ABI instead
+if os.environ.get("PPR_LIB_VARIANT"):
+    LIB_PATH = os.path.join(PKG_DIR, "libppr_hip_" + os.environ["PPR_LIB_VARIANT"] + ".so")
 
 PPR_MAX_ITER_STATS = 256
 PPR_FLAG_STATS = 1

@@ -205,6 +205,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_slice = std::max<int>(std::max<int>(64, (int)L), e6 ? atoi(e6) : HUB_SLICE);
     const char* e7 = getenv("PPR_HUB_STREAMS");
     p->hub_streams = (e7 && atoi(e7) == 1) ? 1 : 2;
+    const char* e8 = getenv("PPR_HUB_BUDGET");
+    if (e8) p->hub_budget = std::max<int64_t>(1024, std::min<int64_t>(1LL << 28, atoll(e8)));
   }
   p->hub_lds_wave = hub_wave_lds(p->hub_wave_t, p->hub_bw_ng) * p->hub_bw_waves;
   if (p->hub_streams == 2) {
@@ -360,7 +362,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   DevGraph g{p->d_rp, p->d_colx, p->n};
   const DevSlab s = dev_slab(p);
   const int64_t L = p->L;
-  const int64_t budget = 1LL << 28;  // staged candidates per batch (4 GiB of 16-B records)
+  const int64_t budget = p->hub_budget;  // staged candidates per batch (default 4 GiB of 16-B records)
   const int slice = p->hub_slice;
   using Batch = HubBatch;
   std::vector<Batch>& batches = p->hub_batches;
@@ -510,6 +512,10 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
                          d_cmx, d_st);
       HIP_OK(hipGetLastError());
+    }
+    // a batch of sources without successors (init of dangling nodes) has no tiles but still has
+    // buckets: the one holding the source's own seed entry
+    if (nbuck) {
       hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, a, d_desc, d_buck,
                          nbuck, d_cmx, d_tau, d_bw);
       HIP_OK(hipGetLastError());
@@ -525,7 +531,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       HIP_OK(hipGetLastError());
       p->merge_launches++;
     }
-    if (ntiles) {
+    if (nbuck) {
       // every bucket goes to a single wave first: a bucket made long by one hot key (a core node
       // present in most successor baskets) still has few distinct keys, and its sequential fma
       // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.

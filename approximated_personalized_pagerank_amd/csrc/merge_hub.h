@@ -86,13 +86,22 @@ __global__ void __launch_bounds__(256) k_hub_expand(const HubDesc* desc, HubTask
   for (int x = threadIdx.x; x < D.nsl; x += blockDim.x) rts[D.rt_off + x] = HubTask{d, x};
 }
 
-// one staged candidate: key and score in one 16-B record, so a scattered store touches one
-// partial line instead of two (separate key / score arrays)
-struct alignas(16) HubRec {
-  int32_t key;
-  int32_t pad;
-  double sc;
+// one staged candidate: key and score packed in 12 bytes (dword aligned, one dwordx3 store /
+// load), so a scattered store touches one partial line instead of two (separate key / score
+// arrays); measured as fast as a padded 16-B record, with 3/4 of its staging memory
+struct HubRec {
+  uint32_t w[3];
 };
+__device__ __forceinline__ HubRec hub_rec(int key, double sc) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(sc);
+  HubRec r{};
+  r.w[0] = (uint32_t)key; r.w[1] = (uint32_t)b; r.w[2] = (uint32_t)(b >> 32);
+  return r;
+}
+__device__ __forceinline__ int rec_key(const HubRec& r) { return (int)r.w[0]; }
+__device__ __forceinline__ double rec_sc(const HubRec& r) {
+  return __longlong_as_double((long long)(((unsigned long long)r.w[2] << 32) | r.w[1]));
+}
 
 __device__ __forceinline__ uint32_t hub_digit(int key, int logP) {
   return logP == 0 ? 0u : (hash_b((uint32_t)key) >> (32 - logP));
@@ -232,7 +241,7 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
     wave_fence();
     if (valid) {
       if (rank == 0) run[dg] = base + (uint32_t)__popcll(match);
-      stv[base + rank] = HubRec{key, 0, sv};
+      stv[base + rank] = hub_rec(key, sv);
     }
     wave_fence();
   });
@@ -423,9 +432,9 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
     for (int k = 0; k < NG; k++) {
       const int q = g0 + k * WAVE + l;
       cv[k] = q < nb;
-      const HubRec r = cv[k] ? st[W.start + q] : HubRec{0, 0, 0.0};
-      kk[k] = r.key;
-      cs[k] = r.sc;
+      const HubRec r = cv[k] ? st[W.start + q] : HubRec{};
+      kk[k] = rec_key(r);
+      cs[k] = rec_sc(r);
     }
     B.chunk<NG>(cv, kk, cs, W.factor);
     if (B.overflow) break;
@@ -585,9 +594,9 @@ __device__ __forceinline__ void hub_bucket_one(const DevSlab& s, const IterArgs&
   auto each = [&](auto&& fn) {
     auto ld = [&](int64_t q, bool& vv, int& kk, double& ss) {
       vv = q < nb;
-      const HubRec r = vv ? st[sb + q] : HubRec{0, 0, 0.0};
-      kk = r.key;
-      ss = r.sc;
+      const HubRec r = vv ? st[sb + q] : HubRec{};
+      kk = rec_key(r);
+      ss = rec_sc(r);
     };
     bool nv0, nv1;
     int nk0, nk1;

@@ -106,6 +106,7 @@ struct ppr_plan {
   // the partition stage of batch i+1 runs on the plan's stream (two scratch regions), and the wave
   // tiers run on stream3 beside the whole hub pipeline (disjoint sources)
   int hub_streams = 2;
+  int64_t hub_budget = 1LL << 28;  // PPR_HUB_BUDGET: staged candidates per hub batch (16-B records)
   hipStream_t stream2 = nullptr, stream3 = nullptr;
   hipEvent_t ev_part[2] = {nullptr, nullptr}, ev_buck[2] = {nullptr, nullptr}, ev_wave = nullptr;
   unsigned long long* d_diag = nullptr;  // PPR_DIAG=1: kernel histograms, printed at destroy

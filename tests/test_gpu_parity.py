@@ -133,7 +133,9 @@ def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
 
 @pytest.mark.parametrize("seg_env", [
     {"PPR_HUB_SEG": "0"},                                                   # staged partition only
-    {"PPR_HUB_SEG": "0", "PPR_HUB_STREAMS": "1", "PPR_HUB_SLICE": "64"},    # one stream, small batches
+    {"PPR_HUB_SEG": "0", "PPR_HUB_BUDGET": "4096"},                         # many batches, two streams
+    {"PPR_HUB_SEG": "0", "PPR_HUB_BUDGET": "4096", "PPR_HUB_STREAMS": "1"},  # many batches, one stream
+    {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "64", "PPR_HUB_BUDGET": "1024"},  # segments over many batches
     {"PPR_HUB_SEG": "0", "PPR_LDS_RANK": "0"},                              # ballot occurrence ranks
     {"PPR_HUB_SEG": "0", "PPR_HUB_WAVE_T": "256", "PPR_HUB_BUCKET": "512"},  # spills to k_hub_bucket
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "16"},                           # many segments, up to 64 buckets
