@@ -205,6 +205,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_slice = std::max<int>(std::max<int>(64, (int)L), e6 ? atoi(e6) : HUB_SLICE);
     const char* e7 = getenv("PPR_HUB_STREAMS");
     p->hub_streams = (e7 && atoi(e7) == 1) ? 1 : 2;
+    const char* e10 = getenv("PPR_HUB_MIX");
+    p->hub_mix = e10 ? std::max(0, std::min(HUB_MAX_LOGP, atoi(e10))) : 8;
+    const char* e9 = getenv("PPR_HUB_TILE_PB");
+    p->hub_tile_pb = e9 ? std::max(0, std::min(64, atoi(e9))) : HUB_TILE_PER_BUCKET;
     const char* e8 = getenv("PPR_HUB_BUDGET");
     if (e8) p->hub_budget = std::max<int64_t>(1024, std::min<int64_t>(1LL << 28, atoll(e8)));
   }
@@ -376,14 +380,30 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   auto logp_of = [&](int64_t need) {
     return std::max(1, std::min(HUB_MAX_LOGP, ceil_log2((need + p->hub_bucket - 1) / p->hub_bucket)));
   };
-  // hubs stay in list order: batches mixing large and small sources hide the long hot-key
-  // buckets of the large ones (grouping them by size measured 10 % slower)
+  // batches mix large and small sources: that hides the long hot-key buckets of the large ones
+  // (grouping them by size measured 10 % slower), and it balances the two pipeline stages, whose
+  // costs differ by source size (large partitions: count + scatter bound; many small sources:
+  // bucket bound). PPR_HUB_MIX > 0 interleaves sources with P >= 2^PPR_HUB_MIX evenly among the
+  // others; 0 keeps the classification's list order.
+  std::vector<uint32_t> order(nbig);
+  if (p->hub_mix > 0) {
+    std::vector<uint32_t> lg, sm;
+    for (size_t i = 0; i < nbig; i++) (logp_of(cand[i]) >= p->hub_mix ? lg : sm).push_back((uint32_t)i);
+    size_t a0 = 0, b0 = 0, k = 0;
+    while (a0 < lg.size() || b0 < sm.size()) {
+      // take from the list that is behind its share (a0 / |lg| vs b0 / |sm|)
+      const bool take_lg = b0 >= sm.size() || (a0 < lg.size() && a0 * sm.size() <= b0 * lg.size());
+      order[k++] = take_lg ? lg[a0++] : sm[b0++];
+    }
+  } else {
+    for (size_t i = 0; i < nbig; i++) order[i] = (uint32_t)i;
+  }
   {
     size_t oi = 0;
     while (oi < nbig) {
       Batch b{nd_all, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1};
       while (oi < nbig) {
-        const size_t i = oi;
+        const size_t i = order[oi];
         const int v = big[i];
         const int64_t need = cand[i];
         const int64_t deg = cand[nbig + i];
@@ -396,7 +416,10 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
             (b.stg + (seg ? 0 : need) > budget || b.pt + ptc0 > budget || b.nseg + (1 << lseg) > (1 << 24))) break;
         const int logP = seg ? lseg : logp_of(need);
         const int P = 1 << logP;
-        const int tw = (int)std::max<int64_t>(1, std::min<int64_t>(HUB_TILE, HUB_TILE_CAND / L));
+        // tile = tw successors (windows of 64 on one wave); large partitions get long tiles
+        const int64_t tcand = std::max<int64_t>(HUB_TILE_CAND, (int64_t)p->hub_tile_pb << logP);
+        const int64_t tw0 = std::max<int64_t>(1, tcand / L);
+        const int tw = (int)(tw0 > WAVE ? (tw0 + WAVE - 1) / WAVE * WAVE : tw0);
         const int T = seg ? 0 : (int)((deg + tw - 1) / tw);
         const int64_t ptc = (int64_t)P * L;
         const int nsl = ptc > 2 * slice ? (int)((ptc + slice - 1) / slice) : 0;

@@ -26,8 +26,9 @@ namespace pprk {
 //     tau = round(f * max_{u: len[u] = L} min(row u))
 // is a lower bound of the L-th largest final value: a bucket never needs to emit a key below tau
 // (ties at tau are kept, the (score desc, id asc) order decides them in k_hub_final).
-constexpr int HUB_TILE = 64;          // max successors per tile (one wave); HubDesc.tw is the actual width
-constexpr int HUB_TILE_CAND = 4096;   // target candidates per tile: tw = clamp(4096 / L, 1, 64)
+constexpr int HUB_TILE_CAND = 4096;   // target candidates per tile: tw = max(1, target / L) successors
+constexpr int HUB_TILE_PER_BUCKET = 4;  // ... and target >= 4 P: the count matrix (P ints per tile) and
+                                        // the scatter's run seeds stay <= 1/4 int per candidate
 constexpr int HUB_BUCKET = 384;       // default target candidates per bucket (PPR_HUB_BUCKET)
 constexpr int HUB_MAX_LOGP = 12;      // per-wave LDS counters of the partition: 16 KB
 constexpr int HUB_WAVE_T = 512;       // default wave bucket table slots (PPR_HUB_WAVE_T): 13 KB of LDS per wave
@@ -107,20 +108,18 @@ __device__ __forceinline__ uint32_t hub_digit(int key, int logP) {
   return logP == 0 ? 0u : (hash_b((uint32_t)key) >> (32 - logP));
 }
 
-// walk the candidates of tile t of source d in successor order, 64 per step
+// walk the candidates of successors [i0, e) (at most one per lane) in successor order, 64 per step
 template <class F>
-__device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
-                                              int v, int t, int tw, F f) {
-  const int64_t b = g.rp[v];
-  const int64_t e = min(g.rp[v + 1], b + (int64_t)(t + 1) * tw);
-  const int64_t i = b + (int64_t)t * tw + lane_id();
+__device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
+                                                int64_t i0, int64_t e, F f) {
+  const int64_t i = i0 + lane_id();
   if (a.unit) {  // init: every successor contributes {u: 1.0}
-    const bool valid = lane_id() < tw && i < e;
+    const bool valid = i < e;
     f(valid, valid ? (g.colx[i] & 0x7fffffff) : 0, 1.0);
     return;
   }
   int u = 0, sl = 0, ln = 0;
-  if (lane_id() < tw && i < e) {
+  if (i < e) {
     const int32_t cx = g.colx[i];
     u = cx & 0x7fffffff;
     sl = read_slot(a, cx);
@@ -171,6 +170,16 @@ __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& 
   }
 }
 
+// walk the candidates of tile t (successors [t * tw, (t + 1) * tw) of source v) in successor
+// order: windows of 64 successors, 64 candidates per step
+template <class F>
+__device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
+                                              int v, int t, int tw, F f) {
+  const int64_t b = g.rp[v] + (int64_t)t * tw;
+  const int64_t e = min(g.rp[v + 1], b + (int64_t)tw);
+  for (int64_t w0 = b; w0 < e; w0 += WAVE) hub_window_walk(g, s, a, w0, min(e, w0 + WAVE), f);
+}
+
 __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterArgs a,
                                                    const HubDesc* desc, const HubTask* tasks,
                                                    int64_t ntasks, int maxP, int32_t* cm,
@@ -183,14 +192,17 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
   const HubDesc d = desc[tk.d];
   const int P = 1 << d.logP;
   if (!a.unit) {  // max over this tile's full-row successors of their row minimum (unscaled)
-    const int64_t e = g.rp[d.v + 1];
-    const int64_t i = g.rp[d.v] + (int64_t)tk.x * d.tw + lane_id();
+    const int64_t b = g.rp[d.v] + (int64_t)tk.x * d.tw;
+    const int64_t e = min(g.rp[d.v + 1], b + (int64_t)d.tw);
     unsigned long long mb = 0;
-    if (lane_id() < d.tw && i < e) {
+    for (int64_t i = b + lane_id(); i < e; i += WAVE) {
       const int32_t cx = g.colx[i];
       const int u = cx & 0x7fffffff;
       const int sl = read_slot(a, cx);
-      if (s.len[s.lrow(sl, u)] == s.L) mb = dbits(s.rmin[s.lrow(sl, u)]);  // row minimum
+      if (s.len[s.lrow(sl, u)] == s.L) {  // row minimum
+        const unsigned long long m = dbits(s.rmin[s.lrow(sl, u)]);
+        mb = m > mb ? m : mb;
+      }
     }
 #pragma unroll
     for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }

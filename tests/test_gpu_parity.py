@@ -136,6 +136,9 @@ def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
     {"PPR_HUB_SEG": "0", "PPR_HUB_BUDGET": "4096"},                         # many batches, two streams
     {"PPR_HUB_SEG": "0", "PPR_HUB_BUDGET": "4096", "PPR_HUB_STREAMS": "1"},  # many batches, one stream
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "64", "PPR_HUB_BUDGET": "1024"},  # segments over many batches
+    {"PPR_HUB_SEG": "0", "PPR_HUB_BUCKET": "64", "PPR_HUB_TILE_PB": "64",   # long multi-window tiles,
+     "PPR_HUB_MIX": "3", "PPR_HUB_BUDGET": "8192"},                         # interleaved batches
+    {"PPR_HUB_SEG": "0", "PPR_HUB_MIX": "0"},                               # list order
     {"PPR_HUB_SEG": "0", "PPR_LDS_RANK": "0"},                              # ballot occurrence ranks
     {"PPR_HUB_SEG": "0", "PPR_HUB_WAVE_T": "256", "PPR_HUB_BUCKET": "512"},  # spills to k_hub_bucket
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "16"},                           # many segments, up to 64 buckets
