@@ -124,10 +124,12 @@ int ppr_grank_plan_iterate(ppr_plan* p, int32_t it, int64_t begin, int64_t end);
 int ppr_grank_plan_read_maxdiff(ppr_plan* p, int32_t it, double* maxdiff); /* syncs */
 int ppr_grank_plan_finish(ppr_plan* p, int32_t iterations_run);
 
-/* Row exchange for source sharding: device pointers (ids int32[L], scores f64[L], len int32)
- * of the basket rows iteration `it` wrote, plus pack/unpack of active-list ranges into a
- * contiguous device buffer of rows: int32 len, int32 pad, int32 ids[Le], f64 scores[L] with Le
- * = L rounded up to even (ppr_grank_plan_row_bytes). Asynchronous on the plan's stream. */
+/* Row exchange for source sharding: pack/unpack of active-list ranges of the rows iteration `it`
+ * wrote into a contiguous device buffer of fixed-size rows: int32 len, int32 pad, int32 ids[Le],
+ * f64 scores[L], f64 row minimum, uint16 range index[64] (Le = L rounded up to even; size from
+ * ppr_grank_plan_row_bytes). Slab rows are kept in key-hash order, not score order; the range
+ * index and minimum travel with them so the receiving rank's merge can use them unchanged.
+ * Asynchronous on the plan's stream. */
 int ppr_grank_plan_row_bytes(ppr_plan* p, int64_t* bytes);
 int ppr_grank_plan_pack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* dev_buf);
 int ppr_grank_plan_unpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* dev_buf);
@@ -140,8 +142,9 @@ int ppr_grank_plan_fold_maxdiff(ppr_plan* p, int32_t it, double maxdiff);
  * Rank 0 creates a 128-byte RCCL unique id, the caller broadcasts it (any channel), and every rank
  * calls ppr_grank_plan_comm_init. ppr_grank_plan_run_sharded then runs the whole job like
  * ppr_grank_plan_run, but each rank merges only its work-balanced range of every iteration's
- * active list (ppr_grank_plan_shard_bounds) and the written rows are exchanged with
- * ncclAllGather on the plan's stream; maxDiff is combined with ncclAllReduce(MAX) so every rank
+ * active list (ppr_grank_plan_shard_bounds) and the written rows are exchanged with one
+ * grouped set of ncclBroadcast calls (an all-gather of variable-size ranges, no padding) on
+ * the plan's stream; maxDiff is combined with ncclAllReduce(MAX) so every rank
  * applies the reference's stopping rule to the same value. Results equal the 1-GPU run. */
 int ppr_device_count(int32_t* count);
 int ppr_comm_unique_id(void* id128);
@@ -152,11 +155,14 @@ int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double toleranc
 int ppr_grank_plan_pack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* host_buf);
 int ppr_grank_plan_unpack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* host_buf);
 
-/* Downloads: final top-K (n*K) and the current L-slab (n*L, rows sorted, len per node). */
+/* Downloads: final top-K (n*K) and the current L-slab (n*L, len per node; each row returned
+ * sorted by (score desc, id asc) -- the device keeps rows in key-hash order). */
 int ppr_grank_plan_fetch(ppr_plan* p, int32_t* out_ids, double* out_scores, int32_t* out_len);
 int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, int32_t* ids, double* scores,
                               int32_t* len);
-/* Device stream the plan runs on (hipStream_t as void*), for event timing by the caller. */
+/* Device stream the plan runs on (hipStream_t as void*), for event timing by the caller. Work the
+ * plan puts on its internal side streams (hub bucket stage, wave tiers) is joined back into this
+ * stream before each merge returns. */
 void* ppr_grank_plan_stream(ppr_plan* p);
 /* Raw basket slab slot (n*L ids / scores, n lengths; only the first len[v] entries of a row are
  * meaningful). MC plans: slot 0 = final baskets, slot 1 = random-walk baskets of the walk set. */
