@@ -24,16 +24,20 @@ def _stale() -> bool:
     return False
 
 
-def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=()) -> str:
-    """Compile the library (only when a source is newer than it, unless `force`). `out` and
-    `defines` (-D flags) build an experiment variant beside it (tools/build_variant.py)."""
+def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=(),
+          csrc: str | None = None) -> str:
+    """Compile the library (only when a source is newer than it, unless `force`). `out`,
+    `defines` (-D flags) and `csrc` (another source tree) build an experiment variant beside it
+    (tools/build_variant.py)."""
     out = out or LIB_PATH
+    src_dir = csrc or CSRC
     if out == LIB_PATH and not force and not _stale():
         return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result", "-Wno-unused-value"] + [f"-D{d}" for d in defines] + [
-           "-o", out + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES] + ["-lrccl", "-lpthread"]
+           "-I", os.path.join(PKG_DIR, "..", "include"),
+           "-o", out + ".tmp"] + [os.path.join(src_dir, s) for s in SOURCES] + ["-lrccl", "-lpthread"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

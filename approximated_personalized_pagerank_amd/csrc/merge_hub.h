@@ -340,15 +340,25 @@ struct BucketWave {
   __device__ __forceinline__ void chunk(const bool (&cv)[NG], const int (&kk)[NG], const double (&cs)[NG],
                                         double factor) {
     uint32_t sl[NG];
+    // the first probe of every group is read up front (NG LDS reads in flight instead of one
+    // round trip per group): a slot only ever goes EMPTY -> key, so a stale EMPTY is caught by
+    // the CAS below and a key read early is final
+    uint32_t h0[NG];
+    int c0[NG];
+#pragma unroll
+    for (int k = 0; k < NG; k++) {
+      h0[k] = hash32((uint32_t)kk[k]) & t.mask;
+      c0[k] = cv[k] ? t.keys[h0[k]] : EMPTY;
+    }
 #pragma unroll
     for (int k = 0; k < NG; k++) {
       if (fill + WAVE > budget) overflow = true;  // uniform: a group may bring 64 new keys
       bool ins = false;
       uint32_t h = 0;
       if (cv[k] && !overflow) {
-        h = hash32((uint32_t)kk[k]) & t.mask;
+        h = h0[k];
+        int c = c0[k];
         for (;;) {
-          const int c = t.keys[h];
           if (c == kk[k]) break;
           if (c == EMPTY) {
             const int prev = atomicCAS(&t.keys[h], EMPTY, kk[k]);
@@ -356,6 +366,7 @@ struct BucketWave {
             if (prev == kk[k]) break;
           }
           h = (h + 1) & t.mask;
+          c = t.keys[h];
         }
       }
       sl[k] = h;

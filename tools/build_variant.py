@@ -1,14 +1,30 @@
 """Build an experiment variant of the library beside the product one, for same-box A/B runs:
 
-    python tools/build_variant.py NAME DEFINE [DEFINE ...]   # -> libppr_hip_NAME.so
-    PPR_LIB_VARIANT=NAME python bench.py ...                  # loads the variant
+    python tools/build_variant.py NAME [--rev GITREV] [DEFINE ...]   # -> libppr_hip_NAME.so
+    PPR_LIB_VARIANT=NAME python bench.py ...                          # loads the variant
+
+--rev builds the sources of a git revision (exported to /tmp) instead of the working tree.
 """
 import os
+import subprocess
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 from approximated_personalized_pagerank_amd import build as b  # noqa: E402
 from approximated_personalized_pagerank_amd._lib import PKG_DIR  # noqa: E402
 
-name, defines = sys.argv[1], sys.argv[2:]
-print(b.build(out=os.path.join(PKG_DIR, f"libppr_hip_{name}.so"), defines=defines, verbose=True))
+args = sys.argv[1:]
+name = args.pop(0)
+csrc = None
+if args and args[0] == "--rev":
+    rev = args[1]
+    args = args[2:]
+    tmp = f"/tmp/ppr_variant_{name}"
+    subprocess.run(["rm", "-rf", tmp], check=True)
+    os.makedirs(tmp)
+    arch = subprocess.run(["git", "-C", ROOT, "archive", rev, "include",
+                           "approximated_personalized_pagerank_amd/csrc"], check=True, capture_output=True).stdout
+    subprocess.run(["tar", "-x", "-C", tmp], input=arch, check=True)
+    csrc = os.path.join(tmp, "approximated_personalized_pagerank_amd", "csrc")
+print(b.build(out=os.path.join(PKG_DIR, f"libppr_hip_{name}.so"), defines=args, csrc=csrc, verbose=False))
