@@ -89,7 +89,7 @@ struct ppr_plan {
   uint32_t lds_rank = 0;           // k_probe_lds_rank passed (PPR_LDS_RANK=0 forces the ballot path)
   bool seg_enabled = false;        // segmented hub buckets (k_hub_seg, PPR_HUB_SEG=1)
   int seg_bucket = 256, seg_t = 512, seg_wpb = 1;
-  int hub_bw_ng = 4;               // PPR_BW_NG: groups per chunk (4 or 8)
+  int hub_bw_ng = 2;               // PPR_BW_NG: groups per chunk (1, 2, 4 or 8)
   int hub_bw_waves = 1;            // PPR_BW_WAVES: waves per block of k_hub_bucket_w
   int hub_slice = 8192;            // PPR_HUB_SLICE: k_hub_reduce slice (>= L)
   // source sharding (ppr_grank_plan_comm_init / ppr_grank_plan_run_sharded)
