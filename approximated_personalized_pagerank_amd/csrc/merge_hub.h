@@ -39,8 +39,8 @@ constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per redu
 
 // wave bucket LDS: acc f64[T] | keys i32[T] | cnt u16[T] | vals f64[CHUNK] | touched u16[CHUNK] |
 // tof u16[CHUNK + 2]; the radix histogram of the final select (1 KB) aliases vals
-__host__ __device__ constexpr size_t hub_wave_lds(int T, int ng) {
-  return (size_t)T * 16 + ((size_t)(ng * WAVE) * 12 > 1024 ? (size_t)(ng * WAVE) * 12 : 1024) + 4;
+__host__ __device__ constexpr size_t hub_wave_lds(int T, int ng) {  // 16-B multiple: acc stays aligned
+  return ((size_t)T * 16 + ((size_t)(ng * WAVE) * 12 > 1024 ? (size_t)(ng * WAVE) * 12 : 1024) + 4 + 15) & ~(size_t)15;
 }
 
 struct HubDesc {
