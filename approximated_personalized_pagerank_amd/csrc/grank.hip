@@ -214,6 +214,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_slice = std::max<int>(std::max<int>(64, (int)L), e6 ? atoi(e6) : HUB_SLICE);
     const char* e7 = getenv("PPR_HUB_STREAMS");
     p->hub_streams = (e7 && atoi(e7) == 1) ? 1 : 2;
+    const char* e14 = getenv("PPR_WAVE_WPB");
+    p->wave_wpb = e14 ? (atoi(e14) >= 4 ? 4 : atoi(e14) >= 2 ? 2 : 1) : 1;
     const char* e10 = getenv("PPR_HUB_MIX");
     p->hub_mix = e10 ? std::max(0, std::min(HUB_MAX_LOGP, atoi(e10))) : 8;
     const char* e9 = getenv("PPR_HUB_TILE_PB");
@@ -660,9 +662,11 @@ static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, i
   hipStream_t sw = p->stream3 ? p->stream3 : st;
   for (int t = 0; t < NT; t++) {
     if (!cnt[t] || !p->tierT[t]) continue;
-    const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * WAVES_PER_BLOCK;
-    const int64_t blocks = ((int64_t)cnt[t] + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-    hipLaunchKernelGGL(k_merge_lds, dim3((unsigned)blocks), dim3(256), bytes, sw, g, s, a,
+    // one wave per block by default: no LDS left unusable by a 4-wave block granularity
+    const int wpb = p->wave_wpb;
+    const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * wpb;
+    const int64_t blocks = ((int64_t)cnt[t] + wpb - 1) / wpb;
+    hipLaunchKernelGGL(k_merge_lds, dim3((unsigned)blocks), dim3(64 * wpb), bytes, sw, g, s, a,
                        p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], p->tierT[t], p->Lp,
                        maxdiff, p->d_stats);
     HIP_OK(hipGetLastError());

@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
                                                    unsigned long long* stats) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
-  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (w >= count) return;
   unsigned char* base = smem + (size_t)wv * lds_wave_bytes(T, Lp);
   LdsTable t;

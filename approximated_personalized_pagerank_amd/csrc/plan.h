@@ -106,6 +106,7 @@ struct ppr_plan {
   // the partition stage of batch i+1 runs on the plan's stream (two scratch regions), and the wave
   // tiers run on stream3 beside the whole hub pipeline (disjoint sources)
   int hub_streams = 2;
+  int wave_wpb = 1;                // PPR_WAVE_WPB: waves per block of k_merge_lds (1, 2 or 4)
   int hub_mix = 8;                 // PPR_HUB_MIX: interleave sources with P >= 2^hub_mix among the others
   int hub_tile_pb = 4;             // PPR_HUB_TILE_PB: tile candidates >= this many per bucket (0: 4096 / L)
   int64_t hub_budget = 1LL << 28;  // PPR_HUB_BUDGET: staged candidates per hub batch (16-B records)

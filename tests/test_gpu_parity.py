@@ -140,7 +140,7 @@ def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
      "PPR_HUB_MIX": "3", "PPR_HUB_BUDGET": "8192"},                         # interleaved batches
     {"PPR_HUB_SEG": "0", "PPR_HUB_MIX": "0", "PPR_BW_NG": "4"},             # list order, 4 groups per chunk
     {"PPR_HUB_SEG": "0", "PPR_BW_NG": "1", "PPR_BW_WAVES": "2"},            # 1 group per chunk, 2 waves per block
-    {"PPR_HUB_SEG": "0", "PPR_BW_NG": "8"},                                 # 8 groups per chunk
+    {"PPR_HUB_SEG": "0", "PPR_BW_NG": "8", "PPR_WAVE_WPB": "4"},            # 8 groups per chunk, 4-wave tier blocks
     {"PPR_HUB_SEG": "0", "PPR_LDS_RANK": "0"},                              # ballot occurrence ranks
     {"PPR_HUB_SEG": "0", "PPR_HUB_WAVE_T": "256", "PPR_HUB_BUCKET": "512"},  # spills to k_hub_bucket
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "16"},                           # many segments, up to 64 buckets
