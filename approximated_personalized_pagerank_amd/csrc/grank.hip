@@ -216,6 +216,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_streams = (e7 && atoi(e7) == 1) ? 1 : 2;
     const char* e14 = getenv("PPR_WAVE_WPB");
     p->wave_wpb = e14 ? (atoi(e14) >= 4 ? 4 : atoi(e14) >= 2 ? 2 : 1) : 1;
+    const char* e15 = getenv("PPR_TILE_WPB_P");
+    p->tile_wpb_p = e15 ? std::max(1, atoi(e15)) : 4096;
     const char* e10 = getenv("PPR_HUB_MIX");
     p->hub_mix = e10 ? std::max(0, std::min(HUB_MAX_LOGP, atoi(e10))) : 8;
     const char* e9 = getenv("PPR_HUB_TILE_PB");
@@ -539,13 +541,16 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     const int64_t ntiles = b.ntiles;
     const int64_t nbuck = b.nbuck;
     if (ntiles) {
-      const size_t lds_tile = (size_t)WAVES_PER_BLOCK * maxP * 4;
-      const unsigned tb = (unsigned)((ntiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
-      hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm,
+      // per-wave bucket counters (maxP ints): with large partitions one wave per block leaves no
+      // LDS stranded by the block granularity
+      const int twpb = maxP >= p->tile_wpb_p ? 1 : WAVES_PER_BLOCK;
+      const size_t lds_tile = (size_t)twpb * maxP * 4;
+      const unsigned tb = (unsigned)((ntiles + twpb - 1) / twpb);
+      hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm,
                          d_tau);
       HIP_OK(hipGetLastError());
       HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, scan_tmp, d_cm, d_cmx, (int)b.cm, st));
-      hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(256), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
+      hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
                          d_cmx, d_st);
       HIP_OK(hipGetLastError());
     }

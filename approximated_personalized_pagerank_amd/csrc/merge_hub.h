@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
                                                    unsigned long long* tau) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
-  const int64_t w = (int64_t)blockIdx.x * WAVES_PER_BLOCK + wv;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (w >= ntasks) return;
   const HubTask tk = tasks[w];
   const HubDesc d = desc[tk.d];
@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   const int wv = threadIdx.x >> 6;
   // consecutive tiles of a source append to the same bucket runs: keep them on one XCD so the
   // partial staging lines merge in its L2 instead of being written back piecemeal
-  const int64_t w = xcd_block(blockIdx.x, gridDim.x) * WAVES_PER_BLOCK + wv;
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
   if (w >= ntasks) return;
   const HubTask tk = tasks[w];
   const HubDesc d = desc[tk.d];
