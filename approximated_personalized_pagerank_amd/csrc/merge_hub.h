@@ -186,7 +186,9 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
                                                    unsigned long long* tau) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
-  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  // neighbouring tiles write neighbouring columns of the count matrix: on one XCD their partial
+  // lines merge in its L2
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + wv;
   if (w >= ntasks) return;
   const HubTask tk = tasks[w];
   const HubDesc d = desc[tk.d];
