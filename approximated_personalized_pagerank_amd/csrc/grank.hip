@@ -188,8 +188,12 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     const char* e1 = getenv("PPR_HUB_BUCKET");
     const char* e2 = getenv("PPR_HUB_WAVE_T");
     p->hub_bucket = e1 ? std::max(64, atoi(e1)) : HUB_BUCKET;
-    p->hub_wave_t = e2 ? pow2_at_least(std::max(256, atoi(e2))) : HUB_WAVE_T;
+    p->hub_wave_t = e2 ? (std::max(256, atoi(e2)) + 63) / 64 * 64 : HUB_WAVE_T;  // a multiple of 64
     p->hub_wave_t = std::min(p->hub_wave_t, 8192);
+    // table fill before a bucket spills (a group may bring 64 new keys): PPR_BW_FILL percent
+    const char* e17 = getenv("PPR_BW_FILL");
+    const int fill = e17 ? std::max(50, std::min(100, atoi(e17))) : 85;  // 448 x 85 %: 380 keys
+    p->hub_bw_budget = std::max(WAVE, std::min(p->hub_wave_t, p->hub_wave_t * fill / 100));
   }
   {
     const char* e4 = getenv("PPR_BW_NG");
@@ -581,16 +585,16 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       const dim3 grid((unsigned)blocks), blk(64 * wpb);
       if (p->hub_bw_ng == 1)
         hipLaunchKernelGGL(k_hub_bucket_w<1>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
-                           d_gl, d_lc + 1, p->hub_wave_t);
+                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget);
       else if (p->hub_bw_ng == 2)
         hipLaunchKernelGGL(k_hub_bucket_w<2>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
-                           d_gl, d_lc + 1, p->hub_wave_t);
+                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget);
       else if (p->hub_bw_ng == 8)
         hipLaunchKernelGGL(k_hub_bucket_w<8>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
-                           d_gl, d_lc + 1, p->hub_wave_t);
+                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget);
       else
         hipLaunchKernelGGL(k_hub_bucket_w<4>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
-                           d_gl, d_lc + 1, p->hub_wave_t);
+                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget);
       HIP_OK(hipGetLastError());
       // spilled buckets (distinct keys beyond the wave table): persistent workgroups over the spill
       // list, whose length only the device knows

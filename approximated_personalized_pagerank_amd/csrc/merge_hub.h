@@ -31,7 +31,8 @@ constexpr int HUB_TILE_PER_BUCKET = 4;  // ... and target >= 4 P: the count matr
                                         // the scatter's run seeds stay <= 1/4 int per candidate
 constexpr int HUB_BUCKET = 384;       // default target candidates per bucket (PPR_HUB_BUCKET)
 constexpr int HUB_MAX_LOGP = 12;      // per-wave LDS counters of the partition: 16 KB
-constexpr int HUB_WAVE_T = 512;       // default wave bucket table slots (PPR_HUB_WAVE_T): 13 KB of LDS per wave
+constexpr int HUB_WAVE_T = 448;       // default wave bucket table slots (PPR_HUB_WAVE_T, a multiple of 64):
+                                      // 8.7 KB of LDS per wave with 2 groups per chunk, 18 waves per CU
 constexpr int HUB_BW_BATCH = 8;       // staged groups a bucket wave keeps in flight
 constexpr int HUB_TW_BATCH = 4;       // candidate groups a tile wave gathers before using them
 constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per reducing workgroup (PPR_HUB_SLICE)
@@ -311,27 +312,32 @@ struct BucketWave {
   bool overflow;
   bool ordered;  // lane-ordered LDS atomics (IterArgs::lds_rank)
 
-  __device__ __forceinline__ void setup(unsigned char* base, int T_, int NG, bool ordered_) {
+  // T: any multiple of 64 (slots by multiply-shift of the key hash, linear probing with wrap)
+  __device__ __forceinline__ void setup(unsigned char* base, int T_, int NG, bool ordered_, int budget_ = -1) {
     T = T_;
     ordered = ordered_;
     t.acc = reinterpret_cast<double*>(base);
     t.keys = reinterpret_cast<int*>(base + (size_t)T * 8);
     t.mask = (uint32_t)T - 1;
-    t.nbits = 31 - __clz(T);
+    t.nbits = 32 - __clz(T - 1);
     ck.cnt = reinterpret_cast<uint32_t*>(base + (size_t)T * 12);
     ck.vals = reinterpret_cast<double*>(base + (size_t)T * 16);
     ck.touched = reinterpret_cast<uint16_t*>(base + (size_t)T * 16 + (size_t)(NG * WAVE) * 8);
     ck.tof = ck.touched + NG * WAVE;
     hist = reinterpret_cast<uint32_t*>(ck.vals);  // final select only (after accumulation)
-    budget = T / 4 * 3;
+    budget = budget_ > 0 ? budget_ : T / 4 * 3;
     fill = 0;
     overflow = false;
     for (int i = lane_id(); i < T; i += WAVE) { t.keys[i] = EMPTY; ck.cnt[i] = 0; }
     wave_fence();
   }
 
+  __device__ __forceinline__ uint32_t slot_of(int key) const {
+    return (uint32_t)(((unsigned long long)hash32((uint32_t)key) * (uint32_t)T) >> 32);
+  }
+
   __device__ __forceinline__ void seed(int key, double val) {
-    if (lane_id() == 0) { const uint32_t sl = table_slot(t, key); t.acc[sl] = val; }
+    if (lane_id() == 0) { const uint32_t sl = slot_of(key); t.keys[sl] = key; t.acc[sl] = val; }  // empty table
     fill = 1;
     wave_fence();
   }
@@ -349,7 +355,7 @@ struct BucketWave {
     int c0[NG];
 #pragma unroll
     for (int k = 0; k < NG; k++) {
-      h0[k] = hash32((uint32_t)kk[k]) & t.mask;
+      h0[k] = slot_of(kk[k]);
       c0[k] = cv[k] ? t.keys[h0[k]] : EMPTY;
     }
 #pragma unroll
@@ -367,7 +373,7 @@ struct BucketWave {
             if (prev == EMPTY) { t.acc[h] = 0.0; ins = true; break; }
             if (prev == kk[k]) break;
           }
-          h = (h + 1) & t.mask;
+          h = (h + 1 == (uint32_t)T) ? 0u : h + 1;
           c = t.keys[h];
         }
       }
@@ -435,7 +441,7 @@ template <int NG>
 __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, const BucketWork* bw,
                                                       int64_t nbuck, const HubRec* st,
                                                       int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
-                                                      HubTask* spill, uint32_t* spill_cnt, int T) {
+                                                      HubTask* spill, uint32_t* spill_cnt, int T, int budget) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   const int l = lane_id();
@@ -446,7 +452,7 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
   const BucketWork W = bw[cur];
   const long long t_start = a.diag ? (long long)clock64() : 0;
   BucketWave B;
-  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0);
+  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0, budget);
   if (W.seed >= 0) B.seed(W.seed, W.selfval);
   const int nb = W.nb;
   for (int g0 = 0; g0 < nb; g0 += NG * WAVE) {

@@ -142,6 +142,8 @@ def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
     {"PPR_HUB_SEG": "0", "PPR_BW_NG": "1", "PPR_BW_WAVES": "2"},            # 1 group per chunk, 2 waves per block
     {"PPR_HUB_SEG": "0", "PPR_BW_NG": "8", "PPR_WAVE_WPB": "4"},            # 8 groups per chunk, 4-wave tier blocks
     {"PPR_HUB_SEG": "0", "PPR_LDS_RANK": "0"},                              # ballot occurrence ranks
+    {"PPR_HUB_SEG": "0", "PPR_HUB_WAVE_T": "320", "PPR_BW_FILL": "90"},     # non-power-of-two table, high fill
+    {"PPR_HUB_SEG": "0", "PPR_HUB_WAVE_T": "384", "PPR_LDS_RANK": "0"},     # ... with ballot ranks (9 slot bits)
     {"PPR_HUB_SEG": "0", "PPR_HUB_WAVE_T": "256", "PPR_HUB_BUCKET": "512"},  # spills to k_hub_bucket
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "16"},                           # many segments, up to 64 buckets
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "4096", "PPR_SEG_T": "4096"},    # one segment spanning all ranges
