@@ -548,7 +548,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       // per-wave bucket counters (maxP ints): with large partitions one wave per block leaves no
       // LDS stranded by the block granularity
       const int twpb = maxP >= p->tile_wpb_p ? 1 : WAVES_PER_BLOCK;
-      const size_t lds_tile = (size_t)twpb * maxP * 4;
+      const size_t lds_tile = (size_t)twpb * (maxP * 4 + HUB_WALK_FLAGS);
       const unsigned tb = (unsigned)((ntiles + twpb - 1) / twpb);
       hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm,
                          d_tau);

@@ -112,7 +112,7 @@ __device__ __forceinline__ uint32_t hub_digit(int key, int logP) {
 // walk the candidates of successors [i0, e) (at most one per lane) in successor order, 64 per step
 template <class F>
 __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
-                                                int64_t i0, int64_t e, F f) {
+                                                int64_t i0, int64_t e, uint8_t* fl, F f) {
   const int64_t i = i0 + lane_id();
   if (a.unit) {  // init: every successor contributes {u: 1.0}
     const bool valid = i < e;
@@ -128,19 +128,35 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
   }
   const int incl = wave_incl_scan(ln);
   const int total = __shfl(incl, WAVE - 1);
+  // successor of candidate c: j = #{successors whose basket ends at or before c}. With every
+  // basket non-empty the ends are distinct, so a batch marks them as byte flags in LDS and a
+  // group reads j off one ballot of its 64 flags (instead of a 6-step cross-lane binary search)
+  const bool flags = fl != nullptr && !__ballot(i < e && ln == 0);
   // HUB_TW_BATCH groups of 64 candidates are gathered together (one memory latency per batch),
   // and the next batch is in flight while f consumes the current one; f still sees the
   // candidates in stream order
   auto load = [&](int g0, int (&key)[HUB_TW_BATCH], double (&sv)[HUB_TW_BATCH]) {
+    if (flags) {
+      reinterpret_cast<uint32_t*>(fl)[lane_id()] = 0u;  // WAVE * HUB_TW_BATCH flag bytes
+      wave_fence();
+      if (incl > g0 && incl < g0 + WAVE * HUB_TW_BATCH) fl[incl - g0] = 1;
+      wave_fence();
+    }
 #pragma unroll
     for (int k = 0; k < HUB_TW_BATCH; k++) {
       const int c = g0 + k * WAVE + lane_id();
       const bool valid = c < total;
       int j = 0;
+      if (flags) {
+        const int G = g0 + k * WAVE;
+        const uint64_t ends = __ballot(fl[k * WAVE + lane_id()] != 0) & ~1ull;  // ends in (G, G + 64)
+        j = __popcll(__ballot(incl <= G)) + __popcll(ends & (lanemask_lt() | (1ull << lane_id())));
+      } else {
 #pragma unroll
-      for (int step = 32; step; step >>= 1) {
-        const int pv = __shfl(incl, j + step - 1);
-        if (pv <= c) j += step;
+        for (int step = 32; step; step >>= 1) {
+          const int pv = __shfl(incl, j + step - 1);
+          if (pv <= c) j += step;
+        }
       }
       const int jj = j < WAVE ? j : WAVE - 1;
       const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
@@ -175,11 +191,13 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
 // order: windows of 64 successors, 64 candidates per step
 template <class F>
 __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
-                                              int v, int t, int tw, F f) {
+                                              int v, int t, int tw, uint8_t* fl, F f) {
   const int64_t b = g.rp[v] + (int64_t)t * tw;
   const int64_t e = min(g.rp[v + 1], b + (int64_t)tw);
-  for (int64_t w0 = b; w0 < e; w0 += WAVE) hub_window_walk(g, s, a, w0, min(e, w0 + WAVE), f);
+  for (int64_t w0 = b; w0 < e; w0 += WAVE) hub_window_walk(g, s, a, w0, min(e, w0 + WAVE), fl, f);
 }
+// flag bytes per wave of hub_window_walk, after the kernels' per-wave counters
+constexpr int HUB_WALK_FLAGS = WAVE * HUB_TW_BATCH;
 
 __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterArgs a,
                                                    const HubDesc* desc, const HubTask* tasks,
@@ -212,9 +230,10 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
     if (lane_id() == 0 && mb) atomicMax(&tau[tk.d], mb);
   }
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * maxP;
+  uint8_t* fl = smem + (size_t)(blockDim.x >> 6) * maxP * 4 + (size_t)wv * HUB_WALK_FLAGS;
   for (int i = lane_id(); i < P; i += WAVE) hist[i] = 0;
   wave_fence();
-  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, [&](bool valid, int key, double) {
+  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid, int key, double) {
     if (valid) atomicAdd(&hist[hub_digit(key, d.logP)], 1u);
   });
   wave_fence();
@@ -243,7 +262,8 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   wave_fence();
   const uint64_t lt = lanemask_lt();
   HubRec* stv = st + base0;
-  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, [&](bool valid, int key, double sv) {
+  uint8_t* fl = smem + (size_t)(blockDim.x >> 6) * maxP * 4 + (size_t)wv * HUB_WALK_FLAGS;
+  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid, int key, double sv) {
     const uint32_t dg = valid ? hub_digit(key, d.logP) : 0u;
     // lanes holding the same digit: AND of per-bit ballots (stable rank = lower lanes first)
     uint64_t match = __ballot(valid);
