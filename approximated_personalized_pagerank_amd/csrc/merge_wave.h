@@ -157,14 +157,27 @@ __host__ __device__ constexpr size_t lds_wave_bytes(int T, int Lp) {
 
 // the candidate of stream position c inside the current successor window (all lanes execute:
 // the binary search and the operand fetches are cross-lane bpermutes)
+// With `fl` (64 bytes of LDS; every basket of the window non-empty, so basket ends are distinct)
+// the successor index comes from end flags and two ballots instead of the binary search.
 __device__ __forceinline__ void window_fetch(const DevSlab& s, int incl, int u, int sl, int total,
-                                             int c, bool& valid, int& key, double& sv) {
+                                             int c, bool& valid, int& key, double& sv, uint8_t* fl) {
   valid = c < total;
   int j = 0;
+  if (fl) {
+    const int G = c - lane_id();  // the group's first stream position
+    reinterpret_cast<uint32_t*>(fl)[lane_id() & 15] = 0u;
+    wave_fence();
+    if (incl > G && incl < G + WAVE) fl[incl - G] = 1;
+    wave_fence();
+    const uint64_t ends = __ballot(fl[lane_id()] != 0) & ~1ull;
+    wave_fence();
+    j = __popcll(__ballot(incl <= G)) + __popcll(ends & (lanemask_lt() | (1ull << lane_id())));
+  } else {
 #pragma unroll
-  for (int step = 32; step; step >>= 1) {
-    const int pv = __shfl(incl, j + step - 1);
-    if (pv <= c) j += step;
+    for (int step = 32; step; step >>= 1) {
+      const int pv = __shfl(incl, j + step - 1);
+      if (pv <= c) j += step;
+    }
   }
   const int jj = j < WAVE ? j : WAVE - 1;
   const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);  // every lane executes the bpermute
@@ -232,15 +245,17 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
       }
       const int incl = wave_incl_scan(ln);
       const int total = __shfl(incl, WAVE - 1);
+      // end flags live in the select histogram's LDS, unused until the epilogue
+      uint8_t* fl = __ballot(i < e && ln == 0) ? nullptr : reinterpret_cast<uint8_t*>(hist);
       bool nv;
       int nk;
       double ns;
-      window_fetch(s, incl, u, sl, total, lane_id(), nv, nk, ns);
+      window_fetch(s, incl, u, sl, total, lane_id(), nv, nk, ns, fl);
       for (int g0 = 0; g0 < total; g0 += WAVE) {
         const bool cv = nv;
         const int ck = nk;
         const double cs = ns;
-        if (g0 + WAVE < total) window_fetch(s, incl, u, sl, total, g0 + WAVE + lane_id(), nv, nk, ns);
+        if (g0 + WAVE < total) window_fetch(s, incl, u, sl, total, g0 + WAVE + lane_id(), nv, nk, ns, fl);
         table_apply_own(t, own, cv, ck, cs, factor);
       }
     }
