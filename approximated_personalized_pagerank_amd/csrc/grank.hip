@@ -222,6 +222,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->wave_wpb = e14 ? (atoi(e14) >= 4 ? 4 : atoi(e14) >= 2 ? 2 : 1) : 1;
     const char* e15 = getenv("PPR_TILE_WPB_P");
     p->tile_wpb_p = e15 ? std::max(1, atoi(e15)) : 4096;
+    const char* e18 = getenv("PPR_HUB_REGIONS");
+    p->hub_regions = e18 ? std::max(2, std::min(ppr_plan::MAX_REGIONS, atoi(e18))) : 3;
     const char* e10 = getenv("PPR_HUB_MIX");
     p->hub_mix = e10 ? std::max(0, std::min(HUB_MAX_LOGP, atoi(e10))) : 8;
     const char* e9 = getenv("PPR_HUB_TILE_PB");
@@ -232,11 +234,13 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   p->hub_lds_wave = hub_wave_lds(p->hub_wave_t, p->hub_bw_ng) * p->hub_bw_waves;
   if (p->hub_streams == 2) {
     if (hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&p->stream4, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&p->stream3, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&p->ev_wave, hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
-    for (int i = 0; i < 2; i++)
+    for (int i = 0; i < ppr_plan::MAX_REGIONS; i++)
       if (hipEventCreateWithFlags(&p->ev_part[i], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&p->ev_buck[i], hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
+          hipEventCreateWithFlags(&p->ev_buck[i], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&p->ev_fin[i], hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
   }
   {
     hipDeviceProp_t prop;
@@ -498,7 +502,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   const size_t o_bw = off;   off = al(off + sizeof(BucketWork) * mx.nbuck);
   const size_t region = off;
   // two streams only pay when there is a next batch to overlap with
-  const int nreg = (p->hub_streams == 2 && batches.size() > 1) ? 2 : 1;
+  const bool ms = p->hub_streams == 2 && batches.size() > 1;
+  const int nreg = ms ? (int)std::min<size_t>(p->hub_regions, batches.size()) : 1;
   int rc = ensure_scratch(p, shared + region * nreg);
   if (rc) return rc;
   char* base = (char*)p->d_scratch;
@@ -509,7 +514,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   // partition stage (expand, count, scan, scatter, prep) of batch i on `st`, its bucket stage
   // (bucket waves, spills, segments, reduce, final) on `sb`; batch i+2 reuses batch i's region
   // once batch i's bucket stage has finished
-  hipStream_t sb = nreg == 2 ? p->stream2 : st;
+  hipStream_t sb = ms ? p->stream2 : st;   // bucket waves, spills, segments
+  hipStream_t sf = ms ? p->stream4 : st;   // reduce + final
   for (size_t bi = 0; bi < batches.size(); bi++) {
     const Batch& b = batches[bi];
     const int r = (int)(bi % nreg);
@@ -535,7 +541,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     const size_t nd = b.d1 - b.d0;
     HubDesc* d_desc = d_desc_all + b.d0;
     const int maxP = b.maxP;
-    if (nreg == 2 && bi >= 2) HIP_OK(hipStreamWaitEvent(st, p->ev_buck[r], 0));
+    if (ms && bi >= (size_t)nreg) HIP_OK(hipStreamWaitEvent(st, p->ev_fin[r], 0));  // region free again
     HIP_OK(hipMemsetAsync(d_pc, 0, 4 * nd, st));
     HIP_OK(hipMemsetAsync(d_tau, 0, 8 * nd, st));
     HIP_OK(hipMemsetAsync(d_oflag, 0, 4 * nd, st));
@@ -565,7 +571,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
                          nbuck, d_cmx, d_tau, d_bw);
       HIP_OK(hipGetLastError());
     }
-    if (nreg == 2) {
+    if (ms) {
       HIP_OK(hipEventRecord(p->ev_part[r], st));
       HIP_OK(hipStreamWaitEvent(sb, p->ev_part[r], 0));
     }
@@ -602,21 +608,25 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
                          d_desc, d_gl, d_lc + 1, d_cmx, d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_oflag, d_ovl);
       HIP_OK(hipGetLastError());
     }
+    if (ms) {
+      HIP_OK(hipEventRecord(p->ev_buck[r], sb));
+      HIP_OK(hipStreamWaitEvent(sf, p->ev_buck[r], 0));
+    }
     // long appended lists are cut (k_hub_reduce) so no k_hub_final workgroup selects from more
     // than a few slices' worth of entries; slices are reserved for the worst case, idle ones exit
     if (b.nrt) {
-      hipLaunchKernelGGL(k_hub_reduce, dim3((unsigned)b.nrt), dim3(WG_THREADS), p->hub_lds_final, sb, s, d_desc,
+      hipLaunchKernelGGL(k_hub_reduce, dim3((unsigned)b.nrt), dim3(WG_THREADS), p->hub_lds_final, sf, s, d_desc,
                          d_rt, d_pc, d_pk, d_ps, d_rk, d_rs, p->Lp, slice);
       HIP_OK(hipGetLastError());
       p->merge_launches++;
     }
-    hipLaunchKernelGGL(k_hub_final, dim3((unsigned)nd), dim3(WG_THREADS), p->hub_lds_final, sb, s, a, d_desc,
+    hipLaunchKernelGGL(k_hub_final, dim3((unsigned)nd), dim3(WG_THREADS), p->hub_lds_final, sf, s, a, d_desc,
                        d_oflag, d_pc, d_pk, d_ps, d_rk, d_rs, slice, p->Lp, maxdiff, p->d_stats);
     HIP_OK(hipGetLastError());
     p->merge_launches += 9;
-    if (nreg == 2) HIP_OK(hipEventRecord(p->ev_buck[r], sb));
+    if (ms) HIP_OK(hipEventRecord(p->ev_fin[r], sf));
   }
-  if (nreg == 2) HIP_OK(hipStreamWaitEvent(st, p->ev_buck[(batches.size() - 1) % 2], 0));
+  if (ms) HIP_OK(hipStreamWaitEvent(st, p->ev_fin[(batches.size() - 1) % nreg], 0));  // finals run in order
   int32_t novf = 0;
   HIP_OK(hipMemcpyAsync(&novf, d_ovl, 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));

@@ -112,8 +112,12 @@ struct ppr_plan {
   int hub_mix = 8;                 // PPR_HUB_MIX: interleave sources with P >= 2^hub_mix among the others
   int hub_tile_pb = 4;             // PPR_HUB_TILE_PB: tile candidates >= this many per bucket (0: 4096 / L)
   int64_t hub_budget = 1LL << 28;  // PPR_HUB_BUDGET: staged candidates per hub batch (16-B records)
-  hipStream_t stream2 = nullptr, stream3 = nullptr;
-  hipEvent_t ev_part[2] = {nullptr, nullptr}, ev_buck[2] = {nullptr, nullptr}, ev_wave = nullptr;
+  // with PPR_HUB_REGIONS (default 3) scratch regions the partition stage runs up to two batches
+  // ahead, and the reduce + final of batch i (stream4) overlap the bucket waves of batch i+1
+  static constexpr int MAX_REGIONS = 4;
+  int hub_regions = 3;
+  hipStream_t stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
+  hipEvent_t ev_part[MAX_REGIONS] = {}, ev_buck[MAX_REGIONS] = {}, ev_fin[MAX_REGIONS] = {}, ev_wave = nullptr;
   unsigned long long* d_diag = nullptr;  // PPR_DIAG=1: kernel histograms, printed at destroy
   // MCCompletePathV2 (mccp2.hip)
   bool mc = false;
@@ -140,13 +144,15 @@ inline void plan_free(ppr_plan* p) {
   if (p->ev_b) hipEventDestroy(p->ev_b);
   if (p->ev_m0) hipEventDestroy(p->ev_m0);
   if (p->ev_m1) hipEventDestroy(p->ev_m1);
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < ppr_plan::MAX_REGIONS; i++) {
     if (p->ev_part[i]) hipEventDestroy(p->ev_part[i]);
     if (p->ev_buck[i]) hipEventDestroy(p->ev_buck[i]);
+    if (p->ev_fin[i]) hipEventDestroy(p->ev_fin[i]);
   }
   if (p->ev_wave) hipEventDestroy(p->ev_wave);
   if (p->stream2) hipStreamDestroy(p->stream2);
   if (p->stream3) hipStreamDestroy(p->stream3);
+  if (p->stream4) hipStreamDestroy(p->stream4);
   if (p->comm) ncclCommDestroy(p->comm);
   hipFree(p->d_xsend); hipFree(p->d_xrecv);
   if (p->h_hub_pin) hipHostFree(p->h_hub_pin);

@@ -133,7 +133,9 @@ def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
 
 @pytest.mark.parametrize("seg_env", [
     {"PPR_HUB_SEG": "0"},                                                   # staged partition only
-    {"PPR_HUB_SEG": "0", "PPR_HUB_BUDGET": "4096"},                         # many batches, two streams
+    {"PPR_HUB_SEG": "0", "PPR_HUB_BUDGET": "4096"},                         # many batches, streams, 3 regions
+    {"PPR_HUB_SEG": "0", "PPR_HUB_BUDGET": "2048", "PPR_HUB_REGIONS": "2"},  # ... 2 regions
+    {"PPR_HUB_SEG": "0", "PPR_HUB_BUDGET": "2048", "PPR_HUB_REGIONS": "4"},  # ... 4 regions
     {"PPR_HUB_SEG": "0", "PPR_HUB_BUDGET": "4096", "PPR_HUB_STREAMS": "1"},  # many batches, one stream
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "64", "PPR_HUB_BUDGET": "1024"},  # segments over many batches
     {"PPR_HUB_SEG": "0", "PPR_HUB_BUCKET": "64", "PPR_HUB_TILE_PB": "64",   # long multi-window tiles,
