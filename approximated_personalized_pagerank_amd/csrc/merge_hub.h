@@ -34,7 +34,10 @@ constexpr int HUB_MAX_LOGP = 12;      // per-wave LDS counters of the partition:
 constexpr int HUB_WAVE_T = 448;       // default wave bucket table slots (PPR_HUB_WAVE_T, a multiple of 64):
                                       // 8.7 KB of LDS per wave with 2 groups per chunk, 18 waves per CU
 constexpr int HUB_BW_BATCH = 8;       // staged groups a bucket wave keeps in flight
-constexpr int HUB_TW_BATCH = 4;       // candidate groups a tile wave gathers before using them
+#ifndef PPR_TW_BATCH
+#define PPR_TW_BATCH 8
+#endif
+constexpr int HUB_TW_BATCH = PPR_TW_BATCH;  // candidate groups a tile wave gathers before using them
 constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per reducing workgroup (PPR_HUB_SLICE)
 
 
@@ -137,7 +140,9 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
   // candidates in stream order
   auto load = [&](int g0, int (&key)[HUB_TW_BATCH], double (&sv)[HUB_TW_BATCH]) {
     if (flags) {
-      reinterpret_cast<uint32_t*>(fl)[lane_id()] = 0u;  // WAVE * HUB_TW_BATCH flag bytes
+#pragma unroll
+      for (int q = 0; q < HUB_TW_BATCH / 4; q++)  // WAVE * HUB_TW_BATCH flag bytes
+        reinterpret_cast<uint32_t*>(fl)[q * WAVE + lane_id()] = 0u;
       wave_fence();
       if (incl > g0 && incl < g0 + WAVE * HUB_TW_BATCH) fl[incl - g0] = 1;
       wave_fence();
