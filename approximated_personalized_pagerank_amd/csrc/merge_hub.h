@@ -34,10 +34,6 @@ constexpr int HUB_MAX_LOGP = 12;      // per-wave LDS counters of the partition:
 constexpr int HUB_WAVE_T = 448;       // default wave bucket table slots (PPR_HUB_WAVE_T, a multiple of 64):
                                       // 8.7 KB of LDS per wave with 2 groups per chunk, 18 waves per CU
 constexpr int HUB_BW_BATCH = 8;       // staged groups a bucket wave keeps in flight
-#ifndef PPR_TW_BATCH
-#define PPR_TW_BATCH 8
-#endif
-constexpr int HUB_TW_BATCH = PPR_TW_BATCH;  // candidate groups a tile wave gathers before using them
 constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per reducing workgroup (PPR_HUB_SLICE)
 
 
@@ -112,86 +108,6 @@ __device__ __forceinline__ uint32_t hub_digit(int key, int logP) {
   return logP == 0 ? 0u : (hash_b((uint32_t)key) >> (32 - logP));
 }
 
-// walk the candidates of successors [i0, e) (at most one per lane) in successor order, 64 per step
-template <class F>
-__device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
-                                                int64_t i0, int64_t e, uint8_t* fl, F f) {
-  const int64_t i = i0 + lane_id();
-  if (a.unit) {  // init: every successor contributes {u: 1.0}
-    const bool valid = i < e;
-    f(valid, valid ? (g.colx[i] & 0x7fffffff) : 0, 1.0);
-    return;
-  }
-  int u = 0, sl = 0, ln = 0;
-  if (i < e) {
-    const int32_t cx = g.colx[i];
-    u = cx & 0x7fffffff;
-    sl = read_slot(a, cx);
-    ln = s.len[s.lrow(sl, u)];
-  }
-  const int incl = wave_incl_scan(ln);
-  const int total = __shfl(incl, WAVE - 1);
-  // successor of candidate c: j = #{successors whose basket ends at or before c}. With every
-  // basket non-empty the ends are distinct, so a batch marks them as byte flags in LDS and a
-  // group reads j off one ballot of its 64 flags (instead of a 6-step cross-lane binary search)
-  const bool flags = fl != nullptr && !__ballot(i < e && ln == 0);
-  // HUB_TW_BATCH groups of 64 candidates are gathered together (one memory latency per batch),
-  // and the next batch is in flight while f consumes the current one; f still sees the
-  // candidates in stream order
-  auto load = [&](int g0, int (&key)[HUB_TW_BATCH], double (&sv)[HUB_TW_BATCH]) {
-    if (flags) {
-#pragma unroll
-      for (int q = 0; q < HUB_TW_BATCH / 4; q++)  // WAVE * HUB_TW_BATCH flag bytes
-        reinterpret_cast<uint32_t*>(fl)[q * WAVE + lane_id()] = 0u;
-      wave_fence();
-      if (incl > g0 && incl < g0 + WAVE * HUB_TW_BATCH) fl[incl - g0] = 1;
-      wave_fence();
-    }
-#pragma unroll
-    for (int k = 0; k < HUB_TW_BATCH; k++) {
-      const int c = g0 + k * WAVE + lane_id();
-      const bool valid = c < total;
-      int j = 0;
-      if (flags) {
-        const int G = g0 + k * WAVE;
-        const uint64_t ends = __ballot(fl[k * WAVE + lane_id()] != 0) & ~1ull;  // ends in (G, G + 64)
-        j = __popcll(__ballot(incl <= G)) + __popcll(ends & (lanemask_lt() | (1ull << lane_id())));
-      } else {
-#pragma unroll
-        for (int step = 32; step; step >>= 1) {
-          const int pv = __shfl(incl, j + step - 1);
-          if (pv <= c) j += step;
-        }
-      }
-      const int jj = j < WAVE ? j : WAVE - 1;
-      const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
-      const int ex = jj > 0 ? exv : 0;
-      const int uj = __shfl(u, jj);
-      const int sj = __shfl(sl, jj);
-      key[k] = 0;
-      sv[k] = 0.0;
-      if (valid) {
-        const int64_t r = s.row(sj, uj) + (c - ex);
-        key[k] = s.ids[r];
-        sv[k] = s.sc[r];
-      }
-    }
-  };
-  int key[HUB_TW_BATCH], nkey[HUB_TW_BATCH];
-  double sv[HUB_TW_BATCH], nsv[HUB_TW_BATCH];
-  if (total > 0) load(0, nkey, nsv);
-  for (int g0 = 0; g0 < total; g0 += WAVE * HUB_TW_BATCH) {
-#pragma unroll
-    for (int k = 0; k < HUB_TW_BATCH; k++) { key[k] = nkey[k]; sv[k] = nsv[k]; }
-    if (g0 + WAVE * HUB_TW_BATCH < total) load(g0 + WAVE * HUB_TW_BATCH, nkey, nsv);
-#pragma unroll
-    for (int k = 0; k < HUB_TW_BATCH; k++) {
-      if (g0 + k * WAVE >= total) break;  // uniform
-      f(g0 + k * WAVE + lane_id() < total, key[k], sv[k]);
-    }
-  }
-}
-
 // walk the candidates of tile t (successors [t * tw, (t + 1) * tw) of source v) in successor
 // order: windows of 64 successors, 64 candidates per step
 template <class F>
@@ -201,8 +117,6 @@ __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& 
   const int64_t e = min(g.rp[v + 1], b + (int64_t)tw);
   for (int64_t w0 = b; w0 < e; w0 += WAVE) hub_window_walk(g, s, a, w0, min(e, w0 + WAVE), fl, f);
 }
-// flag bytes per wave of hub_window_walk, after the kernels' per-wave counters
-constexpr int HUB_WALK_FLAGS = WAVE * HUB_TW_BATCH;
 
 __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterArgs a,
                                                    const HubDesc* desc, const HubTask* tasks,

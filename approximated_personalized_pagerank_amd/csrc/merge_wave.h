@@ -4,9 +4,10 @@
 //                  then route v to the smallest tier whose table holds C_v + 1 keys. Tier
 //                  counters are bumped once per block (64 sources), not once per source.
 //   k_merge_lds    one wave per source, LDS hash table of T = 256 << t slots: candidates are
-//                  streamed in successor order (64 successors per window, prefix scan of their
-//                  basket lengths, binary search per lane), one group ahead of the accumulation
-//                  so the next group's HBM gathers overlap the current group's LDS work.
+//                  streamed in successor order by hub_window_walk (64 successors per window,
+//                  prefix scan of their basket lengths, successor of each candidate from LDS end
+//                  flags), HUB_TW_BATCH groups gathered at once and one batch ahead of the
+//                  accumulation, so the next batch's HBM gathers overlap the current LDS work.
 //   k_stat_written SURVEY s8d bytes of the rows an iteration wrote (12 * len + 4 per source).
 #pragma once
 #include "ppr_common.h"
@@ -155,43 +156,114 @@ __host__ __device__ constexpr size_t lds_wave_bytes(int T, int Lp) {
   return (size_t)T * 13 + (size_t)Lp * 12 + 1024 + (size_t)Lp * 20;
 }
 
-// the candidate of stream position c inside the current successor window (all lanes execute:
-// the binary search and the operand fetches are cross-lane bpermutes)
-// With `fl` (64 bytes of LDS; every basket of the window non-empty, so basket ends are distinct)
-// the successor index comes from end flags and two ballots instead of the binary search.
-__device__ __forceinline__ void window_fetch(const DevSlab& s, int incl, int u, int sl, int total,
-                                             int c, bool& valid, int& key, double& sv, uint8_t* fl) {
-  valid = c < total;
-  int j = 0;
-  if (fl) {
-    const int G = c - lane_id();  // the group's first stream position
-    reinterpret_cast<uint32_t*>(fl)[lane_id() & 15] = 0u;
-    wave_fence();
-    if (incl > G && incl < G + WAVE) fl[incl - G] = 1;
-    wave_fence();
-    const uint64_t ends = __ballot(fl[lane_id()] != 0) & ~1ull;
-    wave_fence();
-    j = __popcll(__ballot(incl <= G)) + __popcll(ends & (lanemask_lt() | (1ull << lane_id())));
-  } else {
+#ifndef PPR_TW_BATCH
+#define PPR_TW_BATCH 8
+#endif
+constexpr int HUB_TW_BATCH = PPR_TW_BATCH;  // candidate groups a walking wave gathers before using them
+
+// walk the candidates of successors [i0, e) (at most one per lane) in successor order, 64 per step
+// `succ(ln, rmin_bits)` (optional) sees every lane's successor basket length and row minimum once
+// per window (non-unit mode; invalid lanes report length 0).
+template <class F, class S>
+__device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
+                                                int64_t i0, int64_t e, uint8_t* fl, F f, S succ) {
+  const int64_t i = i0 + lane_id();
+  if (a.unit) {  // init: every successor contributes {u: 1.0}
+    const bool valid = i < e;
+    f(valid, valid ? (g.colx[i] & 0x7fffffff) : 0, 1.0);
+    return;
+  }
+  int u = 0, sl = 0, ln = 0;
+  unsigned long long rm = 0;
+  if (i < e) {
+    const int32_t cx = g.colx[i];
+    u = cx & 0x7fffffff;
+    sl = read_slot(a, cx);
+    ln = s.len[s.lrow(sl, u)];
+    if (S::kWant) rm = dbits(s.rmin[s.lrow(sl, u)]);  // loaded beside len
+  }
+  succ(ln, rm);
+  const int incl = wave_incl_scan(ln);
+  const int total = __shfl(incl, WAVE - 1);
+  // successor of candidate c: j = #{successors whose basket ends at or before c}. With every
+  // basket non-empty the ends are distinct, so a batch marks them as byte flags in LDS and a
+  // group reads j off one ballot of its 64 flags (instead of a 6-step cross-lane binary search)
+  const bool flags = fl != nullptr && !__ballot(i < e && ln == 0);
+  // HUB_TW_BATCH groups of 64 candidates are gathered together (one memory latency per batch),
+  // and the next batch is in flight while f consumes the current one; f still sees the
+  // candidates in stream order
+  auto load = [&](int g0, int (&key)[HUB_TW_BATCH], double (&sv)[HUB_TW_BATCH]) {
+    if (flags) {
 #pragma unroll
-    for (int step = 32; step; step >>= 1) {
-      const int pv = __shfl(incl, j + step - 1);
-      if (pv <= c) j += step;
+      for (int q = 0; q < HUB_TW_BATCH / 4; q++)  // WAVE * HUB_TW_BATCH flag bytes
+        reinterpret_cast<uint32_t*>(fl)[q * WAVE + lane_id()] = 0u;
+      wave_fence();
+      if (incl > g0 && incl < g0 + WAVE * HUB_TW_BATCH) fl[incl - g0] = 1;
+      wave_fence();
+    }
+#pragma unroll
+    for (int k = 0; k < HUB_TW_BATCH; k++) {
+      const int c = g0 + k * WAVE + lane_id();
+      const bool valid = c < total;
+      int j = 0;
+      if (flags) {
+        const int G = g0 + k * WAVE;
+        const uint64_t ends = __ballot(fl[k * WAVE + lane_id()] != 0) & ~1ull;  // ends in (G, G + 64)
+        j = __popcll(__ballot(incl <= G)) + __popcll(ends & (lanemask_lt() | (1ull << lane_id())));
+      } else {
+#pragma unroll
+        for (int step = 32; step; step >>= 1) {
+          const int pv = __shfl(incl, j + step - 1);
+          if (pv <= c) j += step;
+        }
+      }
+      const int jj = j < WAVE ? j : WAVE - 1;
+      const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
+      const int ex = jj > 0 ? exv : 0;
+      const int uj = __shfl(u, jj);
+      const int sj = __shfl(sl, jj);
+      key[k] = 0;
+      sv[k] = 0.0;
+      if (valid) {
+        const int64_t r = s.row(sj, uj) + (c - ex);
+        key[k] = s.ids[r];
+        sv[k] = s.sc[r];
+      }
+    }
+  };
+  int key[HUB_TW_BATCH], nkey[HUB_TW_BATCH];
+  double sv[HUB_TW_BATCH], nsv[HUB_TW_BATCH];
+  if (total > 0) load(0, nkey, nsv);
+  for (int g0 = 0; g0 < total; g0 += WAVE * HUB_TW_BATCH) {
+#pragma unroll
+    for (int k = 0; k < HUB_TW_BATCH; k++) { key[k] = nkey[k]; sv[k] = nsv[k]; }
+    if (g0 + WAVE * HUB_TW_BATCH < total) load(g0 + WAVE * HUB_TW_BATCH, nkey, nsv);
+#pragma unroll
+    for (int k = 0; k < HUB_TW_BATCH; k++) {
+      if (g0 + k * WAVE >= total) break;  // uniform
+      f(g0 + k * WAVE + lane_id() < total, key[k], sv[k]);
     }
   }
-  const int jj = j < WAVE ? j : WAVE - 1;
-  const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);  // every lane executes the bpermute
-  const int ex = jj > 0 ? exv : 0;
-  const int uj = __shfl(u, jj);
-  const int sj = __shfl(sl, jj);
-  key = 0;
-  sv = 0.0;
-  if (valid) {
-    const int64_t r = s.row(sj, uj) + (c - ex);
-    key = s.ids[r];
-    sv = s.sc[r];
-  }
 }
+
+struct WalkNoSucc {
+  static constexpr bool kWant = false;
+  __device__ void operator()(int, unsigned long long) const {}
+};
+// top-L pruning bound of the wave tier: max row minimum over full successor rows (unscaled bits)
+struct WalkRowMin {
+  static constexpr bool kWant = true;
+  unsigned long long* mb;
+  int L;
+  __device__ void operator()(int ln, unsigned long long rm) const { if (ln == L && rm > *mb) *mb = rm; }
+};
+template <class F>
+__device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
+                                                int64_t i0, int64_t e, uint8_t* fl, F f) {
+  hub_window_walk(g, s, a, i0, e, fl, f, WalkNoSucc{});
+}
+// flag bytes per wave of hub_window_walk
+constexpr int HUB_WALK_FLAGS = WAVE * HUB_TW_BATCH;
 
 __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterArgs a,
                                                    const int32_t* list, int64_t count, int T,
@@ -232,33 +304,11 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
       table_apply_own(t, own, valid, key, 1.0, factor);
     }
   } else {
-    for (int64_t e0 = b; e0 < e; e0 += WAVE) {
-      const int64_t i = e0 + lane_id();
-      int u = 0, sl = 0, ln = 0;
-      if (i < e) {
-        const int32_t cx = g.colx[i];
-        u = cx & 0x7fffffff;
-        sl = read_slot(a, cx);
-        ln = s.len[s.lrow(sl, u)];
-        const unsigned long long rm = dbits(s.rmin[s.lrow(sl, u)]);  // loaded beside len
-        if (ln == s.L && rm > mb) mb = rm;
-      }
-      const int incl = wave_incl_scan(ln);
-      const int total = __shfl(incl, WAVE - 1);
-      // end flags live in the select histogram's LDS, unused until the epilogue
-      uint8_t* fl = __ballot(i < e && ln == 0) ? nullptr : reinterpret_cast<uint8_t*>(hist);
-      bool nv;
-      int nk;
-      double ns;
-      window_fetch(s, incl, u, sl, total, lane_id(), nv, nk, ns, fl);
-      for (int g0 = 0; g0 < total; g0 += WAVE) {
-        const bool cv = nv;
-        const int ck = nk;
-        const double cs = ns;
-        if (g0 + WAVE < total) window_fetch(s, incl, u, sl, total, g0 + WAVE + lane_id(), nv, nk, ns, fl);
-        table_apply_own(t, own, cv, ck, cs, factor);
-      }
-    }
+    // the select histogram's LDS is idle until the epilogue: it holds the walk's end flags
+    for (int64_t e0 = b; e0 < e; e0 += WAVE)
+      hub_window_walk(g, s, a, e0, min(e, e0 + WAVE), reinterpret_cast<uint8_t*>(hist),
+                      [&](bool valid, int key, double sv) { table_apply_own(t, own, valid, key, sv, factor); },
+                      WalkRowMin{&mb, (int)s.L});
   }
   wave_fence();
   // keys below the bound cannot reach the top-L (a full successor row puts L distinct keys at
