@@ -225,7 +225,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     const char* e18 = getenv("PPR_HUB_REGIONS");
     p->hub_regions = e18 ? std::max(2, std::min(ppr_plan::MAX_REGIONS, atoi(e18))) : 3;
     const char* e10 = getenv("PPR_HUB_MIX");
-    p->hub_mix = e10 ? std::max(0, std::min(HUB_MAX_LOGP, atoi(e10))) : 8;
+    p->hub_mix = e10 ? std::max(0, std::min(HUB_MAX_LOGP, atoi(e10))) : 6;
     const char* e9 = getenv("PPR_HUB_TILE_PB");
     p->hub_tile_pb = e9 ? std::max(0, std::min(64, atoi(e9))) : HUB_TILE_PER_BUCKET;
     const char* e8 = getenv("PPR_HUB_BUDGET");

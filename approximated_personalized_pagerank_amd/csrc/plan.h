@@ -109,7 +109,7 @@ struct ppr_plan {
   int wave_wpb = 1;                // PPR_WAVE_WPB: waves per block of k_merge_lds (1, 2 or 4)
   int tile_wpb_p = 4096;           // PPR_TILE_WPB_P: count / scatter run one wave per block from this maxP on
   int hub_bw_budget = 380;         // distinct keys a bucket wave's table takes before it spills
-  int hub_mix = 8;                 // PPR_HUB_MIX: interleave sources with P >= 2^hub_mix among the others
+  int hub_mix = 6;                 // PPR_HUB_MIX: interleave sources with P >= 2^hub_mix among the others
   int hub_tile_pb = 4;             // PPR_HUB_TILE_PB: tile candidates >= this many per bucket (0: 4096 / L)
   int64_t hub_budget = 1LL << 28;  // PPR_HUB_BUDGET: staged candidates per hub batch (16-B records)
   // with PPR_HUB_REGIONS (default 3) scratch regions the partition stage runs up to two batches
