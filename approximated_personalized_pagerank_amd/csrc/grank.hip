@@ -644,13 +644,14 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
 int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
               unsigned long long* maxdiff) {
   if (count <= 0) return PPR_OK;
-  HIP_OK(hipEventRecord(p->ev_m0, p->stream));
+  // MC combine levels are timed as a whole by the caller: no per-level event sync
+  if (!a.mc) HIP_OK(hipEventRecord(p->ev_m0, p->stream));
   int rc = run_merge_impl(p, a, list, count, maxdiff);
   if (p->stream3) {  // the wave tiers ran on stream3
     HIP_OK(hipEventRecord(p->ev_wave, p->stream3));
     HIP_OK(hipStreamWaitEvent(p->stream, p->ev_wave, 0));
   }
-  if (rc) return rc;
+  if (rc || a.mc) return rc;
   HIP_OK(hipEventRecord(p->ev_m1, p->stream));
   HIP_OK(hipEventSynchronize(p->ev_m1));
   float ms = 0.f;

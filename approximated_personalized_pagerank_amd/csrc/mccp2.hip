@@ -175,10 +175,18 @@ extern "C" int ppr_mccp2_plan_combine(ppr_plan* p) {
   a.diag = p->d_diag;
   a.lds_rank = p->lds_rank;
   const int64_t nl = (int64_t)p->mc_level_off.size() - 1;
+  HIP_OK(hipEventRecord(p->ev_m0, p->stream));
   for (int64_t l = 0; l < nl; l++) {
     const int64_t b = p->mc_level_off[l], e = p->mc_level_off[l + 1];
     int rc = run_merge(p, a, p->d_mc_levels + b, e - b, p->d_maxdiff + PPR_MAX_ITER_STATS);
     if (rc) return rc;
+  }
+  HIP_OK(hipEventRecord(p->ev_m1, p->stream));
+  HIP_OK(hipEventSynchronize(p->ev_m1));
+  {
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, p->ev_m0, p->ev_m1));
+    p->merge_ms += ms;
   }
   // final keepTop(K) (:252-256): prefix of every row in slot 0
   return launch_topk(p, 0, 0);
