@@ -110,12 +110,12 @@ __device__ __forceinline__ uint32_t hub_digit(int key, int logP) {
 
 // walk the candidates of tile t (successors [t * tw, (t + 1) * tw) of source v) in successor
 // order: windows of 64 successors, 64 candidates per step
-template <class F>
+template <class F, class S = WalkNoSucc>
 __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
-                                              int v, int t, int tw, uint8_t* fl, F f) {
+                                              int v, int t, int tw, uint8_t* fl, F f, S succ = S{}) {
   const int64_t b = g.rp[v] + (int64_t)t * tw;
   const int64_t e = min(g.rp[v + 1], b + (int64_t)tw);
-  for (int64_t w0 = b; w0 < e; w0 += WAVE) hub_window_walk(g, s, a, w0, min(e, w0 + WAVE), fl, f);
+  for (int64_t w0 = b; w0 < e; w0 += WAVE) hub_window_walk(g, s, a, w0, min(e, w0 + WAVE), fl, f, succ);
 }
 
 __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterArgs a,
@@ -131,30 +131,21 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
   const HubTask tk = tasks[w];
   const HubDesc d = desc[tk.d];
   const int P = 1 << d.logP;
-  if (!a.unit) {  // max over this tile's full-row successors of their row minimum (unscaled)
-    const int64_t b = g.rp[d.v] + (int64_t)tk.x * d.tw;
-    const int64_t e = min(g.rp[d.v + 1], b + (int64_t)d.tw);
-    unsigned long long mb = 0;
-    for (int64_t i = b + lane_id(); i < e; i += WAVE) {
-      const int32_t cx = g.colx[i];
-      const int u = cx & 0x7fffffff;
-      const int sl = read_slot(a, cx);
-      if (s.len[s.lrow(sl, u)] == s.L) {  // row minimum
-        const unsigned long long m = dbits(s.rmin[s.lrow(sl, u)]);
-        mb = m > mb ? m : mb;
-      }
-    }
-#pragma unroll
-    for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
-    if (lane_id() == 0 && mb) atomicMax(&tau[tk.d], mb);
-  }
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * maxP;
   uint8_t* fl = smem + (size_t)(blockDim.x >> 6) * maxP * 4 + (size_t)wv * HUB_WALK_FLAGS;
   for (int i = lane_id(); i < P; i += WAVE) hist[i] = 0;
   wave_fence();
+  // the walk also hands over every successor's row length and minimum: tau = max over this tile's
+  // full-row successors of their row minimum (unscaled)
+  unsigned long long mb = 0;
   hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid, int key, double) {
     if (valid) atomicAdd(&hist[hub_digit(key, d.logP)], 1u);
-  });
+  }, WalkRowMin{&mb, (int)s.L});
+  if (!a.unit) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
+    if (lane_id() == 0 && mb) atomicMax(&tau[tk.d], mb);
+  }
   wave_fence();
   for (int i = lane_id(); i < P; i += WAVE) cm[d.cm_off + (int64_t)i * d.T + tk.x] = (int32_t)hist[i];
 }
