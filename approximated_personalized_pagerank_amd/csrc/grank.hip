@@ -39,6 +39,7 @@
 #include "wg_merge.h"
 #include "merge_hub.h"
 #include "merge_glb.h"
+#include "merge_hot.h"
 
 using namespace pprk;
 
@@ -47,24 +48,27 @@ using namespace pprk;
 namespace pprk {
 // Probe of the LDS atomic order chunk_accumulate's `ordered` mode relies on: every lane of a wave
 // adds 1 to a counter chosen with heavy collisions; the returned old value must equal the number
-// of lower lanes on the same counter, for every collision pattern tried. One block; *ok stays 1
-// only if no lane ever disagrees.
-__global__ void __launch_bounds__(256) k_probe_lds_rank(int* ok, int trials) {
-  __shared__ uint32_t cnt[4][512];
+// of lower lanes on the same counter, for every collision pattern tried. It runs at the bucket
+// waves' own launch shape: the same grid (every CU filled to its LDS limit), the same waves per
+// block, the same per-wave LDS footprint and the counters at the same offset inside it (the
+// T-slot table, ChunkLds::cnt at 12 T). *ok stays 1 only if no lane of any wave ever disagrees.
+__global__ void __launch_bounds__(256) k_probe_lds_rank(int* ok, int trials, int T, int wave_bytes) {
+  extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6, l = lane_id();
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + (size_t)wv * wave_bytes + (size_t)T * 12);
   int bad = 0;
   for (int t = 0; t < trials; t++) {
-    const uint32_t r = hash32(t * 104729u + wv * 31u + 7u);
+    const uint32_t r = hash32(t * 104729u + blockIdx.x * 7919u + wv * 31u + 7u);
     const uint32_t S = 1u << (r % 10);
-    for (int i = l; i < 512; i += WAVE) cnt[wv][i] = 0;
+    for (int i = l; i < T; i += WAVE) cnt[i] = 0;
     wave_fence();
     const uint32_t hl = hash32(r ^ (uint32_t)(l * 2654435761u));
-    const uint32_t slot = hl & (S - 1);
+    const uint32_t slot = (hl & (S - 1)) % (uint32_t)T;
     // odd trials: increments 1..4 and a few inactive lanes (the scatter's run heads)
     const uint32_t inc = (t & 1) ? 1u + ((hl >> 12) & 3u) : 1u;
     const bool act = !(t & 1) || ((hl >> 16) & 7u) != 0;
     uint32_t got = 0;
-    if (act) got = atomicAdd(&cnt[wv][slot], inc);
+    if (act) got = atomicAdd(&cnt[slot], inc);
     uint32_t want = 0;
     for (int j = 0; j < WAVE; j++) {
       const uint32_t sj = (uint32_t)__shfl((int)slot, j);
@@ -83,6 +87,10 @@ __global__ void __launch_bounds__(256) k_probe_lds_rank(int* ok, int trials) {
 int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t K, uint32_t L,
                double damping, const ppr_opts* o, ppr_plan** out) {
   const int64_t m = n ? row_ptr[n] : 0;
+  // per-source candidate counts (<= deg * L + 1) and the hub staging offsets derived from them
+  // are 32-bit on the device: reject a graph whose widest source could exceed that
+  for (int64_t v = 0; v < n; v++)
+    if ((row_ptr[v + 1] - row_ptr[v]) * (int64_t)L + 1 > (int64_t)INT32_MAX) return PPR_ERR_RANGE;
   ppr_plan* p = new (std::nothrow) ppr_plan();
   if (!p) return PPR_ERR_OOM;
   p->n = n; p->m = m; p->K = K; p->L = L; p->damping = damping;
@@ -230,6 +238,17 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_tile_pb = e9 ? std::max(0, std::min(64, atoi(e9))) : HUB_TILE_PER_BUCKET;
     const char* e8 = getenv("PPR_HUB_BUDGET");
     if (e8) p->hub_budget = std::max<int64_t>(1024, std::min<int64_t>(1LL << 28, atoll(e8)));
+    // hot pass (merge_hot.h): PPR_HOT_N members (0 = off), built at iteration PPR_HOT_AT from
+    // every PPR_HOT_STRIDE-th row
+    const char* h1 = getenv("PPR_HOT_N");
+    const char* h2 = getenv("PPR_HOT_AT");
+    const char* h3 = getenv("PPR_HOT_STRIDE");
+    if (h1) p->hot_cap = std::max(0, std::min(16384, atoi(h1)));
+    if (h2) p->hot_at = std::max(0, atoi(h2));
+    if (h3) p->hot_stride = std::max(1, atoi(h3));
+    if (hot_wave_lds(p->hot_cap) > 160 * 1024) p->hot_cap = 0;
+    const char* h4 = getenv("PPR_HOT_MAX");
+    if (h4) p->hot_max_need = std::max(0, atoi(h4));
   }
   p->hub_lds_wave = hub_wave_lds(p->hub_wave_t, p->hub_bw_ng) * p->hub_bw_waves;
   if (p->hub_streams == 2) {
@@ -237,10 +256,13 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         hipStreamCreateWithFlags(&p->stream4, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&p->stream3, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&p->ev_wave, hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
+    if (hipStreamCreateWithFlags(&p->stream5, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&p->ev_hot0, hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
     for (int i = 0; i < ppr_plan::MAX_REGIONS; i++)
       if (hipEventCreateWithFlags(&p->ev_part[i], hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&p->ev_buck[i], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&p->ev_fin[i], hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
+          hipEventCreateWithFlags(&p->ev_fin[i], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&p->ev_hot[i], hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
   }
   {
     hipDeviceProp_t prop;
@@ -258,7 +280,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     if ((!e || atoi(e) != 0) && hipMalloc(&d_ok, sizeof(int)) == hipSuccess) {
       ok = 1;
       if (hipMemcpy(d_ok, &ok, sizeof(int), hipMemcpyHostToDevice) == hipSuccess) {
-        hipLaunchKernelGGL(k_probe_lds_rank, dim3(1), dim3(256), 0, p->stream, d_ok, 4096);
+        hipFuncSetAttribute((const void*)k_probe_lds_rank, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipLaunchKernelGGL(k_probe_lds_rank, dim3((unsigned)p->hub_bw_blocks), dim3(64 * p->hub_bw_waves),
+                           p->hub_lds_wave, p->stream, d_ok, 64, p->hub_wave_t,
+                           (int)hub_wave_lds(p->hub_wave_t, p->hub_bw_ng));
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p->stream) != hipSuccess ||
             hipMemcpy(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
           ok = 0;
@@ -279,7 +304,77 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   hipFuncSetAttribute((const void*)k_topk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_count, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_hot, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_join, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   *out = p;
+  return PPR_OK;
+}
+
+static IterArgs iter_args(const ppr_plan* p, int it, bool unit);
+
+// Hot key set of this run (merge_hot.h), from the rows iteration `it` reads: weights over every
+// hot_stride-th row, a 4096-bin histogram to find the weight bin at which the top hot_cap end,
+// the keys above it plus the heaviest of that bin (weight desc, id asc) on the host.
+static int hot_build(ppr_plan* p, int it) {
+  hipStream_t st = p->stream;
+  const int64_t n = p->n;
+  const IterArgs a = iter_args(p, it, false);
+  HIP_OK(hipMemsetAsync(p->d_hot_w, 0, 4 * (size_t)n, st));
+  HIP_OK(hipMemsetAsync(p->d_hot_hist, 0, 4 * (HOT_BINS + 2), st));
+  const int64_t ns = (n + p->hot_stride - 1) / p->hot_stride;
+  hipLaunchKernelGGL(k_hot_weight, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, st, dev_slab(p), a, p->d_part,
+                     p->d_indeg, p->hot_stride, p->d_hot_w);
+  HIP_OK(hipGetLastError());
+  const unsigned hb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 255) / 256));
+  hipLaunchKernelGGL(k_hot_hist, dim3(hb), dim3(256), 0, st, p->d_hot_w, n, p->d_hot_hist);
+  HIP_OK(hipGetLastError());
+  std::vector<uint32_t> hist(HOT_BINS);
+  HIP_OK(hipMemcpyAsync(hist.data(), p->d_hot_hist, 4 * HOT_BINS, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  int64_t above = 0;
+  int bound = 0;  // no bin overflows the cap: every key with a weight is taken
+  for (int b = HOT_BINS - 1; b > 0; b--) {
+    if (above + hist[b] > p->hot_cap) { bound = b; break; }
+    above += hist[b];
+  }
+  const int64_t room_max = (p->hot_list_cap - p->hot_cap) / 2;
+  hipLaunchKernelGGL(k_hot_collect, dim3(hb), dim3(256), 0, st, p->d_hot_w, n, (uint32_t)bound, p->d_hot_list,
+                     p->hot_list_cap, room_max, p->d_hot_hist + HOT_BINS);
+  HIP_OK(hipGetLastError());
+  uint32_t cnt[2];
+  HIP_OK(hipMemcpyAsync(cnt, p->d_hot_hist + HOT_BINS, 8, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  std::vector<int32_t> keys(cnt[0]);
+  const int64_t nb = std::min<int64_t>(cnt[1], room_max);
+  std::vector<int32_t> tail(2 * nb);
+  if (cnt[0]) HIP_OK(hipMemcpyAsync(keys.data(), p->d_hot_list, 4 * (size_t)cnt[0], hipMemcpyDeviceToHost, st));
+  if (nb) HIP_OK(hipMemcpyAsync(tail.data(), p->d_hot_list + p->hot_list_cap - 2 * nb, 8 * (size_t)nb,
+                                hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (bound > 0 && nb) {
+    // the boundary bin's pairs, heaviest first (ties: smaller id), fill the remaining room
+    std::vector<std::pair<uint32_t, int32_t>> bb(nb);
+    for (int64_t j = 0; j < nb; j++) bb[j] = {(uint32_t)tail[2 * j + 1], tail[2 * j]};
+    std::sort(bb.begin(), bb.end(), [](const std::pair<uint32_t, int32_t>& x, const std::pair<uint32_t, int32_t>& y) {
+      return x.first > y.first || (x.first == y.first && x.second < y.second);
+    });
+    const int64_t take = std::min<int64_t>(nb, p->hot_cap - (int64_t)keys.size());
+    for (int64_t j = 0; j < take; j++) keys.push_back(bb[j].second);
+  }
+  std::sort(keys.begin(), keys.end());  // dense indices in id order (run-to-run identical layout)
+  p->hot_n = (int)keys.size();
+  HIP_OK(hipMemsetAsync(p->d_hot_bits, 0, 4 * (size_t)((n + 31) / 32), st));
+  if (p->hot_n) {
+    HIP_OK(hipMemcpyAsync(p->d_hot_keys, keys.data(), 4 * keys.size(), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_hot_set, dim3((unsigned)((p->hot_n + 255) / 256)), dim3(256), 0, st, p->d_hot_keys,
+                       p->hot_n, p->d_hot_bits, p->d_hot_idx);
+    HIP_OK(hipGetLastError());
+    // stored ids switch to the hot encoding: every row written so far is re-encoded
+    hipLaunchKernelGGL(k_hot_encode, dim3((unsigned)((2 * n + 3) / 4)), dim3(256), 0, st, dev_slab(p));
+    HIP_OK(hipGetLastError());
+  }
+  p->h_hot_keys = keys;
+  HIP_OK(hipStreamSynchronize(st));  // `keys` leaves scope
   return PPR_OK;
 }
 
@@ -325,6 +420,23 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
   }
   p->nact[0] = (int64_t)act[0].size();
   p->nact[1] = (int64_t)act[1].size();
+  if (p->hot_cap > 0 && n > 0) {
+    std::vector<int32_t> indeg(n, 0);
+    for (int64_t e = 0; e < m; e++) indeg[g->col[e]]++;
+    p->hot_list_cap = p->hot_cap + 2 * std::min<int64_t>(n, 1 << 20);
+    TRY(dalloc(&p->d_hot_bits, (n + 31) / 32));
+    TRY(dalloc(&p->d_hot_idx, n));
+    TRY(dalloc(&p->d_hot_keys, p->hot_cap));
+    TRY(dalloc(&p->d_hot_w, n));
+    TRY(dalloc(&p->d_hot_hist, HOT_BINS + 2));
+    TRY(dalloc(&p->d_hot_list, p->hot_list_cap));
+    TRY(dalloc(&p->d_indeg, n));
+    if (hipMemcpy(p->d_indeg, indeg.data(), 4 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess) {
+      plan_free(p); return PPR_ERR_HIP;
+    }
+  } else {
+    p->hot_cap = 0;
+  }
   TRY(dalloc(&p->d_act[0], p->nact[0]));
   TRY(dalloc(&p->d_act[1], p->nact[1]));
   hipStream_t st = p->stream;
@@ -400,6 +512,10 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   }
   HubDesc* desc = (HubDesc*)p->h_desc_pin;
   size_t nd_all = 0;
+  // hot pass for every staged source of this merge (not in init, not in the MC combine); rows
+  // are stored with the hot encoding exactly when hot_n > 0
+  const bool hot = p->hot_n > 0 && !a.unit && !a.mc;
+  const HotSet H{p->d_hot_bits, p->d_hot_idx, p->d_hot_keys, hot ? p->hot_n : 0};
   auto logp_of = [&](int64_t need) {
     return std::max(1, std::min(HUB_MAX_LOGP, ceil_log2((need + p->hub_bucket - 1) / p->hub_bucket)));
   };
@@ -433,7 +549,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
         // segmented path (no partition pass): iterations only (the init has no successor rows),
         // and at most 2^RANGE_BITS buckets of about seg_bucket candidates
         const int lseg = std::max(0, ceil_log2((need + p->seg_bucket - 1) / p->seg_bucket));
-        const bool seg = p->seg_enabled && !a.unit && lseg <= RANGE_BITS;
+        const bool seg = p->seg_enabled && !a.unit && !hot && lseg <= RANGE_BITS;
         const int64_t ptc0 = (int64_t)(1 << (seg ? lseg : logp_of(need))) * L;
         if (nd_all > b.d0 &&
             (b.stg + (seg ? 0 : need) > budget || b.pt + ptc0 > budget || b.nseg + (1 << lseg) > (1 << 24))) break;
@@ -448,8 +564,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
         const int nsl = ptc > 2 * slice ? (int)((ptc + slice - 1) / slice) : 0;
         // staging offsets are cumulative candidate counts in descriptor order, the same order the
         // device scan walks the concatenated count matrices in: scanned cm = absolute offsets
-        desc[nd_all++] = HubDesc{v, logP, T, (int32_t)need, tw, nsl, b.cm, b.stg, b.pt, b.red, b.ntiles, b.nbuck, b.nrt,
-                                 seg ? b.nseg : -1};
+        desc[nd_all++] = HubDesc{v, logP, T, (int32_t)need, tw, nsl, -1, 0, b.cm, b.stg, b.pt, b.red, b.ntiles, b.nbuck,
+                                 b.nrt, seg ? b.nseg : -1};
         b.cm += (int64_t)P * T;
         b.stg += seg ? 0 : need - 1;
         b.pt += ptc;
@@ -464,6 +580,26 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       batches.push_back(b);
     }
   }
+  // hot tasks: every source, in descending candidate count (one launch; the longest fma chains
+  // start first); hot list / cold list j belong to the j-th task
+  std::vector<HotTask> htask;
+  if (hot) {
+    std::vector<uint32_t> ord;
+    for (size_t j = 0; j < nd_all; j++)
+      if (desc[j].need <= p->hot_max_need) ord.push_back((uint32_t)j);
+    std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+      return desc[x].need > desc[y].need || (desc[x].need == desc[y].need && x < y);
+    });
+    htask.resize(ord.size());
+    for (size_t j = 0; j < ord.size(); j++) {
+      desc[ord[j]].hot = (int32_t)j;
+      htask[j] = HotTask{desc[ord[j]].v, (int32_t)j};
+    }
+  }
+  if (p->d_diag && !a.unit)
+    for (size_t j = 0; j < nd_all; j++) p->diag_hub_cand += (double)(desc[j].need - 1);
+  const size_t nht = htask.size();
+  const bool hot_any = nht > 0;
   // one scratch layout for every batch (maxima), so no batch reallocates under a running one
   Batch mx{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1};
   size_t maxnd = 0;
@@ -480,6 +616,14 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   size_t off = 0;
   const size_t o_desc = off; off = al(off + sizeof(HubDesc) * nd_all);
   const size_t o_ovl = off;  off = al(off + 4 * (nd_all + 1));
+  const size_t o_ht = off;   off = al(off + sizeof(HotTask) * (nht + 1));
+  const size_t o_hk = off;   off = al(off + 4 * (size_t)L * nht);
+  const size_t o_hs = off;   off = al(off + 8 * (size_t)L * nht);
+  const size_t o_hc = off;   off = al(off + 4 * (nht + 1));
+  const size_t o_hth = off;  off = al(off + 8 * (nht + 1));
+  const size_t o_ck = off;   off = al(off + 4 * (size_t)L * nht);
+  const size_t o_cs = off;   off = al(off + 8 * (size_t)L * nht);
+  const size_t o_cc = off;   off = al(off + 4 * (nht + 1));
   const size_t shared = off;
   off = 0;
   const size_t o_tile = off; off = al(off + sizeof(HubTask) * mx.ntiles);
@@ -499,6 +643,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   const size_t o_of = off;   off = al(off + 4 * maxnd);
   const size_t o_gl = off;   off = al(off + sizeof(HubTask) * (mx.nbuck + 1));
   const size_t o_cnt = off;  off = al(off + 16);
+  const size_t o_sd = off;   off = al(off + 4 * maxnd);
   const size_t o_bw = off;   off = al(off + sizeof(BucketWork) * mx.nbuck);
   const size_t region = off;
   // two streams only pay when there is a next batch to overlap with
@@ -511,11 +656,38 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   int32_t* d_ovl = (int32_t*)(base + o_ovl);     // [0] count, [1..] sources for the HBM-table path
   HIP_OK(hipMemcpyAsync(d_desc_all, desc, sizeof(HubDesc) * nd_all, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemsetAsync(d_ovl, 0, 4, st));
+  HotTask* d_htask = (HotTask*)(base + o_ht);
+  int32_t* d_hkey = (int32_t*)(base + o_hk);
+  double* d_hsc = (double*)(base + o_hs);
+  uint32_t* d_hcnt = (uint32_t*)(base + o_hc);
+  unsigned long long* d_tau_hot = (unsigned long long*)(base + o_hth);
+  int32_t* d_ckey = (int32_t*)(base + o_ck);
+  double* d_csc = (double*)(base + o_cs);
+  uint32_t* d_ccnt = (uint32_t*)(base + o_cc);
+  if (hot_any) {
+    // the host vector is read by the copy before the plan's stream syncs at the end of run_hubs
+    HIP_OK(hipMemcpyAsync(d_htask, htask.data(), sizeof(HotTask) * nht, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(d_hcnt, 0, 4 * (nht + 1), st));
+    HIP_OK(hipMemsetAsync(d_tau_hot, 0, 8 * (nht + 1), st));
+  }
   // partition stage (expand, count, scan, scatter, prep) of batch i on `st`, its bucket stage
   // (bucket waves, spills, segments, reduce, final) on `sb`; batch i+2 reuses batch i's region
   // once batch i's bucket stage has finished
   hipStream_t sb = ms ? p->stream2 : st;   // bucket waves, spills, segments
   hipStream_t sf = ms ? p->stream4 : st;   // reduce + final
+  hipStream_t sh = ms ? p->stream5 : st;   // hot pass
+  if (hot_any) {
+    if (ms) {
+      HIP_OK(hipEventRecord(p->ev_hot0, st));  // tasks uploaded, hot lists cleared
+      HIP_OK(hipStreamWaitEvent(sh, p->ev_hot0, 0));
+    }
+    // hot lists live outside the regions: the whole hot pass runs beside the batches
+    hipLaunchKernelGGL(k_hub_hot, dim3((unsigned)nht), dim3(64), hot_wave_lds(p->hot_n), sh, g, s, a, d_htask,
+                       (int64_t)nht, d_hkey, d_hsc, d_hcnt, d_tau_hot);
+    HIP_OK(hipGetLastError());
+    p->merge_launches++;
+    if (ms) HIP_OK(hipEventRecord(p->ev_hot[0], sh));
+  }
   for (size_t bi = 0; bi < batches.size(); bi++) {
     const Batch& b = batches[bi];
     const int r = (int)(bi % nreg);
@@ -538,10 +710,12 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     HubTask* d_gl = (HubTask*)(rb + o_gl);
     uint32_t* d_lc = (uint32_t*)(rb + o_cnt);    // [1] spill list length
     BucketWork* d_bw = (BucketWork*)(rb + o_bw);
+    uint32_t* d_sd = (uint32_t*)(rb + o_sd);
     const size_t nd = b.d1 - b.d0;
     HubDesc* d_desc = d_desc_all + b.d0;
     const int maxP = b.maxP;
     if (ms && bi >= (size_t)nreg) HIP_OK(hipStreamWaitEvent(st, p->ev_fin[r], 0));  // region free again
+    HIP_OK(hipMemsetAsync(d_sd, 0, 4 * nd, st));
     HIP_OK(hipMemsetAsync(d_pc, 0, 4 * nd, st));
     HIP_OK(hipMemsetAsync(d_tau, 0, 8 * nd, st));
     HIP_OK(hipMemsetAsync(d_oflag, 0, 4 * nd, st));
@@ -556,8 +730,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       const int twpb = maxP >= p->tile_wpb_p ? 1 : WAVES_PER_BLOCK;
       const size_t lds_tile = (size_t)twpb * (maxP * 4 + HUB_WALK_FLAGS);
       const unsigned tb = (unsigned)((ntiles + twpb - 1) / twpb);
-      hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP, d_cm,
-                         d_tau);
+      hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
+                         d_cm, d_tau, d_sd);
       HIP_OK(hipGetLastError());
       HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, scan_tmp, d_cm, d_cmx, (int)b.cm, st));
       hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
@@ -567,8 +741,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     // a batch of sources without successors (init of dangling nodes) has no tiles but still has
     // buckets: the one holding the source's own seed entry
     if (nbuck) {
-      hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, a, d_desc, d_buck,
-                         nbuck, d_cmx, d_tau, d_bw);
+      hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, a, H, d_desc, d_buck,
+                         nbuck, d_cmx, d_sd, d_tau, d_tau_hot, d_bw);
       HIP_OK(hipGetLastError());
     }
     if (ms) {
@@ -604,8 +778,9 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       HIP_OK(hipGetLastError());
       // spilled buckets (distinct keys beyond the wave table): persistent workgroups over the spill
       // list, whose length only the device knows
-      hipLaunchKernelGGL(k_hub_bucket, dim3((unsigned)p->num_cus), dim3(WG_THREADS), p->hub_lds_wg, sb, s, a, g,
-                         d_desc, d_gl, d_lc + 1, d_cmx, d_st, d_pk, d_ps, d_pc, d_tau, p->Lp, d_oflag, d_ovl);
+      hipLaunchKernelGGL(k_hub_bucket, dim3((unsigned)p->num_cus), dim3(WG_THREADS), p->hub_lds_wg, sb, s, a, g, H,
+                         d_desc, d_gl, d_lc + 1, d_cmx, d_sd, d_st, d_pk, d_ps, d_pc, d_tau, d_tau_hot, p->Lp, d_oflag,
+                         d_ovl);
       HIP_OK(hipGetLastError());
     }
     if (ms) {
@@ -621,12 +796,20 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       p->merge_launches++;
     }
     hipLaunchKernelGGL(k_hub_final, dim3((unsigned)nd), dim3(WG_THREADS), p->hub_lds_final, sf, s, a, d_desc,
-                       d_oflag, d_pc, d_pk, d_ps, d_rk, d_rs, slice, p->Lp, maxdiff, p->d_stats);
+                       d_oflag, d_pc, d_pk, d_ps, d_rk, d_rs, slice, d_ccnt, d_ckey, d_csc, p->Lp, maxdiff, p->d_stats);
     HIP_OK(hipGetLastError());
     p->merge_launches += 9;
     if (ms) HIP_OK(hipEventRecord(p->ev_fin[r], sf));
   }
   if (ms) HIP_OK(hipStreamWaitEvent(st, p->ev_fin[(batches.size() - 1) % nreg], 0));  // finals run in order
+  if (hot_any) {
+    // every hot-pass source's row = top-L of its hot and cold halves
+    if (ms) HIP_OK(hipStreamWaitEvent(st, p->ev_hot[0], 0));
+    hipLaunchKernelGGL(k_hub_join, dim3((unsigned)nht), dim3(WG_THREADS), p->hub_lds_final, st, s, a, d_htask, d_ccnt,
+                       d_ckey, d_csc, d_hcnt, d_hkey, d_hsc, p->Lp, maxdiff, p->d_stats);
+    HIP_OK(hipGetLastError());
+    p->merge_launches++;
+  }
   int32_t novf = 0;
   HIP_OK(hipMemcpyAsync(&novf, d_ovl, 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
@@ -793,6 +976,9 @@ static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, i
 extern "C" int ppr_grank_plan_init(ppr_plan* p) {
   if (!p) return PPR_ERR_ARG;
   HIP_OK(hipSetDevice(p->device));
+  p->md_shared_it = -1;  // a new run: iteration numbers start over
+  p->hot_n = 0;          // the hot set is rebuilt from this run's rows at iteration hot_at
+  p->hot_built_it = -1;
   IterArgs a = iter_args(p, 0, true);
   return run_merge(p, a, p->d_all, p->n, p->d_maxdiff + PPR_MAX_ITER_STATS);
 }
@@ -811,7 +997,17 @@ extern "C" int ppr_grank_plan_iterate(ppr_plan* p, int32_t it, int64_t begin, in
   end = std::min<int64_t>(p->nact[part], end);
   if (end <= begin) return PPR_OK;
   IterArgs a = iter_args(p, it, false);
+  if (p->hot_cap > 0 && it == p->hot_at && p->hot_built_it != it) {
+    int rc0 = hot_build(p, it);
+    if (rc0) return rc0;
+    p->hot_built_it = it;
+  }
   unsigned long long* md = p->d_maxdiff + (it < PPR_MAX_ITER_STATS ? it : PPR_MAX_ITER_STATS);
+  if (it >= PPR_MAX_ITER_STATS && p->md_shared_it != it) {
+    // the shared slot still holds an earlier iteration's maximum (the kernels only atomicMax it)
+    HIP_OK(hipMemsetAsync(md, 0, 8, p->stream));
+    p->md_shared_it = it;
+  }
   int rc = run_merge(p, a, p->d_act[part] + begin, end - begin, md);
   if (rc) return rc;
   if (a.stats) {  // bytes of the rows this iteration wrote (outside the timed merge span)
@@ -945,7 +1141,10 @@ extern "C" int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, in
       if (want != sl) continue;
       const int ln = tl[v];
       if (len) len[v] = ln;
-      for (int i = 0; i < ln; i++) row[i] = {ts[v * L + i], ti[v * L + i]};
+      for (int i = 0; i < ln; i++) {
+        const int32_t id = ti[v * L + i];  // stored id: HOT_TAG | hot index for a hot key
+        row[i] = {ts[v * L + i], id >= 0 ? id : p->h_hot_keys[(uint32_t)id & 0x7fffffffu]};
+      }
       std::sort(row.begin(), row.begin() + ln, [](const std::pair<double, int32_t>& x, const std::pair<double, int32_t>& y) {
         return x.first > y.first || (x.first == y.first && x.second < y.second);
       });

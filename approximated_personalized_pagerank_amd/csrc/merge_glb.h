@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArg
     if (a.unit) ln = 1;
     else { const int sl = read_slot(a, cx); ln = s.len[s.lrow(sl, u)]; r = s.row(sl, u); }
     for (int j = lane_id(); j < ln; j += WAVE) {
-      const int key = a.unit ? u : s.ids[r + j];
+      const int key = a.unit ? u : s.key(s.ids[r + j]);
       const double sv = a.unit ? 1.0 : s.sc[r + j];
       const uint64_t h = slot_of(key);
       const double cur = __hip_atomic_load(&acc[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(256) k_topk(DevSlab s, const uint8_t* part, in
   const int len = s.len[s.lrow(sl, v)];
   const int k = len < K ? len : K;
   const int64_t r = s.row(sl, v);
-  for (int i = lane_id(); i < len; i += WAVE) { rv[i] = dbits(s.sc[r + i]); rk[i] = s.ids[r + i]; }
+  for (int i = lane_id(); i < len; i += WAVE) { rv[i] = dbits(s.sc[r + i]); rk[i] = s.key(s.ids[r + i]); }
   wave_fence();
   row_sort(rv, rk, len, Lp);
   for (int i = lane_id(); i < K; i += WAVE) {

@@ -50,6 +50,9 @@ struct HubDesc {
   int32_t need;    // candidates + 1
   int32_t tw;      // successors per tile (<= 64; about 4096 candidates per tile)
   int32_t nsl;     // k_hub_reduce slices reserved (upper bound from P * L appended entries)
+  int32_t hot;     // >= 0: the hot pass (k_hub_hot) accumulates the source's hot keys into hot list
+                   // `hot`, and the partition carries only its cold keys; -1: no hot pass
+  int32_t pad;
   int64_t cm_off;  // count matrix (P*T ints; after the scan: absolute staging offsets)
   int64_t st_off;  // staging (need-1 keys / scores)
   int64_t pt_off;  // appended bucket results (<= P*L entries, pt_cnt[desc] of them used)
@@ -62,13 +65,15 @@ struct HubDesc {
 // tiles (d, t) for k_hub_count / k_hub_scatter, buckets (d, b) for k_hub_prep, reduce slices (d, x)
 struct HubTask;
 
-// staging range of bucket x of source d (cm holds the scanned, absolute offsets)
-__device__ __forceinline__ void hub_bucket_range(const HubDesc& d, const int32_t* cm, int x,
+// staging range of bucket x of source d (cm holds the scanned, absolute offsets; the source's
+// staged records start at cm[cm_off] and number `staged`, its candidates minus its hot ones)
+__device__ __forceinline__ void hub_bucket_range(const HubDesc& d, const int32_t* cm, uint32_t staged, int x,
                                                  int64_t& start, int64_t& nb) {
   const int P = 1 << d.logP;
   if (d.T == 0) { start = d.st_off; nb = 0; return; }  // no successors (init of a dangling node)
   start = cm[d.cm_off + (int64_t)x * d.T];
-  const int64_t end = (x + 1 < P) ? (int64_t)cm[d.cm_off + (int64_t)(x + 1) * d.T] : d.st_off + d.need - 1;
+  const int64_t end = (x + 1 < P) ? (int64_t)cm[d.cm_off + (int64_t)(x + 1) * d.T]
+                                  : (int64_t)cm[d.cm_off] + (int64_t)staged;
   nb = end - start;
 }
 struct HubTask { int32_t d; int32_t x; };   // (descriptor, tile or bucket)
@@ -121,7 +126,7 @@ __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& 
 __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterArgs a,
                                                    const HubDesc* desc, const HubTask* tasks,
                                                    int64_t ntasks, int maxP, int32_t* cm,
-                                                   unsigned long long* tau) {
+                                                   unsigned long long* tau, uint32_t* staged) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   // neighbouring tiles write neighbouring columns of the count matrix: on one XCD their partial
@@ -138,9 +143,18 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
   // the walk also hands over every successor's row length and minimum: tau = max over this tile's
   // full-row successors of their row minimum (unscaled)
   unsigned long long mb = 0;
-  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid, int key, double) {
-    if (valid) atomicAdd(&hist[hub_digit(key, d.logP)], 1u);
+  // hot keys (stored with HOT_TAG, merge_hot.h) go to k_hub_hot, not to the partition
+  int nst = 0;
+  // (a source without a hot pass stages every key, decoded)
+  const bool hotp = d.hot >= 0;
+  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid, int id, double, bool) {
+    if (valid && (id >= 0 || !hotp)) { atomicAdd(&hist[hub_digit(s.key(id), d.logP)], 1u); nst++; }
   }, WalkRowMin{&mb, (int)s.L});
+  nst = wave_sum(nst);
+  if (lane_id() == 0 && nst) {
+    atomicAdd(&staged[tk.d], (uint32_t)nst);
+    if (a.diag) atomicAdd(&a.diag[140], (unsigned long long)nst);
+  }
   if (!a.unit) {
 #pragma unroll
     for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
@@ -167,14 +181,24 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   // matrix once (one strided gather), so the per-group scatter never waits on global memory
   // (offsets are relative to the source's staging start: they fit 32 bits)
   uint32_t* run = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * maxP;
-  const int64_t base0 = d.st_off;
+  const int64_t base0 = cm[d.cm_off];  // the source's first staged record (scanned counts)
   for (int i = lane_id(); i < P; i += WAVE) run[i] = (uint32_t)(cm[d.cm_off + (int64_t)i * d.T + tk.x] - base0);
   wave_fence();
   const uint64_t lt = lanemask_lt();
   HubRec* stv = st + base0;
   uint8_t* fl = smem + (size_t)(blockDim.x >> 6) * maxP * 4 + (size_t)wv * HUB_WALK_FLAGS;
-  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid, int key, double sv) {
+  const bool hotp = d.hot >= 0;
+  const bool ordered = a.lds_rank != 0;
+  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid0, int id, double sv, bool) {
+    const bool valid = valid0 && (id >= 0 || !hotp);  // with a hot pass: cold keys only
+    const int key = valid ? s.key(id) : 0;
     const uint32_t dg = valid ? hub_digit(key, d.logP) : 0u;
+    if (ordered) {
+      // lane-ordered LDS atomics (probed per plan, k_probe_lds_rank): same-digit lanes get their
+      // run positions in lane order, i.e. stream order -- the stable rank in one instruction
+      if (valid) stv[atomicAdd(&run[dg], 1u)] = hub_rec(key, sv);
+      return;
+    }
     // lanes holding the same digit: AND of per-bit ballots (stable rank = lower lanes first)
     uint64_t match = __ballot(valid);
     for (int bit = 0; bit < d.logP; bit++) {
@@ -204,24 +228,39 @@ struct BucketWork {
   double factor, tau, selfval;
 };
 
-__global__ void __launch_bounds__(256) k_hub_prep(DevGraph g, IterArgs a, const HubDesc* desc,
+// pruning bound of a source's buckets: the larger of tau (full successor rows) and, once the hot
+// pass of the source has published it, the L-th largest hot value (both are lower bounds of the
+// L-th largest final value; a bound read as 0 before it is published only prunes less)
+__device__ __forceinline__ double hub_tau(const HubDesc& d, const unsigned long long* tau_b, int di,
+                                          const unsigned long long* tau_hot, double factor) {
+  double t = tau_b[di] ? bitsd(tau_b[di]) * factor : 0.0;  // no bound: keep all (deg 0: factor inf)
+  if (d.hot >= 0) {
+    const unsigned long long th = __hip_atomic_load(&tau_hot[d.hot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (th && bitsd(th) > t) t = bitsd(th);
+  }
+  return t;
+}
+
+__global__ void __launch_bounds__(256) k_hub_prep(DevGraph g, IterArgs a, HotSet H, const HubDesc* desc,
                                                   const HubTask* tasks, int64_t ntasks, const int32_t* cm,
-                                                  const unsigned long long* tau_b, BucketWork* bw) {
+                                                  const uint32_t* staged, const unsigned long long* tau_b,
+                                                  const unsigned long long* tau_hot, BucketWork* bw) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= ntasks) return;
   const HubTask tk = tasks[i];
   const HubDesc d = desc[tk.d];
   BucketWork w;
   int64_t nb;
-  hub_bucket_range(d, cm, tk.x, w.start, nb);
+  hub_bucket_range(d, cm, staged[tk.d], tk.x, w.start, nb);
   w.nb = (int32_t)nb;
   w.pt_off = d.pt_off;
   w.d = tk.d;
   w.x = tk.x;
-  w.seed = (int)hub_digit(d.v, d.logP) == tk.x ? d.v : -1;
+  // the source's own seed entry goes to its bucket, unless the hot pass owns the key
+  w.seed = ((int)hub_digit(d.v, d.logP) == tk.x && !(d.hot >= 0 && H.has(d.v))) ? d.v : -1;
   const int64_t deg = g.rp[d.v + 1] - g.rp[d.v];
   w.factor = merge_factor(a, deg);
-  w.tau = tau_b[tk.d] ? bitsd(tau_b[tk.d]) * w.factor : 0.0;  // no bound: keep all (deg 0: factor inf)
+  w.tau = hub_tau(d, tau_b, tk.d, tau_hot, w.factor);
   w.selfval = self_seed(a, deg);
   bw[i] = w;
 }
@@ -494,7 +533,7 @@ __global__ void __launch_bounds__(256) k_hub_seg(DevGraph g, DevSlab s, IterArgs
         cs[k] = 0.0;
         if (cv[k]) {
           const int64_t r = s.row(sj, uj) + lj + (c - ex);
-          kk[k] = s.ids[r];
+          kk[k] = s.key(s.ids[r]);
           cs[k] = s.sc[r];
         }
       }
@@ -533,10 +572,11 @@ __global__ void __launch_bounds__(256) k_hub_seg(DevGraph g, DevSlab s, IterArgs
   }
 }
 
-__device__ __forceinline__ void hub_bucket_one(const DevSlab& s, const IterArgs& a, const DevGraph& g,
+__device__ __forceinline__ void hub_bucket_one(const DevSlab& s, const IterArgs& a, const DevGraph& g, const HotSet& H,
                                                const HubDesc* desc, const HubTask tk, const int32_t* cm,
-                                               const HubRec* st, int32_t* pt_key, double* pt_sc,
-                                               uint32_t* pt_cnt, const unsigned long long* tau_b, int Lp,
+                                               const uint32_t* staged, const HubRec* st, int32_t* pt_key, double* pt_sc,
+                                               uint32_t* pt_cnt, const unsigned long long* tau_b,
+                                               const unsigned long long* tau_hot, int Lp,
                                                int32_t* ovf_flag, int32_t* ovf_list) {
   extern __shared__ __align__(16) unsigned char smem[];
   const HubDesc d = desc[tk.d];
@@ -546,8 +586,8 @@ __device__ __forceinline__ void hub_bucket_one(const DevSlab& s, const IterArgs&
   const int l = lane_id();
   const int v = d.v;
   int64_t sb, nb;
-  hub_bucket_range(d, cm, tk.x, sb, nb);
-  const bool seed = (int)hub_digit(v, d.logP) == tk.x;
+  hub_bucket_range(d, cm, staged[tk.d], tk.x, sb, nb);
+  const bool seed = (int)hub_digit(v, d.logP) == tk.x && !(d.hot >= 0 && H.has(v));
   const int64_t deg = g.rp[v + 1] - g.rp[v];
   const double factor = merge_factor(a, deg);
   const int Lw = s.L;
@@ -589,7 +629,7 @@ __device__ __forceinline__ void hub_bucket_one(const DevSlab& s, const IterArgs&
     }
   }
   if (wv == 0) {  // append the bucket's top-L entries >= tau
-    const double tau = tau_b[tk.d] ? bitsd(tau_b[tk.d]) * factor : 0.0;  // no bound: keep all (deg 0: factor inf)
+    const double tau = hub_tau(d, tau_b, tk.d, tau_hot, factor);
     const int n = L.misc[M_PLEN];
     int cnt = 0;
     for (int i = l; i < n; i += WAVE) cnt += L.pv[i] >= tau;
@@ -617,17 +657,19 @@ __device__ __forceinline__ void hub_bucket_one(const DevSlab& s, const IterArgs&
 // the host never waits for it); a bucket that overflows here too flags its source for the
 // HBM-table path (ovf_flag[d], source id appended to ovf_list[1..], count in ovf_list[0])
 __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a,
-                                                           const DevGraph g, const HubDesc* desc,
+                                                           const DevGraph g, HotSet H, const HubDesc* desc,
                                                            const HubTask* tasks, const uint32_t* ntasks_p,
-                                                           const int32_t* cm,
+                                                           const int32_t* cm, const uint32_t* staged,
                                                            const HubRec* st,
                                                            int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
-                                                           const unsigned long long* tau_b, int Lp,
+                                                           const unsigned long long* tau_b,
+                                                           const unsigned long long* tau_hot, int Lp,
                                                            int32_t* ovf_flag, int32_t* ovf_list) {
   const uint32_t ntasks = *ntasks_p;
   for (uint32_t task = blockIdx.x; task < ntasks; task += gridDim.x) {
     __syncthreads();  // LDS of the previous task fully consumed
-    hub_bucket_one(s, a, g, desc, tasks[task], cm, st, pt_key, pt_sc, pt_cnt, tau_b, Lp, ovf_flag, ovf_list);
+    hub_bucket_one(s, a, g, H, desc, tasks[task], cm, staged, st, pt_key, pt_sc, pt_cnt, tau_b, tau_hot, Lp,
+                   ovf_flag, ovf_list);
   }
 }
 // Long appended lists (a hub with thousands of buckets) are cut before k_hub_final: one
@@ -668,17 +710,53 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_reduce(DevSlab s, const HubD
   }
 }
 
+// top-L by (score desc, id asc) of `total` entries (keyat / valat) into L.rv / L.rk, in no
+// particular order; returns their count (every thread of the workgroup)
+template <class KeyAt, class ValAt>
+__device__ __forceinline__ int hub_select_lds(const WgLds& L, int total, int Lw, KeyAt keyat, ValAt valat) {
+  auto occ = [&](int) { return true; };
+  if (threadIdx.x == 0) L.misc[M_PLEN] = 0;
+  __syncthreads();
+  if (total <= Lw) {
+    for (int i = threadIdx.x; i < total; i += WG_THREADS) {
+      const int pos = atomicAdd(&L.misc[M_PLEN], 1);
+      L.rv[pos] = dbits(valat(i));
+      L.rk[pos] = keyat(i);
+    }
+  } else {
+    const SelCrit c = wg_select_top(L, total, Lw, keyat, valat, occ);
+    for (int i = threadIdx.x; i < total; i += WG_THREADS) {
+      const double x = valat(i);
+      const int k = keyat(i);
+      if (sel_test(c, dbits(x), (uint32_t)~k)) {
+        const int pos = atomicAdd(&L.misc[M_PLEN], 1);
+        L.rv[pos] = dbits(x);
+        L.rk[pos] = k;
+      }
+    }
+  }
+  __syncthreads();
+  return L.misc[M_PLEN];
+}
+
+// One workgroup per source of the batch: top-L of the appended bucket results. Without a hot
+// pass that is the source's new row (written, norm1 folded into maxDiff). With one (d.hot >= 0)
+// it is only the cold half: it goes to cold list d.hot (count ~0u when a bucket overflowed and
+// the HBM-table path redoes the source), and k_hub_join unites it with the hot list.
 __global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a, const HubDesc* desc,
                                                           const int32_t* ovf_flag, const uint32_t* pt_cnt,
                                                           const int32_t* pt_key, const double* pt_sc,
                                                           const int32_t* red_key, const double* red_sc, int slice,
-                                                          int Lp,
-                                                          unsigned long long* maxdiff,
+                                                          uint32_t* cold_cnt, int32_t* cold_key, double* cold_sc,
+                                                          int Lp, unsigned long long* maxdiff,
                                                           unsigned long long* stats) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int di = (int)blockIdx.x;
-  if (ovf_flag[di]) return;  // a bucket overflowed every LDS table: the HBM-table path redoes the source
   const HubDesc d = desc[di];
+  if (ovf_flag[di]) {  // a bucket overflowed every LDS table: the HBM-table path redoes the source
+    if (d.hot >= 0 && threadIdx.x == 0) cold_cnt[d.hot] = ~0u;
+    return;
+  }
   const WgLds L = wg_carve(smem, 0, Lp, 0);
   const int Lw = s.L;
   int n = (int)pt_cnt[di];  // appended bucket results, any order
@@ -690,27 +768,15 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a,
     pk = red_key + d.red;
     pv = red_sc + d.red;
   }
-  auto occ = [&](int) { return true; };
-  const int total = n;
-  if (threadIdx.x == 0) L.misc[M_PLEN] = 0;
-  __syncthreads();
-  if (total <= Lw) {
-    for (int i = threadIdx.x; i < n; i += WG_THREADS)
-      if (occ(i)) { const int pos = atomicAdd(&L.misc[M_PLEN], 1); L.rv[pos] = dbits(pv[i]); L.rk[pos] = pk[i]; }
-  } else {
-    const SelCrit c = wg_select_top(L, n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; }, occ);
-    for (int i = threadIdx.x; i < n; i += WG_THREADS) {
-      if (!occ(i)) continue;
-      if (sel_test(c, dbits(pv[i]), (uint32_t)~pk[i])) {
-        const int pos = atomicAdd(&L.misc[M_PLEN], 1);
-        L.rv[pos] = dbits(pv[i]);
-        L.rk[pos] = pk[i];
-      }
-    }
+  const int cnt = hub_select_lds(L, n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; });
+  if (d.hot >= 0) {
+    int32_t* ok = cold_key + (int64_t)d.hot * Lw;
+    double* os = cold_sc + (int64_t)d.hot * Lw;
+    for (int i = threadIdx.x; i < cnt; i += WG_THREADS) { ok[i] = L.rk[i]; os[i] = bitsd(L.rv[i]); }
+    if (threadIdx.x == 0) cold_cnt[d.hot] = (uint32_t)cnt;
+    return;
   }
-  __syncthreads();
   if ((threadIdx.x >> 6) == 0) {
-    const int cnt = L.misc[M_PLEN];
     const uint64_t* rv = L.rv;
     const int* rk = L.rk;
     // rows already hold the final set: finish_source with U <= L only sorts/writes/norm1

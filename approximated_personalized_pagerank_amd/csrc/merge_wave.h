@@ -161,7 +161,10 @@ __host__ __device__ constexpr size_t lds_wave_bytes(int T, int Lp) {
 #endif
 constexpr int HUB_TW_BATCH = PPR_TW_BATCH;  // candidate groups a walking wave gathers before using them
 
-// walk the candidates of successors [i0, e) (at most one per lane) in successor order, 64 per step
+// walk the candidates of successors [i0, e) (at most one per lane) in successor order, 64 per step:
+// f(valid, id, score, one_row) per group: id = the stored id (HOT_TAG-ed for hot keys, DevSlab::key
+// decodes it; in init mode the successor itself), one_row = every candidate of the group comes
+// from the same successor basket (so its keys are distinct; always false in init mode).
 // `succ(ln, rmin_bits)` (optional) sees every lane's successor basket length and row minimum once
 // per window (non-unit mode; invalid lanes report length 0).
 template <class F, class S>
@@ -170,7 +173,7 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
   const int64_t i = i0 + lane_id();
   if (a.unit) {  // init: every successor contributes {u: 1.0}
     const bool valid = i < e;
-    f(valid, valid ? (g.colx[i] & 0x7fffffff) : 0, 1.0);
+    f(valid, valid ? (g.colx[i] & 0x7fffffff) : 0, 1.0, false);
     return;
   }
   int u = 0, sl = 0, ln = 0;
@@ -192,7 +195,7 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
   // HUB_TW_BATCH groups of 64 candidates are gathered together (one memory latency per batch),
   // and the next batch is in flight while f consumes the current one; f still sees the
   // candidates in stream order
-  auto load = [&](int g0, int (&key)[HUB_TW_BATCH], double (&sv)[HUB_TW_BATCH]) {
+  auto load = [&](int g0, int (&key)[HUB_TW_BATCH], double (&sv)[HUB_TW_BATCH], bool (&one)[HUB_TW_BATCH]) {
     if (flags) {
 #pragma unroll
       for (int q = 0; q < HUB_TW_BATCH / 4; q++)  // WAVE * HUB_TW_BATCH flag bytes
@@ -218,6 +221,8 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
         }
       }
       const int jj = j < WAVE ? j : WAVE - 1;
+      // every candidate of the group from one successor basket: its keys are distinct
+      one[k] = !__ballot(valid && jj != __shfl(jj, 0));
       const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
       const int ex = jj > 0 ? exv : 0;
       const int uj = __shfl(u, jj);
@@ -233,15 +238,16 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
   };
   int key[HUB_TW_BATCH], nkey[HUB_TW_BATCH];
   double sv[HUB_TW_BATCH], nsv[HUB_TW_BATCH];
-  if (total > 0) load(0, nkey, nsv);
+  bool one[HUB_TW_BATCH], none[HUB_TW_BATCH];
+  if (total > 0) load(0, nkey, nsv, none);
   for (int g0 = 0; g0 < total; g0 += WAVE * HUB_TW_BATCH) {
 #pragma unroll
-    for (int k = 0; k < HUB_TW_BATCH; k++) { key[k] = nkey[k]; sv[k] = nsv[k]; }
-    if (g0 + WAVE * HUB_TW_BATCH < total) load(g0 + WAVE * HUB_TW_BATCH, nkey, nsv);
+    for (int k = 0; k < HUB_TW_BATCH; k++) { key[k] = nkey[k]; sv[k] = nsv[k]; one[k] = none[k]; }
+    if (g0 + WAVE * HUB_TW_BATCH < total) load(g0 + WAVE * HUB_TW_BATCH, nkey, nsv, none);
 #pragma unroll
     for (int k = 0; k < HUB_TW_BATCH; k++) {
       if (g0 + k * WAVE >= total) break;  // uniform
-      f(g0 + k * WAVE + lane_id() < total, key[k], sv[k]);
+      f(g0 + k * WAVE + lane_id() < total, key[k], sv[k], one[k]);
     }
   }
 }
@@ -307,7 +313,7 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
     // the select histogram's LDS is idle until the epilogue: it holds the walk's end flags
     for (int64_t e0 = b; e0 < e; e0 += WAVE)
       hub_window_walk(g, s, a, e0, min(e, e0 + WAVE), reinterpret_cast<uint8_t*>(hist),
-                      [&](bool valid, int key, double sv) { table_apply_own(t, own, valid, key, sv, factor); },
+                      [&](bool valid, int id, double sv, bool) { table_apply_own(t, own, valid, s.key(id), sv, factor); },
                       WalkRowMin{&mb, (int)s.L});
   }
   wave_fence();

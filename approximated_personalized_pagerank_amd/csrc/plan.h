@@ -63,6 +63,9 @@ struct ppr_plan {
   size_t wg_lds = 0;
   bool hub_enabled = true;
   unsigned long long* d_maxdiff = nullptr;  // PPR_MAX_ITER_STATS + 1
+  // iterations >= PPR_MAX_ITER_STATS share the last maxDiff slot: it is zeroed at the first
+  // ppr_grank_plan_iterate call of each such iteration (a sharded iteration may call it per range)
+  int32_t md_shared_it = -1;
   unsigned long long* d_stats = nullptr;    // 2
   GlbWork* d_work = nullptr;
   int64_t work_cap = 0;
@@ -119,6 +122,24 @@ struct ppr_plan {
   hipStream_t stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;
   hipEvent_t ev_part[MAX_REGIONS] = {}, ev_buck[MAX_REGIONS] = {}, ev_fin[MAX_REGIONS] = {}, ev_wave = nullptr;
   unsigned long long* d_diag = nullptr;  // PPR_DIAG=1: kernel histograms, printed at destroy
+  // hot key set of the hub path (merge_hot.h): chosen at iteration hot_at of every run from rows
+  // sampled every hot_stride nodes; hot_cap = PPR_HOT_N (0 disables the hot pass)
+  int hot_cap = 0, hot_at = 2, hot_stride = 16;  // measured: no net gain at RMAT-22
+  int hot_n = 0;                      // members of the current set (0 until it is built)
+  int32_t hot_built_it = -1;          // iteration of this run that built it (sharded runs iterate per range)
+  std::vector<int32_t> h_hot_keys;    // host copy (fetch_slab decodes stored ids)
+  int hot_max_need = 0x7fffffff;      // PPR_HOT_MAX: sources with more candidates skip the hot pass
+  double diag_hub_cand = 0.0;         // PPR_DIAG: candidates of the hub sources planned (iterations)
+  uint32_t* d_hot_bits = nullptr;     // [ceil(n / 32)]
+  uint16_t* d_hot_idx = nullptr;      // [n]
+  int32_t* d_hot_keys = nullptr;      // [hot_cap]
+  uint32_t* d_hot_w = nullptr;        // [n] weights
+  uint32_t* d_hot_hist = nullptr;     // [HOT_BINS + 2]: histogram, then the collect counters
+  int32_t* d_hot_list = nullptr;      // [hot_list_cap]: collected keys
+  int64_t hot_list_cap = 0;
+  int32_t* d_indeg = nullptr;         // [n] in-degree (how many sources read the node's row)
+  hipStream_t stream5 = nullptr;      // k_hub_hot beside the partition / bucket stages
+  hipEvent_t ev_hot0 = nullptr, ev_hot[MAX_REGIONS] = {};
   // MCCompletePathV2 (mccp2.hip)
   bool mc = false;
   int32_t* d_mc_walk = nullptr;       // walk set W (nodes read before their final basket exists)
@@ -150,6 +171,12 @@ inline void plan_free(ppr_plan* p) {
     if (p->ev_fin[i]) hipEventDestroy(p->ev_fin[i]);
   }
   if (p->ev_wave) hipEventDestroy(p->ev_wave);
+  if (p->ev_hot0) hipEventDestroy(p->ev_hot0);
+  for (int i = 0; i < ppr_plan::MAX_REGIONS; i++)
+    if (p->ev_hot[i]) hipEventDestroy(p->ev_hot[i]);
+  if (p->stream5) hipStreamDestroy(p->stream5);
+  hipFree(p->d_hot_bits); hipFree(p->d_hot_idx); hipFree(p->d_hot_keys); hipFree(p->d_hot_w);
+  hipFree(p->d_hot_hist); hipFree(p->d_hot_list); hipFree(p->d_indeg);
   if (p->stream2) hipStreamDestroy(p->stream2);
   if (p->stream3) hipStreamDestroy(p->stream3);
   if (p->stream4) hipStreamDestroy(p->stream4);
@@ -165,6 +192,11 @@ inline void plan_free(ppr_plan* p) {
         if (h[b] || h[64 + b] || h[96 + b])
           fprintf(stderr, "ppr_diag %2d %12llu %12.1f | %12llu | %12llu\n", b, h[b], h[32 + b] / 1e6,
                   h[64 + b], h[96 + b]);
+      if (h[144])
+        fprintf(stderr, "ppr_diag hot pass: %d keys, %llu tasks, hub candidates %.3e staged (cold) %.3e (%.1f %%), "
+                "task ms: longest %.2f, first %.2f, sum %.1f\n", p->hot_n, h[144], p->diag_hub_cand, (double)h[140],
+                100.0 * (double)h[140] / (p->diag_hub_cand > 0 ? p->diag_hub_cand : 1.0), h[141] / 1e5, h[143] / 1e5,
+                h[142] / 1e5);
       if (h[133])
         fprintf(stderr, "ppr_diag k_hub_seg: %llu waves, %.1f candidates/wave, Mcycles setup %.1f window %.1f "
                 "gather %.1f accumulate %.1f emit %.1f\n", h[133], (double)h[134] / (double)h[133], h[128] / 1e6,
@@ -187,7 +219,8 @@ inline int check_params(uint32_t K, uint32_t L, uint32_t iterations, double damp
 }
 
 inline DevSlab dev_slab(const ppr_plan* p) {
-  return DevSlab{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L, p->d_rix, p->d_rmin};
+  return DevSlab{p->d_ids, p->d_sc, p->d_len, p->n, (int32_t)p->L, p->d_rix, p->d_rmin,
+                 p->d_hot_bits, p->d_hot_idx, p->d_hot_keys, p->hot_n};
 }
 
 // grow-only pinned host buffer

@@ -58,6 +58,12 @@ constexpr int NRANGE = 64;
 constexpr int RANGE_BITS = 6;
 __device__ __forceinline__ uint32_t row_range(int key) { return hash_b((uint32_t)key) >> (32 - RANGE_BITS); }
 
+// Stored ids: once a run has built its hot set (merge_hot.h), a hot key is stored as
+// HOT_TAG | its dense hot index and every other key as itself (ids are < 2^31), so a reader of a
+// row tells hot from cold -- and gets a hot key's accumulator index -- without a lookup.
+// Every reader that needs the key itself decodes through DevSlab::key.
+constexpr uint32_t HOT_TAG = 0x80000000u;
+
 struct DevSlab {
   int32_t* ids;
   double* sc;
@@ -66,9 +72,21 @@ struct DevSlab {
   int32_t L;
   uint16_t* rix;   // [2][n][NRANGE]
   double* rmin;    // [2][n]
+  // hot-key encoding of stored ids (hn = 0: ids are stored as is)
+  const uint32_t* hbits;  // [ceil(n / 32)] membership
+  const uint16_t* hidx;   // [n] dense hot index
+  const int32_t* hkeys;   // [hn] key of each hot index
+  int hn;
   __device__ __forceinline__ int64_t row(int slot, int64_t u) const { return ((int64_t)slot * n + u) * L; }
   __device__ __forceinline__ int64_t lrow(int slot, int64_t u) const { return (int64_t)slot * n + u; }
   __device__ __forceinline__ int64_t xrow(int slot, int64_t u) const { return ((int64_t)slot * n + u) * NRANGE; }
+  // stored id -> key
+  __device__ __forceinline__ int key(int32_t id) const { return id >= 0 ? id : hkeys[(uint32_t)id & 0x7fffffffu]; }
+  // key -> stored id
+  __device__ __forceinline__ int32_t enc(int key) const {
+    if (hn && ((hbits[(uint32_t)key >> 5] >> ((uint32_t)key & 31u)) & 1u)) return (int32_t)(HOT_TAG | hidx[key]);
+    return key;
+  }
 };
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
@@ -88,7 +106,7 @@ __device__ __forceinline__ void write_row(const DevSlab& s, int slot, int v, uin
   for (int i = lane_id(); i < cnt; i += WAVE) {
     double x = bitsd(rv[i]);
     if (scaled) x *= scale;
-    s.ids[r + i] = rk[i];
+    s.ids[r + i] = s.enc(rk[i]);
     s.sc[r + i] = x;
     const uint64_t b = dbits(x);
     mn = b < mn ? b : mn;
@@ -120,6 +138,20 @@ struct IterArgs {
 };
 
 __device__ __forceinline__ int read_slot(const IterArgs& a, int32_t cx) { return (cx < 0) ? a.sB : a.sA; }
+
+// The hot key set (merge_hot.h): up to a few thousand keys that sit in most successor baskets of
+// the hub sources. A hub's hot keys are accumulated densely by k_hub_hot, its other ("cold") keys
+// go through the staged partition. Membership changes only which engine sums a key, never the
+// result: both keep every key's contributions in successor order.
+struct HotSet {
+  const uint32_t* bits;   // [ceil(n / 32)] membership bitmap (512 KB at RMAT-22: L2-resident)
+  const uint16_t* idx;    // [n] dense index of a member (undefined for other keys)
+  const int32_t* keys;    // [members] key of each index
+  int n;                  // members; 0 = no hot pass
+  __device__ __forceinline__ bool has(int key) const {
+    return n != 0 && ((bits[(uint32_t)key >> 5] >> ((uint32_t)key & 31u)) & 1u);
+  }
+};
 
 // Per-source constants of the two combines (deg > 0 for every merged source):
 //   GRank  acc = {v: 1-d};      acc[k] = fma(s, d/deg, acc[k]);      row = topL(acc)
@@ -186,7 +218,8 @@ __device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt v
   write_row(s, nxt, v, rv, rk, cnt, Lp, false, 1.0);
   const int64_t ro = s.row(cur, v);
   const int olen = s.len[s.lrow(cur, v)];
-  const double d1 = row_norm1(rv, rk, cnt, s.ids + ro, s.sc + ro, olen, hk, hv, mf, 2 * Lp);
+  const double d1 = row_norm1(rv, rk, cnt, s.ids + ro, s.sc + ro, olen, hk, hv, mf, 2 * Lp,
+                              [&](int32_t id) { return s.key(id); });
   if (lane_id() == 0) {
     // maxDiff only grows: skip the contended atomic when a larger value is already published
     const unsigned long long b = (unsigned long long)dbits(d1);

@@ -464,16 +464,17 @@ __device__ __forceinline__ void row_sort_hash(uint64_t* rv, int* rk, int cnt, in
 
 // norm1 between the new row (LDS rv/rk, cnt) and the old row (global ids/scores, olen), with
 // the fixed lane pattern of oracle/grank_oracle.c:norm1_rows. hk/hv: LDS hash of 2*Lp slots,
-// mf: LDS flags (Lp).
+// mf: LDS flags (Lp); dec maps a stored id of the old row to its key.
+template <class Dec>
 __device__ __forceinline__ double row_norm1(const uint64_t* rv, const int* rk, int cnt,
                                             const int* oid, const double* osc, int olen,
-                                            int* hk, int* hv, int* mf, int hsize) {
+                                            int* hk, int* hv, int* mf, int hsize, Dec dec) {
   const uint32_t hmask = (uint32_t)hsize - 1;
   for (int i = lane_id(); i < hsize; i += WAVE) hk[i] = EMPTY;
   for (int j = lane_id(); j < olen; j += WAVE) mf[j] = 0;
   wave_fence();
   for (int j = lane_id(); j < olen; j += WAVE) {
-    const int key = oid[j];
+    const int key = dec(oid[j]);  // the old row's stored id -> key
     uint32_t h = hash32((uint32_t)key) & hmask;
     for (;;) {
       const int prev = atomicCAS(&hk[h], EMPTY, key);

@@ -364,7 +364,7 @@ __device__ __forceinline__ void wg_slab_stream(const WgLds& L, const DevGraph& g
           if (L.wpre[j + step - 1] <= q) j += step;
         const int ex = j > 0 ? L.wpre[j - 1] : 0;
         const int64_t r = s.row(L.wsl[j], L.wu[j]) + (q - ex);
-        kk = s.ids[r];
+        kk = s.key(s.ids[r]);
         ss = s.sc[r];
       }
     };

@@ -80,6 +80,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_cpus():
+    """Host threads this process may run on: the CPU affinity set, capped by a cgroup v2 CPU
+    quota when one is set (a GPU box shares its host between GPUs), and the CPU model name."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = max(1, min(n, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return n, model
+
+
 # ------------------------------------------------------------------------------------------
 # CPU baseline: reference combineMaps on a stratified sample (rank 0, N=1 only)
 def cpu_baseline(g, part, slab, L, damping, iters, threads, budget, seed=0):
@@ -151,6 +174,7 @@ def cpu_baseline(g, part, slab, L, damping, iters, threads, budget, seed=0):
         "value": g.n / (job_ms / 1e3),
         "unit": "source-nodes/s",
         "cores": threads,
+        "cpu_model": host_cpus()[1],
         "kind": "reference",
         "sample": (f"reference grankMultiInternal::combineMaps (header-only/grankMulti.h:230-268, "
                    f"-O3 -march=x86-64-v3) on {len(src)} of {n_act} active sources: {len(strata)} work "
@@ -256,7 +280,8 @@ def main():
     ap.add_argument("--damping", type=float, default=0.85)
     ap.add_argument("--tol", type=float, default=-1.0)
     ap.add_argument("--seed", type=int, default=42)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="cpu_baseline threads (0 = every host CPU this process may use, cgroup quota included)")
     ap.add_argument("--cpu-budget", type=float, default=1.5e9, help="sampled candidates for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=["grank", "mc"], default="grank",
@@ -310,8 +335,8 @@ def main():
             try:
                 slab = plan.fetch_slab()
                 plan.close()
-                cpu = cpu_baseline(g, part, slab, args.L, args.damping, args.iters, args.cpu_threads,
-                                   args.cpu_budget)
+                threads = args.cpu_threads if args.cpu_threads > 0 else host_cpus()[0]
+                cpu = cpu_baseline(g, part, slab, args.L, args.damping, args.iters, threads, args.cpu_budget)
             except Exception as exc:  # reported, never fatal
                 log(f"cpu_baseline failed: {exc!r}")
                 cpu = None

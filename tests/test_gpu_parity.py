@@ -151,6 +151,16 @@ def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "4096", "PPR_SEG_T": "4096"},    # one segment spanning all ranges
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "2048", "PPR_SEG_T": "256"},     # table overflow -> HBM-table path
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "64", "PPR_SEG_WPB": "4"},       # four segment waves per block
+    {"PPR_HOT_N": "0"},                                                     # no hot pass
+    {"PPR_HOT_N": "16", "PPR_HOT_AT": "0"},                                 # small hot set from the init rows
+    {"PPR_HOT_N": "128", "PPR_HOT_AT": "1", "PPR_HOT_STRIDE": "1"},         # ... from every row
+    {"PPR_HOT_N": "16384", "PPR_HOT_AT": "0"},                              # every key hot: no cold records
+    {"PPR_HOT_N": "64", "PPR_HOT_AT": "0", "PPR_HUB_BUDGET": "4096"},       # hot pass over many batches, streams
+    {"PPR_HOT_N": "64", "PPR_HOT_AT": "0", "PPR_HUB_STREAMS": "1"},         # ... on one stream
+    {"PPR_HOT_N": "32", "PPR_HOT_AT": "0", "PPR_HUB_WAVE_T": "256",         # hot pass + cold bucket spills
+     "PPR_HUB_BUCKET": "512"},
+    {"PPR_HOT_N": "64", "PPR_HOT_AT": "0", "PPR_HOT_MAX": "3000"},          # large hubs without a hot pass
+                                                                            # (tagged ids decoded in the partition)
 ])
 def test_gpu_hub_bucket_variants_bit_exact(seg_env, monkeypatch):
     """every hub bucket engine -- staged buckets on one wave each (k_hub_bucket_w), spills to the
@@ -168,3 +178,21 @@ def test_gpu_hub_bucket_variants_bit_exact(seg_env, monkeypatch):
         assert np.array_equal(r.lens, o["lens"])
         assert np.array_equal(r.ids, o["ids"])
         assert np.array_equal(r.scores, o["scores"])
+
+
+def test_gpu_tolerance_stop_beyond_256_iterations():
+    """iterations >= PPR_MAX_ITER_STATS share one maxDiff slot, zeroed per iteration: a tolerance
+    that is first met after iteration 256 stops the run where the oracle stops
+    (include/grank.h:90-94,140)"""
+    n = 100
+    d = {i: [(i + 1) % n] for i in range(n)}
+    csr = ppr.Csr.from_dict(d)
+    part = csr.partitions()
+    full = oracle.grank(csr.row_ptr, csr.col, part, 50, 100, 300, 0.85, -1.0)
+    md = full["max_diff"]
+    tol = float(md[262])  # max(md[i-1], md[i]) < tol first holds a few iterations later
+    o = oracle.grank(csr.row_ptr, csr.col, part, 50, 100, 300, 0.85, tol)
+    assert 256 < o["iterations_run"] < 300
+    r = ppr.grank_csr(csr, 50, 100, 300, 0.85, tol, part=part, device=0)
+    assert r.iterations_run == o["iterations_run"]
+    assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])

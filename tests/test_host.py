@@ -106,3 +106,21 @@ def test_import_edge_csv_reference_order_eat():
     f = load("g4_eat_k50_l100")
     assert np.array_equal(np.array(g.keys), f["z"]["order"])
     assert np.array_equal(g.row_ptr, f["rp"]) and np.array_equal(g.col, f["col"])
+
+
+def test_plan_rejects_candidate_count_overflow():
+    """a source whose candidate count could pass 2^31 - 1 (out-degree * L + 1) is refused at plan
+    creation (the device keeps per-source counts and staging offsets in 32 bits), before any
+    device call"""
+    L = _lib.lib()
+    deg = 1 << 19                    # 2^19 * 4096 + 1 > INT32_MAX
+    n = deg + 1
+    rp = np.zeros(n + 1, dtype=np.int64)
+    rp[1:] = deg                     # node 0 -> every other node
+    col = np.arange(1, n, dtype=np.int32)
+    part = np.zeros(n, dtype=np.uint8)
+    part[1:] = 1
+    c = _lib.csr_struct(rp, col)
+    out = ctypes.c_void_p()
+    assert L.ppr_grank_plan_create(ctypes.byref(c), _lib.ptr(part), 2, 4096, 0.85, None, ctypes.byref(out)) == 11
+    assert L.ppr_mccp2_plan_create(ctypes.byref(c), 2, 4096, 0.85, None, ctypes.byref(out)) == 11
