@@ -222,6 +222,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     // measured 3 % faster than four groups on RMAT-22
     p->hub_bw_ng = e4 ? (atoi(e4) == 8 ? 8 : atoi(e4) == 4 ? 4 : atoi(e4) == 1 ? 1 : 2) : 2;
     p->hub_bw_waves = e5 ? std::max(1, std::min(4, atoi(e5))) : 1;
+    const char* e19 = getenv("PPR_HUB_RANGE");
+    if (e19) p->hub_range = std::max(0, std::min(32, atoi(e19)));
     const char* e6 = getenv("PPR_HUB_SLICE");
     p->hub_slice = std::max<int>(std::max<int>(64, (int)L), e6 ? atoi(e6) : HUB_SLICE);
     const char* e7 = getenv("PPR_HUB_STREAMS");
@@ -298,6 +300,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   hipFuncSetAttribute((const void*)k_hub_bucket_w<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket_w<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket_w<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_range<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_range<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_range<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_hub_range<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_seg<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_bucket, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipFuncSetAttribute((const void*)k_hub_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -564,8 +570,9 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
         const int nsl = ptc > 2 * slice ? (int)((ptc + slice - 1) / slice) : 0;
         // staging offsets are cumulative candidate counts in descriptor order, the same order the
         // device scan walks the concatenated count matrices in: scanned cm = absolute offsets
-        desc[nd_all++] = HubDesc{v, logP, T, (int32_t)need, tw, nsl, -1, 0, b.cm, b.stg, b.pt, b.red, b.ntiles, b.nbuck,
-                                 b.nrt, seg ? b.nseg : -1};
+        desc[nd_all++] = HubDesc{v, logP, T, (int32_t)need, tw, nsl, -1, (int32_t)b.nrange, b.cm, b.stg, b.pt, b.red,
+                                 b.ntiles, b.nbuck, b.nrt, seg ? b.nseg : -1};
+        if (!seg && p->hub_range > 0) b.nrange += (P + p->hub_range - 1) / p->hub_range;
         b.cm += (int64_t)P * T;
         b.stg += seg ? 0 : need - 1;
         b.pt += ptc;
@@ -607,6 +614,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     mx.cm = std::max(mx.cm, b.cm); mx.stg = std::max(mx.stg, b.stg); mx.pt = std::max(mx.pt, b.pt);
     mx.ntiles = std::max(mx.ntiles, b.ntiles); mx.nbuck = std::max(mx.nbuck, b.nbuck);
     mx.nrt = std::max(mx.nrt, b.nrt); mx.red = std::max(mx.red, b.red); mx.nseg = std::max(mx.nseg, b.nseg);
+    mx.nrange = std::max(mx.nrange, b.nrange);
     maxnd = std::max(maxnd, b.d1 - b.d0);
   }
   size_t scan_tmp = 0;
@@ -644,6 +652,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   const size_t o_gl = off;   off = al(off + sizeof(HubTask) * (mx.nbuck + 1));
   const size_t o_cnt = off;  off = al(off + 16);
   const size_t o_sd = off;   off = al(off + 4 * maxnd);
+  const size_t o_rg = off;   off = al(off + sizeof(HubTask) * (mx.nrange + 1));
   const size_t o_bw = off;   off = al(off + sizeof(BucketWork) * mx.nbuck);
   const size_t region = off;
   // two streams only pay when there is a next batch to overlap with
@@ -711,6 +720,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     uint32_t* d_lc = (uint32_t*)(rb + o_cnt);    // [1] spill list length
     BucketWork* d_bw = (BucketWork*)(rb + o_bw);
     uint32_t* d_sd = (uint32_t*)(rb + o_sd);
+    HubTask* d_rg = (HubTask*)(rb + o_rg);
     const size_t nd = b.d1 - b.d0;
     HubDesc* d_desc = d_desc_all + b.d0;
     const int maxP = b.maxP;
@@ -720,7 +730,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     HIP_OK(hipMemsetAsync(d_tau, 0, 8 * nd, st));
     HIP_OK(hipMemsetAsync(d_oflag, 0, 4 * nd, st));
     HIP_OK(hipMemsetAsync(d_lc, 0, 8, st));
-    hipLaunchKernelGGL(k_hub_expand, dim3((unsigned)nd), dim3(256), 0, st, d_desc, d_tile, d_buck, d_rt, d_sg);
+    hipLaunchKernelGGL(k_hub_expand, dim3((unsigned)nd), dim3(256), 0, st, d_desc, d_tile, d_buck, d_rt, d_sg, d_rg,
+                       p->hub_range);
     HIP_OK(hipGetLastError());
     const int64_t ntiles = b.ntiles;
     const int64_t nbuck = b.nbuck;
@@ -740,7 +751,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     }
     // a batch of sources without successors (init of dangling nodes) has no tiles but still has
     // buckets: the one holding the source's own seed entry
-    if (nbuck) {
+    if (nbuck && p->hub_range == 0) {
       hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, a, H, d_desc, d_buck,
                          nbuck, d_cmx, d_sd, d_tau, d_tau_hot, d_bw);
       HIP_OK(hipGetLastError());
@@ -763,7 +774,25 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       const int wpb = p->hub_bw_waves;
       const int64_t blocks = (nbuck + wpb - 1) / wpb;
       const dim3 grid((unsigned)blocks), blk(64 * wpb);
-      if (p->hub_bw_ng == 1)
+      if (p->hub_range > 0) {
+        const dim3 rgrid((unsigned)((b.nrange + wpb - 1) / wpb));
+        if (p->hub_bw_ng == 1)
+          hipLaunchKernelGGL(k_hub_range<1>, rgrid, blk, p->hub_lds_wave, sb, g, s, a, H, d_desc, d_rg, b.nrange,
+                             p->hub_range, d_cmx, d_sd, d_tau, d_tau_hot, d_st, d_pk, d_ps, d_pc, d_gl, d_lc + 1,
+                             p->hub_wave_t, p->hub_bw_budget);
+        else if (p->hub_bw_ng == 8)
+          hipLaunchKernelGGL(k_hub_range<8>, rgrid, blk, p->hub_lds_wave, sb, g, s, a, H, d_desc, d_rg, b.nrange,
+                             p->hub_range, d_cmx, d_sd, d_tau, d_tau_hot, d_st, d_pk, d_ps, d_pc, d_gl, d_lc + 1,
+                             p->hub_wave_t, p->hub_bw_budget);
+        else if (p->hub_bw_ng == 4)
+          hipLaunchKernelGGL(k_hub_range<4>, rgrid, blk, p->hub_lds_wave, sb, g, s, a, H, d_desc, d_rg, b.nrange,
+                             p->hub_range, d_cmx, d_sd, d_tau, d_tau_hot, d_st, d_pk, d_ps, d_pc, d_gl, d_lc + 1,
+                             p->hub_wave_t, p->hub_bw_budget);
+        else
+          hipLaunchKernelGGL(k_hub_range<2>, rgrid, blk, p->hub_lds_wave, sb, g, s, a, H, d_desc, d_rg, b.nrange,
+                             p->hub_range, d_cmx, d_sd, d_tau, d_tau_hot, d_st, d_pk, d_ps, d_pc, d_gl, d_lc + 1,
+                             p->hub_wave_t, p->hub_bw_budget);
+      } else if (p->hub_bw_ng == 1)
         hipLaunchKernelGGL(k_hub_bucket_w<1>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
                            d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget);
       else if (p->hub_bw_ng == 2)

@@ -52,7 +52,7 @@ struct HubDesc {
   int32_t nsl;     // k_hub_reduce slices reserved (upper bound from P * L appended entries)
   int32_t hot;     // >= 0: the hot pass (k_hub_hot) accumulates the source's hot keys into hot list
                    // `hot`, and the partition carries only its cold keys; -1: no hot pass
-  int32_t pad;
+  int32_t rg_off;  // first bucket-range task of this source in its batch (k_hub_range)
   int64_t cm_off;  // count matrix (P*T ints; after the scan: absolute staging offsets)
   int64_t st_off;  // staging (need-1 keys / scores)
   int64_t pt_off;  // appended bucket results (<= P*L entries, pt_cnt[desc] of them used)
@@ -79,13 +79,15 @@ __device__ __forceinline__ void hub_bucket_range(const HubDesc& d, const int32_t
 struct HubTask { int32_t d; int32_t x; };   // (descriptor, tile or bucket)
 
 __global__ void __launch_bounds__(256) k_hub_expand(const HubDesc* desc, HubTask* tiles, HubTask* buckets,
-                                                    HubTask* rts, HubTask* segs) {
+                                                    HubTask* rts, HubTask* segs, HubTask* ranges, int krange) {
   const int d = blockIdx.x;
   const HubDesc D = desc[d];
   const int P = 1 << D.logP;
   for (int t = threadIdx.x; t < D.T; t += blockDim.x) tiles[D.tile_off + t] = HubTask{d, t};
   if (D.sg_off >= 0) {
     for (int b = threadIdx.x; b < P; b += blockDim.x) segs[D.sg_off + b] = HubTask{d, b};
+  } else if (krange > 0) {
+    for (int r = threadIdx.x; r * krange < P; r += blockDim.x) ranges[D.rg_off + r] = HubTask{d, r * krange};
   } else {
     for (int b = threadIdx.x; b < P; b += blockDim.x) buckets[D.buck_off + b] = HubTask{d, b};
   }
@@ -301,6 +303,14 @@ struct BucketWave {
     wave_fence();
   }
 
+  // an empty table again (the chunk counters are all-zero after every chunk)
+  __device__ __forceinline__ void reset(int T_) {
+    for (int i = lane_id(); i < T_; i += WAVE) t.keys[i] = EMPTY;
+    fill = 0;
+    overflow = false;
+    wave_fence();
+  }
+
   __device__ __forceinline__ uint32_t slot_of(int key) const {
     return (uint32_t)(((unsigned long long)hash32((uint32_t)key) * (uint32_t)T) >> 32);
   }
@@ -449,6 +459,83 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
     atomicAdd(&a.diag[32 + bin], (unsigned long long)((long long)clock64() - t_start));
   }
   B.emit(W.tau, s.L, &pt_cnt[W.d], pt_key + W.pt_off, pt_sc + W.pt_off, a);
+}
+
+// Bucket ranges: one wave per range of krange consecutive buckets of one source (HubTask (d, x0)),
+// its LDS table reused bucket after bucket. A bucket wave pays a few dependent global round
+// trips that its ~100-300 records cannot hide (its work record, then its records, then the
+// returning atomic of its emission); a range pays the first two once: the bucket bounds of the
+// whole range come from one load of the scanned count matrix, and the records stream through
+// the range with the next chunk -- the next bucket's first chunk included -- in flight while the
+// current one is accumulated or emitted. Per bucket the semantics are k_hub_bucket_w's: seed,
+// ordered accumulation, spill to k_hub_bucket on overflow, keys >= tau (at most L) appended.
+template <int NG>
+__global__ void __launch_bounds__(256) k_hub_range(DevGraph g, DevSlab s, IterArgs a, HotSet H, const HubDesc* desc,
+                                                   const HubTask* tasks, int64_t ntasks, int krange, const int32_t* cm,
+                                                   const uint32_t* staged, const unsigned long long* tau_b,
+                                                   const unsigned long long* tau_hot, const HubRec* st,
+                                                   int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
+                                                   HubTask* spill, uint32_t* spill_cnt, int T, int budget) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int wv = threadIdx.x >> 6;
+  const int l = lane_id();
+  const int64_t cur = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (cur >= ntasks) return;
+  const HubTask tk = tasks[cur];
+  const HubDesc d = desc[tk.d];
+  const int P = 1 << d.logP;
+  const int x0 = tk.x, x1 = min(P, x0 + krange);
+  // lane i: staging start of bucket x0 + i (lane x1 - x0: the end of the last one)
+  int64_t bs = d.st_off;
+  if (d.T > 0 && l <= x1 - x0) {
+    const int x = x0 + l;
+    bs = x < P ? (int64_t)cm[d.cm_off + (int64_t)x * d.T] : (int64_t)cm[d.cm_off] + (int64_t)staged[tk.d];
+  }
+  const int v = d.v;
+  const int64_t deg = g.rp[v + 1] - g.rp[v];
+  const double factor = merge_factor(a, deg);
+  const double tau = hub_tau(d, tau_b, tk.d, tau_hot, factor);
+  const int seed_x = (d.hot >= 0 && H.has(v)) ? -1 : (int)hub_digit(v, d.logP);
+  BucketWave B;
+  unsigned char* base = smem + (size_t)wv * hub_wave_lds(T, NG);
+  B.setup(base, T, NG, a.lds_rank != 0, budget);
+  auto bstart = [&](int x) { return (int64_t)__shfl((long long)bs, x - x0); };
+  bool cv[NG], nv[NG];
+  int kk[NG], nk[NG];
+  double cs[NG], ns[NG];
+  auto load = [&](int x, int g0, bool (&vv)[NG], int (&kv)[NG], double (&sv)[NG]) {
+    const int64_t b0 = bstart(x), nb = bstart(x + 1) - b0;
+#pragma unroll
+    for (int k = 0; k < NG; k++) {
+      const int q = g0 + k * WAVE + l;
+      vv[k] = q < nb;
+      const HubRec r = vv[k] ? st[b0 + q] : HubRec{};
+      kv[k] = rec_key(r);
+      sv[k] = rec_sc(r);
+    }
+  };
+  int x = x0, g0 = 0;
+  load(x, 0, nv, nk, ns);
+  while (x < x1) {
+#pragma unroll
+    for (int k = 0; k < NG; k++) { cv[k] = nv[k]; kk[k] = nk[k]; cs[k] = ns[k]; }
+    const int nb = (int)(bstart(x + 1) - bstart(x));
+    int nx = x, ng0 = g0 + NG * WAVE;
+    if (ng0 >= nb) { nx = x + 1; ng0 = 0; }
+    if (nx < x1) load(nx, ng0, nv, nk, ns);  // in flight while this chunk is used
+    if (g0 == 0 && x == seed_x) B.seed(v, self_seed(a, deg));
+    if (!B.overflow) B.chunk<NG>(cv, kk, cs, factor);
+    if (nx != x) {  // bucket x complete
+      if (B.overflow) {
+        if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = HubTask{tk.d, x}; }
+      } else {
+        B.emit(tau, s.L, &pt_cnt[tk.d], pt_key + d.pt_off, pt_sc + d.pt_off, a);
+      }
+      if (nx < x1) B.reset(T);
+    }
+    x = nx;
+    g0 = ng0;
+  }
 }
 
 // Segmented buckets (no partition pass): basket rows are stored in hash_b order with a range

@@ -94,6 +94,8 @@ struct ppr_plan {
   int seg_bucket = 256, seg_t = 512, seg_wpb = 1;
   int hub_bw_ng = 2;               // PPR_BW_NG: groups per chunk (1, 2, 4 or 8)
   int hub_bw_waves = 1;            // PPR_BW_WAVES: waves per block of k_hub_bucket_w
+  int hub_range = 0;               // PPR_HUB_RANGE: buckets per k_hub_range wave (0 = k_hub_bucket_w, one each;
+                                   // ranges measured no faster: the bucket stage is LDS-latency bound)
   int hub_slice = 8192;            // PPR_HUB_SLICE: k_hub_reduce slice (>= L)
   // source sharding (ppr_grank_plan_comm_init / ppr_grank_plan_run_sharded)
   ncclComm_t comm = nullptr;

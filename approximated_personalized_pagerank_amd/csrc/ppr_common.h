@@ -41,7 +41,7 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
 }
 
 // one batch of the hub pipeline (host planning): descriptor range and the batch's totals
-struct HubBatch { size_t d0, d1; int64_t cm, stg, pt, ntiles, nbuck, nrt, red, nseg; int maxP; };
+struct HubBatch { size_t d0, d1; int64_t cm, stg, pt, ntiles, nbuck, nrt, red, nseg; int maxP; int64_t nrange = 0; };
 
 struct DevGraph {
   const int64_t* rp;

@@ -130,7 +130,7 @@ class MccpPlan:
         lens = np.zeros(n, dtype=np.int32)
         _lib.check(_lib.lib().ppr_plan_fetch_slot(self._p, slot, _lib.ptr(ids), _lib.ptr(sc), _lib.ptr(lens)),
                    "fetch_slot")
-        for v in range(n):
-            ids[v, lens[v]:] = -1
-            sc[v, lens[v]:] = 0.0
+        pad = np.arange(L)[None, :] >= lens[:, None]  # entries past a row's length are stale
+        ids[pad] = -1
+        sc[pad] = 0.0
         return ids, sc, lens

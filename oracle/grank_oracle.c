@@ -335,3 +335,49 @@ int oracle_step(int64_t n, const int64_t* rp, const int32_t* col, int32_t L, dou
   *maxdiff = md;
   return 0;
 }
+
+/* ---- maxDiff of a whole iteration (the sampled-scale GPU tests): the norm1_stored pattern of
+ * every listed source, old row -> new row, in O(L log L) per row: both rows sorted by hash_b (the
+ * stored order; hash_b is a bijection, so equal hashes are equal keys) and matched by a merge,
+ * then the same 64 lane partials as norm1_rows (new entries by position, then the old entries
+ * the new row lacks by position) and the same butterfly. Rows: stride L, first len entries. */
+static int cmp_hash_ent(const void* a, const void* b) { return cmp_hash(a, b); }
+
+int oracle_norm1_max(int32_t L, const int32_t* list, int64_t count, const int32_t* o_ids, const double* o_sc,
+                     const int32_t* o_len, const int32_t* n_ids, const double* n_sc, const int32_t* n_len,
+                     double* out_max) {
+  ent_t* ne = (ent_t*)malloc(sizeof(ent_t) * (size_t)(L + 1));
+  ent_t* oe = (ent_t*)malloc(sizeof(ent_t) * (size_t)(L + 1));
+  uint8_t* hit = (uint8_t*)malloc((size_t)(L + 1));
+  if (!ne || !oe || !hit) return -1;
+  double md = 0.0;
+  for (int64_t q = 0; q < count; q++) {
+    const int64_t v = list[q];
+    const int32_t nl = n_len[v], ol = o_len[v];
+    for (int32_t i = 0; i < nl; i++) { ne[i].key = n_ids[v * L + i]; ne[i].sc = n_sc[v * L + i]; }
+    for (int32_t j = 0; j < ol; j++) { oe[j].key = o_ids[v * L + j]; oe[j].sc = o_sc[v * L + j]; hit[j] = 0; }
+    qsort(ne, (size_t)nl, sizeof(ent_t), cmp_hash_ent);
+    qsort(oe, (size_t)ol, sizeof(ent_t), cmp_hash_ent);
+    double p[64];
+    for (int l = 0; l < 64; l++) p[l] = 0.0;
+    int32_t j = 0;
+    for (int32_t i = 0; i < nl; i++) {
+      const uint32_t hn = hash_b((uint32_t)ne[i].key);
+      while (j < ol && hash_b((uint32_t)oe[j].key) < hn) j++;
+      double o = 0.0;
+      if (j < ol && oe[j].key == ne[i].key) { o = oe[j].sc; hit[j] = 1; }
+      p[i & 63] += fabs(ne[i].sc - o);
+    }
+    for (int32_t k = 0; k < ol; k++)
+      if (!hit[k]) p[k & 63] += oe[k].sc;
+    for (int off = 32; off >= 1; off >>= 1) {
+      double t[64];
+      for (int l = 0; l < 64; l++) t[l] = p[l] + p[l ^ off];
+      memcpy(p, t, sizeof(p));
+    }
+    if (p[0] > md) md = p[0];
+  }
+  free(ne); free(oe); free(hit);
+  *out_max = md;
+  return 0;
+}

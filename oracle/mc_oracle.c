@@ -386,3 +386,56 @@ int oracle_mccp2(int64_t n, const int64_t* rp, const int32_t* col, int32_t K, in
   free(haswalk); free(cnt); free(adm); free(rrc); free(acc); free(touched); free(ent);
   return 0;
 }
+
+/* ---- one combine step of MCCompletePathV2 for listed sources (the sampled RMAT-22 GPU test):
+ * for v, succ s contributes its final basket (f_*) when pos[s] < pos[v], else its walk basket
+ * (w_*), exactly as oracle_mccp2's sweep does (include/mccompletepathv2.h:211-249):
+ * map = {v: 1/f}; map[k] += x over successors in CSR order; keepTop(L); *= f. Output rows
+ * (stride L) by (scaled score desc, key asc). */
+int oracle_mc_combine(int64_t n, const int64_t* rp, const int32_t* col, const int32_t* pos, int32_t L, double d,
+                      const int32_t* f_ids, const double* f_sc, const int32_t* f_len,
+                      const int32_t* w_ids, const double* w_sc, const int32_t* w_len,
+                      const int32_t* list, int64_t count, int32_t* out_ids, double* out_sc, int32_t* out_len) {
+  double* acc = (double*)calloc((size_t)n, sizeof(double));
+  uint8_t* touched = (uint8_t*)calloc((size_t)n, 1);
+  int64_t cap = 16;
+  ment_t* ent = (ment_t*)malloc(sizeof(ment_t) * (size_t)cap);
+  if (!acc || !touched || !ent) return -1;
+  for (int64_t q = 0; q < count; q++) {
+    const int32_t v = list[q];
+    const int64_t deg = rp[v + 1] - rp[v];
+    if (deg == 0) { out_ids[q * L] = v; out_sc[q * L] = 1.0; out_len[q] = 1; continue; }
+    const double f = d / (double)deg;
+    int64_t need = 1;
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) need += pos[col[e]] < pos[v] ? f_len[col[e]] : w_len[col[e]];
+    if (need > cap) { free(ent); cap = need; ent = (ment_t*)malloc(sizeof(ment_t) * (size_t)cap); if (!ent) return -1; }
+    int64_t U = 0;
+    ent[U++].key = v;
+    touched[v] = 1;
+    acc[v] = 1.0 / f;
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
+      const int32_t s = col[e];
+      const int fin = pos[s] < pos[v];
+      const int32_t* rk = (fin ? f_ids : w_ids) + (int64_t)s * L;
+      const double* rs = (fin ? f_sc : w_sc) + (int64_t)s * L;
+      const int32_t rl = fin ? f_len[s] : w_len[s];
+      for (int32_t t = 0; t < rl; t++) {
+        const int32_t k = rk[t];
+        if (!touched[k]) { touched[k] = 1; acc[k] = 0.0; ent[U++].key = k; }
+        acc[k] = acc[k] + rs[t];
+      }
+    }
+    for (int64_t t = 0; t < U; t++) { ent[t].sc = acc[ent[t].key]; touched[ent[t].key] = 0; }
+    qsort(ent, (size_t)U, sizeof(ment_t), cmp_ment);
+    const int64_t keep = U < L ? U : L;
+    for (int64_t t = 0; t < keep; t++) { ent[t].sc = ent[t].sc * f; }
+    qsort(ent, (size_t)keep, sizeof(ment_t), cmp_ment);  /* scaling can tie two scores */
+    for (int32_t t = 0; t < L; t++) {
+      out_ids[q * L + t] = t < keep ? ent[t].key : -1;
+      out_sc[q * L + t] = t < keep ? ent[t].sc : 0.0;
+    }
+    out_len[q] = (int32_t)keep;
+  }
+  free(acc); free(touched); free(ent);
+  return 0;
+}

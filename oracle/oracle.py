@@ -48,6 +48,12 @@ def lib():
         L.oracle_mccp2.argtypes = [ctypes.c_int64, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
                                    ctypes.c_double, ctypes.c_uint64, vp, vp, vp, vp, vp, vp]
         L.oracle_mccp2.restype = ctypes.c_int
+        L.oracle_norm1_max.argtypes = [ctypes.c_int32, vp, ctypes.c_int64, vp, vp, vp, vp, vp, vp,
+                                       ctypes.POINTER(ctypes.c_double)]
+        L.oracle_norm1_max.restype = ctypes.c_int
+        L.oracle_mc_combine.argtypes = [ctypes.c_int64, vp, vp, vp, ctypes.c_int32, ctypes.c_double, vp, vp, vp,
+                                        vp, vp, vp, vp, ctypes.c_int64, vp, vp, vp]
+        L.oracle_mc_combine.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -126,6 +132,61 @@ def mccp2(row_ptr, col, K, L, walks, damping, seed, want_walks=False):
     if want_walks:
         out.update(walk_ids=w_ids, walk_scores=w_sc, walk_lens=w_len)
     return out
+
+
+def step(row_ptr, col, L, damping, slab, lst):
+    """One GRank Jacobi step (oracle_step) for the sources `lst` from the slab (ids [n,L],
+    scores [n,L], lens [n]); returns (ids [len(lst),L], scores, lens, max norm1 over lst), rows by
+    (score desc, id asc)."""
+    ids, sc, ln = (np.ascontiguousarray(a) for a in slab)
+    n = len(ln)
+    lst = np.ascontiguousarray(lst, dtype=np.int32)
+    nids = np.full((n, L), -1, dtype=np.int32)
+    nsc = np.zeros((n, L), dtype=np.float64)
+    nlen = np.zeros(n, dtype=np.int32)
+    md = ctypes.c_double(0.0)
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+    cl = np.ascontiguousarray(col, dtype=np.int32)
+    if len(lst):
+        assert lib().oracle_step(n, _p(rp), _p(cl), L, damping, _p(ids), _p(sc), _p(ln), _p(lst), len(lst),
+                                 _p(nids), _p(nsc), _p(nlen), ctypes.byref(md)) == 0
+    out_ids, out_sc, out_len = nids[lst], nsc[lst], nlen[lst]
+    for r in range(len(lst)):
+        out_ids[r, out_len[r]:] = -1
+        out_sc[r, out_len[r]:] = 0.0
+    return out_ids, out_sc, out_len, md.value
+
+
+def norm1_max(L, lst, old, new):
+    """max over `lst` of norm1(old row, new row) in the engine's summation pattern
+    (oracle_norm1_max: the maxDiff a whole iteration folds)."""
+    lst = np.ascontiguousarray(lst, dtype=np.int32)
+    o = [np.ascontiguousarray(a) for a in old]
+    w = [np.ascontiguousarray(a) for a in new]
+    out = ctypes.c_double(0.0)
+    assert lib().oracle_norm1_max(L, _p(lst), len(lst), _p(o[0]), _p(o[1]), _p(o[2]), _p(w[0]), _p(w[1]),
+                                  _p(w[2]), ctypes.byref(out)) == 0
+    return out.value
+
+
+def mc_combine(row_ptr, col, pos, L, damping, final, walk, lst):
+    """One MCCompletePathV2 combine step (oracle_mc_combine) for the sources `lst`: successor rows
+    come from `final` (ids, scores, lens; [n,L]) when it precedes the source in execution order
+    (pos = position in it), else from `walk`. Returns rows (ids, scores, lens) by (score desc, id asc)."""
+    n = len(row_ptr) - 1
+    lst = np.ascontiguousarray(lst, dtype=np.int32)
+    f = [np.ascontiguousarray(a) for a in final]
+    w = [np.ascontiguousarray(a) for a in walk]
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+    cl = np.ascontiguousarray(col, dtype=np.int32)
+    ps = np.ascontiguousarray(pos, dtype=np.int32)
+    ids = np.full((len(lst), L), -1, dtype=np.int32)
+    sc = np.zeros((len(lst), L), dtype=np.float64)
+    ln = np.zeros(len(lst), dtype=np.int32)
+    if len(lst):
+        assert lib().oracle_mc_combine(n, _p(rp), _p(cl), _p(ps), L, damping, _p(f[0]), _p(f[1]), _p(f[2]), _p(w[0]),
+                                       _p(w[1]), _p(w[2]), _p(lst), len(lst), _p(ids), _p(sc), _p(ln)) == 0
+    return ids, sc, ln
 
 
 def ref_available() -> bool:

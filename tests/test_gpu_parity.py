@@ -151,6 +151,10 @@ def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "4096", "PPR_SEG_T": "4096"},    # one segment spanning all ranges
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "2048", "PPR_SEG_T": "256"},     # table overflow -> HBM-table path
     {"PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "64", "PPR_SEG_WPB": "4"},       # four segment waves per block
+    {"PPR_HUB_RANGE": "0"},                                                 # one bucket per wave (k_hub_bucket_w)
+    {"PPR_HUB_RANGE": "1", "PPR_HUB_BUDGET": "4096"},                       # one-bucket ranges over many batches
+    {"PPR_HUB_RANGE": "3", "PPR_HUB_BUCKET": "64"},                         # ranges ending mid-source, small buckets
+    {"PPR_HUB_RANGE": "32", "PPR_HUB_WAVE_T": "256", "PPR_HUB_BUCKET": "512"},  # long ranges with spills
     {"PPR_HOT_N": "0"},                                                     # no hot pass
     {"PPR_HOT_N": "16", "PPR_HOT_AT": "0"},                                 # small hot set from the init rows
     {"PPR_HOT_N": "128", "PPR_HOT_AT": "1", "PPR_HOT_STRIDE": "1"},         # ... from every row
