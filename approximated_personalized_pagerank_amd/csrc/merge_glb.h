@@ -111,7 +111,8 @@ __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArg
 
 // ---------------------------------------------------------------------------------------------
 // final top-K (include/grank.h:143-147): the stored row is in hash order, so each wave loads it
-// into LDS, sorts it by (score desc, id asc) and writes the first min(K, len) entries
+// into LDS, keeps its top-K by the top-L rule (score desc, tie_w desc) and writes them by (score
+// desc, id asc)
 __global__ void __launch_bounds__(256) k_topk(DevSlab s, const uint8_t* part, int sA, int sB, int K, int Lp,
                                               int32_t* oid, double* osc, int32_t* olen) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -126,7 +127,13 @@ __global__ void __launch_bounds__(256) k_topk(DevSlab s, const uint8_t* part, in
   const int64_t r = s.row(sl, v);
   for (int i = lane_id(); i < len; i += WAVE) { rv[i] = dbits(s.sc[r + i]); rk[i] = s.key(s.ids[r + i]); }
   wave_fence();
-  row_sort(rv, rk, len, Lp);
+  if (len > K) {
+    // the K kept by the top-L tie rule (keepTop(K), include/grank.h:143-147), then output order
+    row_sort(rv, rk, len, Lp, true, tie_salt((int)v));
+    row_sort(rv, rk, K, Lp);
+  } else {
+    row_sort(rv, rk, len, Lp);
+  }
   for (int i = lane_id(); i < K; i += WAVE) {
     oid[v * K + i] = i < k ? rk[i] : -1;
     osc[v * K + i] = i < k ? bitsd(rv[i]) : 0.0;

@@ -119,14 +119,15 @@ __global__ void __launch_bounds__(64) k_hub_hot(DevGraph g, DevSlab s, IterArgs 
     }
     cnt = U;
   } else {
-    const SelCrit c = select_top(U, Lw, [&](int i) { return s.hkeys[ck[i]]; }, [&](int i) { return acc[i]; }, hist);
+    const uint32_t ts = tie_salt(tk.v);
+    const SelCrit c = select_top(U, Lw, [&](int i) { return s.hkeys[ck[i]]; }, [&](int i) { return acc[i]; }, hist, ts);
     int pos0 = 0;
     for (int i0 = 0; i0 < U; i0 += WAVE) {
       const int i = i0 + l;
       bool sel = false;
       int k = 0;
       double x = 0.0;
-      if (i < U) { k = s.hkeys[ck[i]]; x = acc[i]; sel = sel_test(c, dbits(x), (uint32_t)~k); }
+      if (i < U) { k = s.hkeys[ck[i]]; x = acc[i]; sel = sel_test(c, dbits(x), tie_w(k, ts)); }
       const uint64_t m = __ballot(sel);
       if (sel) {
         const int pos = pos0 + __popcll(m & lanemask_lt());
@@ -174,7 +175,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_join(DevSlab s, IterArgs a, 
   const int32_t* hk = hot_key + (int64_t)tk.h * Lw;
   const double* hs = hot_sc + (int64_t)tk.h * Lw;
   const int cnt = hub_select_lds(L, n + nh, Lw, [&](int i) { return i < n ? ck[i] : hk[i - n]; },
-                                 [&](int i) { return i < n ? cs[i] : hs[i - n]; });
+                                 [&](int i) { return i < n ? cs[i] : hs[i - n]; }, tie_salt(tk.v));
   if ((threadIdx.x >> 6) == 0) {
     const uint64_t* rv = L.rv;
     const int* rk = L.rk;

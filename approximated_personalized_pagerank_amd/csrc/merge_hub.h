@@ -228,6 +228,8 @@ struct BucketWork {
   int32_t x;        // bucket (digit)
   int32_t seed;     // the source id when this bucket holds the source's own key, else -1
   double factor, tau, selfval;
+  uint32_t ts;      // tie salt of the source (top-L ties, ppr_device.h)
+  int32_t pad;
 };
 
 // pruning bound of a source's buckets: the larger of tau (full successor rows) and, once the hot
@@ -264,6 +266,8 @@ __global__ void __launch_bounds__(256) k_hub_prep(DevGraph g, IterArgs a, HotSet
   w.factor = merge_factor(a, deg);
   w.tau = hub_tau(d, tau_b, tk.d, tau_hot, w.factor);
   w.selfval = self_seed(a, deg);
+  w.ts = tie_salt(d.v);
+  w.pad = 0;
   bw[i] = w;
 }
 
@@ -364,9 +368,9 @@ struct BucketWave {
     chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor, ordered);
   }
 
-  // keys >= tau (at most L by (score desc, id asc)) appended to the source's list
+  // keys >= tau (at most L by (score desc, tie_w desc)) appended to the source's list
   __device__ __forceinline__ void emit(double tau, int Lw, uint32_t* pt_cnt_d, int32_t* pt_key, double* pt_sc,
-                                       const IterArgs& a) {
+                                       const IterArgs& a, uint32_t ts) {
     const int l = lane_id();
     // compact the occupied slots that can still reach the top-L (value >= tau) to the front, in
     // one pass (writes land at or below the slots already read)
@@ -401,12 +405,12 @@ struct BucketWave {
     }
     const int* keys = t.keys;
     const double* acc = t.acc;
-    const SelCrit c = select_top(U, Lw, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, hist);
+    const SelCrit c = select_top(U, Lw, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, hist, ts);
     int pos0 = 0;
     for (int i0 = 0; i0 < U; i0 += WAVE) {
       const int i = i0 + l;
       bool sel = false;
-      if (i < U) sel = sel_test(c, dbits(acc[i]), (uint32_t)~keys[i]);
+      if (i < U) sel = sel_test(c, dbits(acc[i]), tie_w(keys[i], ts));
       const uint64_t m = __ballot(sel);
       if (sel) { const int pos = pos0 + __popcll(m & lanemask_lt()); ok[pos] = keys[i]; os[pos] = acc[i]; }
       pos0 += __popcll(m);
@@ -458,7 +462,7 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
     atomicAdd(&a.diag[bin], 1ull);
     atomicAdd(&a.diag[32 + bin], (unsigned long long)((long long)clock64() - t_start));
   }
-  B.emit(W.tau, s.L, &pt_cnt[W.d], pt_key + W.pt_off, pt_sc + W.pt_off, a);
+  B.emit(W.tau, s.L, &pt_cnt[W.d], pt_key + W.pt_off, pt_sc + W.pt_off, a, W.ts);
 }
 
 // Bucket ranges: one wave per range of krange consecutive buckets of one source (HubTask (d, x0)),
@@ -529,7 +533,7 @@ __global__ void __launch_bounds__(256) k_hub_range(DevGraph g, DevSlab s, IterAr
       if (B.overflow) {
         if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = HubTask{tk.d, x}; }
       } else {
-        B.emit(tau, s.L, &pt_cnt[tk.d], pt_key + d.pt_off, pt_sc + d.pt_off, a);
+        B.emit(tau, s.L, &pt_cnt[tk.d], pt_key + d.pt_off, pt_sc + d.pt_off, a, tie_salt(v));
       }
       if (nx < x1) B.reset(T);
     }
@@ -648,7 +652,7 @@ __global__ void __launch_bounds__(256) k_hub_seg(DevGraph g, DevSlab s, IterArgs
 #pragma unroll
   for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
   const double tau = mb ? bitsd(mb) * factor : 0.0;
-  B.emit(tau, s.L, &pt_cnt[tk.d], pt_key + d.pt_off, pt_sc + d.pt_off, a);
+  B.emit(tau, s.L, &pt_cnt[tk.d], pt_key + d.pt_off, pt_sc + d.pt_off, a, tie_salt(v));
   if (dg) {
     lap(4);
     if (l == 0) {
@@ -786,10 +790,11 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_reduce(DevSlab s, const HubD
   }
   if (threadIdx.x == 0) L.misc[M_PLEN] = 0;
   __syncthreads();
+  const uint32_t ts = tie_salt(d.v);
   const SelCrit c = wg_select_top(L, n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; },
-                                  [&](int) { return true; });
+                                  [&](int) { return true; }, ts);
   for (int i = threadIdx.x; i < n; i += WG_THREADS) {
-    if (sel_test(c, dbits(pv[i]), (uint32_t)~pk[i])) {
+    if (sel_test(c, dbits(pv[i]), tie_w(pk[i], ts))) {
       const int pos = atomicAdd(&L.misc[M_PLEN], 1);
       ok[pos] = pk[i];
       os[pos] = pv[i];
@@ -797,10 +802,11 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_reduce(DevSlab s, const HubD
   }
 }
 
-// top-L by (score desc, id asc) of `total` entries (keyat / valat) into L.rv / L.rk, in no
+// top-L by (score desc, tie_w desc) of `total` entries (keyat / valat) into L.rv / L.rk, in no
 // particular order; returns their count (every thread of the workgroup)
 template <class KeyAt, class ValAt>
-__device__ __forceinline__ int hub_select_lds(const WgLds& L, int total, int Lw, KeyAt keyat, ValAt valat) {
+__device__ __forceinline__ int hub_select_lds(const WgLds& L, int total, int Lw, KeyAt keyat, ValAt valat,
+                                              uint32_t ts) {
   auto occ = [&](int) { return true; };
   if (threadIdx.x == 0) L.misc[M_PLEN] = 0;
   __syncthreads();
@@ -811,11 +817,11 @@ __device__ __forceinline__ int hub_select_lds(const WgLds& L, int total, int Lw,
       L.rk[pos] = keyat(i);
     }
   } else {
-    const SelCrit c = wg_select_top(L, total, Lw, keyat, valat, occ);
+    const SelCrit c = wg_select_top(L, total, Lw, keyat, valat, occ, ts);
     for (int i = threadIdx.x; i < total; i += WG_THREADS) {
       const double x = valat(i);
       const int k = keyat(i);
-      if (sel_test(c, dbits(x), (uint32_t)~k)) {
+      if (sel_test(c, dbits(x), tie_w(k, ts))) {
         const int pos = atomicAdd(&L.misc[M_PLEN], 1);
         L.rv[pos] = dbits(x);
         L.rk[pos] = k;
@@ -855,7 +861,8 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a,
     pk = red_key + d.red;
     pv = red_sc + d.red;
   }
-  const int cnt = hub_select_lds(L, n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; });
+  const int cnt = hub_select_lds(L, n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; },
+                                 tie_salt(d.v));
   if (d.hot >= 0) {
     int32_t* ok = cold_key + (int64_t)d.hot * Lw;
     double* os = cold_sc + (int64_t)d.hot * Lw;

@@ -184,14 +184,15 @@ __device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt v
     for (int i = lane_id(); i < U; i += WAVE) { rv[i] = dbits(valat(i)); rk[i] = keyat(i); }
     cnt = U;
   } else {
-    const SelCrit c = select_top(U, L, keyat, valat, hist);
+    const uint32_t ts = tie_salt(v);
+    const SelCrit c = select_top(U, L, keyat, valat, hist, ts);
     int base = 0;
     for (int i0 = 0; i0 < U; i0 += WAVE) {
       const int i = i0 + lane_id();
       bool sel = false;
       uint64_t vb = 0;
       int key = 0;
-      if (i < U) { key = keyat(i); vb = dbits(valat(i)); sel = sel_test(c, vb, (uint32_t)~key); }
+      if (i < U) { key = keyat(i); vb = dbits(valat(i)); sel = sel_test(c, vb, tie_w(key, ts)); }
       const uint64_t m = __ballot(sel);
       if (sel) { const int pos = base + __popcll(m & lanemask_lt()); rv[pos] = vb; rk[pos] = key; }
       base += __popcll(m);

@@ -42,6 +42,18 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
 // (a bijection of the 32-bit id space, so distinct keys never tie)
 __device__ __forceinline__ uint32_t hash_b(uint32_t x) { return hash32(x ^ 0x9e3779b9u); }
 
+// Ties at a top-L cut. The reference leaves them to its unordered_map order + nth_element
+// (include/internal/pprInternal.h:115-119): an accident of each map's insertion history, so
+// different rows resolve ties differently. A single global order (say by id) instead makes every
+// row drop the same keys, and the loss compounds through later iterations (RMAT-12 K16/L32: top-K
+// Jaccard vs exact PPR 0.864, the reference 0.90). Here a tie goes to the smaller
+// hash32(key ^ tie_salt(source)): deterministic, a bijection of the key for a fixed source, and
+// independent across sources (RMAT-12: 0.911; Jaccard vs the reference 0.952, the reference vs
+// itself relabelled 0.958). Restated in oracle/grank_oracle.c (tie_key).
+__device__ __forceinline__ uint32_t tie_salt(int v) { return hash32((uint32_t)v * 0x9e3779b9u + 1u); }
+// larger = preferred (selection keeps the largest (score, tie_w) pairs)
+__device__ __forceinline__ uint32_t tie_w(int key, uint32_t ts) { return ~hash32((uint32_t)key ^ ts); }
+
 __device__ __forceinline__ int wave_incl_scan(int x) {
 #pragma unroll
   for (int o = 1; o < WAVE; o <<= 1) {
@@ -314,9 +326,10 @@ __device__ __forceinline__ int table_compact_min(const LdsTable& t, double lo) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Top-`need` selection by (score desc, id asc) over n entries (keys[i], vals[i]) held in LDS or
-// global memory. Result: entry i is selected iff
-//     (v & ma) > pa  ||  ((v & ma) == pa && (!tie || (w & mb) >= pb))      v = bits(score), w = ~id
+// Top-`need` selection by (score desc, tie_w desc) over n entries (keys[i], vals[i]) held in LDS
+// or global memory. Result: entry i is selected iff
+//     (v & ma) > pa  ||  ((v & ma) == pa && (!tie || (w & mb) >= pb))
+// v = bits(score), w = tie_w(key, ts)
 struct SelCrit {
   uint64_t pa, ma;
   uint64_t pb, mb;
@@ -387,7 +400,7 @@ __device__ __forceinline__ void radix_kth_desc(int n, int& k, GetV getv, Filt fi
 
 template <class KeyAt, class ValAt>
 __device__ __forceinline__ SelCrit select_top(int n, int need, KeyAt keyat, ValAt valat,
-                                              uint32_t* hist) {
+                                              uint32_t* hist, uint32_t ts) {
   SelCrit c;
   c.tie = false; c.pb = 0; c.mb = 0;
   int k = need;
@@ -395,10 +408,10 @@ __device__ __forceinline__ SelCrit select_top(int n, int need, KeyAt keyat, ValA
   radix_kth_desc(n, k, [&](int i) { return dbits(valat(i)); }, [&](int) { return true; },
                  hist, c.pa, c.ma, tie);
   if (tie) {
-    // all boundary entries carry exactly the same score: keep the k smallest ids
+    // all boundary entries carry exactly the same score: keep the k with the largest tie_w
     const uint64_t pa = c.pa;
     bool tie2 = false;
-    radix_kth_desc(n, k, [&](int i) { return (uint64_t)(uint32_t)~keyat(i); },
+    radix_kth_desc(n, k, [&](int i) { return (uint64_t)tie_w(keyat(i), ts); },
                    [&](int i) { return dbits(valat(i)) == pa; }, hist, c.pb, c.mb, tie2);
     c.tie = true;
   }
@@ -412,13 +425,15 @@ __device__ __forceinline__ bool sel_test(const SelCrit& c, uint64_t v, uint32_t 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Row buffer (LDS): rv = score bits, rk = id; bitonic sort, (score desc, id asc).
+// Row buffer (LDS): rv = score bits, rk = id; bitonic sort, (score desc, id asc) -- the output
+// order -- or, with `by_tie`, (score desc, tie_w desc) -- the selection order.
 __device__ __forceinline__ bool row_less(uint64_t av, int ak, uint64_t bv, int bk) {
   // "a ranks below b"
   return av < bv || (av == bv && (uint32_t)~ak < (uint32_t)~bk);
 }
 
-__device__ __forceinline__ void row_sort(uint64_t* rv, int* rk, int cnt, int Lp) {
+__device__ __forceinline__ void row_sort(uint64_t* rv, int* rk, int cnt, int Lp, bool by_tie = false,
+                                         uint32_t ts = 0) {
   for (int i = cnt + lane_id(); i < Lp; i += WAVE) { rv[i] = 0; rk[i] = -1; }  // sentinels last
   wave_fence();
   for (int k = 2; k <= Lp; k <<= 1) {
@@ -430,7 +445,11 @@ __device__ __forceinline__ void row_sort(uint64_t* rv, int* rk, int cnt, int Lp)
         const int ak = rk[i], bk = rk[p];
         // descending overall: blocks with (i & k) == 0 descend
         const bool desc = (i & k) == 0;
-        const bool swap = desc ? row_less(av, ak, bv, bk) : row_less(bv, bk, av, ak);
+        // selection order: sentinels (id -1, score 0) rank below every entry of equal score
+        const uint64_t ra = ak < 0 ? 0ull : 1ull + tie_w(ak, ts), rb = bk < 0 ? 0ull : 1ull + tie_w(bk, ts);
+        const bool lt_ab = by_tie ? (av < bv || (av == bv && ra < rb)) : row_less(av, ak, bv, bk);
+        const bool lt_ba = by_tie ? (bv < av || (bv == av && rb < ra)) : row_less(bv, bk, av, ak);
+        const bool swap = desc ? lt_ab : lt_ba;
         if (swap) { rv[i] = bv; rv[p] = av; rk[i] = bk; rk[p] = ak; }
       }
       wave_fence();

@@ -161,7 +161,7 @@ __device__ __forceinline__ void wg_route_apply(const WgLds& w, uint32_t T, uint3
   __syncthreads();
 }
 
-// block-wide radix select of the top-`need` (score desc, id asc) among n entries in LDS.
+// block-wide radix select of the top-`need` (score desc, tie_w desc) among n entries in LDS.
 // Same criterion as select_top (wave version); one wave scans the histogram.
 template <class GetV, class Filt>
 __device__ __forceinline__ void wg_radix_kth(const WgLds& w, int n, int& k, GetV getv, Filt filt,
@@ -222,7 +222,7 @@ __device__ __forceinline__ void wg_radix_kth(const WgLds& w, int n, int& k, GetV
 
 template <class KeyAt, class ValAt, class Occ>
 __device__ __forceinline__ SelCrit wg_select_top(const WgLds& w, int n, int need, KeyAt keyat,
-                                                 ValAt valat, Occ occ) {
+                                                 ValAt valat, Occ occ, uint32_t ts) {
   SelCrit c;
   c.tie = false; c.pb = 0; c.mb = 0;
   int k = need;
@@ -231,7 +231,7 @@ __device__ __forceinline__ SelCrit wg_select_top(const WgLds& w, int n, int need
   if (tie) {
     const uint64_t pa = c.pa;
     bool tie2 = false;
-    wg_radix_kth(w, n, k, [&](int i) { return (uint64_t)(uint32_t)~keyat(i); },
+    wg_radix_kth(w, n, k, [&](int i) { return (uint64_t)tie_w(keyat(i), ts); },
                  [&](int i) { return occ(i) && dbits(valat(i)) == pa; }, c.pb, c.mb, tie2);
     c.tie = true;
   }
@@ -256,12 +256,13 @@ constexpr int WG_MAX_PASSES = 64;
 
 // Accumulate one ordered candidate stream (`each` calls its callback once per chunk with two
 // candidates per lane, in stream order) in P key-bucket passes. On success pk/pv[0..M_PLEN)
-// hold the stream's top-L by (score desc, id asc) (all entries when there are fewer).
+// hold the stream's top-L by (score desc, tie_w desc) (all entries when there are fewer).
 template <class EachChunk>
 __device__ __forceinline__ bool wg_accumulate(const WgLds& L, int P, uint32_t salt, bool seed_here,
                                               int v, double selfval, double factor, int Lw,
                                               EachChunk each) {
   const uint32_t T = WG_T, budget = WG_T - 1024;
+  const uint32_t ts = tie_salt(v);
   if (threadIdx.x == 0) { L.misc[M_PLEN] = 0; L.misc[M_OVF] = 0; }
   for (int pass = 0; pass < P; pass++) {
     for (int i = threadIdx.x; i < (int)T; i += blockDim.x) L.keys[i] = EMPTY;
@@ -285,11 +286,11 @@ __device__ __forceinline__ bool wg_accumulate(const WgLds& L, int P, uint32_t sa
         if (occ(i)) { const int pos = atomicAdd(&L.misc[M_PLEN], 1); L.pk[pos] = L.keys[i]; L.pv[pos] = L.acc[i]; }
     } else {
       const SelCrit c = wg_select_top(L, (int)T, Lw, [&](int i) { return L.keys[i]; },
-                                      [&](int i) { return L.acc[i]; }, occ);
+                                      [&](int i) { return L.acc[i]; }, occ, ts);
       for (int i = threadIdx.x; i < (int)T; i += blockDim.x) {
         if (!occ(i)) continue;
         const int key = L.keys[i];
-        if (sel_test(c, dbits(L.acc[i]), (uint32_t)~key)) {
+        if (sel_test(c, dbits(L.acc[i]), tie_w(key, ts))) {
           const int pos = atomicAdd(&L.misc[M_PLEN], 1);
           L.pk[pos] = key;
           L.pv[pos] = L.acc[i];
@@ -301,12 +302,12 @@ __device__ __forceinline__ bool wg_accumulate(const WgLds& L, int P, uint32_t sa
       const int n = L.misc[M_PLEN];
       const int* pk = L.pk;
       const double* pv = L.pv;
-      const SelCrit c = select_top(n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; }, L.hist);
+      const SelCrit c = select_top(n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; }, L.hist, ts);
       int base = 0;
       for (int i0 = 0; i0 < n; i0 += WAVE) {
         const int i = i0 + lane_id();
         bool sel = false;
-        if (i < n) sel = sel_test(c, dbits(pv[i]), (uint32_t)~pk[i]);
+        if (i < n) sel = sel_test(c, dbits(pv[i]), tie_w(pk[i], ts));
         const uint64_t m = __ballot(sel);
         if (sel) { const int pos = base + __popcll(m & lanemask_lt()); L.rv[pos] = dbits(pv[i]); L.rk[pos] = pk[i]; }
         base += __popcll(m);

@@ -20,10 +20,11 @@
  *                                             (k,s) in B[u]: acc[k] = fma(s, d/deg, acc[k])
  *                                             (-O3 -march=native contracts this into an FMA)
  *   keepTop      include/internal/pprInternal.h:109-137  keep L largest; the reference breaks
- *                                             ties by unordered_map order + nth_element; this
- *                                             restatement (and the HIP path) uses the documented
- *                                             deterministic rule (score desc, dense id asc) and
- *                                             stores rows in that order
+ *                                             ties by unordered_map order + nth_element, which
+ *                                             differs from row to row; this restatement (and the
+ *                                             HIP path) breaks them by a per-source hash of the key
+ *                                             (oracle_tie_key) and stores rows by (score desc, id
+ *                                             asc)
  *   norm1        include/internal/pprInternal.h:147-165  sum |new-old| over the key union; the
  *                                             summation order here is the HIP kernel's fixed
  *                                             64-lane pattern over rows in their stored (hash)
@@ -31,21 +32,38 @@
  *                                             bit-identical too
  *   stop rule    include/grank.h:90-94,140   maxDiff[2] = {tol, tol}; loop while
  *                                             i < iterations && max(maxDiff) >= tol
- *   final top-K  include/grank.h:143-147      first min(K, len) entries of each sorted row
+ *   final top-K  include/grank.h:143-147      keepTop(K) of each row by the same rule (row_topk)
  */
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
-typedef struct { int32_t key; double sc; } ent_t;
+typedef struct { int32_t key; double sc; uint32_t tie; } ent_t;
 
+/* output / storage order: (score desc, key asc) */
 static int cmp_ent(const void* a, const void* b) {
   const ent_t* x = (const ent_t*)a;
   const ent_t* y = (const ent_t*)b;
   if (x->sc > y->sc) return -1;
   if (x->sc < y->sc) return 1;
   return (x->key < y->key) ? -1 : (x->key > y->key);
+}
+
+/* selection order of keepTop (pprInternal.h:109-137), whose ties the reference leaves to each
+ * unordered_map's history (so they fall differently in every row): (score desc, tie asc) with
+ * tie = mix32(key ^ mix32(source * 0x9e3779b9 + 1)), a per-source bijection of the key -- the HIP
+ * path's tie_salt / tie_w (ppr_device.h) */
+static uint32_t mix32(uint32_t x);
+uint32_t oracle_tie_key(int32_t source, int32_t key) {
+  return mix32((uint32_t)key ^ mix32((uint32_t)source * 0x9e3779b9u + 1u));
+}
+static int cmp_sel(const void* a, const void* b) {
+  const ent_t* x = (const ent_t*)a;
+  const ent_t* y = (const ent_t*)b;
+  if (x->sc > y->sc) return -1;
+  if (x->sc < y->sc) return 1;
+  return (x->tie < y->tie) ? -1 : (x->tie > y->tie);
 }
 
 /* ---- open-addressing accumulator (keys unique, insertion-order independent) ---- */
@@ -98,15 +116,34 @@ static double* acc_find(acc_t* a, int32_t key) {
 
 static void acc_free(acc_t* a) { free(a->keys); free(a->acc); free(a->slots); memset(a, 0, sizeof(*a)); }
 
-/* collect, order by (score desc, key asc), keep first L -> out row; returns len */
-static int32_t acc_top(acc_t* a, int32_t L, ent_t** buf, int64_t* bufcap, int32_t* ids, double* sc) {
+/* keepTop(L) of source v's accumulator: the first L by the selection order, stored by the output
+ * order; returns len */
+static int32_t acc_top(acc_t* a, int32_t v, int32_t L, ent_t** buf, int64_t* bufcap, int32_t* ids, double* sc) {
   if (a->used > *bufcap) { free(*buf); *bufcap = a->used; *buf = (ent_t*)malloc(sizeof(ent_t) * (*bufcap)); }
   ent_t* e = *buf;
-  for (int64_t i = 0; i < a->used; i++) { int64_t s = a->slots[i]; e[i].key = a->keys[s]; e[i].sc = a->acc[s]; }
-  qsort(e, (size_t)a->used, sizeof(ent_t), cmp_ent);
+  for (int64_t i = 0; i < a->used; i++) {
+    int64_t s = a->slots[i];
+    e[i].key = a->keys[s]; e[i].sc = a->acc[s]; e[i].tie = oracle_tie_key(v, e[i].key);
+  }
   int32_t len = a->used < L ? (int32_t)a->used : L;
+  if (a->used > L) qsort(e, (size_t)a->used, sizeof(ent_t), cmp_sel);
+  qsort(e, (size_t)len, sizeof(ent_t), cmp_ent);
   for (int32_t i = 0; i < len; i++) { ids[i] = e[i].key; sc[i] = e[i].sc; }
   return len;
+}
+
+/* final keepTop(K) of a stored row of source v (include/grank.h:143-147): out = the K kept by the
+ * selection order, by the output order; returns their count */
+static int32_t row_topk(int32_t v, const int32_t* ids, const double* sc, int32_t len, int32_t K,
+                        int32_t* out_ids, double* out_sc) {
+  ent_t* e = (ent_t*)malloc(sizeof(ent_t) * (size_t)(len + 1));
+  for (int32_t i = 0; i < len; i++) { e[i].key = ids[i]; e[i].sc = sc[i]; e[i].tie = oracle_tie_key(v, ids[i]); }
+  const int32_t k = len < K ? len : K;
+  if (len > K) qsort(e, (size_t)len, sizeof(ent_t), cmp_sel);
+  qsort(e, (size_t)k, sizeof(ent_t), cmp_ent);
+  for (int32_t j = 0; j < K; j++) { out_ids[j] = j < k ? e[j].key : -1; out_sc[j] = j < k ? e[j].sc : 0.0; }
+  free(e);
+  return k;
 }
 
 /* norm1 with the HIP kernel's fixed summation pattern: 64 lane partials, entry i of the new row
@@ -226,7 +263,7 @@ int oracle_grank(int64_t n, const int64_t* rp, const int32_t* col, const uint8_t
       double* p = acc_find(&a, col[e]);
       *p = *p + factor;
     }
-    cl[v] = acc_top(&a, L, &buf, &bufcap, ci + v * L, cs + v * L);
+    cl[v] = acc_top(&a, (int32_t)v, L, &buf, &bufcap, ci + v * L, cs + v * L);
     acc_reset(&a);
   }
 
@@ -252,7 +289,7 @@ int oracle_grank(int64_t n, const int64_t* rp, const int32_t* col, const uint8_t
           *p = fma(us[j], factor, *p);
         }
       }
-      nl[v] = acc_top(&a, L, &buf, &bufcap, ni + v * L, ns + v * L);
+      nl[v] = acc_top(&a, (int32_t)v, L, &buf, &bufcap, ni + v * L, ns + v * L);
       acc_reset(&a);
       double d1 = norm1_stored(ni + v * L, ns + v * L, nl[v], ci + v * L, cs + v * L, cl[v]);
       if (d1 > md[0]) md[0] = d1;
@@ -268,14 +305,8 @@ int oracle_grank(int64_t n, const int64_t* rp, const int32_t* col, const uint8_t
   }
   if (iters_run) *iters_run = it;
 
-  for (int64_t v = 0; v < n; v++) {
-    int32_t k = cl[v] < K ? cl[v] : K;
-    out_len[v] = k;
-    for (int32_t j = 0; j < K; j++) {
-      out_ids[v * K + j] = j < k ? ci[v * L + j] : -1;
-      out_sc[v * K + j] = j < k ? cs[v * L + j] : 0.0;
-    }
-  }
+  for (int64_t v = 0; v < n; v++)
+    out_len[v] = row_topk((int32_t)v, ci + v * L, cs + v * L, cl[v], K, out_ids + v * K, out_sc + v * K);
   if (slab_ids) memcpy(slab_ids, ci, sizeof(int32_t) * (size_t)(n * L));
   if (slab_sc) memcpy(slab_sc, cs, sizeof(double) * (size_t)(n * L));
   if (slab_len) memcpy(slab_len, cl, sizeof(int32_t) * (size_t)n);
@@ -296,7 +327,7 @@ int oracle_init_state(int64_t n, const int64_t* rp, const int32_t* col, int32_t 
     acc_init(&a, deg + 1);
     *acc_find(&a, (int32_t)v) = 1.0 - damping;
     for (int64_t e = rp[v]; e < rp[v + 1]; e++) { double* p = acc_find(&a, col[e]); *p = *p + factor; }
-    len[v] = acc_top(&a, L, &buf, &bufcap, ids + v * L, sc + v * L);
+    len[v] = acc_top(&a, (int32_t)v, L, &buf, &bufcap, ids + v * L, sc + v * L);
     acc_reset(&a);
   }
   free(buf); acc_free(&a);
@@ -325,7 +356,7 @@ int oracle_step(int64_t n, const int64_t* rp, const int32_t* col, int32_t L, dou
         *p = fma(sc[(int64_t)u * L + j], factor, *p);
       }
     }
-    nlen[v] = acc_top(&a, L, &buf, &bufcap, nids + (int64_t)v * L, nsc + (int64_t)v * L);
+    nlen[v] = acc_top(&a, v, L, &buf, &bufcap, nids + (int64_t)v * L, nsc + (int64_t)v * L);
     acc_reset(&a);
     double d1 = norm1_stored(nids + (int64_t)v * L, nsc + (int64_t)v * L, nlen[v], ids + (int64_t)v * L,
                            sc + (int64_t)v * L, len[v]);

@@ -291,13 +291,31 @@ static int walk_node(int64_t n, const int64_t* rp, const int32_t* col, int32_t s
   return size;
 }
 
-typedef struct { int32_t key; double sc; } ment_t;
+typedef struct { int32_t key; double sc; uint32_t tie; } ment_t;
+/* output order: (score desc, key asc) */
 static int cmp_ment(const void* a, const void* b) {
   const ment_t* x = (const ment_t*)a;
   const ment_t* y = (const ment_t*)b;
   if (x->sc > y->sc) return -1;
   if (x->sc < y->sc) return 1;
   return (x->key < y->key) ? -1 : (x->key > y->key);
+}
+/* keepTop selection order: (score desc, per-source tie key asc), as in GRank (grank_oracle.c) */
+uint32_t oracle_tie_key(int32_t source, int32_t key);
+static int cmp_msel(const void* a, const void* b) {
+  const ment_t* x = (const ment_t*)a;
+  const ment_t* y = (const ment_t*)b;
+  if (x->sc > y->sc) return -1;
+  if (x->sc < y->sc) return 1;
+  return (x->tie < y->tie) ? -1 : (x->tie > y->tie);
+}
+/* keep the top `keep` of ent[0..U) of source v by the selection order, then order them for output */
+static void mkeep(ment_t* ent, int64_t U, int64_t keep, int32_t v) {
+  if (U > keep) {
+    for (int64_t t = 0; t < U; t++) ent[t].tie = oracle_tie_key(v, ent[t].key);
+    qsort(ent, (size_t)U, sizeof(ment_t), cmp_msel);
+  }
+  qsort(ent, (size_t)keep, sizeof(ment_t), cmp_ment);
 }
 
 /* Whole MCCompletePathV2. out_* n*K / n; walk_* (optional) n*L / n: walk basket of every node
@@ -354,8 +372,8 @@ int oracle_mccp2(int64_t n, const int64_t* rp, const int32_t* col, int32_t K, in
       }
     }
     for (int64_t t = 0; t < U; t++) { ent[t].sc = acc[ent[t].key]; touched[ent[t].key] = 0; }
-    qsort(ent, (size_t)U, sizeof(ment_t), cmp_ment);  /* keepTop(L) (:243) */
     const int64_t keep = U < L ? U : L;
+    mkeep(ent, U, keep, v);                            /* keepTop(L) (:243) */
     for (int64_t t = 0; t < keep; t++) {              /* *= factor (:246-247) */
       fid[(int64_t)v * L + t] = ent[t].key;
       fsc[(int64_t)v * L + t] = ent[t].sc * f;
@@ -365,7 +383,7 @@ int oracle_mccp2(int64_t n, const int64_t* rp, const int32_t* col, int32_t K, in
   for (int64_t v = 0; v < n; v++) {                   /* keepTop(K) (:252-256) on the scaled map */
     const int32_t k = flen[v] < K ? flen[v] : K;
     for (int32_t t = 0; t < flen[v]; t++) { ent[t].key = fid[v * L + t]; ent[t].sc = fsc[v * L + t]; }
-    qsort(ent, (size_t)flen[v], sizeof(ment_t), cmp_ment);  /* scaling can tie two scores */
+    mkeep(ent, flen[v], k, (int32_t)v);                /* scaling can tie two scores */
     for (int32_t t = 0; t < K; t++) {
       out_ids[v * K + t] = t < k ? ent[t].key : -1;
       out_sc[v * K + t] = t < k ? ent[t].sc : 0.0;
@@ -426,8 +444,8 @@ int oracle_mc_combine(int64_t n, const int64_t* rp, const int32_t* col, const in
       }
     }
     for (int64_t t = 0; t < U; t++) { ent[t].sc = acc[ent[t].key]; touched[ent[t].key] = 0; }
-    qsort(ent, (size_t)U, sizeof(ment_t), cmp_ment);
     const int64_t keep = U < L ? U : L;
+    mkeep(ent, U, keep, v);
     for (int64_t t = 0; t < keep; t++) { ent[t].sc = ent[t].sc * f; }
     qsort(ent, (size_t)keep, sizeof(ment_t), cmp_ment);  /* scaling can tie two scores */
     for (int32_t t = 0; t < L; t++) {

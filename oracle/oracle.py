@@ -54,6 +54,8 @@ def lib():
         L.oracle_mc_combine.argtypes = [ctypes.c_int64, vp, vp, vp, ctypes.c_int32, ctypes.c_double, vp, vp, vp,
                                         vp, vp, vp, vp, ctypes.c_int64, vp, vp, vp]
         L.oracle_mc_combine.restype = ctypes.c_int
+        L.oracle_tie_key.argtypes = [ctypes.c_int32, ctypes.c_int32]
+        L.oracle_tie_key.restype = ctypes.c_uint32
         _lib = L
     return _lib
 
@@ -189,6 +191,19 @@ def mc_combine(row_ptr, col, pos, L, damping, final, walk, lst):
     return ids, sc, ln
 
 
+def topk_row(v, ids, scores, K):
+    """keepTop(K) of source v's row (ids, scores): the K kept by the tie rule (score desc,
+    oracle_tie_key(v, key) asc), in output order (score desc, id asc)"""
+    ids = np.asarray(ids)
+    scores = np.asarray(scores)
+    if len(ids) > K:
+        tie = np.array([lib().oracle_tie_key(int(v), int(k)) for k in ids], dtype=np.uint64)
+        keep = np.lexsort((tie, -scores))[:K]
+        ids, scores = ids[keep], scores[keep]
+    o = np.lexsort((ids, -scores))
+    return ids[o], scores[o]
+
+
 def ref_available() -> bool:
     return os.path.exists(REF_DRIVER)
 
@@ -273,7 +288,6 @@ class OracleEngine:
         k = np.minimum(self.len, self.K)
         ids = np.full((self.n, self.K), -1, dtype=np.int32)
         sc = np.zeros((self.n, self.K), dtype=np.float64)
-        for v in range(self.n):
-            ids[v, :k[v]] = self.ids[v, :k[v]]
-            sc[v, :k[v]] = self.sc[v, :k[v]]
+        for v in range(self.n):  # final keepTop(K) by the engine's tie rule
+            ids[v, :k[v]], sc[v, :k[v]] = topk_row(v, self.ids[v, :self.len[v]], self.sc[v, :self.len[v]], self.K)
         return ids, sc, k.astype(np.int32)

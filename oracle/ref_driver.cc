@@ -224,6 +224,15 @@ int main(int argc, char** argv) {
   else if (mode == "grankmulti") r = ppr::grankMulti(g, K, L, it, d, tol, nth);
   else if (mode == "mc") {
     r = ppr::mccompletepathv2(g, K, L, it, d);
+  } else if (mode == "pprss_list") {
+    // exact single-source PPR for the dense sources listed (int32) in file argv[10]
+    if (argc < 11) die("pprss_list needs a list file");
+    FILE* lf = fopen(argv[10], "rb");
+    if (!lf) die("cannot open list");
+    int32_t x;
+    while (fread(&x, 4, 1, lf) == 1)
+      r[dn.order[x]] = ppr::pprInternal::pprSingleSource(g, it, d, tol, dn.order[x]);
+    fclose(lf);
   } else if (mode == "pprss") {
     // exact single-source PPR (include/internal/pprSingleSource.h:28-75) for the first K
     // dense sources listed in iteration order starting at dense index L (quality oracle);

@@ -15,11 +15,12 @@ EXACT = [
     "g5_ring100_k10_l20", "g5_ring100_full", "g5_instar_full", "g5_instar_loop_full",
     "g5_instar_all_full", "g5_random5000_full", "g5_complete_full",
 ]
-# truncating runs: statistical parity (P3/P4), thresholds = measured restatement-vs-reference
-# agreement with margin, next to the reference-vs-relabelled-reference ceiling of SURVEY s0.4
+# truncating runs: statistical parity (P3/P4, tests/test_parity_p34.py), top-K Jaccard thresholds
+# just under the reference-vs-relabelled-reference agreement (fixture field self_jaccard)
 STAT = {
-    "g3_rmat12_k16_l32": 0.88,
-    "g3_rmat14_k32_l64": 0.96,
+    "g3_rmat12_k16_l32": 0.945,   # the reference vs itself relabelled: 0.958-0.963
+    "g3_rmat14_k32_l64": 0.975,   # ... 0.986-0.987
+    "g3_rmat14_k64_l128": 0.915,  # ... 0.921-0.934
     "g4_eat_k50_l100": 0.99,
 }
 

@@ -44,6 +44,7 @@ def test_mc_combine_reproduces_the_sweep():
         fid[v], fsc[v], fln[v] = ids[0], sc[0], ln[0]
     k = np.minimum(fln, K)
     assert np.array_equal(k, o["lens"])
-    for v in range(g.n):
-        assert np.array_equal(fid[v, :k[v]], o["ids"][v, :k[v]])
-        assert np.array_equal(fsc[v, :k[v]], o["scores"][v, :k[v]])
+    for v in range(g.n):  # final keepTop(K) of the scaled rows (include/mccompletepathv2.h:252-256)
+        ids, sc = oracle.topk_row(v, fid[v, :fln[v]], fsc[v, :fln[v]], K)
+        assert np.array_equal(ids, o["ids"][v, :k[v]])
+        assert np.array_equal(sc, o["scores"][v, :k[v]])

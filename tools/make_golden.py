@@ -182,9 +182,140 @@ def main_mc():
         save("m4_eat_k50_l200", res, [50, 200, 1000, 0.85, -1.0], sample)
 
 
+def pprss_rows(name, K, keys, succ, n_src=200, tol=1e-4, seed=7):
+    """exact PPR (pprSingleSource, 100 iterations, d .85, tol 1e-4: the reference's quality harness,
+    include/benchmarkAlgorithm.h:91) of `n_src` sampled non-dangling sources of fixture `name`,
+    kept to the top K + 32 (room for ties at the K-th score), appended to the fixture"""
+    path = os.path.join(GOLDEN, name + ".npz")
+    z = dict(np.load(path))
+    rp, order = z["rp"], z["order"]
+    deg = np.diff(rp)
+    rng = np.random.default_rng(seed)
+    pool = np.nonzero(deg > 0)[0]
+    if "sample" in z:  # sources whose reference rows the fixture holds
+        pool = np.intersect1d(pool, z["sample"])
+    src = np.sort(rng.choice(pool, n_src, replace=False)).astype(np.int32)
+    with tempfile.TemporaryDirectory() as td:
+        gp = os.path.join(td, "g.bin")
+        lp = os.path.join(td, "list.bin")
+        # the graph file exactly as the fixture was made from it: the reference then iterates it
+        # in the same order, so the dense ids (the fixture's) coincide
+        write_graph_bin(gp, keys, succ)
+        src.tofile(lp)
+        out = os.path.join(td, "out.bin")
+        subprocess.run([DRIVER, "pprss_list", gp, out, str(K + 32), "0", "100", "0.85", repr(tol), "1", lp],
+                       check=True)
+        ex = read_out(out, K + 32)
+    assert np.array_equal(ex["order"], order), "dense order changed"
+    z.update(pprss_src=src, pprss_ids=ex["ids"][src], pprss_scores=ex["scores"][src], pprss_cnt=ex["cnt"][src])
+    np.savez_compressed(path, **z)
+    print(f"{name}: exact PPR of {len(src)} sources -> {os.path.getsize(path) / 1024:.0f} KiB")
+
+
+def self_ceiling(name, keys, succ, n_perm=3, seed=11):
+    """the reference against itself on randomly relabelled input: mean top-K Jaccard
+    and max sorted-score-profile difference over the fixture's rows, and its top-K Jaccard vs
+    the fixture's exact-PPR rows -- the bar the P3/P4 checks are stated against"""
+    path = os.path.join(GOLDEN, name + ".npz")
+    z = dict(np.load(path))
+    K, L, it, d, tol = z["params"]
+    K, L, it, d, tol = int(K), int(L), int(it), float(d), float(tol)  # repr() of numpy scalars is not a number
+    mode = "grankmulti" if "sample" in z else "grank"
+    n = len(z["order"])
+    rows = z["sample"] if "sample" in z else np.arange(n)
+    dense_of_key = np.empty(n, dtype=np.int64)
+    dense_of_key[z["order"]] = np.arange(n)
+    rng = np.random.default_rng(seed)
+    js, profs, qual = [], [], []
+    for _ in range(n_perm):
+        perm = rng.permutation(n)  # original key k -> new key perm[k]
+        with tempfile.TemporaryDirectory() as td:
+            gp = os.path.join(td, "g.bin")
+            write_graph_bin(gp, [int(perm[k]) for k in keys], [[int(perm[x]) for x in s] for s in succ])
+            r = run_ref(mode, gp, K, L, it, d, tol, 8)
+        # r's dense id -> new key -> original key -> fixture dense id
+        inv = np.argsort(perm)
+        fx = dense_of_key[inv[r["order"]]]
+        ids = np.full((n, K), -1, dtype=np.int64)
+        cnt = np.zeros(n, dtype=np.int64)
+        sc = np.zeros((n, K))
+        ids[fx] = np.where(r["ids"] >= 0, fx[np.maximum(r["ids"], 0)], -1)
+        cnt[fx] = np.minimum(r["cnt"], K)
+        sc[fx] = r["scores"]
+        zc = np.minimum(z["cnt"], K)
+        zi = z["ids"] if "sample" in z else z["ids"]
+        zs = z["scores"]
+        j, p = [], 0.0
+        for q, v in enumerate(rows):
+            a, b = set(ids[v, :cnt[v]].tolist()), set(zi[q, :zc[q]].tolist())
+            j.append(1.0 if not (a or b) else len(a & b) / len(a | b))
+            if cnt[v] == zc[q] and cnt[v]:
+                p = max(p, float(np.abs(np.sort(sc[v, :cnt[v]]) - np.sort(zs[q, :zc[q]])).max()))
+        js.append(np.mean(j))
+        profs.append(p)
+        if "pprss_src" in z:
+            kq = []
+            for t, v in enumerate(z["pprss_src"]):
+                a = set(ids[v, :cnt[v]].tolist())
+                b = set(z["pprss_ids"][t, :min(K, z["pprss_cnt"][t])].tolist())
+                kq.append(1.0 if not (a or b) else len(a & b) / len(a | b))
+            qual.append(np.mean(kq))
+    z.update(self_jaccard=np.array(js), self_profile=np.array(profs))
+    if qual:
+        z.update(self_quality=np.array(qual))
+    np.savez_compressed(path, **z)
+    print(f"{name}: reference vs relabelled reference: Jaccard {np.round(js, 4)} profile {np.round(profs, 6)} "
+          f"quality {np.round(qual, 4)}")
+
+
+def tie_replay(name, scale, L, its, d=0.85):
+    """the reference's full baskets (K = L: keepTop(K) keeps the whole basket) after `it` and
+    `it + 1` iterations, for the per-iteration ties-only check (tests/test_oracle_golden.py)"""
+    keys, succ = rmat_lists(scale)
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        gp = os.path.join(td, "g.bin")
+        write_graph_bin(gp, keys, succ)
+        for it in its:
+            for k in (it, it + 1):
+                if f"ids_{k}" in out:
+                    continue
+                r = run_ref("grank", gp, L, L, k, d, -1.0)
+                out.update({f"ids_{k}": r["ids"], f"scores_{k}": r["scores"], f"cnt_{k}": r["cnt"]})
+            out.update(rp=r["rp"], col=r["col"], part=r["part"], order=r["order"])
+    out["params"] = np.array([L, L, 0, d, -1.0])
+    out["its"] = np.array(its, dtype=np.int32)
+    path = os.path.join(GOLDEN, name + ".npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: -> {os.path.getsize(path) / 1024:.0f} KiB")
+
+
+def main_p34():
+    """P3/P4 fixtures: exact-PPR rows for sampled sources of the truncating RMAT runs,
+    a K64/L128 RMAT-14 run, and reference states for the ties-only replay"""
+    rng = np.random.default_rng(34)
+    k14, s14 = rmat_lists(14)
+    if not os.path.exists(os.path.join(GOLDEN, "g3_rmat14_k64_l128.npz")):
+        sample = np.sort(rng.choice(1 << 14, 2048, replace=False)).astype(np.int64)
+        gen_graph("g3_rmat14_k64_l128", k14, s14, 64, 128, 30, 0.85, -1.0, mode="grankmulti", threads=8,
+                  sample=sample)
+    k12, s12 = rmat_lists(12)
+    if "--pprss-only" not in sys.argv:
+        pprss_rows("g3_rmat12_k16_l32", 16, k12, s12)
+    pprss_rows("g3_rmat14_k32_l64", 32, k14, s14)
+    pprss_rows("g3_rmat14_k64_l128", 64, k14, s14)
+    if "--pprss-only" not in sys.argv:
+        tie_replay("r1_rmat12_l32", 12, 32, (3, 8))
+    self_ceiling("g3_rmat12_k16_l32", k12, s12)
+    self_ceiling("g3_rmat14_k32_l64", k14, s14)
+    self_ceiling("g3_rmat14_k64_l128", k14, s14)
+
+
 def main():
     if "--mc" in sys.argv:
         return main_mc()
+    if "--p34" in sys.argv:
+        return main_p34()
     os.makedirs(GOLDEN, exist_ok=True)
     if not os.path.exists(DRIVER):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
