@@ -5,7 +5,11 @@ MI355X guide prescribes) into per-kernel HBM traffic.
 
 FETCH_SIZE / WRITE_SIZE are reported in KiB. gfx950 correction (MI355X_MICROARCH.md "HBM"):
 FETCH_SIZE counts 128-B requests at 64 B, so fetched bytes = 2 x FETCH_SIZE; WRITE_SIZE is used
-as is. Totals are per step (one whole job) over the kernels of the merge phase.
+as is. Both factors are calibrated for this engine's own access patterns by tools/pmc_calib.hip
+(profiles/r02_pmc_calibration.json): 4-B and 8-B per-lane basket-row gathers and 12-B staging
+record streams read 2.00x FETCH_SIZE, 12-B record stores write 1.00x WRITE_SIZE; the stable
+partition's short runs (48 B per bucket per tile) really do cost 3.4x their bytes in HBM writes.
+Totals are per step (one whole job) over the kernels of the merge phase.
 """
 from __future__ import annotations
 
@@ -36,7 +40,8 @@ def main(fetch_csv, write_csv, steps):
                       "write_bytes": w.get(k, 0.0) / steps}
     merge = [k for k in kernels if any(t in k for t in MERGE_KERNELS)]
     out = {
-        "note": "bytes per step; fetch = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE; KiB -> bytes",
+        "note": ("bytes per step; fetch = 2 x FETCH_SIZE, write = WRITE_SIZE (gfx950; factors calibrated on "
+                 "this engine's access patterns, profiles/r02_pmc_calibration.json); KiB -> bytes"),
         "merge_phase_traffic_bytes": sum(kernels[k]["fetch_bytes"] + kernels[k]["write_bytes"] for k in merge),
         "merge_kernels": merge,
         "kernels": kernels,
