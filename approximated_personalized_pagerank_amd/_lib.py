@@ -32,6 +32,7 @@ ERRORS = {
     9: "HIP runtime error",
     10: "device out of memory",
     11: "parameter outside the supported range",
+    12: "source node not part of the graph",
 }
 
 
@@ -130,6 +131,11 @@ def lib() -> ctypes.CDLL:
         "ppr_mccp2_plan_walk": (ctypes.c_int, [vp, u32, ctypes.c_uint64, i64, i64]),
         "ppr_mccp2_plan_combine": (ctypes.c_int, [vp]),
         "ppr_mccp2_plan_run": (ctypes.c_int, [vp, u32, ctypes.c_uint64, vp]),
+        "ppr_exact_create": (ctypes.c_int, [vp, vp, i32, f64, vp, ctypes.POINTER(vp)]),
+        "ppr_exact_run": (ctypes.c_int, [vp, u32, f64, vp]),
+        "ppr_exact_topk": (ctypes.c_int, [vp, u32, vp, vp, vp]),
+        "ppr_exact_gather": (ctypes.c_int, [vp, i32, vp, vp]),
+        "ppr_exact_destroy": (None, [vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)

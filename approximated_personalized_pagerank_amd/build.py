@@ -7,7 +7,7 @@ import subprocess
 from ._lib import LIB_PATH, PKG_DIR
 
 CSRC = os.path.join(PKG_DIR, "csrc")
-SOURCES = ["grank.hip", "mccp2.hip", "host_graph.cpp"]
+SOURCES = ["grank.hip", "mccp2.hip", "exact_ppr.hip", "host_graph.cpp"]
 HEADERS = ["ppr_device.h", "ppr_common.h", "merge_wave.h", "wg_merge.h", "merge_hub.h", "merge_glb.h",
            "merge_mc.h", "plan.h",
            os.path.join("..", "..", "include", "ppr_hip.h")]

@@ -1458,6 +1458,7 @@ extern "C" const char* ppr_strerror(int code) {
     case PPR_ERR_HIP: return "HIP runtime error";
     case PPR_ERR_OOM: return "device out of memory";
     case PPR_ERR_RANGE: return "parameter outside the supported range";
+    case PPR_ERR_SOURCE: return "source node not part of the graph";
     default: return "unknown error";
   }
 }

@@ -389,7 +389,7 @@ __device__ __forceinline__ void wg_slab_stream(const WgLds& L, const DevGraph& g
 }
 
 // one workgroup (8 waves) per source read from the slab
-__global__ void __launch_bounds__(WG_THREADS) k_merge_wg(DevGraph g, DevSlab s, IterArgs a,
+static __global__ void __launch_bounds__(WG_THREADS) k_merge_wg(DevGraph g, DevSlab s, IterArgs a,
                                                          const int32_t* list, int64_t count,
                                                          const int32_t* cand, int Lp,
                                                          unsigned long long* maxdiff,

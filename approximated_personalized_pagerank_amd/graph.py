@@ -82,6 +82,14 @@ class Csr:
     def key(self, i: int):
         return i if self.keys is None else self.keys[i]
 
+    def index(self, key) -> int:
+        """dense id of a user key"""
+        if self.keys is None:
+            return int(key)
+        if getattr(self, "_index", None) is None:
+            self._index = {k: i for i, k in enumerate(self.keys)}
+        return self._index[key]
+
 
 def rmat(scale: int, edge_factor: int = 16, a: float = 0.57, b: float = 0.19, c: float = 0.19,
          seed: int = 42) -> Csr:

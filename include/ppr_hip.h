@@ -37,7 +37,8 @@ enum {
   PPR_ERR_GRAPH = 8,     /* successor id out of range (UB in the reference, README.md:69-73) */
   PPR_ERR_HIP = 9,       /* HIP runtime failure (no device, launch failure, ...) */
   PPR_ERR_OOM = 10,      /* device allocation failed */
-  PPR_ERR_RANGE = 11     /* L / K / node count beyond what the kernels support */
+  PPR_ERR_RANGE = 11,    /* L / K / node count beyond what the kernels support */
+  PPR_ERR_SOURCE = 12    /* "source node not part of the graph" include/internal/pprSingleSource.h:39 */
 };
 
 /* graph in dense CSR form (borrowed; host memory unless a *_dev entry point says otherwise) */
@@ -198,6 +199,23 @@ int ppr_mccp2_plan_info(ppr_plan* p, int64_t* walk_nodes, int64_t* levels, int64
 int ppr_mccp2_plan_walk(ppr_plan* p, uint32_t walks, uint64_t seed, int64_t begin, int64_t end);
 int ppr_mccp2_plan_combine(ppr_plan* p);
 int ppr_mccp2_plan_run(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_stats* st);
+
+/* ---- Exact single-source PPR, batched (the reference's quality oracle) -------------------------
+ * Replaces ppr::pprInternal::pprSingleSource(graph, iterations, damping, tolerance, source)
+ * (include/internal/pprSingleSource.h:28-75) for S sources at once, and the keepTop(K) +
+ * score lookups benchmarkAlgorithm does on its result (include/benchmarkAlgorithm.h:91-121).
+ * Scores agree with the reference to rounding (the per-node summation order differs). */
+typedef struct ppr_exact ppr_exact;
+int ppr_exact_create(const ppr_csr* g, const int32_t* sources, int32_t S, double damping,
+                     const ppr_opts* o, ppr_exact** out);
+/* power iteration of every source until its norm1 step < tolerance or `iterations`;
+ * iters_run[S] (optional): iterations each source ran */
+int ppr_exact_run(ppr_exact* h, uint32_t iterations, double tolerance, int32_t* iters_run);
+/* keepTop(K) of every source's vector (nonzero entries), rows [S][K] by (score desc, id asc) */
+int ppr_exact_topk(ppr_exact* h, uint32_t K, int32_t* out_ids, double* out_scores, int32_t* out_len);
+/* out[s][q] = score of node keys[s][q] for source s (0 for a node it never reached) */
+int ppr_exact_gather(ppr_exact* h, int32_t Q, const int32_t* keys, double* out);
+void ppr_exact_destroy(ppr_exact* h);
 
 #ifdef __cplusplus
 }
