@@ -9,7 +9,7 @@ from ._lib import LIB_PATH, PKG_DIR
 CSRC = os.path.join(PKG_DIR, "csrc")
 SOURCES = ["grank.hip", "mccp2.hip", "exact_ppr.hip", "host_graph.cpp"]
 HEADERS = ["ppr_device.h", "ppr_common.h", "merge_wave.h", "wg_merge.h", "merge_hub.h", "merge_glb.h",
-           "merge_mc.h", "plan.h",
+           "merge_mc.h", "merge_hot.h", "plan.h",
            os.path.join("..", "..", "include", "ppr_hip.h")]
 ARCH = os.environ.get("PPR_OFFLOAD_ARCH", "gfx950")
 
@@ -43,3 +43,21 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
     return out
+
+
+DROPIN_SRC = os.path.join(PKG_DIR, "..", "tests", "cpp", "dropin_test.cc")
+DROPIN_BIN = os.path.join(PKG_DIR, "..", "tests", "cpp", "_dropin_test")
+
+
+def build_dropin(force: bool = False) -> str:
+    """g++ the reference-API program tests/cpp/dropin_test.cc (include/ppr/*.h over libppr_hip.so):
+    the C++ drop-in tests and bench.py's end_to_end leg run it."""
+    lib = build()
+    if (not force and os.path.exists(DROPIN_BIN)
+            and os.path.getmtime(DROPIN_BIN) > max(os.path.getmtime(DROPIN_SRC), os.path.getmtime(lib))):
+        return DROPIN_BIN
+    inc = os.path.join(PKG_DIR, "..", "include")
+    subprocess.run(["g++", "-std=c++11", "-O2", "-I", inc, DROPIN_SRC, "-o", DROPIN_BIN + ".tmp", "-pthread",
+                    "-L", PKG_DIR, "-lppr_hip", f"-Wl,-rpath,{PKG_DIR}"], check=True)
+    os.replace(DROPIN_BIN + ".tmp", DROPIN_BIN)
+    return DROPIN_BIN

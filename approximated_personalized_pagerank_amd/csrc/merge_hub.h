@@ -27,12 +27,13 @@ namespace pprk {
 // is a lower bound of the L-th largest final value: a bucket never needs to emit a key below tau
 // (ties at tau are kept, the (score desc, id asc) order decides them in k_hub_final).
 constexpr int HUB_TILE_CAND = 4096;   // target candidates per tile: tw = max(1, target / L) successors
-constexpr int HUB_TILE_PER_BUCKET = 4;  // ... and target >= 4 P: the count matrix (P ints per tile) and
-                                        // the scatter's run seeds stay <= 1/4 int per candidate
-constexpr int HUB_BUCKET = 384;       // default target candidates per bucket (PPR_HUB_BUCKET)
+constexpr int HUB_TILE_PER_BUCKET = 16;  // ... and target >= 16 P (capped by tw <= 64): runs of ~16
+                                         // records per bucket per tile keep the scatter's stores near
+                                         // whole 128-B lines, and the count matrix <= 1/16 int per candidate
+constexpr int HUB_BUCKET = 448;       // default target candidates per bucket (PPR_HUB_BUCKET)
 constexpr int HUB_MAX_LOGP = 12;      // per-wave LDS counters of the partition: 16 KB
-constexpr int HUB_WAVE_T = 448;       // default wave bucket table slots (PPR_HUB_WAVE_T, a multiple of 64):
-                                      // 8.7 KB of LDS per wave with 2 groups per chunk, 18 waves per CU
+constexpr int HUB_WAVE_T = 512;       // default wave bucket table slots (PPR_HUB_WAVE_T, a multiple of 64):
+                                      // 9.7 KB of LDS per wave with 2 groups per chunk, 16 waves per CU
 constexpr int HUB_BW_BATCH = 8;       // staged groups a bucket wave keeps in flight
 constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per reducing workgroup (PPR_HUB_SLICE)
 

@@ -77,7 +77,7 @@ struct ppr_plan {
   int flags = 0;
   std::vector<int64_t> h_rp;       // host row pointers (hub planning)
   size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0, hub_lds_wave = 0;
-  int hub_bucket = 384, hub_wave_t = 448;  // PPR_HUB_BUCKET, PPR_HUB_WAVE_T (merge_hub.h defaults)
+  int hub_bucket = 448, hub_wave_t = 512;  // PPR_HUB_BUCKET, PPR_HUB_WAVE_T (merge_hub.h defaults)
   // pinned host staging of the hub planning (hub list + candidate counts down, descriptors up):
   // pageable copies of these (tens of MB per iteration) stalled the stream for milliseconds
   int32_t* h_hub_pin = nullptr;    // [2 * cap]: hub ids | candidate counts
@@ -115,7 +115,7 @@ struct ppr_plan {
   int tile_wpb_p = 4096;           // PPR_TILE_WPB_P: count / scatter run one wave per block from this maxP on
   int hub_bw_budget = 380;         // distinct keys a bucket wave's table takes before it spills
   int hub_mix = 6;                 // PPR_HUB_MIX: interleave sources with P >= 2^hub_mix among the others
-  int hub_tile_pb = 4;             // PPR_HUB_TILE_PB: tile candidates >= this many per bucket (0: 4096 / L)
+  int hub_tile_pb = 16;             // PPR_HUB_TILE_PB: tile candidates >= this many per bucket (0: 4096 / L)
   int64_t hub_budget = 1LL << 28;  // PPR_HUB_BUDGET: staged candidates per hub batch (16-B records)
   // with PPR_HUB_REGIONS (default 3) scratch regions the partition stage runs up to two batches
   // ahead, and the reduce + final of batch i (stream4) overlap the bucket waves of batch i+1

@@ -15,6 +15,8 @@ value = |V| * steps / max-over-ranks time; scaling "strong" (the job is fixed, s
 Extra objects on the JSON line (DESIGN.md "measurement"):
   roofline      merge phase: SURVEY s8d algorithmic bytes / merge-phase time (hipEvents on the
                 plan's stream), against 8 TB/s HBM
+  end_to_end    the reference's API end to end (tests/cpp/dropin_test.cc: unordered_map graph in,
+                unordered_map result out) with its flatten / plan / device / materialise split
   cpu_baseline  the reference's own combineMaps (oracle/_ref/ref_driver, compiled from
                 /root/reference) timed on a stratified sample of the end-state workload on this
                 host, extrapolated to the whole job
@@ -74,6 +76,34 @@ def mc_cpu_baseline(scale, K, L, walks, damping, seed):
                        f"sequential by design) whole job on RMAT-{scale} ({g.n} nodes, {g.m} edges, same K/L/R/d), "
                        f"{wall:.1f} s incl. graph load; its per-node cost grows with scale (1.5x per 2 scales "
                        f"measured at RMAT-14..18), so this overstates the RMAT-22 rate")}
+
+
+def end_to_end(scale, iters, K, L):
+    """f1: the reference's own API end to end -- tests/cpp/dropin_test.cc calls
+    ppr::grank(unordered_map graph, K=64, L=128, iters) through include/ppr/grank.h, so the timing
+    covers flattening the map graph, plan creation + upload, the device job and materialising the
+    unordered_map<int, unordered_map<int, double>> result (PPR_TIMING=1 split)."""
+    if (K, L) != (64, 128):
+        return None
+    from approximated_personalized_pagerank_amd import build as _build
+    binary = _build.build_dropin()
+    env = dict(os.environ, PPR_TIMING="1")
+    p = subprocess.run([binary, "e2e", str(scale), str(iters)], capture_output=True, text=True, env=env,
+                       check=True, timeout=900)
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    split = {}
+    for ln in p.stderr.splitlines():
+        if ln.startswith("ppr_timing"):
+            f = ln.split()[1:]
+            split = {f[i]: float(f[i + 1]) for i in range(0, len(f) - 1, 2)}
+    out = {"total_s": d["total_s"], "graph": "RMAT-%d as unordered_map<int, vector<int>> (%d nodes, %d edges)"
+           % (scale, d["nodes"], d["edges"]), "result_entries": d["entries"],
+           "call": f"ppr::grank(graph, K={K}, L={L}, {iters}, 0.85, nThreads, -1) via include/ppr/grank.h"}
+    if split:
+        out.update(flatten_s=split.get("flatten_s"), device_s=split.get("device_s"),
+                   plan_and_upload_s=split["csr_call_s"] - split["device_s"] if "csr_call_s" in split else None,
+                   materialize_s=split.get("materialize_s"))
+    return out
 
 
 def log(*a):
@@ -284,6 +314,7 @@ def main():
                     help="cpu_baseline threads (0 = every host CPU this process may use, cgroup quota included)")
     ap.add_argument("--cpu-budget", type=float, default=1.5e9, help="sampled candidates for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end_to_end leg (reference-API call)")
     ap.add_argument("--workload", choices=["grank", "mc"], default="grank",
                     help="mc: MCCompletePathV2 (configs[4]) with --K 50 --L 200 --walks 1000 defaults")
     ap.add_argument("--walks", type=int, default=1000, help="mc: random walks per node (R)")
@@ -313,7 +344,7 @@ def main():
         if rank != 0:
             return
         elapsed, stats = res
-        cpu = None
+        cpu = e2e = None
     else:
         plan = ppr.GrankPlan(g, args.K, args.L, args.damping, part=part, device=local, stats=True)
         for _ in range(args.warmup):
@@ -330,7 +361,7 @@ def main():
         elapsed = time.perf_counter() - t0
         stats = dict(merge_ms=merge_ms, algo_bytes=algo, device_ms=dev_ms, iterations=st.iterations_run,
                      launches=launches)
-        cpu = None
+        cpu = e2e = None
         if not args.no_cpu_baseline:
             try:
                 slab = plan.fetch_slab()
@@ -340,6 +371,12 @@ def main():
             except Exception as exc:  # reported, never fatal
                 log(f"cpu_baseline failed: {exc!r}")
                 cpu = None
+        plan.close()
+        if not args.no_e2e:
+            try:
+                e2e = end_to_end(args.scale, args.iters, args.K, args.L)
+            except Exception as exc:  # reported, never fatal
+                log(f"end_to_end failed: {exc!r}")
 
     steps = args.steps
     value = g.n * steps / elapsed
@@ -374,6 +411,7 @@ def main():
                      "merge_launches_per_step": stats["launches"] / steps,
                      "traffic": traffic, "traffic_source": traffic_src},
         "cpu_baseline": cpu,
+        "end_to_end": e2e,
     }
     print(json.dumps(line), flush=True)
 

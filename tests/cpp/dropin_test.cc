@@ -5,7 +5,8 @@
 //   dropin_test ring         README ring of 100, K50 L100 30 it 1e-3: prints "src key score" rows
 //   dropin_test known        known answers of test/grankTest.cc (exit 0 when all hold)
 //   dropin_test mcbad <case> / mcknown   the same for mccompletepathv2 (test/mccompletepathv2Test.cc)
-//   dropin_test e2e <scale>  RMAT graph as unordered_map, ppr::grank(K64, L128, 10 it) end to end
+//   dropin_test e2e <scale> [iters]  RMAT graph as unordered_map, ppr::grank(K64, L128, iters (10)) end
+//                                    to end (PPR_TIMING=1: flatten / device / materialise split on stderr)
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -86,6 +87,7 @@ int main(int argc, char** argv) {
   }
   if (mode == "e2e") {
     const int scale = atoi(argv[2]);
+    const int iters = argc > 3 ? atoi(argv[3]) : 10;
     const int64_t n = 1LL << scale;
     std::vector<int64_t> rp(n + 1);
     const int64_t m = ppr_rmat_generate(scale, 16, 0.57, 0.19, 0.19, 42, rp.data(), nullptr, 0);
@@ -97,7 +99,7 @@ int main(int argc, char** argv) {
       s.assign(col.begin() + rp[v], col.begin() + rp[v + 1]);
     }
     auto t1 = std::chrono::steady_clock::now();
-    auto res = ppr::grank(graph, 64, 128, 10, 0.85, -1.0);
+    auto res = ppr::grank(graph, 64, 128, iters, 0.85, -1.0);
     auto t2 = std::chrono::steady_clock::now();
     size_t entries = 0;
     for (auto& kv : res) entries += kv.second.size();

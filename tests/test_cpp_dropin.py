@@ -15,10 +15,8 @@ BIN = os.path.join(ROOT, "tests", "cpp", "_dropin_test")
 
 @pytest.fixture(scope="module")
 def dropin():
-    subprocess.run(["g++", "-std=c++11", "-O2", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "tests", "cpp", "dropin_test.cc"), "-o", BIN, "-pthread", "-L", PKG, "-lppr_hip",
-                    f"-Wl,-rpath,{PKG}"], check=True)
-    return BIN
+    from approximated_personalized_pagerank_amd import build
+    return build.build_dropin(force=True)
 
 
 @pytest.mark.parametrize("case,msg", [(0, "K must be positive"), (1, "L must be positive"), (2, "K must be <= L"),
