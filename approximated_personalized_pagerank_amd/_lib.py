@@ -109,7 +109,7 @@ def lib() -> ctypes.CDLL:
         "ppr_grank_plan_read_maxdiff": (ctypes.c_int, [vp, i32, ctypes.POINTER(f64)]),
         "ppr_grank_plan_finish": (ctypes.c_int, [vp, i32]),
         "ppr_grank_plan_row_bytes": (ctypes.c_int, [vp, ctypes.POINTER(i64)]),
-        "ppr_grank_plan_pack": (ctypes.c_int, [vp, i32, i64, i64, vp]),
+        "ppr_grank_plan_pack": (ctypes.c_int, [vp, i32, i64, i64, vp, i64]),
         "ppr_grank_plan_unpack": (ctypes.c_int, [vp, i32, i64, i64, vp]),
         "ppr_grank_plan_fetch": (ctypes.c_int, [vp, vp, vp, vp]),
         "ppr_grank_plan_fetch_slab": (ctypes.c_int, [vp, i32, vp, vp, vp]),
@@ -121,8 +121,8 @@ def lib() -> ctypes.CDLL:
         "ppr_grank_plan_comm_init": (ctypes.c_int, [vp, vp, i32, i32]),
         "ppr_grank_plan_shard_bounds": (ctypes.c_int, [vp, i32, i32, vp]),
         "ppr_grank_plan_run_sharded": (ctypes.c_int, [vp, u32, f64, vp]),
-        "ppr_grank_plan_pack_host": (ctypes.c_int, [vp, i32, i64, i64, vp]),
-        "ppr_grank_plan_unpack_host": (ctypes.c_int, [vp, i32, i64, i64, vp]),
+        "ppr_grank_plan_pack_host": (ctypes.c_int, [vp, i32, i64, i64, vp, i64, ctypes.POINTER(i64)]),
+        "ppr_grank_plan_unpack_host": (ctypes.c_int, [vp, i32, i64, i64, vp, i64]),
         "ppr_plan_fetch_slot": (ctypes.c_int, [vp, i32, vp, vp, vp]),
         "ppr_import_edge_csv": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(i64), ctypes.POINTER(i64), vp, vp, vp]),
         "ppr_mccp2_csr": (ctypes.c_int, [vp, u32, u32, u32, f64, ctypes.c_uint64, vp, vp, vp, vp, vp]),

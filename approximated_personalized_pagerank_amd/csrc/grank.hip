@@ -1188,43 +1188,88 @@ extern "C" int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, in
 }
 
 extern "C" int ppr_grank_plan_row_bytes(ppr_plan* p, int64_t* bytes) {
+  // bound of one row's share of a compact exchange block (merge_glb.h): offset + ids + scores
   if (!p || !bytes) return PPR_ERR_ARG;
   const int64_t Le = ((int64_t)p->L + 1) & ~1LL;
-  *bytes = 8 + 4 * Le + 8 * (int64_t)p->L + 8 + 2 * NRANGE;
+  *bytes = 8 + 4 * Le + 8 * (int64_t)p->L;
   return PPR_OK;
 }
 
-static int pack_common(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* buf, bool pack) {
-  if (!p || it < 0 || (!buf && end > begin)) return PPR_ERR_ARG;
+static int ensure_dev(unsigned char** ptr, size_t* cap, size_t need);
+
+struct XRange {
+  int64_t begin, cnt;
+  int nxt;
+  const int32_t* list;
+};
+
+static int xrange(ppr_plan* p, int32_t it, int64_t begin, int64_t end, XRange* x) {
+  if (!p || it < 0) return PPR_ERR_ARG;
   const int part = it & 1;
   begin = std::max<int64_t>(0, begin);
   end = std::min<int64_t>(p->nact[part], end);
-  if (end <= begin) return PPR_OK;
-  HIP_OK(hipSetDevice(p->device));
+  x->begin = begin;
+  x->cnt = std::max<int64_t>(0, end - begin);
   const IterArgs a = iter_args(p, it, false);
-  const int nxt = ((a.active == 1) ? a.sB : a.sA) ^ 1;
-  const DevSlab s = dev_slab(p);
+  x->nxt = ((a.active == 1) ? a.sB : a.sA) ^ 1;
+  x->list = p->d_act[part] + begin;
+  return PPR_OK;
+}
+
+// compact block of a range into buf (capacity cap >= 8 + cnt * row_bytes); the block's size is
+// also written to the device int64 *d_total when given. Asynchronous on the plan's stream.
+static int xpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, unsigned char* buf, int64_t cap,
+                 int64_t* d_total) {
+  XRange x;
+  int rc = xrange(p, it, begin, end, &x);
+  if (rc) return rc;
   int64_t rb = 0;
   ppr_grank_plan_row_bytes(p, &rb);
-  const int Le = (int)(((int64_t)p->L + 1) & ~1LL);
-  const int64_t cnt = end - begin;
-  const unsigned blocks = (unsigned)((cnt + 3) / 4);
-  if (pack)
-    hipLaunchKernelGGL(k_pack_rows, dim3(blocks), dim3(256), 0, p->stream, s, nxt, p->d_act[part] + begin, cnt,
-                       (unsigned char*)buf, rb, Le);
-  else
-    hipLaunchKernelGGL(k_unpack_rows, dim3(blocks), dim3(256), 0, p->stream, s, nxt, p->d_act[part] + begin, cnt,
-                       (const unsigned char*)buf, rb, Le);
+  if (!buf || cap < 8 + x.cnt * rb) return PPR_ERR_ARG;
+  HIP_OK(hipSetDevice(p->device));
+  hipStream_t st = p->stream;
+  int64_t* off = reinterpret_cast<int64_t*>(buf);
+  if (x.cnt == 0) {
+    HIP_OK(hipMemsetAsync(buf, 0, 8, st));
+    if (d_total) hipLaunchKernelGGL(k_xtotal, dim3(1), dim3(64), 0, st, (const int64_t*)off, (int64_t)0, d_total);
+    HIP_OK(hipGetLastError());
+    return PPR_OK;
+  }
+  const DevSlab s = dev_slab(p);
+  // row sizes into the payload area (free until the pack), scanned into the offset header
+  int64_t* sz = reinterpret_cast<int64_t*>(buf + 8 * (x.cnt + 1));
+  hipLaunchKernelGGL(k_xsize, dim3((unsigned)((x.cnt + 256) / 256)), dim3(256), 0, st, s, x.nxt, x.list, x.cnt, sz);
+  size_t tmp = 0;
+  HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, sz, off, (int)(x.cnt + 1), st));
+  rc = ensure_dev(&p->d_xtmp, &p->xtmp_bytes, tmp);
+  if (rc) return rc;
+  HIP_OK(hipcub::DeviceScan::ExclusiveSum(p->d_xtmp, tmp, sz, off, (int)(x.cnt + 1), st));
+  hipLaunchKernelGGL(k_xpack, dim3((unsigned)((x.cnt + 3) / 4)), dim3(256), 0, st, s, x.nxt, x.list, x.cnt, buf);
+  if (d_total) hipLaunchKernelGGL(k_xtotal, dim3(1), dim3(64), 0, st, (const int64_t*)off, x.cnt, d_total);
   HIP_OK(hipGetLastError());
   return PPR_OK;
 }
 
-extern "C" int ppr_grank_plan_pack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* dev_buf) {
-  return pack_common(p, it, begin, end, dev_buf, true);
+static int xunpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const unsigned char* buf) {
+  XRange x;
+  int rc = xrange(p, it, begin, end, &x);
+  if (rc) return rc;
+  if (x.cnt == 0) return PPR_OK;
+  if (!buf) return PPR_ERR_ARG;
+  HIP_OK(hipSetDevice(p->device));
+  hipLaunchKernelGGL(k_xunpack, dim3((unsigned)((x.cnt + 3) / 4)), dim3(256), 0, p->stream, dev_slab(p), x.nxt,
+                     x.list, x.cnt, buf);
+  HIP_OK(hipGetLastError());
+  return PPR_OK;
+}
+
+extern "C" int ppr_grank_plan_pack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* dev_buf,
+                                   int64_t cap) {
+  return xpack(p, it, begin, end, (unsigned char*)dev_buf, cap, nullptr);
 }
 
 extern "C" int ppr_grank_plan_unpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* dev_buf) {
-  return pack_common(p, it, begin, end, const_cast<void*>(dev_buf), false);
+  return xunpack(p, it, begin, end, (const unsigned char*)dev_buf);
 }
 
 extern "C" int ppr_grank_plan_fold_maxdiff(ppr_plan* p, int32_t it, double maxdiff) {
@@ -1279,6 +1324,8 @@ extern "C" int ppr_grank_plan_comm_init(ppr_plan* p, const void* id, int32_t nra
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   NCCL_OK(ncclCommInitRank(&p->comm, nranks, uid, rank));
+  int rc = ensure_dev(&p->d_xsz, &p->xsz_bytes, 8 * (size_t)nranks);
+  if (rc) return rc;
   p->nranks = nranks;
   p->rank = rank;
   return PPR_OK;
@@ -1329,6 +1376,7 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
   HIP_OK(hipMemsetAsync(p->d_stats, 0, 16, s));
   p->merge_launches = 0;
   p->merge_ms = 0.0;
+  p->x_bytes = 0;
   HIP_OK(hipEventRecord(p->ev_a, s));
   int rc = ppr_grank_plan_init(p);
   if (rc) return rc;
@@ -1345,26 +1393,36 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
     if (rc) return rc;
     unsigned long long* mdp = p->d_maxdiff + (it < PPR_MAX_ITER_STATS ? it : PPR_MAX_ITER_STATS);
     if (p->nranks > 1) {
-      // variable-size all-gather: every rank broadcasts its own rows (grouped). Ranges are balanced
-      // by work, not rows, so padding every rank to the largest range would multiply the bytes;
-      // each rank packs its rows in place at its offset of the receive buffer.
+      // variable-size all-gather of compact blocks (merge_glb.h): only the entries travel. The
+      // block sizes are all-gathered first (8 bytes per rank, read back to size the broadcasts),
+      // then every rank broadcasts its block from its send buffer (grouped; the root broadcasts
+      // in place, so it copies nothing) and unpacks the others'.
+      const int64_t mine = b[p->rank + 1] - b[p->rank];
+      rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, (size_t)(8 + mine * rb));
+      if (rc) return rc;
+      int64_t* d_sz = reinterpret_cast<int64_t*>(p->d_xsz);
+      rc = xpack(p, (int32_t)it, b[p->rank], b[p->rank + 1], p->d_xsend, (int64_t)p->xsend_bytes, d_sz + p->rank);
+      if (rc) return rc;
+      NCCL_OK(ncclAllGather(d_sz + p->rank, d_sz, 1, ncclInt64, p->comm, s));
+      std::vector<int64_t> sz(p->nranks);
+      HIP_OK(hipMemcpyAsync(sz.data(), d_sz, 8 * (size_t)p->nranks, hipMemcpyDeviceToHost, s));
+      HIP_OK(hipStreamSynchronize(s));
       std::vector<size_t> xo(p->nranks + 1, 0);
-      for (int r = 0; r < p->nranks; r++) xo[r + 1] = xo[r] + (size_t)(b[r + 1] - b[r]) * (size_t)rb;
-      if (xo[p->nranks]) {
-        rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, xo[p->nranks]);
+      for (int r = 0; r < p->nranks; r++) xo[r + 1] = xo[r] + (r == p->rank ? 0 : (size_t)sz[r]);
+      rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, std::max<size_t>(8, xo[p->nranks]));
+      if (rc) return rc;
+      p->x_bytes += xo[p->nranks];
+      NCCL_OK(ncclGroupStart());
+      for (int r = 0; r < p->nranks; r++) {
+        if (b[r + 1] == b[r]) continue;
+        unsigned char* dst = r == p->rank ? p->d_xsend : p->d_xrecv + xo[r];
+        NCCL_OK(ncclBroadcast(p->d_xsend, dst, (size_t)sz[r], ncclUint8, r, p->comm, s));
+      }
+      NCCL_OK(ncclGroupEnd());
+      for (int r = 0; r < p->nranks; r++) {
+        if (r == p->rank || b[r + 1] == b[r]) continue;
+        rc = xunpack(p, (int32_t)it, b[r], b[r + 1], p->d_xrecv + xo[r]);
         if (rc) return rc;
-        rc = ppr_grank_plan_pack(p, (int32_t)it, b[p->rank], b[p->rank + 1], p->d_xrecv + xo[p->rank]);
-        if (rc) return rc;
-        NCCL_OK(ncclGroupStart());
-        for (int r = 0; r < p->nranks; r++)
-          if (xo[r + 1] > xo[r])
-            NCCL_OK(ncclBroadcast(p->d_xrecv + xo[r], p->d_xrecv + xo[r], xo[r + 1] - xo[r], ncclUint8, r, p->comm, s));
-        NCCL_OK(ncclGroupEnd());
-        for (int r = 0; r < p->nranks; r++) {
-          if (r == p->rank || b[r + 1] == b[r]) continue;
-          rc = ppr_grank_plan_unpack(p, (int32_t)it, b[r], b[r + 1], p->d_xrecv + xo[r]);
-          if (rc) return rc;
-        }
       }
       // maxDiff >= 0: the IEEE bit patterns order like the values, so an integer MAX is exact
       NCCL_OK(ncclAllReduce(mdp, mdp, 1, ncclUint64, ncclMax, p->comm, s));
@@ -1396,32 +1454,45 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
   return PPR_OK;
 }
 
-// host-staged row exchange (gloo rehearsal on a single GPU; the RCCL path never uses these)
-extern "C" int ppr_grank_plan_pack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* host) {
-  if (!p || it < 0) return PPR_ERR_ARG;
+// host-staged row exchange (gloo rehearsal on a single GPU; the RCCL path never uses these):
+// the same compact blocks, copied through host memory. Synchronous.
+extern "C" int ppr_grank_plan_pack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* host,
+                                        int64_t cap, int64_t* bytes) {
+  if (!p || it < 0 || !host || !bytes) return PPR_ERR_ARG;
+  XRange x;
+  int rc = xrange(p, it, begin, end, &x);
+  if (rc) return rc;
+  rc = ensure_dev(&p->d_xsz, &p->xsz_bytes, 8);
+  if (rc) return rc;
   int64_t rb = 0;
   ppr_grank_plan_row_bytes(p, &rb);
-  const int64_t cnt = std::max<int64_t>(0, end - begin);
-  if (!cnt) return PPR_OK;
-  int rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, (size_t)cnt * rb);
+  rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, (size_t)(8 + x.cnt * rb));
   if (rc) return rc;
-  rc = ppr_grank_plan_pack(p, it, begin, end, p->d_xsend);
+  int64_t* d_tot = reinterpret_cast<int64_t*>(p->d_xsz);
+  rc = xpack(p, it, begin, end, p->d_xsend, (int64_t)p->xsend_bytes, d_tot);
   if (rc) return rc;
-  HIP_OK(hipMemcpyAsync(host, p->d_xsend, (size_t)cnt * rb, hipMemcpyDeviceToHost, p->stream));
+  int64_t tot = 0;
+  HIP_OK(hipMemcpyAsync(&tot, d_tot, 8, hipMemcpyDeviceToHost, p->stream));
   HIP_OK(hipStreamSynchronize(p->stream));
+  if (tot > cap) return PPR_ERR_ARG;
+  HIP_OK(hipMemcpyAsync(host, p->d_xsend, (size_t)tot, hipMemcpyDeviceToHost, p->stream));
+  HIP_OK(hipStreamSynchronize(p->stream));
+  *bytes = tot;
   return PPR_OK;
 }
 
-extern "C" int ppr_grank_plan_unpack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* host) {
+extern "C" int ppr_grank_plan_unpack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* host,
+                                          int64_t bytes) {
   if (!p || it < 0) return PPR_ERR_ARG;
-  int64_t rb = 0;
-  ppr_grank_plan_row_bytes(p, &rb);
-  const int64_t cnt = std::max<int64_t>(0, end - begin);
-  if (!cnt) return PPR_OK;
-  int rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, (size_t)cnt * rb);
+  XRange x;
+  int rc = xrange(p, it, begin, end, &x);
   if (rc) return rc;
-  HIP_OK(hipMemcpyAsync(p->d_xrecv, host, (size_t)cnt * rb, hipMemcpyHostToDevice, p->stream));
-  rc = ppr_grank_plan_unpack(p, it, begin, end, p->d_xrecv);
+  if (x.cnt == 0) return PPR_OK;
+  if (!host || bytes < 8 * (x.cnt + 1)) return PPR_ERR_ARG;
+  rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, (size_t)bytes);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(p->d_xrecv, host, (size_t)bytes, hipMemcpyHostToDevice, p->stream));
+  rc = xunpack(p, it, begin, end, p->d_xrecv);
   if (rc) return rc;
   HIP_OK(hipStreamSynchronize(p->stream));
   return PPR_OK;

@@ -141,50 +141,71 @@ __global__ void __launch_bounds__(256) k_topk(DevSlab s, const uint8_t* part, in
   if (lane_id() == 0) olen[v] = k;
 }
 
-// Row exchange for source sharding. Packed row r (of sources list[0..count)) occupies
-// row_bytes = 8 + 4*Le + 8*L + 8 + 2*NRANGE bytes: int32 len, int32 pad, int32 ids[Le] (Le = L
-// rounded up to even, so the f64 scores stay 8-byte aligned), f64 scores[L], f64 row minimum,
-// u16 range index[NRANGE]. Rows are the next-slot baskets the iteration wrote (stored order).
-__device__ __forceinline__ void packed_row_parts(unsigned char* row, int Le, int L, int32_t*& rid, double*& rsc,
-                                                 double*& rmn, uint16_t*& rix) {
-  rid = reinterpret_cast<int32_t*>(row + 8);
-  rsc = reinterpret_cast<double*>(row + 8 + 4 * (int64_t)Le);
-  rmn = reinterpret_cast<double*>(row + 8 + 4 * (int64_t)Le + 8 * (int64_t)L);
-  rix = reinterpret_cast<uint16_t*>(row + 8 + 4 * (int64_t)Le + 8 * (int64_t)L + 8);
+// Row exchange for source sharding: one compact block per active-list range of `count` rows (the
+// next-slot rows the iteration wrote, in stored order):
+//   int64 off[count + 1]                payload offset of row r (off[0] = 0, off[count] = payload bytes)
+//   payload: per row int32 ids[Le] f64 scores[len]   (Le = len rounded up to even: 8-B aligned)
+// A row of len entries takes 12 len (+4 when len is odd) bytes, so len = (off[r+1] - off[r]) / 12.
+// Only the entries travel: the receiver rebuilds the row minimum and the 64-range index from them
+// exactly as write_row does (ppr_common.h), so a block is 8 + 12 len bytes per row instead of the
+// slab's fixed 4 Le + 8 L + 8 + 128.
+__device__ __forceinline__ int64_t xrow_bytes(int len) { return 12 * (int64_t)len + 4 * (len & 1); }
+
+__global__ void k_xsize(DevSlab s, int nxt, const int32_t* list, int64_t count, int64_t* sz) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < count) sz[r] = xrow_bytes(s.len[s.lrow(nxt, list[r])]);
+  else if (r == count) sz[r] = 0;
 }
 
-__global__ void k_pack_rows(DevSlab s, int nxt, const int32_t* list, int64_t count,
-                            unsigned char* buf, int64_t row_bytes, int Le) {
+// block bytes of a packed range -> *total (the size the ranks exchange before the payload)
+__global__ void k_xtotal(const int64_t* off, int64_t count, int64_t* total) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *total = 8 * (count + 1) + off[count];
+}
+
+__global__ void k_xpack(DevSlab s, int nxt, const int32_t* list, int64_t count, unsigned char* buf) {
   const int64_t r = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
   if (r >= count) return;
+  const int64_t* off = reinterpret_cast<const int64_t*>(buf);
   const int v = list[r];
-  unsigned char* row = buf + r * row_bytes;
   const int len = s.len[s.lrow(nxt, v)];
-  int32_t* rid; double* rsc; double* rmn; uint16_t* rix;
-  packed_row_parts(row, Le, s.L, rid, rsc, rmn, rix);
+  unsigned char* row = buf + 8 * (count + 1) + off[r];
+  int32_t* rid = reinterpret_cast<int32_t*>(row);
+  double* rsc = reinterpret_cast<double*>(row + 4 * (int64_t)((len + 1) & ~1));
   const int64_t src = s.row(nxt, v);
   for (int i = lane_id(); i < len; i += WAVE) { rid[i] = s.ids[src + i]; rsc[i] = s.sc[src + i]; }
-  rix[lane_id()] = s.rix[s.xrow(nxt, v) + lane_id()];
-  if (lane_id() == 0) {
-    reinterpret_cast<int32_t*>(row)[0] = len;
-    reinterpret_cast<int32_t*>(row)[1] = 0;
-    *rmn = s.rmin[s.lrow(nxt, v)];
-  }
 }
 
-__global__ void k_unpack_rows(DevSlab s, int nxt, const int32_t* list, int64_t count,
-                              const unsigned char* buf, int64_t row_bytes, int Le) {
+__global__ void k_xunpack(DevSlab s, int nxt, const int32_t* list, int64_t count, const unsigned char* buf) {
   const int64_t r = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
   if (r >= count) return;
+  const int64_t* off = reinterpret_cast<const int64_t*>(buf);
   const int v = list[r];
-  unsigned char* row = const_cast<unsigned char*>(buf) + r * row_bytes;
-  const int len = reinterpret_cast<const int32_t*>(row)[0];
-  int32_t* rid; double* rsc; double* rmn; uint16_t* rix;
-  packed_row_parts(row, Le, s.L, rid, rsc, rmn, rix);
+  const int len = (int)((off[r + 1] - off[r]) / 12);
+  const unsigned char* row = buf + 8 * (count + 1) + off[r];
+  const int32_t* rid = reinterpret_cast<const int32_t*>(row);
+  const double* rsc = reinterpret_cast<const double*>(row + 4 * (int64_t)((len + 1) & ~1));
   const int64_t dst = s.row(nxt, v);
-  for (int i = lane_id(); i < len; i += WAVE) { s.ids[dst + i] = rid[i]; s.sc[dst + i] = rsc[i]; }
-  s.rix[s.xrow(nxt, v) + lane_id()] = rix[lane_id()];
-  if (lane_id() == 0) { s.len[s.lrow(nxt, v)] = len; s.rmin[s.lrow(nxt, v)] = *rmn; }
+  uint64_t mn = ~0ull;
+  for (int i = lane_id(); i < len; i += WAVE) {
+    const double x = rsc[i];
+    s.ids[dst + i] = rid[i];
+    s.sc[dst + i] = x;
+    const uint64_t b = dbits(x);
+    mn = b < mn ? b : mn;
+  }
+  mn = wave_min_u64(mn);
+  // lane q: entries whose key's hash range is <= q (the row ascends in hash_b order)
+  const uint32_t q = (uint32_t)lane_id();
+  int lp = 1;
+  while (lp < len) lp <<= 1;
+  int pos = 0;
+  for (int b = lp; b; b >>= 1)
+    if (pos + b <= len && row_range(s.key(rid[pos + b - 1])) <= q) pos += b;
+  s.rix[s.xrow(nxt, v) + q] = (uint16_t)pos;
+  if (lane_id() == 0) {
+    s.len[s.lrow(nxt, v)] = len;
+    s.rmin[s.lrow(nxt, v)] = len ? bitsd(mn) : 0.0;
+  }
 }
 
 __global__ void k_zero_u64(unsigned long long* p, int n) {

@@ -101,9 +101,12 @@ struct ppr_plan {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   std::vector<double> work[2];        // per active source: merge work estimate (list order)
-  unsigned char* d_xsend = nullptr;   // packed rows of this rank
-  unsigned char* d_xrecv = nullptr;   // all-gathered rows
-  size_t xsend_bytes = 0, xrecv_bytes = 0;
+  unsigned char* d_xsend = nullptr;   // compact block of this rank's rows (merge_glb.h)
+  unsigned char* d_xrecv = nullptr;   // the other ranks' blocks
+  unsigned char* d_xsz = nullptr;     // int64 block size per rank (all-gathered)
+  unsigned char* d_xtmp = nullptr;    // scan temporary of the block offsets
+  size_t xsend_bytes = 0, xrecv_bytes = 0, xsz_bytes = 0, xtmp_bytes = 0;
+  int64_t x_bytes = 0;                // block bytes received by this rank in the last sharded run
   int64_t merge_launches = 0;
   double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_m0 = nullptr, ev_m1 = nullptr;
@@ -183,7 +186,7 @@ inline void plan_free(ppr_plan* p) {
   if (p->stream3) hipStreamDestroy(p->stream3);
   if (p->stream4) hipStreamDestroy(p->stream4);
   if (p->comm) ncclCommDestroy(p->comm);
-  hipFree(p->d_xsend); hipFree(p->d_xrecv);
+  hipFree(p->d_xsend); hipFree(p->d_xrecv); hipFree(p->d_xsz); hipFree(p->d_xtmp);
   if (p->h_hub_pin) hipHostFree(p->h_hub_pin);
   if (p->h_desc_pin) hipHostFree(p->h_desc_pin);
   if (p->d_diag) {

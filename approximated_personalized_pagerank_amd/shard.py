@@ -10,7 +10,10 @@ stopping rule (include/grank.h:90-94,140) is evaluated identically on every rank
 bit-identical to the single-GPU run (the per-source maths does not depend on the sharding).
 
 The driver is generic over an *engine* (GpuEngine below wraps GrankPlan; the CPU tests use the
-oracle-backed oracle.OracleEngine) and a *comm* (all_gather of byte rows, all_reduce max).
+oracle-backed oracle.OracleEngine) and a *comm* (all-gather of variable-size byte blocks,
+all_reduce max). Rows travel as compact blocks (include/ppr_hip.h, ppr_grank_plan_pack): an int64
+offset per row, then each row's ids and scores -- only the entries, 8 + 12 len bytes per row;
+pack_block / unpack_block below are the format's host-side statement.
 """
 from __future__ import annotations
 
@@ -44,20 +47,65 @@ def balanced_bounds(weights: np.ndarray, world: int) -> List[int]:
     return b
 
 
-class TorchComm:  # collectives on torch tensors (tests; the GPU path never touches torch's HIP)
-    """all_gather / all_reduce over torch.distributed (RCCL on GPUs, gloo on CPU)."""
+def pack_block(rows) -> np.ndarray:
+    """Compact exchange block of a list of rows [(ids int32[len], scores f64[len]), ...] in stored
+    order: int64 off[cnt + 1], then per row int32 ids padded to an even count and f64 scores."""
+    sizes = np.array([12 * len(i) + 4 * (len(i) & 1) for i, _ in rows], dtype=np.int64)
+    off = np.zeros(len(rows) + 1, dtype=np.int64)
+    np.cumsum(sizes, out=off[1:])
+    hdr = 8 * (len(rows) + 1)
+    out = np.zeros(hdr + int(off[-1]), dtype=np.uint8)
+    out[:hdr] = off.view(np.uint8)
+    for r, (ids, sc) in enumerate(rows):
+        n = len(ids)
+        o = hdr + int(off[r])
+        out[o:o + 4 * n] = np.ascontiguousarray(ids, dtype=np.int32).view(np.uint8)
+        o += 4 * (n + (n & 1))
+        out[o:o + 8 * n] = np.ascontiguousarray(sc, dtype=np.float64).view(np.uint8)
+    return out
 
-    def __init__(self, device):
+
+def unpack_block(block: np.ndarray, cnt: int):
+    """Rows of a compact block of cnt rows (inverse of pack_block)."""
+    block = np.asarray(block, dtype=np.uint8)
+    hdr = 8 * (cnt + 1)
+    off = block[:hdr].view(np.int64)
+    rows = []
+    for r in range(cnt):
+        n = int((off[r + 1] - off[r]) // 12)
+        o = hdr + int(off[r])
+        ids = block[o:o + 4 * n].view(np.int32).copy()
+        o += 4 * (n + (n & 1))
+        rows.append((ids, block[o:o + 8 * n].view(np.float64).copy()))
+    return rows
+
+
+class TorchComm:  # collectives on torch tensors (tests; the GPU path never touches torch's HIP)
+    """all-gather of variable-size blocks / all_reduce over torch.distributed (gloo on CPU)."""
+
+    def __init__(self, device=None):
         import torch
         import torch.distributed as dist
-        self.torch, self.dist, self.device = torch, dist, device
+        self.torch, self.dist = torch, dist
+        self.device = device if device is not None else torch.device("cpu")
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
 
-    def all_gather_rows(self, send, nbytes_max: int):
+    def all_gather_blocks(self, block: np.ndarray) -> List[np.ndarray]:
+        """Every rank's block (sizes all-gathered first, then the blocks padded to the largest)."""
         torch = self.torch
-        out = torch.empty(self.world * nbytes_max, dtype=torch.uint8, device=self.device)
+        sz = torch.tensor([len(block)], dtype=torch.int64, device=self.device)
+        sizes = torch.empty(self.world, dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(sizes, sz)
+        sizes = [int(x) for x in sizes.cpu()]
+        mx = max(sizes)
+        if mx == 0:
+            return [np.zeros(0, dtype=np.uint8) for _ in sizes]
+        send = torch.zeros(mx, dtype=torch.uint8, device=self.device)
+        send[:len(block)] = torch.from_numpy(np.ascontiguousarray(block)).to(self.device)
+        out = torch.empty(self.world * mx, dtype=torch.uint8, device=self.device)
         self.dist.all_gather_into_tensor(out, send)
-        return out
+        out = out.cpu().numpy()
+        return [out[r * mx:r * mx + sizes[r]] for r in range(self.world)]
 
     def all_reduce_max(self, x: float) -> float:
         torch = self.torch
@@ -69,17 +117,15 @@ class TorchComm:  # collectives on torch tensors (tests; the GPU path never touc
         self.dist.barrier()
 
 
-def run_sharded(engine, comm, iterations: int, tolerance: float, weights, alloc_send, to_engine_buf,
-                bounds=None) -> int:
+def run_sharded(engine, comm, iterations: int, tolerance: float, weights, bounds=None) -> int:
     """GRank with the active sources of every iteration split over comm.world ranks.
     weights[p]: work estimate of partition p's active list (engine.active_list order), or
-    bounds[p]: explicit range boundaries per partition.
-    alloc_send(nbytes) -> a send buffer the engine can pack into; to_engine_buf(t) -> what
-    engine.unpack accepts. Returns the number of iterations run."""
+    bounds[p]: explicit range boundaries per partition. engine.pack(it, b, e) -> compact block
+    (np.uint8) of the rows the rank wrote; engine.unpack(it, b, e, block) installs another rank's.
+    Returns the number of iterations run."""
     rank, world = comm.rank, comm.world
     if bounds is None:
         bounds = [balanced_bounds(weights[p], world) for p in (0, 1)]
-    rb = engine.row_bytes
     engine.init()
     md = [tolerance, tolerance]
     it = 0
@@ -87,14 +133,11 @@ def run_sharded(engine, comm, iterations: int, tolerance: float, weights, alloc_
         bd = bounds[it & 1]
         b, e = bd[rank], bd[rank + 1]
         engine.iterate(it, b, e)
-        rows_max = max(bd[r + 1] - bd[r] for r in range(world))
-        if rows_max > 0:
-            send = alloc_send(rows_max * rb)
-            engine.pack_into(it, b, e, send)
-            recv = comm.all_gather_rows(send, rows_max * rb)
+        if bd[world] > bd[0]:
+            blocks = comm.all_gather_blocks(engine.pack(it, b, e))
             for r in range(world):
                 if r != rank and bd[r + 1] > bd[r]:
-                    engine.unpack(it, bd[r], bd[r + 1], to_engine_buf(recv, r * rows_max * rb))
+                    engine.unpack(it, bd[r], bd[r + 1], blocks[r])
         engine.commit(it)
         d = comm.all_reduce_max(engine.read_maxdiff(it))
         engine.fold_maxdiff(it, d)
@@ -132,11 +175,18 @@ class GpuEngine:
     def iterate(self, it, b, e):
         self.plan.iterate(it, b, e)
 
-    def pack_into(self, it, b, e, send):
-        self._lib.check(self._lib.lib().ppr_grank_plan_pack_host(self.plan._p, it, b, e, send.data_ptr()), "pack")
+    def pack(self, it, b, e):
+        cap = 8 + max(0, e - b) * self.row_bytes
+        out = np.empty(cap, dtype=np.uint8)
+        nb = self._ct.c_int64(0)
+        self._lib.check(self._lib.lib().ppr_grank_plan_pack_host(self.plan._p, it, b, e, self._lib.ptr(out), cap,
+                                                                 self._ct.byref(nb)), "pack")
+        return out[:nb.value]
 
-    def unpack(self, it, b, e, buf):
-        self._lib.check(self._lib.lib().ppr_grank_plan_unpack_host(self.plan._p, it, b, e, buf), "unpack")
+    def unpack(self, it, b, e, block):
+        block = np.ascontiguousarray(block, dtype=np.uint8)
+        self._lib.check(self._lib.lib().ppr_grank_plan_unpack_host(self.plan._p, it, b, e, self._lib.ptr(block),
+                                                                   len(block)), "unpack")
 
     def commit(self, it):
         pass  # the slot flip is implicit on the device
@@ -151,27 +201,8 @@ class GpuEngine:
         self.plan.finish(iterations_run)
 
 
-class CpuComm:
+class CpuComm(TorchComm):
     """gloo collectives on host tensors (bootstrap and rehearsal)."""
-
-    def __init__(self):
-        import torch
-        import torch.distributed as dist
-        self.torch, self.dist = torch, dist
-        self.rank, self.world = dist.get_rank(), dist.get_world_size()
-
-    def all_gather_rows(self, send, nbytes_max):
-        out = self.torch.empty(self.world * nbytes_max, dtype=self.torch.uint8)
-        self.dist.all_gather_into_tensor(out, send)
-        return out
-
-    def all_reduce_max(self, x):
-        t = self.torch.tensor([x], dtype=self.torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def barrier(self):
-        self.dist.barrier()
 
 
 def device_count() -> int:
@@ -229,9 +260,7 @@ class ShardedGrank:
             self._lib.check(self._lib.lib().ppr_grank_plan_shard_bounds(self.plan._p, p, self.comm.world,
                                                                         self._lib.ptr(b)), "bounds")
             weights.append([int(x) for x in b])  # python ints: ctypes rejects numpy scalars
-        its = run_sharded(self.eng, self.comm, iterations, tolerance, None,
-                          lambda nb: self.torch.empty(nb, dtype=self.torch.uint8),
-                          lambda recv, off: int(recv.data_ptr() + off), bounds=weights)
+        its = run_sharded(self.eng, self.comm, iterations, tolerance, None, bounds=weights)
         self.plan.iterations_run = its
         return its
 

@@ -125,14 +125,15 @@ int ppr_grank_plan_iterate(ppr_plan* p, int32_t it, int64_t begin, int64_t end);
 int ppr_grank_plan_read_maxdiff(ppr_plan* p, int32_t it, double* maxdiff); /* syncs */
 int ppr_grank_plan_finish(ppr_plan* p, int32_t iterations_run);
 
-/* Row exchange for source sharding: pack/unpack of active-list ranges of the rows iteration `it`
- * wrote into a contiguous device buffer of fixed-size rows: int32 len, int32 pad, int32 ids[Le],
- * f64 scores[L], f64 row minimum, uint16 range index[64] (Le = L rounded up to even; size from
- * ppr_grank_plan_row_bytes). Slab rows are kept in key-hash order, not score order; the range
- * index and minimum travel with them so the receiving rank's merge can use them unchanged.
+/* Row exchange for source sharding: pack/unpack of an active-list range of the rows iteration `it`
+ * wrote, as one compact block: int64 off[cnt + 1] (payload offset per row, off[cnt] = payload
+ * bytes), then per row int32 ids[Le] and f64 scores[len] (Le = len rounded up to even; a row
+ * takes 12 len (+4 if len is odd) bytes, so len = (off[r+1] - off[r]) / 12). Only the entries
+ * travel; the receiver rebuilds each row's minimum and hash-range index. Block size =
+ * 8 (cnt + 1) + off[cnt] <= 8 + cnt * ppr_grank_plan_row_bytes; `cap` is the buffer's capacity.
  * Asynchronous on the plan's stream. */
 int ppr_grank_plan_row_bytes(ppr_plan* p, int64_t* bytes);
-int ppr_grank_plan_pack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* dev_buf);
+int ppr_grank_plan_pack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* dev_buf, int64_t cap);
 int ppr_grank_plan_unpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* dev_buf);
 /* Active sources of iteration `it` in list order (host copy, nact entries), and the write-back of
  * an all-reduced maxDiff for a sharded iteration. */
@@ -143,18 +144,21 @@ int ppr_grank_plan_fold_maxdiff(ppr_plan* p, int32_t it, double maxdiff);
  * Rank 0 creates a 128-byte RCCL unique id, the caller broadcasts it (any channel), and every rank
  * calls ppr_grank_plan_comm_init. ppr_grank_plan_run_sharded then runs the whole job like
  * ppr_grank_plan_run, but each rank merges only its work-balanced range of every iteration's
- * active list (ppr_grank_plan_shard_bounds) and the written rows are exchanged with one
- * grouped set of ncclBroadcast calls (an all-gather of variable-size ranges, no padding) on
- * the plan's stream; maxDiff is combined with ncclAllReduce(MAX) so every rank
+ * active list (ppr_grank_plan_shard_bounds) and the written rows are exchanged as compact blocks:
+ * an ncclAllGather of the block sizes, then one grouped set of ncclBroadcast calls (an
+ * all-gather of variable-size blocks, no padding) on the plan's stream; maxDiff is combined with ncclAllReduce(MAX) so every rank
  * applies the reference's stopping rule to the same value. Results equal the 1-GPU run. */
 int ppr_device_count(int32_t* count);
 int ppr_comm_unique_id(void* id128);
 int ppr_grank_plan_comm_init(ppr_plan* p, const void* id128, int32_t nranks, int32_t rank);
 int ppr_grank_plan_shard_bounds(ppr_plan* p, int32_t it, int32_t nranks, int64_t* bounds);
 int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance, ppr_stats* st);
-/* host-staged variants of pack/unpack (rehearsal without RCCL; synchronous) */
-int ppr_grank_plan_pack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* host_buf);
-int ppr_grank_plan_unpack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* host_buf);
+/* host-staged variants of pack/unpack (rehearsal without RCCL; synchronous): pack_host writes the
+ * block (at most cap bytes) and its size to *bytes; unpack_host takes a block of `bytes` bytes */
+int ppr_grank_plan_pack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* host_buf, int64_t cap,
+                             int64_t* bytes);
+int ppr_grank_plan_unpack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const void* host_buf,
+                               int64_t bytes);
 
 /* Downloads: final top-K (n*K) and the current L-slab (n*L, len per node; each row returned
  * sorted by (score desc, id asc) -- the device keeps rows in key-hash order). */

@@ -31,9 +31,7 @@ def _worker(rank, world, port, scale, K, L, iters, tol, outdir):
     comm = shard.TorchComm(torch.device("cpu"))
     w = shard.work_estimate(g.row_ptr, g.col, L)
     weights = [w[eng.active_list(p)] for p in (0, 1)]
-    its = shard.run_sharded(eng, comm, iters, tol, weights,
-                            lambda nb: torch.zeros(nb, dtype=torch.uint8),
-                            lambda recv, off: recv.numpy()[off:])
+    its = shard.run_sharded(eng, comm, iters, tol, weights)
     ids, sc, lens = eng.fetch()
     np.savez(os.path.join(outdir, f"r{rank}.npz"), ids=ids, sc=sc, lens=lens, its=its,
              md=np.array([eng.md[i] for i in range(its)]))
@@ -64,3 +62,19 @@ def test_balanced_bounds():
     assert shard.balanced_bounds(np.zeros(0), 3) == [0, 0, 0, 0]
     b = shard.balanced_bounds(np.ones(10), 4)
     assert b == sorted(b) and b[-1] == 10
+
+
+def test_compact_block_round_trip():
+    """pack_block / unpack_block: empty rows, odd and even lengths, sizes 8 + 12 len (+4 if odd)"""
+    rng = np.random.default_rng(3)
+    rows = []
+    for n in [0, 1, 2, 3, 7, 64, 0, 5]:
+        rows.append((rng.integers(0, 1 << 30, n).astype(np.int32), rng.random(n)))
+    blk = shard.pack_block(rows)
+    assert len(blk) == 8 * (len(rows) + 1) + sum(12 * len(i) + 4 * (len(i) & 1) for i, _ in rows)
+    assert len(blk) % 8 == 0
+    back = shard.unpack_block(blk, len(rows))
+    for (i0, s0), (i1, s1) in zip(rows, back):
+        assert np.array_equal(i0, i1) and np.array_equal(s0.view(np.uint64), s1.view(np.uint64))
+    assert shard.unpack_block(shard.pack_block([]), 0) == []
+    assert len(shard.pack_block([])) == 8
