@@ -238,6 +238,12 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_mix = e10 ? std::max(0, std::min(HUB_MAX_LOGP, atoi(e10))) : 6;
     const char* e9 = getenv("PPR_HUB_TILE_PB");
     p->hub_tile_pb = e9 ? std::max(0, std::min(64, atoi(e9))) : HUB_TILE_PER_BUCKET;
+    const char* e9b = getenv("PPR_HUB_TILE_CAND");
+    if (e9b) p->hub_tile_cand = std::max(256, std::min(1 << 20, atoi(e9b)));
+    const char* e9d = getenv("PPR_FUSED_MAX");
+    if (e9d) p->fused_max = std::max(0LL, atoll(e9d));
+    const char* e9c = getenv("PPR_HUB_LONG_MIN");
+    if (e9c) p->hub_long_min = std::max(0LL, atoll(e9c));
     const char* e8 = getenv("PPR_HUB_BUDGET");
     if (e8) p->hub_budget = std::max<int64_t>(1024, std::min<int64_t>(1LL << 28, atoll(e8)));
     // hot pass (merge_hot.h): PPR_HOT_N members (0 = off), built at iteration PPR_HOT_AT from
@@ -543,6 +549,12 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   } else {
     for (size_t i = 0; i < nbig; i++) order[i] = (uint32_t)i;
   }
+  // Long tiles (tile_pb candidates per bucket) cut the scatter's partial-line stores but leave
+  // fewer tiles per source: they pay only when the call has hub work enough to fill the chip
+  // anyway (a GRank iteration: billions of candidates), not for the few lone hubs of an MC level.
+  int64_t need_all = 0;
+  for (size_t i = 0; i < nbig; i++) need_all += cand[i];
+  const int tile_pb = need_all >= p->hub_long_min ? p->hub_tile_pb : 1;
   {
     size_t oi = 0;
     while (oi < nbig) {
@@ -562,7 +574,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
         const int logP = seg ? lseg : logp_of(need);
         const int P = 1 << logP;
         // tile = tw successors (windows of 64 on one wave); large partitions get long tiles
-        const int64_t tcand = std::max<int64_t>(HUB_TILE_CAND, (int64_t)p->hub_tile_pb << logP);
+        const int64_t tcand = std::max<int64_t>(p->hub_tile_cand, (int64_t)tile_pb << logP);
         const int64_t tw0 = std::max<int64_t>(1, tcand / L);
         const int tw = (int)(tw0 > WAVE ? (tw0 + WAVE - 1) / WAVE * WAVE : tw0);
         const int T = seg ? 0 : (int)((deg + tw - 1) / tw);
@@ -839,6 +851,12 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     HIP_OK(hipGetLastError());
     p->merge_launches++;
   }
+  if (a.mc && !hot_any) {
+    // MC combine: the overflow count is read with the next level's classification (one host
+    // sync per level; run_merge_impl redoes that level's classification when it is non-zero)
+    p->ovl_pending = d_ovl;
+    return PPR_OK;
+  }
   int32_t novf = 0;
   HIP_OK(hipMemcpyAsync(&novf, d_ovl, 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
@@ -872,89 +890,11 @@ int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count
   return PPR_OK;
 }
 
-static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
-                          unsigned long long* maxdiff) {
+// HBM-table path (k_merge_glb) for sources beyond every LDS tier and LDS-table overflows
+static int run_glb(ppr_plan* p, const IterArgs& a, std::vector<int32_t>& big, unsigned long long* maxdiff) {
   hipStream_t st = p->stream;
   DevGraph g{p->d_rp, p->d_colx, p->n};
   const DevSlab s = dev_slab(p);
-  HIP_OK(hipMemsetAsync(p->d_tier_cnt, 0, sizeof(uint32_t) * (NLISTS + 2), st));
-  const int64_t nb = (count + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-  hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(256), 0, st, g, s, a, list, count,
-                     p->d_tier_cap, p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big);
-  HIP_OK(hipGetLastError());
-  if (!a.unit && p->max_deg > CLS_BIG_DEG) {
-    hipLaunchKernelGGL(k_classify_big, dim3(256), dim3(CLS_BIG_THREADS), 0, st, g, s, a, p->d_tier_cap,
-                       p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big);
-  }
-  HIP_OK(hipGetLastError());
-  uint32_t cnt[NLISTS + 1];
-  HIP_OK(hipMemcpyAsync(cnt, p->d_tier_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
-  HIP_OK(hipStreamSynchronize(st));
-  // the classification is complete (host sync): the wave tiers need no event to start on stream3
-  hipStream_t sw = p->stream3 ? p->stream3 : st;
-  for (int t = 0; t < NT; t++) {
-    if (!cnt[t] || !p->tierT[t]) continue;
-    // one wave per block by default: no LDS left unusable by a 4-wave block granularity
-    const int wpb = p->wave_wpb;
-    const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * wpb;
-    const int64_t blocks = ((int64_t)cnt[t] + wpb - 1) / wpb;
-    hipLaunchKernelGGL(k_merge_lds, dim3((unsigned)blocks), dim3(64 * wpb), bytes, sw, g, s, a,
-                       p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], p->tierT[t], p->Lp,
-                       maxdiff, p->d_stats);
-    HIP_OK(hipGetLastError());
-    p->merge_launches++;
-  }
-  if (cnt[TIER_WG]) {
-    hipLaunchKernelGGL(k_merge_wg, dim3(cnt[TIER_WG]), dim3(WG_THREADS), p->wg_lds, st, g, s, a,
-                       p->d_tier_lists + (int64_t)TIER_WG * p->n, (int64_t)cnt[TIER_WG], p->d_cand,
-                       p->Lp, maxdiff, p->d_stats, p->d_ovf, p->d_tier_cnt + NLISTS);
-    HIP_OK(hipGetLastError());
-    p->merge_launches++;
-    HIP_OK(hipMemcpyAsync(&cnt[NLISTS], p->d_tier_cnt + NLISTS, 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-  }
-  // sources beyond the workgroup tier, plus workgroup-tier overflows
-  std::vector<int32_t> big;
-  auto pull = [&](const int32_t* dptr, uint32_t k) -> int {
-    if (!k) return PPR_OK;
-    std::vector<int32_t> tmp(k);
-    HIP_OK(hipMemcpyAsync(tmp.data(), dptr, 4 * (size_t)k, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    big.insert(big.end(), tmp.begin(), tmp.end());
-    return PPR_OK;
-  };
-  for (int t = 0; t < NT; t++)
-    if (cnt[t] && !p->tierT[t]) { int r = pull(p->d_tier_lists + (int64_t)t * p->n, cnt[t]); if (r) return r; }
-  { int r = pull(p->d_ovf, cnt[NLISTS]); if (r) return r; }
-  if (cnt[TIER_BIG]) {
-    const size_t nh = cnt[TIER_BIG];
-    {
-      size_t capb = p->h_hub_cap * 12;
-      void* ptr = p->h_hub_pin;
-      int r = ensure_pinned(&ptr, &capb, 12 * nh);
-      if (r) return r;
-      p->h_hub_pin = (int32_t*)ptr;
-      p->h_hub_cap = capb / 12;
-    }
-    int32_t* hubs = p->h_hub_pin;
-    int32_t* hcand = p->h_hub_pin + nh;  // | out-degrees at hcand + nh
-    HIP_OK(hipMemcpyAsync(hubs, p->d_tier_lists + (int64_t)TIER_BIG * p->n, 4 * nh, hipMemcpyDeviceToHost, st));
-    // candidate counts and degrees of the hub sources only (gathered on the device, so the host
-    // planning loop reads them sequentially)
-    if (2 * nh > (size_t)p->n) { int r = ensure_dev((unsigned char**)&p->d_gath, &p->gath_bytes, 8 * nh); if (r) return r; }
-    int32_t* d_g = 2 * nh > (size_t)p->n ? p->d_gath : p->d_ovf;
-    hipLaunchKernelGGL(k_gather_cand_deg, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st,
-                       p->d_tier_lists + (int64_t)TIER_BIG * p->n, (int64_t)nh, p->d_cand, p->d_rp, d_g);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(hcand, d_g, 8 * nh, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (p->hub_enabled) {
-      int r = run_hubs(p, a, hubs, hcand, nh, maxdiff, big);
-      if (r) return r;
-    } else {
-      big.insert(big.end(), hubs, hubs + nh);
-    }
-  }
   if (big.empty()) return PPR_OK;
   std::vector<int32_t> cand(p->n);
   HIP_OK(hipMemcpyAsync(cand.data(), p->d_cand, 4 * (size_t)p->n, hipMemcpyDeviceToHost, st));
@@ -1000,6 +940,159 @@ static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, i
     i0 = i;
   }
   return PPR_OK;
+}
+
+// an MC level's deferred hub overflow list (run_hubs): read it (host sync) and redo those sources
+static int flush_ovl(ppr_plan* p, const IterArgs& a, unsigned long long* maxdiff) {
+  int32_t* ovl = p->ovl_pending;
+  if (!ovl) return PPR_OK;
+  p->ovl_pending = nullptr;
+  hipStream_t st = p->stream;
+  int32_t novf = 0;
+  HIP_OK(hipMemcpyAsync(&novf, ovl, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (!novf) return PPR_OK;
+  if (p->d_diag) fprintf(stderr, "ppr_diag: deferred hub overflow redo %d\n", novf);
+  std::vector<int32_t> big(novf);
+  HIP_OK(hipMemcpyAsync(big.data(), ovl + 1, 4 * (size_t)novf, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  return run_glb(p, a, big, maxdiff);
+}
+
+int run_merge_flush(ppr_plan* p, const IterArgs& a, unsigned long long* maxdiff) {
+  return flush_ovl(p, a, maxdiff);
+}
+
+static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
+                          unsigned long long* maxdiff) {
+  hipStream_t st = p->stream;
+  DevGraph g{p->d_rp, p->d_colx, p->n};
+  const DevSlab s = dev_slab(p);
+  // small MC levels: classification, the hub sources' gather and the previous level's deferred
+  // overflow count come back in one host sync (the combine's ~1800 levels are latency-bound)
+  const bool fused = a.mc && count <= p->fused_max && 2 * count <= p->n;
+  if (!fused) {
+    int r = flush_ovl(p, a, maxdiff);
+    if (r) return r;
+  } else {
+    size_t capb = p->h_hub_cap * 12;
+    void* ptr = p->h_hub_pin;
+    int r = ensure_pinned(&ptr, &capb, 12 * (size_t)count);
+    if (r) return r;
+    p->h_hub_pin = (int32_t*)ptr;
+    p->h_hub_cap = capb / 12;
+  }
+reclassify:
+  HIP_OK(hipMemsetAsync(p->d_tier_cnt, 0, sizeof(uint32_t) * (NLISTS + 2), st));
+  const int64_t nb = (count + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+  hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(256), 0, st, g, s, a, list, count,
+                     p->d_tier_cap, p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big);
+  HIP_OK(hipGetLastError());
+  if (!a.unit && p->max_deg > CLS_BIG_DEG) {
+    hipLaunchKernelGGL(k_classify_big, dim3(256), dim3(CLS_BIG_THREADS), 0, st, g, s, a, p->d_tier_cap,
+                       p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big);
+  }
+  HIP_OK(hipGetLastError());
+  uint32_t cnt[NLISTS + 1];
+  if (fused) {
+    hipLaunchKernelGGL(k_gather_cand_deg_dev, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st,
+                       p->d_tier_lists + (int64_t)TIER_BIG * p->n, p->d_tier_cnt + TIER_BIG, count, p->d_cand,
+                       p->d_rp, p->d_ovf);
+    HIP_OK(hipGetLastError());
+    int32_t pend = 0;
+    HIP_OK(hipMemcpyAsync(cnt, p->d_tier_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(p->h_hub_pin, p->d_tier_lists + (int64_t)TIER_BIG * p->n, 4 * (size_t)count,
+                          hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(p->h_hub_pin + count, p->d_ovf, 8 * (size_t)count, hipMemcpyDeviceToHost, st));
+    if (p->ovl_pending) HIP_OK(hipMemcpyAsync(&pend, p->ovl_pending, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (p->ovl_pending) {
+      if (pend) {  // the previous level left sources to redo: their rows feed this classification
+        int r = flush_ovl(p, a, maxdiff);
+        if (r) return r;
+        goto reclassify;
+      }
+      p->ovl_pending = nullptr;
+    }
+  } else {
+    HIP_OK(hipMemcpyAsync(cnt, p->d_tier_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
+  // the classification is complete (host sync): the wave tiers need no event to start on stream3
+  hipStream_t sw = p->stream3 ? p->stream3 : st;
+  for (int t = 0; t < NT; t++) {
+    if (!cnt[t] || !p->tierT[t]) continue;
+    // one wave per block by default: no LDS left unusable by a 4-wave block granularity
+    const int wpb = p->wave_wpb;
+    const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * wpb;
+    const int64_t blocks = ((int64_t)cnt[t] + wpb - 1) / wpb;
+    hipLaunchKernelGGL(k_merge_lds, dim3((unsigned)blocks), dim3(64 * wpb), bytes, sw, g, s, a,
+                       p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], p->tierT[t], p->Lp,
+                       maxdiff, p->d_stats);
+    HIP_OK(hipGetLastError());
+    p->merge_launches++;
+  }
+  if (cnt[TIER_WG]) {
+    hipLaunchKernelGGL(k_merge_wg, dim3(cnt[TIER_WG]), dim3(WG_THREADS), p->wg_lds, st, g, s, a,
+                       p->d_tier_lists + (int64_t)TIER_WG * p->n, (int64_t)cnt[TIER_WG], p->d_cand,
+                       p->Lp, maxdiff, p->d_stats, p->d_ovf, p->d_tier_cnt + NLISTS);
+    HIP_OK(hipGetLastError());
+    p->merge_launches++;
+    HIP_OK(hipMemcpyAsync(&cnt[NLISTS], p->d_tier_cnt + NLISTS, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+  }
+  // sources beyond the workgroup tier, plus workgroup-tier overflows
+  std::vector<int32_t> big;
+  auto pull = [&](const int32_t* dptr, uint32_t k) -> int {
+    if (!k) return PPR_OK;
+    std::vector<int32_t> tmp(k);
+    HIP_OK(hipMemcpyAsync(tmp.data(), dptr, 4 * (size_t)k, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    big.insert(big.end(), tmp.begin(), tmp.end());
+    return PPR_OK;
+  };
+  for (int t = 0; t < NT; t++)
+    if (cnt[t] && !p->tierT[t]) { int r = pull(p->d_tier_lists + (int64_t)t * p->n, cnt[t]); if (r) return r; }
+  { int r = pull(p->d_ovf, cnt[NLISTS]); if (r) return r; }
+  if (cnt[TIER_BIG] && fused) {
+    // hub list and gathered counts | degrees arrived with the classification
+    const size_t nh = cnt[TIER_BIG];
+    if (p->hub_enabled) {
+      int r = run_hubs(p, a, p->h_hub_pin, p->h_hub_pin + count, nh, maxdiff, big);
+      if (r) return r;
+    } else {
+      big.insert(big.end(), p->h_hub_pin, p->h_hub_pin + nh);
+    }
+  } else if (cnt[TIER_BIG]) {
+    const size_t nh = cnt[TIER_BIG];
+    {
+      size_t capb = p->h_hub_cap * 12;
+      void* ptr = p->h_hub_pin;
+      int r = ensure_pinned(&ptr, &capb, 12 * nh);
+      if (r) return r;
+      p->h_hub_pin = (int32_t*)ptr;
+      p->h_hub_cap = capb / 12;
+    }
+    int32_t* hubs = p->h_hub_pin;
+    int32_t* hcand = p->h_hub_pin + nh;  // | out-degrees at hcand + nh
+    HIP_OK(hipMemcpyAsync(hubs, p->d_tier_lists + (int64_t)TIER_BIG * p->n, 4 * nh, hipMemcpyDeviceToHost, st));
+    // candidate counts and degrees of the hub sources only (gathered on the device, so the host
+    // planning loop reads them sequentially)
+    if (2 * nh > (size_t)p->n) { int r = ensure_dev((unsigned char**)&p->d_gath, &p->gath_bytes, 8 * nh); if (r) return r; }
+    int32_t* d_g = 2 * nh > (size_t)p->n ? p->d_gath : p->d_ovf;
+    hipLaunchKernelGGL(k_gather_cand_deg, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st,
+                       p->d_tier_lists + (int64_t)TIER_BIG * p->n, (int64_t)nh, p->d_cand, p->d_rp, d_g);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(hcand, d_g, 8 * nh, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (p->hub_enabled) {
+      int r = run_hubs(p, a, hubs, hcand, nh, maxdiff, big);
+      if (r) return r;
+    } else {
+      big.insert(big.end(), hubs, hubs + nh);
+    }
+  }
+  return run_glb(p, a, big, maxdiff);
 }
 
 extern "C" int ppr_grank_plan_init(ppr_plan* p) {

@@ -176,9 +176,14 @@ extern "C" int ppr_mccp2_plan_combine(ppr_plan* p) {
   a.lds_rank = p->lds_rank;
   const int64_t nl = (int64_t)p->mc_level_off.size() - 1;
   HIP_OK(hipEventRecord(p->ev_m0, p->stream));
+  p->ovl_pending = nullptr;
   for (int64_t l = 0; l < nl; l++) {
     const int64_t b = p->mc_level_off[l], e = p->mc_level_off[l + 1];
     int rc = run_merge(p, a, p->d_mc_levels + b, e - b, p->d_maxdiff + PPR_MAX_ITER_STATS);
+    if (rc) return rc;
+  }
+  {  // a level's hub overflow list is read with the next level's classification; the last one here
+    int rc = run_merge_flush(p, a, p->d_maxdiff + PPR_MAX_ITER_STATS);
     if (rc) return rc;
   }
   HIP_OK(hipEventRecord(p->ev_m1, p->stream));

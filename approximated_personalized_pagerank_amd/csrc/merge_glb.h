@@ -28,6 +28,18 @@ __global__ void __launch_bounds__(256) k_gather_cand_deg(const int32_t* list, in
   out[count + i] = (int32_t)(rp[v + 1] - rp[v]);
 }
 
+// the same gather with the hub count read on the device (at most cap): out[i] = cand, out[nh + i]
+// = out-degree, so the classification and the gather reach the host in one copy
+__global__ void __launch_bounds__(256) k_gather_cand_deg_dev(const int32_t* list, const uint32_t* nh_p, int64_t cap,
+                                                             const int32_t* cand, const int64_t* rp, int32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nh = min((int64_t)*nh_p, cap);
+  if (i >= nh) return;
+  const int v = list[i];
+  out[i] = cand[v];
+  out[nh + i] = (int32_t)(rp[v + 1] - rp[v]);
+}
+
 __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArgs a,
                                                   const GlbWork* work, int64_t count,
                                                   int32_t* gkeys, double* gacc, int32_t* ckeys,

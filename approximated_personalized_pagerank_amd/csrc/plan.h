@@ -106,6 +106,8 @@ struct ppr_plan {
   unsigned char* d_xsz = nullptr;     // int64 block size per rank (all-gathered)
   unsigned char* d_xtmp = nullptr;    // scan temporary of the block offsets
   size_t xsend_bytes = 0, xrecv_bytes = 0, xsz_bytes = 0, xtmp_bytes = 0;
+  int64_t fused_max = 16384;          // PPR_FUSED_MAX: MC levels up to this many sources take one host sync
+  int32_t* ovl_pending = nullptr;     // MC combine: a level's hub overflow list not yet read (run_hubs)
   int64_t x_bytes = 0;                // block bytes received by this rank in the last sharded run
   int64_t merge_launches = 0;
   double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
@@ -118,6 +120,8 @@ struct ppr_plan {
   int tile_wpb_p = 4096;           // PPR_TILE_WPB_P: count / scatter run one wave per block from this maxP on
   int hub_bw_budget = 380;         // distinct keys a bucket wave's table takes before it spills
   int hub_mix = 6;                 // PPR_HUB_MIX: interleave sources with P >= 2^hub_mix among the others
+  int hub_tile_cand = 4096;         // PPR_HUB_TILE_CAND: minimum tile candidates (HUB_TILE_CAND)
+  int64_t hub_long_min = 1LL << 26; // PPR_HUB_LONG_MIN: hub candidates of a call from which tile_pb applies
   int hub_tile_pb = 16;             // PPR_HUB_TILE_PB: tile candidates >= this many per bucket (0: 4096 / L)
   int64_t hub_budget = 1LL << 28;  // PPR_HUB_BUDGET: staged candidates per hub batch (16-B records)
   // with PPR_HUB_REGIONS (default 3) scratch regions the partition stage runs up to two batches
@@ -256,5 +260,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
 // final top-K: prefix K of the row in slot sA (partition 0 nodes) / sB (partition 1 nodes)
 int launch_topk(ppr_plan* p, int sA, int sB);
 // classify + every merge tier for `count` sources of the device list `list`
+// MC combine: read and redo the last level's deferred hub overflow list (host sync)
+int run_merge_flush(ppr_plan* p, const IterArgs& a, unsigned long long* maxdiff);
 int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
               unsigned long long* maxdiff);

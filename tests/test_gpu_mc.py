@@ -69,6 +69,25 @@ def test_gpu_mc_merge_paths_bit_exact(mask, monkeypatch):
     check_vs_oracle(ppr.rmat(10, seed=91), 16, 48, 100, 0.85, walks=False)
 
 
+@pytest.mark.parametrize("env", [
+    {"PPR_TIER_MASK": "0x20", "PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "2048", "PPR_SEG_T": "256"},  # overflows
+    {"PPR_TIER_MASK": "0x20", "PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "2048", "PPR_SEG_T": "256",
+     "PPR_FUSED_MAX": "6"},                                        # ... with fused and unfused levels mixed
+    {"PPR_TIER_MASK": "0x21", "PPR_FUSED_MAX": "0"},               # every level unfused
+    {"PPR_HUB_TILE_PB": "16", "PPR_HUB_LONG_MIN": "0"},            # long tiles at every level
+    {"PPR_HUB_TILE_CAND": "256"},                                  # shortest tiles
+])
+def test_gpu_mc_level_scheduling_bit_exact(env, monkeypatch, capfd):
+    """level scheduling variants: one host sync per small level with the hub overflow list read
+    (and its sources redone) at the next level's classification, unfused levels, tile lengths"""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("PPR_DIAG", "1")
+    check_vs_oracle(ppr.rmat(11, seed=93), 16, 48, 100, 0.85, walks=False)
+    if "PPR_SEG_T" in env:  # the forced table overflows did take the deferred path
+        assert "deferred hub overflow redo" in capfd.readouterr().err
+
+
 @pytest.mark.parametrize("d", [0.5, 1.0])
 def test_gpu_mc_damping_edges(d):
     # d = 1: walks end only at dangling nodes or the step cap (the reference loops forever)
