@@ -278,7 +278,7 @@ def main_mc(args):
     if not args.no_cpu_baseline:
         try:
             plan.close()
-            cpu = mc_cpu_baseline(max(8, args.scale - 8), K, L, args.walks, args.damping, args.seed)
+            cpu = mc_cpu_baseline(max(8, args.scale - 6), K, L, args.walks, args.damping, args.seed)
         except Exception as exc:  # reported, never fatal
             log(f"mc cpu_baseline failed: {exc!r}")
     line = {
