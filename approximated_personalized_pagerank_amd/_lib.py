@@ -15,6 +15,8 @@ LIB_PATH = os.path.join(PKG_DIR, "libppr_hip.so")
 # A/B experiments only (tools/build_variant.py): load a variant build of the same ABI instead
 if os.environ.get("PPR_LIB_VARIANT"):
     LIB_PATH = os.path.join(PKG_DIR, "libppr_hip_" + os.environ["PPR_LIB_VARIANT"] + ".so")
+    if not os.path.exists(LIB_PATH):  # never let build() compile the product sources under its name
+        raise FileNotFoundError(f"PPR_LIB_VARIANT: {LIB_PATH} missing (tools/build_variant.py builds it)")
 
 PPR_MAX_ITER_STATS = 256
 PPR_FLAG_STATS = 1
