@@ -9,7 +9,7 @@ from ._lib import LIB_PATH, PKG_DIR
 CSRC = os.path.join(PKG_DIR, "csrc")
 SOURCES = ["grank.hip", "mccp2.hip", "exact_ppr.hip", "host_graph.cpp"]
 HEADERS = ["ppr_device.h", "ppr_common.h", "merge_wave.h", "wg_merge.h", "merge_hub.h", "merge_glb.h",
-           "merge_mc.h", "merge_hot.h", "plan.h",
+           "merge_mc.h", "merge_hot.h", "plan.h", "host_par.h",
            os.path.join("..", "..", "include", "ppr_hip.h")]
 ARCH = os.environ.get("PPR_OFFLOAD_ARCH", "gfx950")
 

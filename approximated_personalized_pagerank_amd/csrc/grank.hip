@@ -28,6 +28,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,6 +46,7 @@
 using namespace pprk;
 
 #include "plan.h"
+#include "host_par.h"
 
 namespace pprk {
 // Probe of the LDS atomic order chunk_accumulate's `ordered` mode relies on: every lane of a wave
@@ -401,18 +404,36 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
   if (g->n >= (1LL << 31) - 1) return PPR_ERR_RANGE;
   const int64_t n = g->n;
   const int64_t m = n ? g->row_ptr[n] : 0;
-  for (int64_t e = 0; e < m; e++)
-    if (g->col[e] < 0 || g->col[e] >= n) return PPR_ERR_GRAPH;
+  const bool timing = getenv("PPR_TIMING") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+  };
+  const auto t0 = now();
+  const int nth = pprh::host_threads();
   std::vector<uint8_t> part(n > 0 ? n : 1, 0);
+  {
+    std::atomic<bool> bad(false);
+    pprh::parallel_for(m, nth, [&](int64_t b, int64_t e, int) {
+      for (int64_t i = b; i < e; i++)
+        if (g->col[i] < 0 || g->col[i] >= n) { bad = true; return; }
+    });
+    if (bad) return PPR_ERR_GRAPH;
+  }
   if (part_in) std::memcpy(part.data(), part_in, n);
   else if (n) { rc = ppr_find_partitions_csr(g, part.data()); if (rc) return rc; }
+  const auto t1 = now();
 
   // host-side CSR with partition bit of the successor
   std::vector<int32_t> colx(m > 0 ? m : 1);
-  for (int64_t e = 0; e < m; e++) colx[e] = g->col[e] | (part[g->col[e]] ? (int32_t)0x80000000 : 0);
+  pprh::parallel_for(m, nth, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; i++) colx[i] = g->col[i] | (part[g->col[i]] ? (int32_t)0x80000000 : 0);
+  });
+  const auto t2 = now();
   ppr_plan* p = nullptr;
   rc = plan_alloc(n, g->row_ptr, colx.data(), K, L, damping, o, &p);
   if (rc) return rc;
+  const auto t3 = now();
   std::vector<int32_t> act[2];
   for (int64_t v = 0; v < n; v++)
     if (g->row_ptr[v + 1] > g->row_ptr[v]) act[part[v]].push_back((int32_t)v);
@@ -420,16 +441,21 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
   // initial basket bound min(L, deg(u) + 1)
   for (int q = 0; q < 2; q++) {
     p->work[q].resize(act[q].size());
-    for (size_t i = 0; i < act[q].size(); i++) {
-      const int v = act[q][i];
-      double w = 1.0;
-      for (int64_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; e++) {
-        const int u = g->col[e];
-        w += (double)std::min<int64_t>(L, g->row_ptr[u + 1] - g->row_ptr[u] + 1);
+    pprh::parallel_for((int64_t)act[q].size(), nth, [&](int64_t b, int64_t e2, int) {
+      for (int64_t i = b; i < e2; i++) {
+        const int v = act[q][i];
+        double w = 1.0;
+        for (int64_t e = g->row_ptr[v]; e < g->row_ptr[v + 1]; e++) {
+          const int u = g->col[e];
+          w += (double)std::min<int64_t>(L, g->row_ptr[u + 1] - g->row_ptr[u] + 1);
+        }
+        p->work[q][i] = w;
       }
-      p->work[q][i] = w;
-    }
+    });
   }
+  if (timing)
+    fprintf(stderr, "ppr_timing plan_create partitions_s %.3f colx_s %.3f alloc_upload_s %.3f work_s %.3f\n",
+            sec(t0, t1), sec(t1, t2), sec(t2, t3), sec(t3, now()));
   p->nact[0] = (int64_t)act[0].size();
   p->nact[1] = (int64_t)act[1].size();
   if (p->hot_cap > 0 && n > 0) {

@@ -17,6 +17,7 @@
 
 #include "../../include/ppr_hip.h"
 #include "../../include/ppr/importGraph.h"
+#include "host_par.h"
 
 namespace {
 
@@ -41,32 +42,9 @@ inline uint64_t scramble(uint64_t x, int bits, uint64_t seed) {
   return x & mask;
 }
 
-template <class F>
-void parallel_for(int64_t n, int nthreads, F f) {
-  if (nthreads <= 1 || n < 4096) { f(0, n, 0); return; }
-  std::vector<std::thread> th;
-  int64_t chunk = (n + nthreads - 1) / nthreads;
-  for (int t = 0; t < nthreads; t++) {
-    int64_t b = t * chunk, e = std::min<int64_t>(n, b + chunk);
-    if (b >= e) break;
-    th.emplace_back(f, b, e, t);
-  }
-  for (auto& t : th) t.join();
-}
-
-int hw_threads() {
-  unsigned h = std::thread::hardware_concurrency();
-  if (h == 0) h = 1;
-  return (int)std::min<unsigned>(h, 16);
-}
-
-// PPR_HOST_THREADS, else OMP_NUM_THREADS (the CPU share on shared hosts), else hw_threads()
-int host_threads() {
-  const char* e = getenv("PPR_HOST_THREADS");
-  if (!e || !*e) e = getenv("OMP_NUM_THREADS");
-  if (e && *e && atoi(e) > 0) return std::min(atoi(e), 64);
-  return hw_threads();
-}
+using pprh::parallel_for;
+using pprh::host_threads;
+using pprh::hw_threads;
 
 }  // namespace
 
