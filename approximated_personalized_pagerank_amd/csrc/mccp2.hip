@@ -177,10 +177,20 @@ extern "C" int ppr_mccp2_plan_combine(ppr_plan* p) {
   const int64_t nl = (int64_t)p->mc_level_off.size() - 1;
   HIP_OK(hipEventRecord(p->ev_m0, p->stream));
   p->ovl_pending = nullptr;
+  const bool lvlog = getenv("PPR_MC_LEVEL_LOG") != nullptr;  // diagnostics: one line per level
   for (int64_t l = 0; l < nl; l++) {
     const int64_t b = p->mc_level_off[l], e = p->mc_level_off[l + 1];
+    if (lvlog) { HIP_OK(hipEventRecord(p->ev_a, p->stream)); p->last_nbig = p->last_maxneed = 0; }
     int rc = run_merge(p, a, p->d_mc_levels + b, e - b, p->d_maxdiff + PPR_MAX_ITER_STATS);
     if (rc) return rc;
+    if (lvlog) {
+      HIP_OK(hipEventRecord(p->ev_b, p->stream));
+      HIP_OK(hipEventSynchronize(p->ev_b));
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, p->ev_a, p->ev_b);
+      fprintf(stderr, "mc_level %lld %lld %lld %lld %.4f\n", (long long)l, (long long)(e - b),
+              (long long)p->last_nbig, (long long)p->last_maxneed, ms);
+    }
   }
   {  // a level's hub overflow list is read with the next level's classification; the last one here
     int rc = run_merge_flush(p, a, p->d_maxdiff + PPR_MAX_ITER_STATS);

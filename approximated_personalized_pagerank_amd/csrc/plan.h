@@ -107,6 +107,7 @@ struct ppr_plan {
   unsigned char* d_xtmp = nullptr;    // scan temporary of the block offsets
   size_t xsend_bytes = 0, xrecv_bytes = 0, xsz_bytes = 0, xtmp_bytes = 0;
   int64_t fused_max = 16384;          // PPR_FUSED_MAX: MC levels up to this many sources take one host sync
+  int64_t last_nbig = 0, last_maxneed = 0;  // the last hub pass: sources, largest candidate count
   int32_t* ovl_pending = nullptr;     // MC combine: a level's hub overflow list not yet read (run_hubs)
   int64_t x_bytes = 0;                // block bytes received by this rank in the last sharded run
   int64_t merge_launches = 0;
