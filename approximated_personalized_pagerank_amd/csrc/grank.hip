@@ -30,10 +30,13 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/ppr_hip.h"
@@ -1487,11 +1490,99 @@ static int ensure_dev(unsigned char** ptr, size_t* cap, size_t need) {
   return PPR_OK;
 }
 
+// ---- the sharded loop's three collectives: RCCL, or an in-process group of plans ----
+// LocalGroup: N plans of one process, one thread each, running the same native loop; block
+// sizes, blocks (device-to-device copies) and maxDiff go through host-side rendezvous. It tests
+// everything of ppr_grank_plan_run_sharded but the RCCL calls on a one-GPU box (RCCL refuses two
+// ranks on one device). A rank that fails marks the group, and the others leave their barriers.
+struct LocalGroup {
+  int n;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  int64_t gen = 0;
+  bool failed = false;
+  std::vector<int64_t> sizes;
+  std::vector<unsigned char*> bufs;
+  std::vector<unsigned long long> md;
+  explicit LocalGroup(int n_) : n(n_), sizes(n_), bufs(n_), md(n_) {}
+  bool barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (failed) return false;
+    const int64_t g = gen;
+    if (++arrived == n) { arrived = 0; gen++; cv.notify_all(); return true; }
+    const bool ok = cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || failed; });
+    if (!ok || failed) { failed = true; cv.notify_all(); return false; }
+    return true;
+  }
+  void fail() { std::lock_guard<std::mutex> lk(mu); failed = true; cv.notify_all(); }
+};
+
+static int x_allgather_sizes(ppr_plan* p, int64_t* d_sz, std::vector<int64_t>& sz, hipStream_t s) {
+  if (p->lgroup) {
+    LocalGroup& G = *p->lgroup;
+    int64_t v = 0;
+    HIP_OK(hipMemcpyAsync(&v, d_sz + p->rank, 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    G.sizes[p->rank] = v;
+    if (!G.barrier()) return PPR_ERR_HIP;
+    sz.assign(G.sizes.begin(), G.sizes.end());
+    return G.barrier() ? PPR_OK : PPR_ERR_HIP;
+  }
+  NCCL_OK(ncclAllGather(d_sz + p->rank, d_sz, 1, ncclInt64, p->comm, s));
+  HIP_OK(hipMemcpyAsync(sz.data(), d_sz, 8 * (size_t)p->nranks, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return PPR_OK;
+}
+
+// every non-empty rank's block (its d_xsend, sz[r] bytes) into d_xrecv + xo[r] of every other rank
+static int x_blocks(ppr_plan* p, const std::vector<int64_t>& b, const std::vector<int64_t>& sz,
+                    const std::vector<size_t>& xo, hipStream_t s) {
+  if (p->lgroup) {
+    LocalGroup& G = *p->lgroup;
+    HIP_OK(hipStreamSynchronize(s));  // this rank's block is complete
+    G.bufs[p->rank] = p->d_xsend;
+    if (!G.barrier()) return PPR_ERR_HIP;
+    for (int r = 0; r < p->nranks; r++)
+      if (r != p->rank && b[r + 1] > b[r])
+        HIP_OK(hipMemcpyAsync(p->d_xrecv + xo[r], G.bufs[r], (size_t)sz[r], hipMemcpyDeviceToDevice, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return G.barrier() ? PPR_OK : PPR_ERR_HIP;  // no rank reuses its send buffer before all copied
+  }
+  NCCL_OK(ncclGroupStart());
+  for (int r = 0; r < p->nranks; r++) {
+    if (b[r + 1] == b[r]) continue;
+    unsigned char* dst = r == p->rank ? p->d_xsend : p->d_xrecv + xo[r];
+    NCCL_OK(ncclBroadcast(p->d_xsend, dst, (size_t)sz[r], ncclUint8, r, p->comm, s));
+  }
+  NCCL_OK(ncclGroupEnd());
+  return PPR_OK;
+}
+
+// maxDiff >= 0: the IEEE bit patterns order like the values, so an integer MAX is exact
+static int x_allreduce_max(ppr_plan* p, unsigned long long* mdp, hipStream_t s) {
+  if (p->lgroup) {
+    LocalGroup& G = *p->lgroup;
+    unsigned long long v = 0;
+    HIP_OK(hipMemcpyAsync(&v, mdp, 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    G.md[p->rank] = v;
+    if (!G.barrier()) return PPR_ERR_HIP;
+    for (unsigned long long x : G.md) v = x > v ? x : v;
+    if (!G.barrier()) return PPR_ERR_HIP;
+    HIP_OK(hipMemcpyAsync(mdp, &v, 8, hipMemcpyHostToDevice, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return PPR_OK;
+  }
+  NCCL_OK(ncclAllReduce(mdp, mdp, 1, ncclUint64, ncclMax, p->comm, s));
+  return PPR_OK;
+}
+
 extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance,
                                           ppr_stats* st) {
   if (!p) return PPR_ERR_ARG;
   if (iterations == 0) return PPR_ERR_ITERS;
-  if (p->nranks > 1 && !p->comm) return PPR_ERR_ARG;
+  if (p->nranks > 1 && !p->comm && !p->lgroup) return PPR_ERR_ARG;
   HIP_OK(hipSetDevice(p->device));
   hipStream_t s = p->stream;
   HIP_OK(hipMemsetAsync(p->d_maxdiff, 0, 8 * (PPR_MAX_ITER_STATS + 1), s));
@@ -1525,29 +1616,23 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
       int64_t* d_sz = reinterpret_cast<int64_t*>(p->d_xsz);
       rc = xpack(p, (int32_t)it, b[p->rank], b[p->rank + 1], p->d_xsend, (int64_t)p->xsend_bytes, d_sz + p->rank);
       if (rc) return rc;
-      NCCL_OK(ncclAllGather(d_sz + p->rank, d_sz, 1, ncclInt64, p->comm, s));
       std::vector<int64_t> sz(p->nranks);
-      HIP_OK(hipMemcpyAsync(sz.data(), d_sz, 8 * (size_t)p->nranks, hipMemcpyDeviceToHost, s));
-      HIP_OK(hipStreamSynchronize(s));
+      rc = x_allgather_sizes(p, d_sz, sz, s);
+      if (rc) return rc;
       std::vector<size_t> xo(p->nranks + 1, 0);
       for (int r = 0; r < p->nranks; r++) xo[r + 1] = xo[r] + (r == p->rank ? 0 : (size_t)sz[r]);
       rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, std::max<size_t>(8, xo[p->nranks]));
       if (rc) return rc;
       p->x_bytes += xo[p->nranks];
-      NCCL_OK(ncclGroupStart());
-      for (int r = 0; r < p->nranks; r++) {
-        if (b[r + 1] == b[r]) continue;
-        unsigned char* dst = r == p->rank ? p->d_xsend : p->d_xrecv + xo[r];
-        NCCL_OK(ncclBroadcast(p->d_xsend, dst, (size_t)sz[r], ncclUint8, r, p->comm, s));
-      }
-      NCCL_OK(ncclGroupEnd());
+      rc = x_blocks(p, b, sz, xo, s);
+      if (rc) return rc;
       for (int r = 0; r < p->nranks; r++) {
         if (r == p->rank || b[r + 1] == b[r]) continue;
         rc = xunpack(p, (int32_t)it, b[r], b[r + 1], p->d_xrecv + xo[r]);
         if (rc) return rc;
       }
-      // maxDiff >= 0: the IEEE bit patterns order like the values, so an integer MAX is exact
-      NCCL_OK(ncclAllReduce(mdp, mdp, 1, ncclUint64, ncclMax, p->comm, s));
+      rc = x_allreduce_max(p, mdp, s);
+      if (rc) return rc;
     }
     double d = 0.0;
     rc = ppr_grank_plan_read_maxdiff(p, (int32_t)it, &d);
@@ -1573,6 +1658,35 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
     st->algo_bytes = (int64_t)sv[1];
     st->merge_launches = p->merge_launches;
   }
+  return PPR_OK;
+}
+
+// Test entry: the native sharded loop with n plans of this process as the ranks (LocalGroup),
+// one thread each; every plan must be built on the same graph and parameters. st: n stats or null.
+extern "C" int ppr_grank_plan_run_local_group(ppr_plan** plans, int32_t n, uint32_t iterations, double tolerance,
+                                              ppr_stats* st) {
+  if (!plans || n < 1) return PPR_ERR_ARG;
+  for (int i = 0; i < n; i++)
+    if (!plans[i] || plans[i]->comm || plans[i]->n != plans[0]->n) return PPR_ERR_ARG;
+  LocalGroup G(n);
+  std::vector<int> rcs(n, PPR_OK);
+  for (int i = 0; i < n; i++) {
+    plans[i]->lgroup = &G;
+    plans[i]->nranks = n;
+    plans[i]->rank = i;
+    int rc = ensure_dev(&plans[i]->d_xsz, &plans[i]->xsz_bytes, 8 * (size_t)n);
+    if (rc) return rc;
+  }
+  std::vector<std::thread> th;
+  for (int i = 0; i < n; i++)
+    th.emplace_back([&, i] {
+      rcs[i] = ppr_grank_plan_run_sharded(plans[i], iterations, tolerance, st ? st + i : nullptr);
+      if (rcs[i]) G.fail();
+    });
+  for (auto& t : th) t.join();
+  for (int i = 0; i < n; i++) { plans[i]->lgroup = nullptr; plans[i]->nranks = 1; plans[i]->rank = 0; }
+  for (int i = 0; i < n; i++)
+    if (rcs[i]) return rcs[i];
   return PPR_OK;
 }
 

@@ -99,6 +99,7 @@ struct ppr_plan {
   int hub_slice = 8192;            // PPR_HUB_SLICE: k_hub_reduce slice (>= L)
   // source sharding (ppr_grank_plan_comm_init / ppr_grank_plan_run_sharded)
   ncclComm_t comm = nullptr;
+  struct LocalGroup* lgroup = nullptr;  // tests: the ranks are plans of this process (grank.hip)
   int nranks = 1, rank = 0;
   std::vector<double> work[2];        // per active source: merge work estimate (list order)
   unsigned char* d_xsend = nullptr;   // compact block of this rank's rows (merge_glb.h)

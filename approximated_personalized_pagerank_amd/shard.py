@@ -205,6 +205,21 @@ class CpuComm(TorchComm):
     """gloo collectives on host tensors (bootstrap and rehearsal)."""
 
 
+def run_local_group(plans, iterations: int, tolerance: float):
+    """The native sharded loop (ppr_grank_plan_run_sharded) with these GrankPlans of one process as
+    its ranks, one thread each, blocks exchanged by device copies (tests: RCCL refuses two ranks
+    on one GPU). Returns the per-rank PprStats."""
+    import ctypes
+    from . import _lib
+    n = len(plans)
+    arr = (ctypes.c_void_p * n)(*[pl._p for pl in plans])
+    st = (_lib.PprStats * n)()
+    _lib.check(_lib.lib().ppr_grank_plan_run_local_group(arr, n, iterations, tolerance, st), "run_local_group")
+    for pl, s in zip(plans, st):
+        pl.iterations_run = int(s.iterations_run)
+    return list(st)
+
+
 def device_count() -> int:
     import ctypes
     from . import _lib

@@ -153,6 +153,11 @@ int ppr_comm_unique_id(void* id128);
 int ppr_grank_plan_comm_init(ppr_plan* p, const void* id128, int32_t nranks, int32_t rank);
 int ppr_grank_plan_shard_bounds(ppr_plan* p, int32_t it, int32_t nranks, int64_t* bounds);
 int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance, ppr_stats* st);
+/* Tests: the same native loop with n plans of this process as the ranks (one thread each, block
+ * exchange by device copies instead of RCCL: RCCL refuses two ranks on one GPU). st: n stats or
+ * null. Every plan must be built on the same graph and parameters. */
+int ppr_grank_plan_run_local_group(ppr_plan** plans, int32_t n, uint32_t iterations, double tolerance,
+                                   ppr_stats* st);
 /* host-staged variants of pack/unpack (rehearsal without RCCL; synchronous): pack_host writes the
  * block (at most cap bytes) and its size to *bytes; unpack_host takes a block of `bytes` bytes */
 int ppr_grank_plan_pack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* host_buf, int64_t cap,

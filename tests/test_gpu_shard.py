@@ -113,3 +113,25 @@ def test_gpu_compact_block_round_trip(hot, monkeypatch):
     assert np.array_equal(ra.ids, ref.ids) and np.array_equal(ra.scores, ref.scores)
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("world,tol", [(2, 1e-4), (3, -1.0), (4, 1e-3)])
+def test_gpu_native_loop_multi_rank_local_group(world, tol):
+    """ppr_grank_plan_run_sharded with world > 1 -- work-balanced ranges, compact blocks, size
+    all-gather, block exchange, unpack, maxDiff all-reduce and the stop rule -- with `world` plans
+    of this process as the ranks (device copies stand in for RCCL): every rank ends with the
+    single-GPU result bit for bit"""
+    import approximated_personalized_pagerank_amd as ppr
+    from approximated_personalized_pagerank_amd.shard import run_local_group
+    g = ppr.rmat(13, seed=31)
+    part = g.partitions()
+    K, L, iters = 32, 64, 12
+    ref = ppr.grank_csr(g, K, L, iters, 0.85, tol, part=part, device=0)
+    plans = [ppr.GrankPlan(g, K, L, 0.85, part=part, device=0, stats=True) for _ in range(world)]
+    st = run_local_group(plans, iters, tol)
+    for pl, s in zip(plans, st):
+        assert int(s.iterations_run) == ref.iterations_run
+        r = pl.fetch()
+        assert np.array_equal(r.lens, ref.lens) and np.array_equal(r.ids, ref.ids)
+        assert np.array_equal(r.scores.view(np.uint64), ref.scores.view(np.uint64))
+        pl.close()
