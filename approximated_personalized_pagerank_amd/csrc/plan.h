@@ -208,6 +208,9 @@ inline void plan_free(ppr_plan* p) {
                 "task ms: longest %.2f, first %.2f, sum %.1f\n", p->hot_n, h[144], p->diag_hub_cand, (double)h[140],
                 100.0 * (double)h[140] / (p->diag_hub_cand > 0 ? p->diag_hub_cand : 1.0), h[141] / 1e5, h[143] / 1e5,
                 h[142] / 1e5);
+      if (h[150])
+        fprintf(stderr, "ppr_diag rows merged %llu, unchanged (norm1 = 0) %llu (%.2f %%)\n", h[150], h[151],
+                100.0 * (double)h[151] / (double)h[150]);
       if (h[133])
         fprintf(stderr, "ppr_diag k_hub_seg: %llu waves, %.1f candidates/wave, Mcycles setup %.1f window %.1f "
                 "gather %.1f accumulate %.1f emit %.1f\n", h[133], (double)h[134] / (double)h[133], h[128] / 1e6,

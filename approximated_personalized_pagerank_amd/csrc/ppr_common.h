@@ -225,6 +225,10 @@ __device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt v
     // maxDiff only grows: skip the contended atomic when a larger value is already published
     const unsigned long long b = (unsigned long long)dbits(d1);
     if (b > __hip_atomic_load(maxdiff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(maxdiff, b);
+    if (a.diag) {  // PPR_DIAG: merged rows, and rows left bit-identical (norm1 = 0)
+      atomicAdd(&a.diag[150], 1ull);
+      if (d1 == 0.0) atomicAdd(&a.diag[151], 1ull);
+    }
   }
   (void)stats;  // written-row bytes are summed by k_stat_written (no per-source atomics)
 }
