@@ -385,7 +385,7 @@ def main():
     if (args.scale, args.K, args.L, args.iters) == (22, 64, 128, 30):
         traffic, traffic_src = pmc_traffic(f"grank_rmat22_k64_l128")
     line = {
-        "metric": "source-nodes/sec grank K=64 L=128 on RMAT-22; 1/2/4/8 MI355X + HBM GB/s",
+        "metric": f"source-nodes/sec grank K={args.K} L={args.L} on RMAT-{args.scale}; 1/2/4/8 MI355X + HBM GB/s",
         "value": value,
         "unit": "source-nodes/s",
         "n_gpus": world,
