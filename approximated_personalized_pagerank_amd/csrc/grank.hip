@@ -542,10 +542,10 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   DevGraph g{p->d_rp, p->d_colx, p->n};
   const DevSlab s = dev_slab(p);
   const int64_t L = p->L;
-  const int64_t budget = p->hub_budget;
+  const int64_t budget = p->hub_budget;  // staged candidates per batch (default 4 GiB of 16-B records)
   p->last_nbig = (int64_t)nbig;  // PPR_MC_LEVEL_LOG
   p->last_maxneed = 0;
-  for (size_t i = 0; i < nbig; i++) p->last_maxneed = std::max<int64_t>(p->last_maxneed, cand[i]);  // staged candidates per batch (default 4 GiB of 16-B records)
+  for (size_t i = 0; i < nbig; i++) p->last_maxneed = std::max<int64_t>(p->last_maxneed, cand[i]);
   const int slice = p->hub_slice;
   using Batch = HubBatch;
   std::vector<Batch>& batches = p->hub_batches;
