@@ -10,8 +10,8 @@
 //   2. ppr_grank_csr(): BFS partitions (include/internal/pprInternal.h:29-99), upload, init,
 //      iterations, final top-K on the device, download;
 //   3. the top-K rows are materialised back into unordered_map<Key, unordered_map<Key,double>>.
-// Ties at a top-L/top-K cut are broken by (score desc, dense id asc); the reference leaves them to
-// its hash-map order.
+// Which keys survive among those tied at a top-L/top-K cut: a per-source hash of the key (the
+// reference leaves it to its hash-map history); untied results are bit-identical.
 #ifndef PPR_HIP_DROPIN_GRANK_H
 #define PPR_HIP_DROPIN_GRANK_H
 
