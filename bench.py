@@ -78,6 +78,23 @@ def mc_cpu_baseline(scale, K, L, walks, damping, seed):
                        f"measured at RMAT-14..18), so this overstates the RMAT-22 rate")}
 
 
+def parse_ppr_timing(text):
+    """key -> seconds from the library's PPR_TIMING lines ("ppr_timing [section] key value ...")"""
+    split = {}
+    for ln in text.splitlines():
+        if not ln.startswith("ppr_timing"):
+            continue
+        f = ln.split()[1:]
+        i = 0
+        while i + 1 < len(f):
+            try:
+                split[f[i]] = float(f[i + 1])
+                i += 2
+            except ValueError:
+                i += 1
+    return split
+
+
 def end_to_end(scale, iters, K, L):
     """f1: the reference's own API end to end -- tests/cpp/dropin_test.cc calls
     ppr::grank(unordered_map graph, K=64, L=128, iters) through include/ppr/grank.h, so the timing
@@ -91,18 +108,16 @@ def end_to_end(scale, iters, K, L):
     p = subprocess.run([binary, "e2e", str(scale), str(iters)], capture_output=True, text=True, env=env,
                        check=True, timeout=900)
     d = json.loads(p.stdout.strip().splitlines()[-1])
-    split = {}
-    for ln in p.stderr.splitlines():
-        if ln.startswith("ppr_timing"):
-            f = ln.split()[1:]
-            split = {f[i]: float(f[i + 1]) for i in range(0, len(f) - 1, 2)}
+    split = parse_ppr_timing(p.stderr)
     out = {"total_s": d["total_s"], "graph": "RMAT-%d as unordered_map<int, vector<int>> (%d nodes, %d edges)"
            % (scale, d["nodes"], d["edges"]), "result_entries": d["entries"],
            "call": f"ppr::grank(graph, K={K}, L={L}, {iters}, 0.85, nThreads, -1) via include/ppr/grank.h"}
     if split:
         out.update(flatten_s=split.get("flatten_s"), device_s=split.get("device_s"),
                    plan_and_upload_s=split["csr_call_s"] - split["device_s"] if "csr_call_s" in split else None,
-                   materialize_s=split.get("materialize_s"))
+                   materialize_s=split.get("materialize_s"),
+                   plan_create={k: split[k] for k in ("partitions_s", "colx_s", "alloc_upload_s", "work_s")
+                                if k in split})
     return out
 
 

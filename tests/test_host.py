@@ -124,3 +124,18 @@ def test_plan_rejects_candidate_count_overflow():
     out = ctypes.c_void_p()
     assert L.ppr_grank_plan_create(ctypes.byref(c), _lib.ptr(part), 2, 4096, 0.85, None, ctypes.byref(out)) == 11
     assert L.ppr_mccp2_plan_create(ctypes.byref(c), 2, 4096, 0.85, None, ctypes.byref(out)) == 11
+
+
+def test_bench_parses_timing_lines():
+    """bench.py's end_to_end leg reads the PPR_TIMING split off the drop-in program's stderr"""
+    import importlib
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    bench = importlib.import_module("bench")
+    txt = ("noise\nppr_timing plan_create partitions_s 0.786 colx_s 0.050 alloc_upload_s 0.142 work_s 0.051\n"
+           "ppr_timing flatten_s 1.17 csr_call_s 4.82 device_s 3.56 materialize_s 2.81\n")
+    d = bench.parse_ppr_timing(txt)
+    assert d["partitions_s"] == 0.786 and d["work_s"] == 0.051
+    assert d["flatten_s"] == 1.17 and d["csr_call_s"] == 4.82 and d["materialize_s"] == 2.81
+    assert bench.parse_ppr_timing("") == {}
