@@ -140,8 +140,13 @@ def lib() -> ctypes.CDLL:
         "ppr_exact_gather": (ctypes.c_int, [vp, i32, vp, vp]),
         "ppr_exact_destroy": (None, [vp]),
     }
+    variant = bool(os.environ.get("PPR_LIB_VARIANT"))
     for name, (res, args) in sigs.items():
-        fn = getattr(L, name)
+        fn = getattr(L, name, None)
+        if fn is None:
+            if variant:  # an experiment build of an older revision: its ABI may predate the symbol
+                continue
+            raise AttributeError(f"{LIB_PATH} lacks {name}")
         fn.restype = res
         fn.argtypes = args
     _lib = L

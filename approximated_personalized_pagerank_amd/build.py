@@ -37,7 +37,9 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result", "-Wno-unused-value"] + [f"-D{d}" for d in defines] + [
            "-I", os.path.join(PKG_DIR, "..", "include"),
-           "-o", out + ".tmp"] + [os.path.join(src_dir, s) for s in SOURCES] + ["-lrccl", "-lpthread"]
+           "-o", out + ".tmp"] + [os.path.join(src_dir, s) for s in SOURCES
+                                  # an older revision (tools/build_variant.py --rev) may predate a source
+                                  if csrc is None or os.path.exists(os.path.join(src_dir, s))] + ["-lrccl", "-lpthread"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
