@@ -1668,14 +1668,16 @@ extern "C" int ppr_grank_plan_run_local_group(ppr_plan** plans, int32_t n, uint3
   if (!plans || n < 1) return PPR_ERR_ARG;
   for (int i = 0; i < n; i++)
     if (!plans[i] || plans[i]->comm || plans[i]->n != plans[0]->n) return PPR_ERR_ARG;
+  for (int i = 0; i < n; i++) {
+    int rc = ensure_dev(&plans[i]->d_xsz, &plans[i]->xsz_bytes, 8 * (size_t)n);
+    if (rc) return rc;
+  }
   LocalGroup G(n);
   std::vector<int> rcs(n, PPR_OK);
   for (int i = 0; i < n; i++) {
     plans[i]->lgroup = &G;
     plans[i]->nranks = n;
     plans[i]->rank = i;
-    int rc = ensure_dev(&plans[i]->d_xsz, &plans[i]->xsz_bytes, 8 * (size_t)n);
-    if (rc) return rc;
   }
   std::vector<std::thread> th;
   for (int i = 0; i < n; i++)
@@ -1684,6 +1686,7 @@ extern "C" int ppr_grank_plan_run_local_group(ppr_plan** plans, int32_t n, uint3
       if (rcs[i]) G.fail();
     });
   for (auto& t : th) t.join();
+  // the group lives on this stack frame: no plan keeps it
   for (int i = 0; i < n; i++) { plans[i]->lgroup = nullptr; plans[i]->nranks = 1; plans[i]->rank = 0; }
   for (int i = 0; i < n; i++)
     if (rcs[i]) return rcs[i];
