@@ -543,6 +543,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   const DevSlab s = dev_slab(p);
   const int64_t L = p->L;
   const int64_t budget = p->hub_budget;  // staged candidates per batch (default 4 GiB of 16-B records)
+  const auto t_plan0 = std::chrono::steady_clock::now();
   p->last_nbig = (int64_t)nbig;  // PPR_MC_LEVEL_LOG
   p->last_maxneed = 0;
   for (size_t i = 0; i < nbig; i++) p->last_maxneed = std::max<int64_t>(p->last_maxneed, cand[i]);
@@ -560,9 +561,15 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   // are stored with the hot encoding exactly when hot_n > 0
   const bool hot = p->hot_n > 0 && !a.unit && !a.mc;
   const HotSet H{p->d_hot_bits, p->d_hot_idx, p->d_hot_keys, hot ? p->hot_n : 0};
+  // need < 2^31 (plan-create range check): 32-bit divisions; the planning loop below runs once per
+  // hub source per iteration (hundreds of thousands), on the critical path before the first batch
+  const uint32_t hb = (uint32_t)p->hub_bucket, sgb = (uint32_t)p->seg_bucket;
+  auto cdiv32 = [](uint32_t x, uint32_t d) { return x / d + (x % d != 0); };
   auto logp_of = [&](int64_t need) {
-    return std::max(1, std::min(HUB_MAX_LOGP, ceil_log2((need + p->hub_bucket - 1) / p->hub_bucket)));
+    return std::max(1, std::min(HUB_MAX_LOGP, ceil_log2((int64_t)cdiv32((uint32_t)need, hb))));
   };
+  std::vector<uint8_t> lpv(nbig);
+  for (size_t i = 0; i < nbig; i++) lpv[i] = (uint8_t)logp_of(cand[i]);
   // batches mix large and small sources: that hides the long hot-key buckets of the large ones
   // (grouping them by size measured 10 % slower), and it balances the two pipeline stages, whose
   // costs differ by source size (large partitions: count + scatter bound; many small sources:
@@ -571,7 +578,9 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   std::vector<uint32_t> order(nbig);
   if (p->hub_mix > 0) {
     std::vector<uint32_t> lg, sm;
-    for (size_t i = 0; i < nbig; i++) (logp_of(cand[i]) >= p->hub_mix ? lg : sm).push_back((uint32_t)i);
+    lg.reserve(nbig);
+    sm.reserve(nbig);
+    for (size_t i = 0; i < nbig; i++) (lpv[i] >= p->hub_mix ? lg : sm).push_back((uint32_t)i);
     size_t a0 = 0, b0 = 0, k = 0;
     while (a0 < lg.size() || b0 < sm.size()) {
       // take from the list that is behind its share (a0 / |lg| vs b0 / |sm|)
@@ -584,9 +593,21 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   // Long tiles (tile_pb candidates per bucket) cut the scatter's partial-line stores but leave
   // fewer tiles per source: they pay only when the call has hub work enough to fill the chip
   // anyway (a GRank iteration: billions of candidates), not for the few lone hubs of an MC level.
+  const auto t_plan1 = std::chrono::steady_clock::now();
   int64_t need_all = 0;
   for (size_t i = 0; i < nbig; i++) need_all += cand[i];
   const int tile_pb = need_all >= p->hub_long_min ? p->hub_tile_pb : 1;
+  // per partition size 2^lp: successors per tile, list-region entries, reduce slices
+  int tw_of[HUB_MAX_LOGP + 1], nsl_of[HUB_MAX_LOGP + 1];
+  int64_t ptc_of[HUB_MAX_LOGP + 1];
+  for (int lp = 0; lp <= HUB_MAX_LOGP; lp++) {
+    // tile = tw successors (windows of 64 on one wave); large partitions get long tiles
+    const int64_t tcand = std::max<int64_t>(p->hub_tile_cand, (int64_t)tile_pb << lp);
+    const int64_t tw0 = std::max<int64_t>(1, tcand / L);
+    tw_of[lp] = (int)(tw0 > WAVE ? (tw0 + WAVE - 1) / WAVE * WAVE : tw0);
+    ptc_of[lp] = (int64_t)(1 << lp) * L;
+    nsl_of[lp] = ptc_of[lp] > 2 * slice ? (int)((ptc_of[lp] + slice - 1) / slice) : 0;
+  }
   {
     size_t oi = 0;
     while (oi < nbig) {
@@ -598,20 +619,17 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
         const int64_t deg = cand[nbig + i];
         // segmented path (no partition pass): iterations only (the init has no successor rows),
         // and at most 2^RANGE_BITS buckets of about seg_bucket candidates
-        const int lseg = std::max(0, ceil_log2((need + p->seg_bucket - 1) / p->seg_bucket));
+        const int lseg = p->seg_enabled ? std::max(0, ceil_log2((int64_t)cdiv32((uint32_t)need, sgb))) : RANGE_BITS + 1;
         const bool seg = p->seg_enabled && !a.unit && !hot && lseg <= RANGE_BITS;
-        const int64_t ptc0 = (int64_t)(1 << (seg ? lseg : logp_of(need))) * L;
+        const int logP = seg ? lseg : (int)lpv[i];
+        const int64_t ptc = ptc_of[logP];
         if (nd_all > b.d0 &&
-            (b.stg + (seg ? 0 : need) > budget || b.pt + ptc0 > budget || b.nseg + (1 << lseg) > (1 << 24))) break;
-        const int logP = seg ? lseg : logp_of(need);
+            (b.stg + (seg ? 0 : need) > budget || b.pt + ptc > budget || (seg && b.nseg + (1 << lseg) > (1 << 24))))
+          break;
         const int P = 1 << logP;
-        // tile = tw successors (windows of 64 on one wave); large partitions get long tiles
-        const int64_t tcand = std::max<int64_t>(p->hub_tile_cand, (int64_t)tile_pb << logP);
-        const int64_t tw0 = std::max<int64_t>(1, tcand / L);
-        const int tw = (int)(tw0 > WAVE ? (tw0 + WAVE - 1) / WAVE * WAVE : tw0);
-        const int T = seg ? 0 : (int)((deg + tw - 1) / tw);
-        const int64_t ptc = (int64_t)P * L;
-        const int nsl = ptc > 2 * slice ? (int)((ptc + slice - 1) / slice) : 0;
+        const int tw = tw_of[logP];
+        const int T = seg ? 0 : (int)cdiv32((uint32_t)deg, (uint32_t)tw);  // tiles cover every successor
+        const int nsl = nsl_of[logP];
         // staging offsets are cumulative candidate counts in descriptor order, the same order the
         // device scan walks the concatenated count matrices in: scanned cm = absolute offsets
         desc[nd_all++] = HubDesc{v, logP, T, (int32_t)need, tw, nsl, -1, (int32_t)b.nrange, b.cm, b.stg, b.pt, b.red,
@@ -631,6 +649,10 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       batches.push_back(b);
     }
   }
+  const auto t_plan2 = std::chrono::steady_clock::now();
+  p->host_plan_part[0] += std::chrono::duration<double>(t_plan1 - t_plan0).count();
+  p->host_plan_part[1] += std::chrono::duration<double>(t_plan2 - t_plan1).count();
+  p->host_plan_hubs += (int64_t)nbig;
   // hot tasks: every source, in descending candidate count (one launch; the longest fma chains
   // start first); hot list / cold list j belong to the j-th task
   std::vector<HotTask> htask;
@@ -707,6 +729,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   char* base = (char*)p->d_scratch;
   HubDesc* d_desc_all = (HubDesc*)(base + o_desc);
   int32_t* d_ovl = (int32_t*)(base + o_ovl);     // [0] count, [1..] sources for the HBM-table path
+  p->host_plan_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_plan0).count();
+  p->host_plan_calls++;
   HIP_OK(hipMemcpyAsync(d_desc_all, desc, sizeof(HubDesc) * nd_all, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemsetAsync(d_ovl, 0, 4, st));
   HotTask* d_htask = (HotTask*)(base + o_ht);

@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/ppr_hip.h"
@@ -108,7 +109,10 @@ struct ppr_plan {
   unsigned char* d_xtmp = nullptr;    // scan temporary of the block offsets
   size_t xsend_bytes = 0, xrecv_bytes = 0, xsz_bytes = 0, xtmp_bytes = 0;
   int64_t fused_max = 16384;          // PPR_FUSED_MAX: MC levels up to this many sources take one host sync
-  int64_t last_nbig = 0, last_maxneed = 0;  // the last hub pass: sources, largest candidate count
+  int64_t last_nbig = 0, last_maxneed = 0;
+  double host_plan_s = 0.0;                  // host time planning hub batches (PPR_TIMING, at destroy)
+  int64_t host_plan_calls = 0, host_plan_hubs = 0;
+  double host_plan_part[2] = {0.0, 0.0};     // ordering, batch/descriptor loop  // the last hub pass: sources, largest candidate count
   int32_t* ovl_pending = nullptr;     // MC combine: a level's hub overflow list not yet read (run_hubs)
   int64_t x_bytes = 0;                // block bytes received by this rank in the last sharded run
   int64_t merge_launches = 0;
@@ -195,6 +199,10 @@ inline void plan_free(ppr_plan* p) {
   hipFree(p->d_xsend); hipFree(p->d_xrecv); hipFree(p->d_xsz); hipFree(p->d_xtmp);
   if (p->h_hub_pin) hipHostFree(p->h_hub_pin);
   if (p->h_desc_pin) hipHostFree(p->h_desc_pin);
+  if (getenv("PPR_TIMING") && p->host_plan_calls)
+    fprintf(stderr, "ppr_timing hub_planning host_s %.4f calls %lld hubs %lld order_s %.4f batches_s %.4f\n",
+            p->host_plan_s, (long long)p->host_plan_calls, (long long)p->host_plan_hubs, p->host_plan_part[0],
+            p->host_plan_part[1]);
   if (p->d_diag) {
     unsigned long long h[160];
     if (hipMemcpy(h, p->d_diag, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
