@@ -397,7 +397,7 @@ struct BucketWave {
     if (cnt == 0) return;
     int at = 0;
     if (l == 0) at = (int)atomicAdd(pt_cnt_d, (uint32_t)cnt);
-    at = __shfl(at, 0);
+    at = __builtin_amdgcn_readlane(at, 0);
     int32_t* ok = pt_key + at;
     double* os = pt_sc + at;
     if (U <= Lw) {
@@ -598,7 +598,7 @@ __global__ void __launch_bounds__(256) k_hub_seg(DevGraph g, DevSlab s, IterArgs
       }
     }
     const int incl = wave_incl_scan(ln);
-    const int total = __shfl(incl, WAVE - 1);
+    const int total = __builtin_amdgcn_readlane(incl, WAVE - 1);
     ncand += (unsigned long long)total;
     lap(1);
     for (int g0 = 0; g0 < total; g0 += NG * WAVE) {
@@ -729,7 +729,7 @@ __device__ __forceinline__ void hub_bucket_one(const DevSlab& s, const IterArgs&
     if (cnt == 0) return;
     int at = 0;
     if (l == 0) at = (int)atomicAdd(&pt_cnt[tk.d], (uint32_t)cnt);
-    at = __shfl(at, 0);
+    at = __builtin_amdgcn_readlane(at, 0);
     int pos0 = 0;
     for (int i0 = 0; i0 < n; i0 += WAVE) {
       const int i = i0 + l;

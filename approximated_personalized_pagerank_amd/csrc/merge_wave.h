@@ -187,7 +187,7 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
   }
   succ(ln, rm);
   const int incl = wave_incl_scan(ln);
-  const int total = __shfl(incl, WAVE - 1);
+  const int total = __builtin_amdgcn_readlane(incl, WAVE - 1);
   // successor of candidate c: j = #{successors whose basket ends at or before c}. With every
   // basket non-empty the ends are distinct, so a batch marks them as byte flags in LDS and a
   // group reads j off one ballot of its 64 flags (instead of a 6-step cross-lane binary search)
@@ -222,7 +222,7 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
       }
       const int jj = j < WAVE ? j : WAVE - 1;
       // every candidate of the group from one successor basket: its keys are distinct
-      one[k] = !__ballot(valid && jj != __shfl(jj, 0));
+      one[k] = !__ballot(valid && jj != __builtin_amdgcn_readlane(jj, 0));
       const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
       const int ex = jj > 0 ? exv : 0;
       const int uj = __shfl(u, jj);

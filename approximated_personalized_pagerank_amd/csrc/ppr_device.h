@@ -54,12 +54,17 @@ __device__ __forceinline__ uint32_t tie_salt(int v) { return hash32((uint32_t)v 
 // larger = preferred (selection keeps the largest (score, tie_w) pairs)
 __device__ __forceinline__ uint32_t tie_w(int key, uint32_t ts) { return ~hash32((uint32_t)key ^ ts); }
 
+// Inclusive wave64 scan with DPP (no LDS round trip, unlike __shfl_up's ds_bpermute): Hillis-
+// Steele within each 16-lane row (row_shr 1, 2, 4, 8), then row 15's total into rows 1 and 3
+// (row_bcast:15) and lane 31's into rows 2 and 3 (row_bcast:31). A lane whose DPP source does not
+// exist keeps `old` = 0. Every lane of the wave must be active.
 __device__ __forceinline__ int wave_incl_scan(int x) {
-#pragma unroll
-  for (int o = 1; o < WAVE; o <<= 1) {
-    const int y = __shfl_up(x, o);
-    if (lane_id() >= o) x += y;
-  }
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
   return x;
 }
 __device__ __forceinline__ uint64_t wave_or(uint64_t x) {
@@ -72,10 +77,8 @@ __device__ __forceinline__ uint64_t wave_and(uint64_t x) {
   for (int o = 32; o; o >>= 1) x &= (uint64_t)__shfl_xor((unsigned long long)x, o);
   return x;
 }
-__device__ __forceinline__ int wave_sum(int x) {
-#pragma unroll
-  for (int o = 32; o; o >>= 1) x += __shfl_xor(x, o);
-  return x;
+__device__ __forceinline__ int wave_sum(int x) {  // every lane of the wave active
+  return __builtin_amdgcn_readlane(wave_incl_scan(x), WAVE - 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -254,7 +257,7 @@ __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c,
     const int n = i < nt ? c.cnt[c.touched[i]] : 0;
     const int incl = wave_incl_scan(n);
     if (i < nt) { c.tof[i] = (uint16_t)(run + incl - n); c.cnt[c.touched[i]] = (uint32_t)(run + incl - n); }
-    run += __shfl(incl, WAVE - 1);
+    run += __builtin_amdgcn_readlane(incl, WAVE - 1);
   }
   if (lane_id() == 0) c.tof[nt] = (uint16_t)run;
   wave_fence();
