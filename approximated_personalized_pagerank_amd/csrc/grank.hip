@@ -732,7 +732,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   p->host_plan_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_plan0).count();
   p->host_plan_calls++;
   HIP_OK(hipMemcpyAsync(d_desc_all, desc, sizeof(HubDesc) * nd_all, hipMemcpyHostToDevice, st));
-  HIP_OK(hipMemsetAsync(d_ovl, 0, 4, st));
+  // (d_ovl[0] is cleared by the first batch's k_hub_expand)
   HotTask* d_htask = (HotTask*)(base + o_ht);
   int32_t* d_hkey = (int32_t*)(base + o_hk);
   double* d_hsc = (double*)(base + o_hs);
@@ -793,13 +793,9 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     HubDesc* d_desc = d_desc_all + b.d0;
     const int maxP = b.maxP;
     if (ms && bi >= (size_t)nreg) HIP_OK(hipStreamWaitEvent(st, p->ev_fin[r], 0));  // region free again
-    HIP_OK(hipMemsetAsync(d_sd, 0, 4 * nd, st));
-    HIP_OK(hipMemsetAsync(d_pc, 0, 4 * nd, st));
-    HIP_OK(hipMemsetAsync(d_tau, 0, 8 * nd, st));
-    HIP_OK(hipMemsetAsync(d_oflag, 0, 4 * nd, st));
-    HIP_OK(hipMemsetAsync(d_lc, 0, 8, st));
+    // (k_hub_expand also clears d_sd, d_pc, d_tau, d_oflag, d_lc and, in the first batch, d_ovl[0])
     hipLaunchKernelGGL(k_hub_expand, dim3((unsigned)nd), dim3(256), 0, st, d_desc, d_tile, d_buck, d_rt, d_sg, d_rg,
-                       p->hub_range);
+                       p->hub_range, d_sd, d_pc, d_tau, d_oflag, d_lc, bi == 0 ? d_ovl : nullptr);
     HIP_OK(hipGetLastError());
     const int64_t ntiles = b.ntiles;
     const int64_t nbuck = b.nbuck;
@@ -1026,23 +1022,25 @@ static int run_merge_impl(ppr_plan* p, const IterArgs& a, const int32_t* list, i
   const DevSlab s = dev_slab(p);
   // small MC levels: classification, the hub sources' gather and the previous level's deferred
   // overflow count come back in one host sync (the combine's ~1800 levels are latency-bound)
-  const bool fused = a.mc && count <= p->fused_max && 2 * count <= p->n;
+  const bool fused = a.mc && count <= p->fused_max && GATHER_HDR + 3 * count <= p->n;
   if (!fused) {
     int r = flush_ovl(p, a, maxdiff);
     if (r) return r;
   } else {
     size_t capb = p->h_hub_cap * 12;
     void* ptr = p->h_hub_pin;
-    int r = ensure_pinned(&ptr, &capb, 12 * (size_t)count);
+    int r = ensure_pinned(&ptr, &capb, 4 * (GATHER_HDR + 3 * (size_t)count));
     if (r) return r;
     p->h_hub_pin = (int32_t*)ptr;
     p->h_hub_cap = capb / 12;
   }
 reclassify:
   HIP_OK(hipMemsetAsync(p->d_tier_cnt, 0, sizeof(uint32_t) * (NLISTS + 2), st));
-  const int64_t nb = (count + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+  const int cls_pw = count <= CLS_SMALL ? 1 : CLS_PER_WAVE;
+  const int64_t cls_pb = (int64_t)cls_pw * WAVES_PER_BLOCK;
+  const int64_t nb = (count + cls_pb - 1) / cls_pb;
   hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(256), 0, st, g, s, a, list, count,
-                     p->d_tier_cap, p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big);
+                     p->d_tier_cap, p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big, cls_pw);
   HIP_OK(hipGetLastError());
   if (!a.unit && p->max_deg > CLS_BIG_DEG) {
     hipLaunchKernelGGL(k_classify_big, dim3(256), dim3(CLS_BIG_THREADS), 0, st, g, s, a, p->d_tier_cap,
@@ -1051,17 +1049,16 @@ reclassify:
   HIP_OK(hipGetLastError());
   uint32_t cnt[NLISTS + 1];
   if (fused) {
+    static_assert(NLISTS + 1 < GATHER_HDR, "tier counters and the pending count fit the header");
     hipLaunchKernelGGL(k_gather_cand_deg_dev, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st,
-                       p->d_tier_lists + (int64_t)TIER_BIG * p->n, p->d_tier_cnt + TIER_BIG, count, p->d_cand,
-                       p->d_rp, p->d_ovf);
+                       p->d_tier_lists + (int64_t)TIER_BIG * p->n, p->d_tier_cnt, NLISTS + 1, TIER_BIG,
+                       p->ovl_pending, count, p->d_cand, p->d_rp, p->d_ovf);
     HIP_OK(hipGetLastError());
-    int32_t pend = 0;
-    HIP_OK(hipMemcpyAsync(cnt, p->d_tier_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(p->h_hub_pin, p->d_tier_lists + (int64_t)TIER_BIG * p->n, 4 * (size_t)count,
-                          hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(p->h_hub_pin + count, p->d_ovf, 8 * (size_t)count, hipMemcpyDeviceToHost, st));
-    if (p->ovl_pending) HIP_OK(hipMemcpyAsync(&pend, p->ovl_pending, 4, hipMemcpyDeviceToHost, st));
+    // one copy: counters, pending overflow count, hub list, candidate counts, degrees
+    HIP_OK(hipMemcpyAsync(p->h_hub_pin, p->d_ovf, 4 * (GATHER_HDR + 3 * (size_t)count), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    std::memcpy(cnt, p->h_hub_pin, sizeof(cnt));
+    const int32_t pend = p->h_hub_pin[NLISTS + 1];
     if (p->ovl_pending) {
       if (pend) {  // the previous level left sources to redo: their rows feed this classification
         int r = flush_ovl(p, a, maxdiff);
@@ -1114,10 +1111,10 @@ reclassify:
     // hub list and gathered counts | degrees arrived with the classification
     const size_t nh = cnt[TIER_BIG];
     if (p->hub_enabled) {
-      int r = run_hubs(p, a, p->h_hub_pin, p->h_hub_pin + count, nh, maxdiff, big);
+      int r = run_hubs(p, a, p->h_hub_pin + GATHER_HDR, p->h_hub_pin + GATHER_HDR + count, nh, maxdiff, big);
       if (r) return r;
     } else {
-      big.insert(big.end(), p->h_hub_pin, p->h_hub_pin + nh);
+      big.insert(big.end(), p->h_hub_pin + GATHER_HDR, p->h_hub_pin + GATHER_HDR + nh);
     }
   } else if (cnt[TIER_BIG]) {
     const size_t nh = cnt[TIER_BIG];

@@ -28,16 +28,26 @@ __global__ void __launch_bounds__(256) k_gather_cand_deg(const int32_t* list, in
   out[count + i] = (int32_t)(rp[v + 1] - rp[v]);
 }
 
-// the same gather with the hub count read on the device (at most cap): out[i] = cand, out[nh + i]
-// = out-degree, so the classification and the gather reach the host in one copy
-__global__ void __launch_bounds__(256) k_gather_cand_deg_dev(const int32_t* list, const uint32_t* nh_p, int64_t cap,
+// the same gather with the hub count read on the device (at most cap), for the fused small-level
+// path: everything the host needs after a classification lands in ONE buffer, so it comes back in
+// one copy: out[0, ncnt) = the tier counters, out[ncnt] = the previous level's deferred overflow
+// count (*pend_p, 0 without one), then from out + GATHER_HDR: the hub list (cap slots), its
+// candidate counts (nh) and its out-degrees (nh)
+constexpr int GATHER_HDR = 16;
+__global__ void __launch_bounds__(256) k_gather_cand_deg_dev(const int32_t* list, const uint32_t* tier_cnt, int ncnt,
+                                                             int tier_big, const int32_t* pend_p, int64_t cap,
                                                              const int32_t* cand, const int64_t* rp, int32_t* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nh = min((int64_t)*nh_p, cap);
+  if (blockIdx.x == 0 && threadIdx.x < GATHER_HDR)
+    out[threadIdx.x] = (int)threadIdx.x < ncnt ? (int32_t)tier_cnt[threadIdx.x]
+                       : ((int)threadIdx.x == ncnt && pend_p ? *pend_p : 0);
+  const int64_t nh = min((int64_t)tier_cnt[tier_big], cap);
   if (i >= nh) return;
   const int v = list[i];
-  out[i] = cand[v];
-  out[nh + i] = (int32_t)(rp[v + 1] - rp[v]);
+  int32_t* o = out + GATHER_HDR;
+  o[i] = v;
+  o[cap + i] = cand[v];
+  o[cap + nh + i] = (int32_t)(rp[v + 1] - rp[v]);
 }
 
 __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArgs a,

@@ -79,10 +79,26 @@ __device__ __forceinline__ void hub_bucket_range(const HubDesc& d, const int32_t
 }
 struct HubTask { int32_t d; int32_t x; };   // (descriptor, tile or bucket)
 
+// It also clears the batch's per-source counters (staged count, appended-list length, pruning
+// bound, overflow flag), the spill list length and, for a merge call's first batch, the overflow
+// list count: one launch instead of a fill per array (an MC level is latency-bound)
 __global__ void __launch_bounds__(256) k_hub_expand(const HubDesc* desc, HubTask* tiles, HubTask* buckets,
-                                                    HubTask* rts, HubTask* segs, HubTask* ranges, int krange) {
+                                                    HubTask* rts, HubTask* segs, HubTask* ranges, int krange,
+                                                    uint32_t* staged, uint32_t* pt_cnt, unsigned long long* tau,
+                                                    int32_t* oflag, uint32_t* lc, int32_t* ovl) {
   const int d = blockIdx.x;
   const HubDesc D = desc[d];
+  if (threadIdx.x == 0) {
+    staged[d] = 0u;
+    pt_cnt[d] = 0u;
+    tau[d] = 0ull;
+    oflag[d] = 0;
+    if (d == 0) {
+      lc[0] = 0u;
+      lc[1] = 0u;
+      if (ovl) ovl[0] = 0;
+    }
+  }
   const int P = 1 << D.logP;
   for (int t = threadIdx.x; t < D.T; t += blockDim.x) tiles[D.tile_off + t] = HubTask{d, t};
   if (D.sg_off >= 0) {

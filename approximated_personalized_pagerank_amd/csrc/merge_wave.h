@@ -14,8 +14,11 @@
 
 namespace pprk {
 
-constexpr int CLS_PER_WAVE = 16;
+constexpr int CLS_PER_WAVE = 16;     // sources per wave of a large list (throughput: an iteration)
 constexpr int CLS_PER_BLOCK = CLS_PER_WAVE * WAVES_PER_BLOCK;
+constexpr int64_t CLS_SMALL = 65536;  // lists up to this size take one source per wave: a wave's
+                                      // sources are summed one after another (three dependent
+                                      // loads each), which bounds a small MC level's latency
 constexpr int CLS_BIG_DEG = 512;      // sources with more successors are summed by k_classify_big
 constexpr int CLS_BIG_THREADS = 1024;
 
@@ -24,16 +27,18 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
                                                   const int32_t* tier_cap, int32_t* tier_lists,
                                                   uint32_t* tier_cnt, int64_t list_cap,
                                                   int32_t* cand, unsigned long long* stats,
-                                                  int32_t* big_list) {
+                                                  int32_t* big_list, int per_wave) {
+  // per_wave sources per wave (CLS_PER_WAVE, or 1 for a short list), per_block per block
+  const int per_block = per_wave * WAVES_PER_BLOCK;
   __shared__ int s_tier[CLS_PER_BLOCK];
   __shared__ int s_src[CLS_PER_BLOCK];
   __shared__ uint32_t s_base[NLISTS];
   __shared__ unsigned long long s_red[2][WAVES_PER_BLOCK];
   const int wv = threadIdx.x >> 6;
   unsigned long long my_c = 0, my_b = 0;
-  for (int k = 0; k < CLS_PER_WAVE; k++) {
-    const int slot = wv * CLS_PER_WAVE + k;
-    const int64_t idx = (int64_t)blockIdx.x * CLS_PER_BLOCK + slot;
+  for (int k = 0; k < per_wave; k++) {
+    const int slot = wv * per_wave + k;
+    const int64_t idx = (int64_t)blockIdx.x * per_block + slot;
     if (idx >= count) { if (lane_id() == 0) s_tier[slot] = -1; continue; }
     const int v = list[idx];
     const int64_t b = g.rp[v], e = g.rp[v + 1];
@@ -71,12 +76,12 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
   __syncthreads();
   if (threadIdx.x < NLISTS) {
     uint32_t n = 0;
-    for (int i = 0; i < CLS_PER_BLOCK; i++) n += s_tier[i] == (int)threadIdx.x;
+    for (int i = 0; i < per_block; i++) n += s_tier[i] == (int)threadIdx.x;
     s_base[threadIdx.x] = n ? atomicAdd(&tier_cnt[threadIdx.x], n) : 0u;
   }
   if (a.stats && lane_id() == 0) { s_red[0][wv] = my_c; s_red[1][wv] = my_b; }
   __syncthreads();
-  if (threadIdx.x < CLS_PER_BLOCK) {
+  if ((int)threadIdx.x < per_block) {
     const int t = s_tier[threadIdx.x];
     if (t >= 0) {
       uint32_t r = 0;
