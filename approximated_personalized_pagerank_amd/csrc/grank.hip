@@ -232,6 +232,13 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     if (e19) p->hub_range = std::max(0, std::min(32, atoi(e19)));
     const char* e6 = getenv("PPR_HUB_SLICE");
     p->hub_slice = std::max<int>(std::max<int>(64, (int)L), e6 ? atoi(e6) : HUB_SLICE);
+    // k_hub_reduce stages its slice in LDS when it fits beside the select's arrays (PPR_RED_LDS=0: off)
+    const char* e21 = getenv("PPR_RED_LDS");
+    const size_t red_lds = wg_lds_bytes(0, p->Lp, p->hub_slice);
+    p->red_pl = (!(e21 && atoi(e21) == 0) && red_lds <= 160 * 1024) ? p->hub_slice : 0;
+    p->hub_lds_red = p->red_pl ? red_lds : p->hub_lds_final;
+    if (p->red_pl)
+      hipFuncSetAttribute((const void*)k_hub_reduce, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     const char* e7 = getenv("PPR_HUB_STREAMS");
     p->hub_streams = (e7 && atoi(e7) == 1) ? 1 : 2;
     const char* e14 = getenv("PPR_WAVE_WPB");
@@ -883,8 +890,12 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     // long appended lists are cut (k_hub_reduce) so no k_hub_final workgroup selects from more
     // than a few slices' worth of entries; slices are reserved for the worst case, idle ones exit
     if (b.nrt) {
-      hipLaunchKernelGGL(k_hub_reduce, dim3((unsigned)b.nrt), dim3(WG_THREADS), p->hub_lds_final, sf, s, d_desc,
-                         d_rt, d_pc, d_pk, d_ps, d_rk, d_rs, p->Lp, slice);
+      // LDS-staged slices in the MC combine only: beside a GRank iteration's bucket waves (other
+      // streams, same CUs) a 100-KB workgroup crowds them out (measured 3.34 -> 3.66 s per job)
+      const bool rstage = a.mc && p->red_pl > 0;
+      hipLaunchKernelGGL(k_hub_reduce, dim3((unsigned)b.nrt), dim3(WG_THREADS),
+                         rstage ? p->hub_lds_red : p->hub_lds_final, sf, s, d_desc, d_rt, d_pc, d_pk, d_ps, d_rk,
+                         d_rs, p->Lp, slice, rstage ? p->red_pl : 0);
       HIP_OK(hipGetLastError());
       p->merge_launches++;
     }

@@ -360,7 +360,11 @@ struct BucketWave {
     }
 #pragma unroll
     for (int k = 0; k < NG; k++) {
-      if (fill + WAVE > budget) overflow = true;  // uniform: a group may bring 64 new keys
+      // uniform: at most the lanes whose early probe did not already show their key can bring a
+      // new key (a stale EMPTY counts as new), so a bucket spills only when the table could
+      // really pass its budget -- not whenever it holds more than budget - 64 keys
+      const int maybe_new = __popcll(__ballot(cv[k] && c0[k] != kk[k]));
+      if (fill + maybe_new > budget) overflow = true;
       bool ins = false;
       uint32_t h = 0;
       if (cv[k] && !overflow) {
@@ -786,11 +790,13 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_bucket(DevSlab s, IterArgs a
 __global__ void __launch_bounds__(WG_THREADS) k_hub_reduce(DevSlab s, const HubDesc* desc, const HubTask* tasks,
                                                            const uint32_t* pt_cnt, const int32_t* pt_key,
                                                            const double* pt_sc, int32_t* red_key, double* red_sc,
-                                                           int Lp, int slice) {
+                                                           int Lp, int slice, int pl) {
   extern __shared__ __align__(16) unsigned char smem[];
   const HubTask tk = tasks[blockIdx.x];
   const HubDesc d = desc[tk.d];
-  const WgLds L = wg_carve(smem, 0, Lp, 0);
+  // pl > 0: the slice is staged in LDS once (pk / pv of pl entries), so the radix passes of the
+  // select and the output pass read LDS instead of re-reading the list from L2 / HBM
+  const WgLds L = wg_carve(smem, 0, Lp, pl);
   const int Lw = s.L;
   const int n_all = (int)pt_cnt[tk.d];
   if (n_all <= 2 * slice) return;  // short list: k_hub_final selects from it directly
@@ -806,15 +812,20 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_reduce(DevSlab s, const HubD
     return;
   }
   if (threadIdx.x == 0) L.misc[M_PLEN] = 0;
+  const bool staged = n <= pl;
+  if (staged)
+    for (int i = threadIdx.x; i < n; i += WG_THREADS) { L.pk[i] = pk[i]; L.pv[i] = pv[i]; }
   __syncthreads();
+  const int32_t* ck = staged ? L.pk : pk;
+  const double* cv = staged ? L.pv : pv;
   const uint32_t ts = tie_salt(d.v);
-  const SelCrit c = wg_select_top(L, n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; },
+  const SelCrit c = wg_select_top(L, n, Lw, [&](int i) { return ck[i]; }, [&](int i) { return cv[i]; },
                                   [&](int) { return true; }, ts);
   for (int i = threadIdx.x; i < n; i += WG_THREADS) {
-    if (sel_test(c, dbits(pv[i]), tie_w(pk[i], ts))) {
+    if (sel_test(c, dbits(cv[i]), tie_w(ck[i], ts))) {
       const int pos = atomicAdd(&L.misc[M_PLEN], 1);
-      ok[pos] = pk[i];
-      os[pos] = pv[i];
+      ok[pos] = ck[i];
+      os[pos] = cv[i];
     }
   }
 }

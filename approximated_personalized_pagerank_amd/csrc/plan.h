@@ -78,6 +78,8 @@ struct ppr_plan {
   int flags = 0;
   std::vector<int64_t> h_rp;       // host row pointers (hub planning)
   size_t hub_lds_count = 0, hub_lds_wg = 0, hub_lds_final = 0, hub_lds_wave = 0;
+  size_t hub_lds_red = 0;  // k_hub_reduce: hub_lds_final + the LDS-staged slice (red_pl entries, 0 = unstaged)
+  int red_pl = 0;
   int hub_bucket = 448, hub_wave_t = 512;  // PPR_HUB_BUCKET, PPR_HUB_WAVE_T (merge_hub.h defaults)
   // pinned host staging of the hub planning (hub list + candidate counts down, descriptors up):
   // pageable copies of these (tens of MB per iteration) stalled the stream for milliseconds
