@@ -677,7 +677,10 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     }
   }
   if (p->d_diag && !a.unit)
-    for (size_t j = 0; j < nd_all; j++) p->diag_hub_cand += (double)(desc[j].need - 1);
+    for (size_t j = 0; j < nd_all; j++) {
+      p->diag_hub_cand += (double)(desc[j].need - 1);
+      if ((int64_t)desc[j].need > ((int64_t)hb << HUB_MAX_LOGP)) { p->diag_cap_src += 1; p->diag_cap_cand += desc[j].need - 1; }
+    }
   const size_t nht = htask.size();
   const bool hot_any = nht > 0;
   // one scratch layout for every batch (maxima), so no batch reallocates under a running one

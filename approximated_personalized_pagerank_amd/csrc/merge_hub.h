@@ -476,6 +476,10 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
   }
   if (B.overflow) {
     if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = HubTask{W.d, W.x}; }
+    if (a.diag && l == 0) {  // spilled buckets and their records
+      atomicAdd(&a.diag[152], 1ull);
+      atomicAdd(&a.diag[153], (unsigned long long)nb);
+    }
     return;
   }
   if (a.diag && l == 0) {  // bucket length histogram: count and cycles per log2(length) bin

@@ -146,6 +146,7 @@ struct ppr_plan {
   int32_t hot_built_it = -1;          // iteration of this run that built it (sharded runs iterate per range)
   std::vector<int32_t> h_hot_keys;    // host copy (fetch_slab decodes stored ids)
   int hot_max_need = 0x7fffffff;      // PPR_HOT_MAX: sources with more candidates skip the hot pass
+  double diag_cap_cand = 0.0, diag_cap_src = 0.0;  // PPR_DIAG: hub sources past 2^HUB_MAX_LOGP full buckets
   double diag_hub_cand = 0.0;         // PPR_DIAG: candidates of the hub sources planned (iterations)
   uint32_t* d_hot_bits = nullptr;     // [ceil(n / 32)]
   uint16_t* d_hot_idx = nullptr;      // [n]
@@ -218,6 +219,12 @@ inline void plan_free(ppr_plan* p) {
                 "task ms: longest %.2f, first %.2f, sum %.1f\n", p->hot_n, h[144], p->diag_hub_cand, (double)h[140],
                 100.0 * (double)h[140] / (p->diag_hub_cand > 0 ? p->diag_hub_cand : 1.0), h[141] / 1e5, h[143] / 1e5,
                 h[142] / 1e5);
+      if (p->diag_cap_src > 0)
+        fprintf(stderr, "ppr_diag sources beyond the bucket cap %.0f, candidates %.3e of %.3e\n", p->diag_cap_src,
+                p->diag_cap_cand, p->diag_hub_cand);
+      if (h[152])
+        fprintf(stderr, "ppr_diag spilled buckets %llu, records %llu (%.1f per bucket)\n", h[152], h[153],
+                (double)h[153] / (double)h[152]);
       if (h[150])
         fprintf(stderr, "ppr_diag rows merged %llu, unchanged (norm1 = 0) %llu (%.2f %%)\n", h[150], h[151],
                 100.0 * (double)h[151] / (double)h[150]);
