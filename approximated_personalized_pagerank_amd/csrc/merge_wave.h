@@ -22,6 +22,27 @@ constexpr int64_t CLS_SMALL = 65536;  // lists up to this size take one source p
 constexpr int CLS_BIG_DEG = 512;      // sources with more successors are summed by k_classify_big
 constexpr int CLS_BIG_THREADS = 1024;
 
+// sum of the current basket lengths of successors [b, e) taken from i0 in steps of `stride`:
+// four successor ids loaded before their four lengths, so a long list costs a quarter of the
+// dependent round trips (a short MC level waits on exactly these)
+__device__ __forceinline__ long long succ_len_sum(const DevGraph& g, const DevSlab& s, const IterArgs& a,
+                                                  int64_t i0, int64_t e, int stride) {
+  long long c = 0;
+  int64_t i = i0;
+  for (; i + 3 * (int64_t)stride < e; i += 4 * (int64_t)stride) {
+    int32_t cx[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) cx[k] = g.colx[i + k * (int64_t)stride];
+#pragma unroll
+    for (int k = 0; k < 4; k++) c += s.len[s.lrow(read_slot(a, cx[k]), cx[k] & 0x7fffffff)];
+  }
+  for (; i < e; i += stride) {
+    const int32_t cx = g.colx[i];
+    c += s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)];
+  }
+  return c;
+}
+
 __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArgs a,
                                                   const int32_t* list, int64_t count,
                                                   const int32_t* tier_cap, int32_t* tier_lists,
@@ -54,10 +75,7 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
     if (a.unit) {
       c = e - b;
     } else {
-      for (int64_t i = b + lane_id(); i < e; i += WAVE) {
-        const int32_t cx = g.colx[i];
-        c += s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)];
-      }
+      c = succ_len_sum(g, s, a, b + lane_id(), e, WAVE);
 #pragma unroll
       for (int o = 32; o; o >>= 1) c += __shfl_xor(c, o);
     }
@@ -109,11 +127,7 @@ __global__ void __launch_bounds__(CLS_BIG_THREADS) k_classify_big(DevGraph g, De
   for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
     const int v = big_list[i];
     const int64_t b = g.rp[v], e = g.rp[v + 1];
-    long long c = 0;
-    for (int64_t k = b + threadIdx.x; k < e; k += CLS_BIG_THREADS) {
-      const int32_t cx = g.colx[k];
-      c += s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)];
-    }
+    long long c = succ_len_sum(g, s, a, b + threadIdx.x, e, CLS_BIG_THREADS);
 #pragma unroll
     for (int o = 32; o; o >>= 1) c += __shfl_xor(c, o);
     if (lane_id() == 0) red[threadIdx.x >> 6] = c;
