@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(256) k_probe_lds_rank(int* ok, int trials, int
 }  // namespace pprk
 
 int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t K, uint32_t L,
-               double damping, const ppr_opts* o, ppr_plan** out) {
+               double damping, const ppr_opts* o, ppr_plan** out, bool mc) {
   const int64_t m = n ? row_ptr[n] : 0;
   // per-source candidate counts (<= deg * L + 1) and the hub staging offsets derived from them
   // are 32-bit on the device: reject a graph whose widest source could exceed that
@@ -201,8 +201,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   {
     const char* e1 = getenv("PPR_HUB_BUCKET");
     const char* e2 = getenv("PPR_HUB_WAVE_T");
-    p->hub_bucket = e1 ? std::max(64, atoi(e1)) : HUB_BUCKET;
-    p->hub_wave_t = e2 ? (std::max(256, atoi(e2)) + 63) / 64 * 64 : HUB_WAVE_T;  // a multiple of 64
+    p->hub_bucket = e1 ? std::max(64, atoi(e1)) : (mc ? HUB_BUCKET_MC : HUB_BUCKET);
+    p->hub_wave_t = e2 ? (std::max(256, atoi(e2)) + 63) / 64 * 64 : (mc ? HUB_WAVE_T_MC : HUB_WAVE_T);  // a multiple of 64
     p->hub_wave_t = std::min(p->hub_wave_t, 8192);
     // table fill before a bucket spills (a group may bring 64 new keys): PPR_BW_FILL percent
     const char* e17 = getenv("PPR_BW_FILL");

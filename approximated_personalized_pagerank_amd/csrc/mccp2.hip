@@ -73,7 +73,7 @@ extern "C" int ppr_mccp2_plan_create(const ppr_csr* g, uint32_t K, uint32_t L, d
     maxlev = std::max(maxlev, lv);
   }
   ppr_plan* p = nullptr;
-  rc = plan_alloc(n, rp, colx.data(), K, L, damping, o, &p);
+  rc = plan_alloc(n, rp, colx.data(), K, L, damping, o, &p, true);
   if (rc) return rc;
   p->mc = true;
   std::vector<int64_t> off(maxlev + 2, 0);

@@ -277,8 +277,9 @@ inline int dalloc(T** p, size_t count) {
 
 // plan buffers + merge tiers for a CSR whose colx (successor | read-slot bit << 31) is given;
 // no partitions, no active lists (grank.hip / mccp2.hip add their own)
+// (mc: the MCCompletePathV2 combine's bucket defaults, HUB_BUCKET_MC / HUB_WAVE_T_MC)
 int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t K, uint32_t L,
-               double damping, const ppr_opts* o, ppr_plan** out);
+               double damping, const ppr_opts* o, ppr_plan** out, bool mc = false);
 // final top-K: prefix K of the row in slot sA (partition 0 nodes) / sB (partition 1 nodes)
 int launch_topk(ppr_plan* p, int sA, int sB);
 // classify + every merge tier for `count` sources of the device list `list`
