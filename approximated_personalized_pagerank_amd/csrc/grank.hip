@@ -1057,7 +1057,9 @@ reclassify:
                      p->d_tier_cap, p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big, cls_pw);
   HIP_OK(hipGetLastError());
   if (!a.unit && p->max_deg > CLS_BIG_DEG) {
-    hipLaunchKernelGGL(k_classify_big, dim3(256), dim3(CLS_BIG_THREADS), 0, st, g, s, a, p->d_tier_cap,
+    // grid-stride over the long-list sources, at most one block per listed source
+    hipLaunchKernelGGL(k_classify_big, dim3((unsigned)std::min<int64_t>(256, count)), dim3(CLS_BIG_THREADS), 0, st, g,
+                       s, a, p->d_tier_cap,
                        p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big);
   }
   HIP_OK(hipGetLastError());
