@@ -2,16 +2,50 @@
 
 The library is built in-tree by ``build.build()`` (hipcc --offload-arch=gfx950). There is no
 fallback: if the shared object is missing or cannot be loaded, every entry point raises.
+
+Provenance: the build embeds the SHA-256 of every source it compiles (``source_digest()``,
+``-DPPR_SRC_SHA256``; ``ppr_build_info()`` returns it), and loading refuses a library whose
+embedded digest differs from the sources beside it -- a GPU run can only execute a binary compiled
+from exactly the committed sources it travelled with.
 """
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
+import re
 
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libppr_hip.so")
+CSRC = os.path.join(PKG_DIR, "csrc")
+# every file the library is compiled from (csrc/ plus the public header), in digest order
+CSRC_SOURCES = ["grank.hip", "mccp2.hip", "exact_ppr.hip", "host_graph.cpp"]
+CSRC_HEADERS = ["ppr_device.h", "ppr_common.h", "merge_wave.h", "wg_merge.h", "merge_hub.h", "merge_glb.h",
+                "merge_mc.h", "merge_hot.h", "plan.h", "host_par.h", os.path.join("..", "..", "include", "ppr_hip.h")]
+
+
+def source_digest(src_dir: str = CSRC) -> str:
+    """SHA-256 over (name, contents) of the library's sources and headers"""
+    h = hashlib.sha256()
+    for f in CSRC_SOURCES + CSRC_HEADERS:
+        path = os.path.join(src_dir, f)
+        if not os.path.exists(path):  # an older revision (tools/build_variant.py) may predate a file
+            continue
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def embedded_digest(path: str = LIB_PATH):
+    """the source digest a library was built from (read from the file, without loading it)"""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as fh:
+        m = re.search(rb"ppr_src_sha256=([0-9a-f]{64})", fh.read())
+    return m.group(1).decode() if m else None
 # A/B experiments only (tools/build_variant.py): load a variant build of the same ABI instead
 if os.environ.get("PPR_LIB_VARIANT"):
     LIB_PATH = os.path.join(PKG_DIR, "libppr_hip_" + os.environ["PPR_LIB_VARIANT"] + ".so")
@@ -94,10 +128,16 @@ def lib() -> ctypes.CDLL:
         raise RuntimeError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
         )
+    if not os.environ.get("PPR_LIB_VARIANT"):
+        emb, src = embedded_digest(LIB_PATH), source_digest()
+        if emb != src:
+            raise RuntimeError(f"{LIB_PATH} was built from other sources (embedded digest {emb}, sources {src}): "
+                               "rebuild it with `python -c 'import __graft_entry__ as g; g.build()'`")
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64, u32, f64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_double
     sigs = {
         "ppr_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+        "ppr_build_info": (ctypes.c_char_p, []),
         "ppr_find_partitions_csr": (ctypes.c_int, [vp, vp]),
         "ppr_execution_order_csr": (ctypes.c_int, [vp, vp]),
         "ppr_rmat_generate": (i64, [i32, i32, f64, f64, f64, ctypes.c_uint64, vp, vp, i64]),
@@ -151,6 +191,11 @@ def lib() -> ctypes.CDLL:
         fn.argtypes = args
     _lib = L
     return L
+
+
+def build_info() -> str:
+    """the loaded library's path and build record (source digest, target, compiler)"""
+    return f"{LIB_PATH}: " + lib().ppr_build_info().decode()
 
 
 def check(rc: int, where: str = "") -> None:

@@ -4,24 +4,15 @@ from __future__ import annotations
 import os
 import subprocess
 
-from ._lib import LIB_PATH, PKG_DIR
+from ._lib import CSRC, CSRC_HEADERS as HEADERS, CSRC_SOURCES as SOURCES, LIB_PATH, PKG_DIR, embedded_digest, \
+    source_digest
 
-CSRC = os.path.join(PKG_DIR, "csrc")
-SOURCES = ["grank.hip", "mccp2.hip", "exact_ppr.hip", "host_graph.cpp"]
-HEADERS = ["ppr_device.h", "ppr_common.h", "merge_wave.h", "wg_merge.h", "merge_hub.h", "merge_glb.h",
-           "merge_mc.h", "merge_hot.h", "plan.h", "host_par.h",
-           os.path.join("..", "..", "include", "ppr_hip.h")]
 ARCH = os.environ.get("PPR_OFFLOAD_ARCH", "gfx950")
 
 
 def _stale() -> bool:
-    if not os.path.exists(LIB_PATH):
-        return True
-    t = os.path.getmtime(LIB_PATH)
-    for f in SOURCES + HEADERS:
-        if os.path.getmtime(os.path.join(CSRC, f)) > t:
-            return True
-    return False
+    # by content, not mtime: the library must embed the digest of exactly these sources
+    return embedded_digest(LIB_PATH) != source_digest()
 
 
 def build(force: bool = False, verbose: bool = False, out: str | None = None, defines=(),
@@ -34,8 +25,10 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
     if out == LIB_PATH and not force and not _stale():
         return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    digest = source_digest(src_dir)
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-Wno-unused-value"] + [f"-D{d}" for d in defines] + [
+           "-Wno-unused-result", "-Wno-unused-value", f'-DPPR_SRC_SHA256="{digest}"',
+           f'-DPPR_OFFLOAD_ARCH="{ARCH}"'] + [f"-D{d}" for d in defines] + [
            "-I", os.path.join(PKG_DIR, "..", "include"),
            "-o", out + ".tmp"] + [os.path.join(src_dir, s) for s in SOURCES
                                   # an older revision (tools/build_variant.py --rev) may predate a source

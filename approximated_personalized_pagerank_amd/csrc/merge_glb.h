@@ -194,7 +194,9 @@ __global__ void k_xpack(DevSlab s, int nxt, const int32_t* list, int64_t count, 
   int32_t* rid = reinterpret_cast<int32_t*>(row);
   double* rsc = reinterpret_cast<double*>(row + 4 * (int64_t)((len + 1) & ~1));
   const int64_t src = s.row(nxt, v);
-  for (int i = lane_id(); i < len; i += WAVE) { rid[i] = s.ids[src + i]; rsc[i] = s.sc[src + i]; }
+  // blocks carry plain keys: a hot index (HOT_TAG | index) is this rank's own encoding, and each
+  // rank builds its hot set on its own (k_xunpack re-encodes with the receiver's set)
+  for (int i = lane_id(); i < len; i += WAVE) { rid[i] = s.key(s.ids[src + i]); rsc[i] = s.sc[src + i]; }
 }
 
 __global__ void k_xunpack(DevSlab s, int nxt, const int32_t* list, int64_t count, const unsigned char* buf) {
@@ -210,7 +212,7 @@ __global__ void k_xunpack(DevSlab s, int nxt, const int32_t* list, int64_t count
   uint64_t mn = ~0ull;
   for (int i = lane_id(); i < len; i += WAVE) {
     const double x = rsc[i];
-    s.ids[dst + i] = rid[i];
+    s.ids[dst + i] = s.enc(rid[i]);  // plain key -> this rank's stored id
     s.sc[dst + i] = x;
     const uint64_t b = dbits(x);
     mn = b < mn ? b : mn;
@@ -222,7 +224,7 @@ __global__ void k_xunpack(DevSlab s, int nxt, const int32_t* list, int64_t count
   while (lp < len) lp <<= 1;
   int pos = 0;
   for (int b = lp; b; b >>= 1)
-    if (pos + b <= len && row_range(s.key(rid[pos + b - 1])) <= q) pos += b;
+    if (pos + b <= len && row_range(rid[pos + b - 1]) <= q) pos += b;
   s.rix[s.xrow(nxt, v) + q] = (uint16_t)pos;
   if (lane_id() == 0) {
     s.len[s.lrow(nxt, v)] = len;

@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
   nst = wave_sum(nst);
   if (lane_id() == 0 && nst) {
     atomicAdd(&staged[tk.d], (uint32_t)nst);
-    if (a.diag) atomicAdd(&a.diag[140], (unsigned long long)nst);
+    if (a.diag) diag_add(a.diag, 140, (unsigned long long)nst);
   }
   if (!a.unit) {
 #pragma unroll
@@ -351,7 +351,7 @@ struct BucketWave {
   // (uniform) instead when the table could run out of slots
   template <int NG>
   __device__ __forceinline__ void chunk(const bool (&cv)[NG], const int (&kk)[NG], const double (&cs)[NG],
-                                        double factor) {
+                                        double factor, unsigned long long* ph = nullptr) {
     uint32_t sl[NG];
     // the first probe of every group is read up front (NG LDS reads in flight instead of one
     // round trip per group): a slot only ever goes EMPTY -> key, so a stale EMPTY is caught by
@@ -391,12 +391,24 @@ struct BucketWave {
       wave_fence();
     }
     if (overflow) return;
+    long long t1 = 0;
+    if (ph) {  // PPR_DIAG phase split: find-or-insert (with the probes) | ordered accumulation
+      t1 = (long long)clock64();
+      ph[2] += (unsigned long long)(t1 - (long long)ph[8]);
+    }
     chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor, ordered);
+    if (ph) {
+      const int z = t.keys[0];  // wait for the chains' LDS traffic before reading the clock
+      if (z == 0x7ffffffe) wave_fence();
+      const long long t2 = (long long)clock64();
+      ph[3] += (unsigned long long)(t2 - t1);
+      ph[8] = (unsigned long long)t2;
+    }
   }
 
   // keys >= tau (at most L by (score desc, tie_w desc)) appended to the source's list
   __device__ __forceinline__ void emit(double tau, int Lw, uint32_t* pt_cnt_d, int32_t* pt_key, double* pt_sc,
-                                       const IterArgs& a, uint32_t ts) {
+                                       const IterArgs& a, uint32_t ts, unsigned long long* ph = nullptr) {
     const int l = lane_id();
     // compact the occupied slots that can still reach the top-L (value >= tau) to the front, in
     // one pass (writes land at or below the slots already read)
@@ -415,23 +427,31 @@ struct BucketWave {
       wave_fence();
     }
     if (a.diag && l == 0) {  // distinct keys / kept keys per bucket
-      atomicAdd(&a.diag[64 + (31 - __clz(Uall | 1))], 1ull);
-      atomicAdd(&a.diag[96 + (31 - __clz(U | 1))], 1ull);
+      diag_add(a.diag, 64 + (31 - __clz(Uall | 1)), 1ull);
+      diag_add(a.diag, 96 + (31 - __clz(U | 1)), 1ull);
     }
     const int cnt = U <= Lw ? U : Lw;
     if (cnt == 0) return;
+    SelCrit c;
+    const int* keys = t.keys;
+    const double* acc = t.acc;
+    if (U > Lw) c = select_top(U, Lw, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, hist, ts);
+    long long t1 = 0;
+    if (ph) {
+      t1 = (long long)clock64();
+      ph[4] += (unsigned long long)(t1 - (long long)ph[8]);
+      if (l == 0) { ph[9] += U > Lw ? 1ull : 0ull; ph[10] += (unsigned long long)cnt; }
+    }
     int at = 0;
     if (l == 0) at = (int)atomicAdd(pt_cnt_d, (uint32_t)cnt);
     at = __builtin_amdgcn_readlane(at, 0);
     int32_t* ok = pt_key + at;
     double* os = pt_sc + at;
+    if (ph) ph[5] += (unsigned long long)((long long)clock64() - t1);
     if (U <= Lw) {
       for (int i = l; i < U; i += WAVE) { ok[i] = t.keys[i]; os[i] = t.acc[i]; }
       return;
     }
-    const int* keys = t.keys;
-    const double* acc = t.acc;
-    const SelCrit c = select_top(U, Lw, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, hist, ts);
     int pos0 = 0;
     for (int i0 = 0; i0 < U; i0 += WAVE) {
       const int i = i0 + l;
@@ -450,7 +470,7 @@ template <int NG>
 __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, const BucketWork* bw,
                                                       int64_t nbuck, const HubRec* st,
                                                       int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
-                                                      HubTask* spill, uint32_t* spill_cnt, int T, int budget) {
+                                                      HubTask* spill, uint32_t* spill_cnt, int T, int budget, int dry) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   const int l = lane_id();
@@ -458,12 +478,18 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
   // slower: the hardware refills CUs better than a fixed grid balances hot buckets)
   const int64_t cur = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (cur >= nbuck) return;
-  const BucketWork W = bw[cur];
   const long long t_start = a.diag ? (long long)clock64() : 0;
+  const BucketWork W = bw[cur];
+  // PPR_DIAG: per-phase cycles of this wave (lane-uniform registers; [8] = last stamp):
+  // 0 work record + table setup, 1 record loads, 2 find-or-insert, 3 ordered accumulation,
+  // 4 compaction + select, 5 appending atomic; 9 buckets that select (U > L), 10 entries appended
+  unsigned long long phv[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long* ph = (a.diag && (cur & 7) == 0) ? phv : nullptr;  // one wave in 8 (the clock reads cost)
   BucketWave B;
   B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0, budget);
   if (W.seed >= 0) B.seed(W.seed, W.selfval);
   const int nb = W.nb;
+  if (ph) { ph[8] = (unsigned long long)clock64(); ph[0] = ph[8] - (unsigned long long)t_start; }
   for (int g0 = 0; g0 < nb; g0 += NG * WAVE) {
     bool cv[NG];
     double cs[NG];
@@ -476,23 +502,43 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
       kk[k] = rec_key(r);
       cs[k] = rec_sc(r);
     }
-    B.chunk<NG>(cv, kk, cs, W.factor);
+    if (ph) {  // wait for the loads before timing them
+      int z = 0;
+#pragma unroll
+      for (int k = 0; k < NG; k++) z += kk[k] + (int)(cs[k] > 2.0);
+      if (z == 0x7fffffff) wave_fence();
+      const long long t2 = (long long)clock64();
+      ph[1] += (unsigned long long)(t2 - (long long)ph[8]);
+      ph[8] = (unsigned long long)t2;
+    }
+    B.chunk<NG>(cv, kk, cs, W.factor, ph);
     if (B.overflow) break;
+  }
+  if (dry) {  // PPR_WHATIF timing pass: accumulate only (keep the table live)
+    if (l == 0 && B.t.keys[0] == 0x7ffffffe) pt_cnt[W.d] = 0;
+    return;
   }
   if (B.overflow) {
     if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = HubTask{W.d, W.x}; }
     if (a.diag && l == 0) {  // spilled buckets and their records
-      atomicAdd(&a.diag[152], 1ull);
-      atomicAdd(&a.diag[153], (unsigned long long)nb);
+      diag_add(a.diag, 152, 1ull);
+      diag_add(a.diag, 153, (unsigned long long)nb);
     }
     return;
   }
   if (a.diag && l == 0) {  // bucket length histogram: count and cycles per log2(length) bin
     const int bin = 31 - __clz(nb | 1);
-    atomicAdd(&a.diag[bin], 1ull);
-    atomicAdd(&a.diag[32 + bin], (unsigned long long)((long long)clock64() - t_start));
+    diag_add(a.diag, bin, 1ull);
+    diag_add(a.diag, 32 + bin, (unsigned long long)((long long)clock64() - t_start));
   }
-  B.emit(W.tau, s.L, &pt_cnt[W.d], pt_key + W.pt_off, pt_sc + W.pt_off, a, W.ts);
+  B.emit(W.tau, s.L, &pt_cnt[W.d], pt_key + W.pt_off, pt_sc + W.pt_off, a, W.ts, ph);
+  if (ph && l == 0) {
+    for (int k = 0; k < 6; k++) diag_add(a.diag, 160 + k, ph[k]);
+    diag_add(a.diag, 166, 1ull);
+    diag_add(a.diag, 167, (unsigned long long)nb);
+    diag_add(a.diag, 168, ph[9]);
+    diag_add(a.diag, 169, ph[10]);
+  }
 }
 
 // Bucket ranges: one wave per range of krange consecutive buckets of one source (HubTask (d, x0)),
@@ -686,9 +732,9 @@ __global__ void __launch_bounds__(256) k_hub_seg(DevGraph g, DevSlab s, IterArgs
   if (dg) {
     lap(4);
     if (l == 0) {
-      for (int k = 0; k < 5; k++) atomicAdd(&a.diag[128 + k], ph[k]);
-      atomicAdd(&a.diag[133], 1ull);
-      atomicAdd(&a.diag[134], ncand);
+      for (int k = 0; k < 5; k++) diag_add(a.diag, 128 + k, ph[k]);
+      diag_add(a.diag, 133, 1ull);
+      diag_add(a.diag, 134, ncand);
     }
   }
 }
@@ -890,6 +936,11 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a,
   const WgLds L = wg_carve(smem, 0, Lp, 0);
   const int Lw = s.L;
   int n = (int)pt_cnt[di];  // appended bucket results, any order
+  if (a.diag && threadIdx.x == 0) {  // appended entries per source (vs L)
+    diag_add(a.diag, 170, 1ull);
+    diag_add(a.diag, 171, (unsigned long long)n);
+    diag_add(a.diag, 192 + (31 - __clz(n | 1)), 1ull);
+  }
   const int32_t* pk = pt_key + d.pt_off;
   const double* pv = pt_sc + d.pt_off;
   if (n > 2 * slice) {  // the list was cut to the top-L of every HUB_SLICE entries by k_hub_reduce

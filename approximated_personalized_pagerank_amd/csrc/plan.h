@@ -62,6 +62,11 @@ struct ppr_plan {
   int tierT[NT] = {0, 0, 0, 0};
   int tierCap[NT + 1] = {0, 0, 0, 0, 0};
   size_t wg_lds = 0;
+  // PPR_WHATIF (timing experiments only; tools/whatif.py): 1 no spill grid, 2 no reduce (k_hub_final
+  // selects from the whole list), 4 count twice, 8 scatter twice, 16 an extra dry bucket-wave pass
+  // (no emission), 32 final twice, 64 reduce twice
+  int whatif = 0;
+  int wg_max_passes = 64;  // (WG_MAX_PASSES) PPR_WG_PASSES (tests): workgroup-tier key-bucket passes before overflow
   bool hub_enabled = true;
   unsigned long long* d_maxdiff = nullptr;  // PPR_MAX_ITER_STATS + 1
   // iterations >= PPR_MAX_ITER_STATS share the last maxDiff slot: it is zeroed at the first
@@ -207,8 +212,13 @@ inline void plan_free(ppr_plan* p) {
             p->host_plan_s, (long long)p->host_plan_calls, (long long)p->host_plan_hubs, p->host_plan_part[0],
             p->host_plan_part[1]);
   if (p->d_diag) {
-    unsigned long long h[160];
-    if (hipMemcpy(h, p->d_diag, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+    std::vector<unsigned long long> hv(PPR_DIAG_SLOTS);
+    if (hipMemcpy(hv.data(), p->d_diag, 8 * hv.size(), hipMemcpyDeviceToHost) == hipSuccess) {
+      unsigned long long h[PPR_DIAG_BASE];
+      for (int i = 0; i < PPR_DIAG_BASE; i++) {  // shards summed (max-type counters are unsharded)
+        h[i] = hv[i];
+        for (int sh = 1; sh <= PPR_DIAG_SHARDS; sh++) h[i] += hv[(size_t)sh * PPR_DIAG_BASE + i];
+      }
       fprintf(stderr, "ppr_diag bucket_w: log2(x) | buckets by len, Mcycles | by distinct keys | by kept keys\n");
       for (int b = 0; b < 32; b++)
         if (h[b] || h[64 + b] || h[96 + b])
@@ -228,6 +238,21 @@ inline void plan_free(ppr_plan* p) {
       if (h[150])
         fprintf(stderr, "ppr_diag rows merged %llu, unchanged (norm1 = 0) %llu (%.2f %%)\n", h[150], h[151],
                 100.0 * (double)h[151] / (double)h[150]);
+      if (h[166]) {
+        const double tot = (double)(h[160] + h[161] + h[162] + h[163] + h[164] + h[165]);
+        fprintf(stderr, "ppr_diag bucket_w phases, 1 wave in 8 (%llu waves, %.3e records, %.1f Gcycles): work+setup %.1f %% loads %.1f %% "
+                "insert %.1f %% accumulate %.1f %% compact+select %.1f %% append %.1f %%; buckets selecting (U > L) %llu, "
+                "entries appended %.3e\n", h[166], (double)h[167], tot / 1e9, 100.0 * h[160] / tot, 100.0 * h[161] / tot,
+                100.0 * h[162] / tot, 100.0 * h[163] / tot, 100.0 * h[164] / tot, 100.0 * h[165] / tot, h[168],
+                (double)h[169]);
+      }
+      if (h[170]) {
+        fprintf(stderr, "ppr_diag hub final: %llu sources, appended entries %.3e (%.1f per source, %.1f x L); by log2(entries):",
+                h[170], (double)h[171], (double)h[171] / (double)h[170], (double)h[171] / (double)h[170] / (double)p->L);
+        for (int b = 0; b < 32; b++)
+          if (h[192 + b]) fprintf(stderr, " %d:%llu", b, h[192 + b]);
+        fprintf(stderr, "\n");
+      }
       if (h[133])
         fprintf(stderr, "ppr_diag k_hub_seg: %llu waves, %.1f candidates/wave, Mcycles setup %.1f window %.1f "
                 "gather %.1f accumulate %.1f emit %.1f\n", h[133], (double)h[134] / (double)h[133], h[128] / 1e6,

@@ -23,6 +23,16 @@ constexpr int TIER_BIG = NT + 1;      // hub pipeline
 constexpr int NLISTS = NT + 2;
 constexpr int MAX_L = 4096;           // widest basket the kernels accept
 constexpr int WAVES_PER_BLOCK = 4;
+// PPR_DIAG counters (u64, printed at plan destruction, plan.h): PPR_DIAG_BASE counters, plus as
+// many per shard -- per-wave counters go to a shard picked by block and wave, so hundreds of
+// millions of waves do not serialise on a few addresses (that contention distorted the timings)
+constexpr int PPR_DIAG_BASE = 256;
+constexpr int PPR_DIAG_SHARDS = 256;
+constexpr int PPR_DIAG_SLOTS = PPR_DIAG_BASE * (1 + PPR_DIAG_SHARDS);
+__device__ __forceinline__ void diag_add(unsigned long long* d, int idx, unsigned long long v) {
+  const uint32_t sh = (blockIdx.x * 7u + (threadIdx.x >> 6)) & (uint32_t)(PPR_DIAG_SHARDS - 1);
+  atomicAdd(&d[(size_t)PPR_DIAG_BASE * (1 + sh) + idx], v);
+}
 
 // one source of the HBM-table path (k_merge_glb)
 struct GlbWork {

@@ -394,7 +394,7 @@ static __global__ void __launch_bounds__(WG_THREADS) k_merge_wg(DevGraph g, DevS
                                                          const int32_t* cand, int Lp,
                                                          unsigned long long* maxdiff,
                                                          unsigned long long* stats,
-                                                         int32_t* ovf_list, uint32_t* ovf_cnt) {
+                                                         int32_t* ovf_list, uint32_t* ovf_cnt, int max_passes) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int64_t w = blockIdx.x;
   if (w >= count) return;
@@ -403,12 +403,16 @@ static __global__ void __launch_bounds__(WG_THREADS) k_merge_wg(DevGraph g, DevS
   const int64_t deg = g.rp[v + 1] - g.rp[v];
   const double factor = merge_factor(a, deg);
   int P = (cand[v] + WG_PASS_CAP - 1) / WG_PASS_CAP;
+  if (P > max_passes) {  // (PPR_WG_PASSES below the pass count a source needs: tests of the overflow path)
+    if (threadIdx.x == 0) { const uint32_t pos = atomicAdd(ovf_cnt, 1u); ovf_list[pos] = v; }
+    return;
+  }
   for (;;) {
     const bool ok = wg_accumulate(L, P, 0x9e3779b9u, true, v, self_seed(a, deg), factor, s.L,
                                   [&](auto&& fn) { wg_slab_stream(L, g, s, a, v, fn); });
     if (ok) break;
     P *= 2;
-    if (P > WG_MAX_PASSES) {
+    if (P > max_passes) {
       if (threadIdx.x == 0) { const uint32_t pos = atomicAdd(ovf_cnt, 1u); ovf_list[pos] = v; }
       return;
     }

@@ -22,6 +22,7 @@
 #include <atomic>
 #include <chrono>
 #include <iostream>
+#include <memory>
 #include <thread>
 #include <unordered_map>
 #include <utility>
@@ -61,16 +62,55 @@ struct Flat {
   std::vector<int32_t> col;
 };
 
+// key -> dense id: open addressing over a mix of std::hash<Key>, filled by all host threads at
+// once (slots claimed by CAS; the graph's keys are unique) -- a serial unordered_map of 4 M keys
+// took most of flatten's time
+template <typename Key>
+struct KeyIndex {
+  std::unique_ptr<std::atomic<int32_t>[]> slot;
+  uint64_t mask = 0;
+  const std::vector<const Key*>* keys = nullptr;
+  static uint64_t mix(uint64_t x) {  // splitmix64 finaliser: std::hash of integers is the identity
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL; x ^= x >> 27; x *= 0x94d049bb133111ebULL; x ^= x >> 31;
+    return x;
+  }
+  void build(const std::vector<const Key*>& k) {
+    keys = &k;
+    uint64_t cap = 16;
+    while (cap < 2 * (uint64_t)k.size()) cap <<= 1;
+    mask = cap - 1;
+    slot.reset(new std::atomic<int32_t>[cap]);
+    parallel_ranges((size_t)cap, [&](size_t b, size_t e) {
+      for (size_t i = b; i < e; i++) slot[i].store(-1, std::memory_order_relaxed);
+    });
+    parallel_ranges(k.size(), [&](size_t b, size_t e) {
+      for (size_t v = b; v < e; v++) {
+        uint64_t h = mix((uint64_t)std::hash<Key>()(*k[v])) & mask;
+        for (;;) {
+          int32_t expect = -1;
+          if (slot[h].compare_exchange_strong(expect, (int32_t)v, std::memory_order_relaxed)) break;
+          h = (h + 1) & mask;
+        }
+      }
+    });
+  }
+  int32_t find(const Key& key) const {  // -1: not a key of the graph
+    uint64_t h = mix((uint64_t)std::hash<Key>()(key)) & mask;
+    for (;;) {
+      const int32_t s = slot[h].load(std::memory_order_relaxed);
+      if (s < 0 || *(*keys)[(size_t)s] == key) return s;
+      h = (h + 1) & mask;
+    }
+  }
+};
+
 template <typename Key>
 inline Flat<Key> flatten(const std::unordered_map<Key, std::vector<Key>>& graph) {
   Flat<Key> f;
-  std::unordered_map<Key, int32_t> idx;
-  idx.reserve(graph.size());
   f.keys.reserve(graph.size());
-  for (const auto& kv : graph) {
-    idx.emplace(kv.first, (int32_t)f.keys.size());
-    f.keys.push_back(&kv.first);
-  }
+  for (const auto& kv : graph) f.keys.push_back(&kv.first);
+  KeyIndex<Key> idx;
+  idx.build(f.keys);  // (threads joined: every slot is published to the readers below)
   const size_t n = f.keys.size();
   std::vector<const std::vector<Key>*> succ(n);
   f.rp.assign(n + 1, 0);
@@ -88,10 +128,10 @@ inline Flat<Key> flatten(const std::unordered_map<Key, std::vector<Key>>& graph)
     for (size_t v = b; v < e; v++) {
       int64_t o = f.rp[v];
       for (const Key& s : *succ[v]) {
-        auto it = idx.find(s);
+        const int32_t id = idx.find(s);
         // every successor must be a key (README.md:69-73); the reference's behaviour is undefined
-        if (it == idx.end()) { bad = true; return; }
-        f.col[(size_t)o++] = it->second;
+        if (id < 0) { bad = true; return; }
+        f.col[(size_t)o++] = id;
       }
     }
   });
@@ -113,23 +153,32 @@ inline void fail(int rc) {
   exit(EXIT_FAILURE);
 }
 
+// The result's outer map: one (empty) inner map per source, in dense order. It needs only the
+// keys, so it is built on a host thread of its own WHILE the device computes (the outer inserts
+// are one thread's work: ~1 s at 4 M sources, hidden behind the device call).
 template <typename Key>
-inline std::unordered_map<Key, std::unordered_map<Key, double>> materialize(
-    const Flat<Key>& f, size_t K, const std::vector<int32_t>& ids, const std::vector<double>& sc,
-    const std::vector<int32_t>& len) {
+struct Outer {
   std::unordered_map<Key, std::unordered_map<Key, double>> out;
-  const size_t n = f.keys.size();
-  out.reserve(n);
-  std::vector<std::unordered_map<Key, double>*> row(n);
-  for (size_t v = 0; v < n; v++) row[v] = &out[*f.keys[v]];  // outer inserts: one thread
-  parallel_ranges(n, [&](size_t b, size_t e) {               // inner maps are independent
+  std::vector<std::unordered_map<Key, double>*> row;  // dense id -> its inner map (stable: node-based)
+  void build(const Flat<Key>& f) {
+    const size_t n = f.keys.size();
+    out.reserve(n);
+    row.resize(n);
+    for (size_t v = 0; v < n; v++) row[v] = &out[*f.keys[v]];
+  }
+};
+
+// inner maps from the device's top-K rows (independent per source: all host threads)
+template <typename Key>
+inline void materialize_rows(const Flat<Key>& f, Outer<Key>& o, size_t K, const std::vector<int32_t>& ids,
+                             const std::vector<double>& sc, const std::vector<int32_t>& len) {
+  parallel_ranges(f.keys.size(), [&](size_t b, size_t e) {
     for (size_t v = b; v < e; v++) {
-      std::unordered_map<Key, double>& m = *row[v];
+      std::unordered_map<Key, double>& m = *o.row[v];
       m.reserve((size_t)len[v]);
       for (int32_t i = 0; i < len[v]; i++) m.emplace(*f.keys[ids[v * K + i]], sc[v * K + i]);
     }
   });
-  return out;
 }
 
 template <typename Key>
@@ -146,20 +195,30 @@ inline std::unordered_map<Key, std::unordered_map<Key, double>> grank_device(
   std::vector<double> sc(n * K);
   ppr_stats st;
   const auto t1 = std::chrono::steady_clock::now();
+  Outer<Key> o;
+  double outer_s = 0.0;
+  std::thread outer([&] {  // beside the device call
+    const auto a = std::chrono::steady_clock::now();
+    o.build(f);
+    outer_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+  });
   const int rc = ppr_grank_csr(&g, nullptr, (uint32_t)K, (uint32_t)L, (uint32_t)iterations, damping,
                                tolerance, nullptr, ids.data(), sc.data(), len.data(), &st);
-  if (rc != PPR_OK) fail(rc);
   const auto t2 = std::chrono::steady_clock::now();
-  auto out = materialize(f, K, ids, sc, len);
+  outer.join();
+  if (rc != PPR_OK) fail(rc);
+  const auto t2b = std::chrono::steady_clock::now();
+  materialize_rows(f, o, K, ids, sc, len);
   if (getenv("PPR_TIMING")) {  // phase breakdown of one call (stderr)
     const auto t3 = std::chrono::steady_clock::now();
     auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double>(b - a).count();
     };
     std::cerr << "ppr_timing flatten_s " << sec(t0, t1) << " csr_call_s " << sec(t1, t2) << " device_s "
-              << st.device_ms / 1e3 << " materialize_s " << sec(t2, t3) << std::endl;
+              << st.device_ms / 1e3 << " materialize_s " << sec(t2, t3) << " outer_build_s " << outer_s
+              << " outer_wait_s " << sec(t2, t2b) << " inner_fill_s " << sec(t2b, t3) << std::endl;
   }
-  return out;
+  return std::move(o.out);
 }
 
 }  // namespace hipdetail

@@ -73,6 +73,12 @@ typedef struct ppr_stats {
 
 const char* ppr_strerror(int code);
 
+/* Build record of this library: "ppr_src_sha256=<hex> arch=<gfx target> hipcc=<clang version>".
+ * The digest covers every source and header the library was compiled from (build.py); the Python
+ * loader refuses a library whose digest differs from the sources beside it. No reference
+ * counterpart (provenance of the drop-in binary). */
+const char* ppr_build_info(void);
+
 /* ---- host-side graph preparation (no GPU) ---- */
 
 /* BFS 2-colouring of include/internal/pprInternal.h:29-99; part[i] = 0 for partitions.first */

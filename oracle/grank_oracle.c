@@ -367,6 +367,46 @@ int oracle_step(int64_t n, const int64_t* rp, const int32_t* col, int32_t L, dou
   return 0;
 }
 
+/* oracle_step without the per-source norm1 (the whole-iteration maxDiff comes from
+ * oracle_norm1_max): the full-size digests (tools/make_c3_digest.py) run it on chunks of one
+ * iteration's sources in parallel host threads -- it keeps no state between calls. */
+int oracle_step_rows(const int64_t* rp, const int32_t* col, int32_t L, double damping, const int32_t* ids,
+                     const double* sc, const int32_t* len, const int32_t* list, int64_t count, int32_t* nids,
+                     double* nsc, int32_t* nlen) {
+  acc_t a; memset(&a, 0, sizeof(a));
+  ent_t* buf = NULL; int64_t bufcap = 0;
+  for (int64_t q = 0; q < count; q++) {
+    int32_t v = list[q];
+    int64_t deg = rp[v + 1] - rp[v];
+    double factor = damping / (double)deg;
+    int64_t cand = 1;
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) cand += len[col[e]];
+    acc_init(&a, cand);
+    *acc_find(&a, v) = 1.0 - damping;
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
+      int32_t u = col[e];
+      for (int32_t j = 0; j < len[u]; j++) {
+        double* p = acc_find(&a, ids[(int64_t)u * L + j]);
+        *p = fma(sc[(int64_t)u * L + j], factor, *p);
+      }
+    }
+    nlen[v] = acc_top(&a, v, L, &buf, &bufcap, nids + (int64_t)v * L, nsc + (int64_t)v * L);
+    acc_reset(&a);
+  }
+  free(buf); acc_free(&a);
+  return 0;
+}
+
+/* final keepTop(K) (include/grank.h:143-147) of the listed rows of a slab, into [n][K] outputs */
+int oracle_topk_rows(int32_t L, int32_t K, const int32_t* ids, const double* sc, const int32_t* len,
+                     const int32_t* list, int64_t count, int32_t* out_ids, double* out_sc, int32_t* out_len) {
+  for (int64_t q = 0; q < count; q++) {
+    const int64_t v = list[q];
+    out_len[v] = row_topk((int32_t)v, ids + v * L, sc + v * L, len[v], K, out_ids + v * K, out_sc + v * K);
+  }
+  return 0;
+}
+
 /* ---- maxDiff of a whole iteration (the sampled-scale GPU tests): the norm1_stored pattern of
  * every listed source, old row -> new row, in O(L log L) per row: both rows sorted by hash_b (the
  * stored order; hash_b is a bijection, so equal hashes are equal keys) and matched by a merge,

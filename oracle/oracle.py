@@ -54,6 +54,11 @@ def lib():
         L.oracle_mc_combine.argtypes = [ctypes.c_int64, vp, vp, vp, ctypes.c_int32, ctypes.c_double, vp, vp, vp,
                                         vp, vp, vp, vp, ctypes.c_int64, vp, vp, vp]
         L.oracle_mc_combine.restype = ctypes.c_int
+        L.oracle_step_rows.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_double, vp, vp, vp, vp, ctypes.c_int64,
+                                       vp, vp, vp]
+        L.oracle_step_rows.restype = ctypes.c_int
+        L.oracle_topk_rows.argtypes = [ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, ctypes.c_int64, vp, vp, vp]
+        L.oracle_topk_rows.restype = ctypes.c_int
         L.oracle_tie_key.argtypes = [ctypes.c_int32, ctypes.c_int32]
         L.oracle_tie_key.restype = ctypes.c_uint32
         _lib = L
@@ -157,6 +162,50 @@ def step(row_ptr, col, L, damping, slab, lst):
         out_ids[r, out_len[r]:] = -1
         out_sc[r, out_len[r]:] = 0.0
     return out_ids, out_sc, out_len, md.value
+
+
+def _chunks(lst, weight, parts):
+    """split `lst` into about `parts` consecutive pieces of similar total weight"""
+    if len(lst) == 0:
+        return []
+    cw = np.cumsum(weight, dtype=np.float64)
+    cuts = np.searchsorted(cw, cw[-1] * np.arange(1, parts) / parts)
+    bounds = np.unique(np.concatenate([[0], cuts, [len(lst)]]))
+    return [lst[a:b] for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
+
+
+def step_rows_parallel(row_ptr, col, L, damping, slab, new, lst, threads=8):
+    """One Jacobi step of every source in `lst` (oracle_step_rows, no norm1) from `slab` = (ids [n,L],
+    scores [n,L], lens [n]) into the rows of `new` (same shapes, written in place), on `threads`
+    host threads (ctypes releases the GIL; sources are independent within a step)."""
+    from concurrent.futures import ThreadPoolExecutor
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+    cl = np.ascontiguousarray(col, dtype=np.int32)
+    ids, sc, ln = slab
+    nids, nsc, nln = new
+    assert all(a.flags.c_contiguous for a in (ids, sc, ln, nids, nsc, nln))
+    lst = np.ascontiguousarray(lst, dtype=np.int32)
+    deg = rp[lst + 1] - rp[lst]
+    # work estimate: candidates (successor row lengths), via the running sum over the successor list
+    src_w = np.add.reduceat(ln[cl].astype(np.int64), rp[:-1][lst]) if len(cl) else np.zeros(len(lst))
+    src_w = np.where(deg > 0, src_w, 1) + 64
+    parts = _chunks(lst, src_w, threads * 16)
+
+    def run(part):
+        part = np.ascontiguousarray(part)
+        return lib().oracle_step_rows(_p(rp), _p(cl), L, damping, _p(ids), _p(sc), _p(ln), _p(part), len(part),
+                                      _p(nids), _p(nsc), _p(nln))
+
+    with ThreadPoolExecutor(threads) as ex:
+        assert all(r == 0 for r in ex.map(run, parts))
+
+
+def topk_rows(L, K, slab, lst, out):
+    """final keepTop(K) of the listed rows of `slab` into out = (ids [n,K], scores [n,K], lens [n])"""
+    ids, sc, ln = slab
+    lst = np.ascontiguousarray(lst, dtype=np.int32)
+    assert lib().oracle_topk_rows(L, K, _p(ids), _p(sc), _p(ln), _p(lst), len(lst), _p(out[0]), _p(out[1]),
+                                  _p(out[2])) == 0
 
 
 def norm1_max(L, lst, old, new):

@@ -7,6 +7,8 @@
 //   dropin_test mcbad <case> / mcknown   the same for mccompletepathv2 (test/mccompletepathv2Test.cc)
 //   dropin_test e2e <scale> [iters]  RMAT graph as unordered_map, ppr::grank(K64, L128, iters (10)) end
 //                                    to end (PPR_TIMING=1: flatten / device / materialise split on stderr)
+//   dropin_test e2echeck <scale> <iters> <stride>  the same call; every stride-th result row compared
+//                                    with the device rows of ppr_grank_csr on the same CSR, bit for bit
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -107,6 +109,42 @@ int main(int argc, char** argv) {
            (long long)n, (long long)m, res.size(), entries,
            std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count());
     return 0;
+  }
+  if (mode == "e2echeck") {  // e2echeck <scale> <iters> <stride>: the materialised maps == the device rows
+    const int scale = atoi(argv[2]);
+    const int iters = atoi(argv[3]);
+    const int64_t stride = atoll(argv[4]);
+    const int64_t n = 1LL << scale;
+    std::vector<int64_t> rp(n + 1);
+    const int64_t m = ppr_rmat_generate(scale, 16, 0.57, 0.19, 0.19, 42, rp.data(), nullptr, 0);
+    std::vector<int32_t> col(m);
+    ppr_rmat_generate(scale, 16, 0.57, 0.19, 0.19, 42, rp.data(), col.data(), m);
+    for (int64_t v = 0; v < n; v++) graph[(int)v].assign(col.begin() + rp[v], col.begin() + rp[v + 1]);
+    const size_t K = 64, L = 128;
+    auto res = ppr::grank(graph, K, L, iters, 0.85, -1.0);
+    // the same call through the C ABI on the same flattening (dense id = graph iteration order)
+    ppr::hipdetail::Flat<int> f = ppr::hipdetail::flatten(graph);
+    ppr_csr g{(int64_t)f.keys.size(), f.rp.data(), f.col.data()};
+    std::vector<int32_t> ids(f.keys.size() * K), len(f.keys.size());
+    std::vector<double> sc(f.keys.size() * K);
+    if (ppr_grank_csr(&g, nullptr, (uint32_t)K, (uint32_t)L, (uint32_t)iters, 0.85, -1.0, nullptr, ids.data(), sc.data(),
+                      len.data(), nullptr) != PPR_OK)
+      return 3;
+    int bad = check(res.size() == f.keys.size(), "one result row per source");
+    int64_t rows = 0, entries = 0;
+    for (size_t v = 0; v < f.keys.size(); v += (size_t)stride) {
+      const auto it = res.find(*f.keys[v]);
+      if (it == res.end()) { bad += check(false, "row present"); continue; }
+      bad += check(it->second.size() == (size_t)len[v], "row length");
+      for (int32_t i = 0; i < len[v]; i++) {
+        const auto e = it->second.find(*f.keys[(size_t)ids[v * K + i]]);
+        bad += check(e != it->second.end() && e->second == sc[v * K + i], "entry key and score (bit for bit)");
+      }
+      rows++;
+      entries += len[v];
+    }
+    printf("{\"rows_checked\": %lld, \"entries_checked\": %lld, \"bad\": %d}\n", (long long)rows, (long long)entries, bad);
+    return bad ? 1 : 0;
   }
   if (mode == "empty") {
     auto res = ppr::grank(graph, 10, 30, 100, 0.85, 0.0001);

@@ -73,3 +73,15 @@ def test_end_to_end_timing_rmat(dropin):
     import json
     d = json.loads(out.strip().splitlines()[-1])
     assert d["nodes"] == 1 << 16 and d["rows"] == 1 << 16 and d["total_s"] > 0
+
+
+@pytest.mark.gpu
+def test_end_to_end_materialised_rows_rmat20(dropin):
+    """f1: the reference-API call on an unordered_map RMAT-20 graph (1 M sources,
+    K64/L128, 10 iterations) -- every 16th materialised row equals the device's row for the same
+    source (ppr_grank_csr on the same flattening), keys and scores bit for bit"""
+    out = subprocess.run([dropin, "e2echeck", "20", "10", "16"], capture_output=True, text=True, timeout=600)
+    import json
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert out.returncode == 0 and d["bad"] == 0, out.stderr[-2000:]
+    assert d["rows_checked"] == (1 << 20) // 16 and d["entries_checked"] > 30 * d["rows_checked"]

@@ -88,6 +88,20 @@ def test_gpu_mc_level_scheduling_bit_exact(env, monkeypatch, capfd):
         assert "deferred hub overflow redo" in capfd.readouterr().err
 
 
+def test_gpu_mc_deferred_overflow_beside_hbm_table_path(monkeypatch, capfd):
+    """levels whose hubs defer an overflow list (kept in the hub scratch until the next
+    level's classification) AND whose workgroup tier overflows to the HBM-table path, which reuses
+    that scratch: the deferred list must be read and its sources redone first. Forced here: every
+    source up to 18 K candidates takes the workgroup tier (wave tiers off), which may make only one
+    key-bucket pass (PPR_WG_PASSES=1, so sources past 6 K candidates overflow to the HBM table), and
+    the hubs take 8 K-candidate segments into 256-slot tables (they overflow)."""
+    for k, v in {"PPR_TIER_MASK": "0x30", "PPR_WG_PASSES": "1", "PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "8192",
+                 "PPR_SEG_T": "256", "PPR_DIAG": "1"}.items():
+        monkeypatch.setenv(k, v)
+    check_vs_oracle(ppr.rmat(13, seed=93), 16, 64, 100, 0.85, walks=False)
+    assert "deferred hub overflow redo" in capfd.readouterr().err
+
+
 @pytest.mark.parametrize("d", [0.5, 1.0])
 def test_gpu_mc_damping_edges(d):
     # d = 1: walks end only at dangling nodes or the step cap (the reference loops forever)

@@ -2,6 +2,9 @@
 
   C2  RMAT-18 K32/L64/20 it      whole run on the GPU == the CPU oracle's run, through SHA-256
                                  digests committed by tools/make_scale_digests.py
+  C3  RMAT-22 K64/L128/30 it     whole run on the GPU == the CPU oracle's whole run (digests of the
+                                 final top-K, of the full L-slab after iterations 1 and 28, and the
+                                 maxDiff of all 30 iterations; tools/make_c3_digest.py), and:
   C3  RMAT-22 K64/L128/30 it     the production hub regime (12 M-candidate sources, 2^28-record
                                  batches, four streams, three scratch regions): GPU iteration 29
                                  re-done by the oracle from the GPU's own iteration-29 state for
@@ -58,6 +61,46 @@ def test_gpu_c2_rmat18_whole_run_digest():
     assert dig(r.lens) == ref["lens_sha256"]
     assert dig(r.ids) == ref["ids_sha256"]
     assert dig(r.scores) == ref["scores_sha256"]
+
+
+C3_DIGEST = os.path.join(GOLDEN, "c3_rmat22_k64_l128_i30.json")
+
+
+def _dig(*arrays):
+    import hashlib
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.skipif(not os.path.exists(C3_DIGEST), reason="C3 oracle digest not generated")
+def test_gpu_c3_rmat22_whole_run_vs_oracle_digest():
+    """the headline workload end to end, bit for bit against the CPU oracle: final rows, the
+    whole slab after an early (1, partition 1) and a late partition-0 iteration (28), and every
+    iteration's maxDiff (include/grank.h:96-147)"""
+    with open(C3_DIGEST) as f:
+        ref = json.load(f)
+    t0 = time.time()
+    g = ppr.rmat(ref["scale"], seed=ref["seed"])
+    part = g.partitions()
+    assert (g.n, g.m, _dig(g.col), _dig(part)) == (ref["n"], ref["m"], ref["graph_sha256"], ref["part_sha256"])
+    K, L, d = ref["K"], ref["L"], ref["damping"]
+    plan = ppr.GrankPlan(g, K, L, d, part=part, device=0)
+    for it in (1, 28):  # state after iteration `it` = after it + 1 iterations
+        plan.run(it + 1, -1.0)
+        ids, sc, ln = plan.fetch_slab(it + 1)
+        assert _dig(ids, sc, ln) == ref["slab_after_iteration_sha256"][it], f"slab after iteration {it}"
+        progress(f"C3 slab after iteration {it} == oracle ({time.time() - t0:.1f} s)")
+    st = plan.run(ref["iters"], ref["tol"])
+    r = plan.fetch()
+    plan.close()
+    assert int(st.iterations_run) == ref["iterations_run"]
+    assert [float(x).hex() for x in st.max_diff[: ref["iterations_run"]]] == ref["max_diff"]
+    assert _dig(r.lens) == ref["lens_sha256"]
+    assert _dig(r.ids) == ref["ids_sha256"]
+    assert _dig(r.scores) == ref["scores_sha256"]
+    progress(f"C3 whole run == oracle ({time.time() - t0:.1f} s)")
 
 
 def test_gpu_c3_rmat22_sampled_iteration():

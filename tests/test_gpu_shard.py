@@ -135,3 +135,41 @@ def test_gpu_native_loop_multi_rank_local_group(world, tol):
         assert np.array_equal(r.lens, ref.lens) and np.array_equal(r.ids, ref.ids)
         assert np.array_equal(r.scores.view(np.uint64), ref.scores.view(np.uint64))
         pl.close()
+
+
+@pytest.mark.parametrize("hot", [False, True])
+def test_gpu_local_group_more_ranks_than_sources_past_256_iterations(hot, monkeypatch):
+    """a rank with an empty source range must still reset the shared maxDiff slot of
+    iterations >= 256 (PPR_MAX_ITER_STATS) and build the run's hot set. A 10-node ring at damping
+    0.99 converges slowly enough that maxDiff stays > 0 past iteration 300; tol is set to the
+    single-GPU maxDiff of iteration 300, so the stop falls beyond 256; 8 ranks share 5 active
+    sources per iteration, so at least 3 ranks merge nothing. Every rank must stop at the same
+    iteration as the single GPU and hold its result bit for bit."""
+    import approximated_personalized_pagerank_amd as ppr
+    from approximated_personalized_pagerank_amd.shard import run_local_group
+    if hot:
+        monkeypatch.setenv("PPR_HOT_N", "4")
+        monkeypatch.setenv("PPR_HOT_AT", "1")
+    n = 10
+    g = ppr.Csr(np.arange(n + 1, dtype=np.int64), np.array([(i + 1) % n for i in range(n)], dtype=np.int32))
+    part = g.partitions()
+    K, L, d, iters = 4, 8, 0.99, 420
+    probe = ppr.GrankPlan(g, K, L, d, part=part, device=0)
+    probe.init()
+    md = []
+    for it in range(320):
+        probe.iterate(it, 0, probe.active_count(it))
+        md.append(probe.read_maxdiff(it))
+    probe.close()
+    tol = md[300]
+    assert tol > 0 and md[299] > tol
+    ref = ppr.grank_csr(g, K, L, iters, d, tol, part=part, device=0)
+    assert 256 < ref.iterations_run < iters
+    plans = [ppr.GrankPlan(g, K, L, d, part=part, device=0) for _ in range(8)]
+    st = run_local_group(plans, iters, tol)
+    for pl, s in zip(plans, st):
+        assert int(s.iterations_run) == ref.iterations_run
+        r = pl.fetch()
+        assert np.array_equal(r.lens, ref.lens) and np.array_equal(r.ids, ref.ids)
+        assert np.array_equal(r.scores.view(np.uint64), ref.scores.view(np.uint64))
+        pl.close()

@@ -26,6 +26,20 @@ def test_abi_exports_every_declared_symbol():
         assert hasattr(L, s), s
 
 
+def test_library_built_from_these_sources(tmp_path):
+    """provenance: the loaded library embeds the digest of exactly the sources beside it, and the
+    loader refuses a library whose embedded digest differs"""
+    info = _lib.lib().ppr_build_info().decode()
+    assert f"ppr_src_sha256={_lib.source_digest()}" in info and "arch=gfx950" in info
+    assert _lib.embedded_digest(_lib.LIB_PATH) == _lib.source_digest()
+    other = tmp_path / "csrc"
+    other.mkdir()
+    for f in _lib.CSRC_SOURCES:  # the same tree with one edited source has another digest
+        txt = open(os.path.join(_lib.CSRC, f)).read()
+        (other / f).write_text(txt + ("\n// edited\n" if f == "grank.hip" else ""))
+    assert _lib.source_digest(str(other)) != _lib.source_digest()
+
+
 def test_strerror_messages_match_reference():
     L = _lib.lib()
     # include/grank.h:51-55, header-only/grankMulti.h:304
