@@ -253,6 +253,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     p->hub_tile_pb = e9 ? std::max(0, std::min(64, atoi(e9))) : HUB_TILE_PER_BUCKET;
     const char* e9b = getenv("PPR_HUB_TILE_CAND");
     if (e9b) p->hub_tile_cand = std::max(256, std::min(1 << 20, atoi(e9b)));
+    const char* ets = getenv("PPR_TILE_SPLIT_LOGP");  // 12 (HUB_MAX_LOGP): one tile list
+    if (ets) p->tile_split_logp = std::max(0, std::min(HUB_MAX_LOGP, atoi(ets)));
+    const char* ent = getenv("PPR_NT");
+    if (ent) p->nt_loads = (int)strtol(ent, nullptr, 0) & 3;
     const char* ewi = getenv("PPR_WHATIF");
     if (ewi) p->whatif = (int)strtol(ewi, nullptr, 0);
     const char* e9e = getenv("PPR_WG_PASSES");  // tests: force workgroup-tier overflows
@@ -516,6 +520,7 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   a.unit = unit ? 1u : 0u;
   a.stats = (p->flags & PPR_FLAG_STATS) ? 1u : 0u;
   a.lds_rank = p->lds_rank;
+  a.nt = (uint32_t)p->nt_loads;
   if (unit) { a.sA = 0; a.sB = 0; a.active = -1; return a; }
   a.sA = ((it + 1) / 2) & 1;
   a.sB = (it / 2) & 1;
@@ -643,20 +648,29 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
         const int nsl = nsl_of[logP];
         // staging offsets are cumulative candidate counts in descriptor order, the same order the
         // device scan walks the concatenated count matrices in: scanned cm = absolute offsets
+        // tiles of small-partition sources (logP <= split) and of large ones go to two lists,
+        // small first: count / scatter run them as separate launches, the small ones with LDS for
+        // their own few bucket counters (maxP_s) instead of the batch's largest P -- one 2^12-bucket
+        // source in a batch otherwise held every tile of the batch to 16 KB of LDS (9 waves per CU)
+        const bool small = logP <= p->tile_split_logp;
         desc[nd_all++] = HubDesc{v, logP, T, (int32_t)need, tw, nsl, -1, (int32_t)b.nrange, b.cm, b.stg, b.pt, b.red,
-                                 b.ntiles, b.nbuck, b.nrt, seg ? b.nseg : -1};
+                                 small ? b.ntiles_s : b.ntiles - b.ntiles_s, b.nbuck, b.nrt, seg ? b.nseg : -1};
         if (!seg && p->hub_range > 0) b.nrange += (P + p->hub_range - 1) / p->hub_range;
         b.cm += (int64_t)P * T;
         b.stg += seg ? 0 : need - 1;
         b.pt += ptc;
         b.red += (int64_t)nsl * L;
         b.ntiles += T;
+        if (small) { b.ntiles_s += T; if (T) b.maxP_s = std::max(b.maxP_s, P); }
         if (seg) b.nseg += P; else b.nbuck += P;
         b.nrt += nsl;
         b.maxP = std::max(b.maxP, P);
         oi++;
       }
       b.d1 = nd_all;
+      // large sources' tiles follow the small ones
+      for (size_t j = b.d0; j < b.d1; j++)
+        if (desc[j].logP > p->tile_split_logp) desc[j].tile_off += b.ntiles_s;
       batches.push_back(b);
     }
   }
@@ -814,22 +828,36 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     const int64_t ntiles = b.ntiles;
     const int64_t nbuck = b.nbuck;
     if (ntiles) {
-      // per-wave bucket counters (maxP ints): with large partitions one wave per block leaves no
-      // LDS stranded by the block granularity
-      const int twpb = maxP >= p->tile_wpb_p ? 1 : WAVES_PER_BLOCK;
-      const size_t lds_tile = (size_t)twpb * (maxP * 4 + HUB_WALK_FLAGS);
-      const unsigned tb = (unsigned)((ntiles + twpb - 1) / twpb);
+      // two tile lists (small-partition sources first): per-wave bucket counters (maxP ints) sized
+      // for each list's own largest P; with large partitions one wave per block leaves no LDS
+      // stranded by the block granularity
+      struct TileList { const HubTask* t; int64_t n; int maxP; };
+      const TileList tl[2] = {{d_tile, b.ntiles_s, b.maxP_s}, {d_tile + b.ntiles_s, ntiles - b.ntiles_s, maxP}};
+      auto launch_tiles = [&](bool scatter) -> int {
+        for (const TileList& x : tl) {
+          if (!x.n) continue;
+          const int twpb = x.maxP >= p->tile_wpb_p ? 1 : WAVES_PER_BLOCK;
+          const size_t lds_tile = (size_t)twpb * (x.maxP * 4 + HUB_WALK_FLAGS);
+          const unsigned tb = (unsigned)((x.n + twpb - 1) / twpb);
+          if (scatter)
+            hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, x.t, x.n,
+                               x.maxP, d_cmx, d_st);
+          else
+            hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, x.t, x.n, x.maxP,
+                               d_cm, d_tau, d_sd);
+          HIP_OK(hipGetLastError());
+        }
+        return PPR_OK;
+      };
       for (int rep = 0; rep < ((p->whatif & 4) ? 2 : 1); rep++) {
         if (rep) HIP_OK(hipMemsetAsync(d_sd, 0, 4 * nd, st));  // (the staged counts are summed)
-        hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
-                           d_cm, d_tau, d_sd);
-        HIP_OK(hipGetLastError());
+        int rc1 = launch_tiles(false);
+        if (rc1) return rc1;
       }
       HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, scan_tmp, d_cm, d_cmx, (int)b.cm, st));
       for (int rep = 0; rep < ((p->whatif & 8) ? 2 : 1); rep++) {
-        hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, d_tile, ntiles, maxP,
-                           d_cmx, d_st);
-        HIP_OK(hipGetLastError());
+        int rc1 = launch_tiles(true);
+        if (rc1) return rc1;
       }
     }
     // a batch of sources without successors (init of dangling nodes) has no tiles but still has

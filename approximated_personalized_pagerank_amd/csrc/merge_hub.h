@@ -396,7 +396,7 @@ struct BucketWave {
       t1 = (long long)clock64();
       ph[2] += (unsigned long long)(t1 - (long long)ph[8]);
     }
-    chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor, ordered);
+    chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor, ordered, ph);
     if (ph) {
       const int z = t.keys[0];  // wait for the chains' LDS traffic before reading the clock
       if (z == 0x7ffffffe) wave_fence();
@@ -483,7 +483,7 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
   // PPR_DIAG: per-phase cycles of this wave (lane-uniform registers; [8] = last stamp):
   // 0 work record + table setup, 1 record loads, 2 find-or-insert, 3 ordered accumulation,
   // 4 compaction + select, 5 appending atomic; 9 buckets that select (U > L), 10 entries appended
-  unsigned long long phv[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long phv[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // (11-14: chunk phases A-D)
   unsigned long long* ph = (a.diag && (cur & 7) == 0) ? phv : nullptr;  // one wave in 8 (the clock reads cost)
   BucketWave B;
   B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0, budget);
@@ -498,7 +498,17 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
     for (int k = 0; k < NG; k++) {
       const int q = g0 + k * WAVE + l;
       cv[k] = q < nb;
-      const HubRec r = cv[k] ? st[W.start + q] : HubRec{};
+      HubRec r{};
+      if (cv[k]) {
+        if (a.nt & 2u) {
+          const uint32_t* w = st[W.start + q].w;
+          r.w[0] = __builtin_nontemporal_load(w);
+          r.w[1] = __builtin_nontemporal_load(w + 1);
+          r.w[2] = __builtin_nontemporal_load(w + 2);
+        } else {
+          r = st[W.start + q];
+        }
+      }
       kk[k] = rec_key(r);
       cs[k] = rec_sc(r);
     }
@@ -538,6 +548,7 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
     diag_add(a.diag, 167, (unsigned long long)nb);
     diag_add(a.diag, 168, ph[9]);
     diag_add(a.diag, 169, ph[10]);
+    for (int k = 11; k < 15; k++) diag_add(a.diag, 172 + k - 11, ph[k]);
   }
 }
 

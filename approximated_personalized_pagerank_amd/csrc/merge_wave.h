@@ -250,8 +250,8 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
       sv[k] = 0.0;
       if (valid) {
         const int64_t r = s.row(sj, uj) + (c - ex);
-        key[k] = s.ids[r];
-        sv[k] = s.sc[r];
+        key[k] = ld_nt(&s.ids[r], a.nt & 1u);
+        sv[k] = ld_nt(&s.sc[r], a.nt & 1u);
       }
     }
   };

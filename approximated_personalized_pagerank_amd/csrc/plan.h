@@ -66,6 +66,7 @@ struct ppr_plan {
   // selects from the whole list), 4 count twice, 8 scatter twice, 16 an extra dry bucket-wave pass
   // (no emission), 32 final twice, 64 reduce twice
   int whatif = 0;
+  int nt_loads = 0;    // PPR_NT (IterArgs::nt): non-temporal candidate gathers (1) / staged-record reads (2)
   int wg_max_passes = 64;  // (WG_MAX_PASSES) PPR_WG_PASSES (tests): workgroup-tier key-bucket passes before overflow
   bool hub_enabled = true;
   unsigned long long* d_maxdiff = nullptr;  // PPR_MAX_ITER_STATS + 1
@@ -131,6 +132,8 @@ struct ppr_plan {
   int hub_streams = 2;
   int wave_wpb = 1;                // PPR_WAVE_WPB: waves per block of k_merge_lds (1, 2 or 4)
   int tile_wpb_p = 4096;           // PPR_TILE_WPB_P: count / scatter run one wave per block from this maxP on
+  int tile_split_logp = 10;        // PPR_TILE_SPLIT_LOGP: count / scatter tiles of sources with P <= 2^this
+                                   // in a launch of their own (LDS for their P counters only)
   int hub_bw_budget = 380;         // distinct keys a bucket wave's table takes before it spills
   int hub_mix = 6;                 // PPR_HUB_MIX: interleave sources with P >= 2^hub_mix among the others
   int hub_tile_cand = 4096;         // PPR_HUB_TILE_CAND: minimum tile candidates (HUB_TILE_CAND)
@@ -245,6 +248,11 @@ inline void plan_free(ppr_plan* p) {
                 "entries appended %.3e\n", h[166], (double)h[167], tot / 1e9, 100.0 * h[160] / tot, 100.0 * h[161] / tot,
                 100.0 * h[162] / tot, 100.0 * h[163] / tot, 100.0 * h[164] / tot, 100.0 * h[165] / tot, h[168],
                 (double)h[169]);
+        const double acc = (double)(h[172] + h[173] + h[174] + h[175]);
+        if (acc > 0)
+          fprintf(stderr, "ppr_diag bucket_w accumulate phases: A occurrence ranks %.1f %% B slot offsets %.1f %% "
+                  "C value placement %.1f %% D per-slot chains %.1f %%\n", 100.0 * h[172] / acc, 100.0 * h[173] / acc,
+                  100.0 * h[174] / acc, 100.0 * h[175] / acc);
       }
       if (h[170]) {
         fprintf(stderr, "ppr_diag hub final: %llu sources, appended entries %.3e (%.1f per source, %.1f x L); by log2(entries):",

@@ -51,7 +51,12 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
 }
 
 // one batch of the hub pipeline (host planning): descriptor range and the batch's totals
-struct HubBatch { size_t d0, d1; int64_t cm, stg, pt, ntiles, nbuck, nrt, red, nseg; int maxP; int64_t nrange = 0; };
+// (ntiles_s / maxP_s: the tiles of the batch's small-partition sources, listed first, which count
+// and scatter launch separately with LDS for maxP_s counters -- see run_hubs)
+struct HubBatch {
+  size_t d0, d1; int64_t cm, stg, pt, ntiles, nbuck, nrt, red, nseg; int maxP; int64_t nrange = 0;
+  int64_t ntiles_s = 0; int maxP_s = 1;
+};
 
 struct DevGraph {
   const int64_t* rp;
@@ -145,7 +150,13 @@ struct IterArgs {
   const int64_t* rp; // row pointers (out-degree of the source in the epilogue)
   unsigned long long* diag;  // PPR_DIAG: per-kernel histograms (nullptr = off)
   uint32_t lds_rank;         // LDS atomics return same-address lanes in lane order (probed per plan)
+  uint32_t nt;               // PPR_NT: 1 = basket-row gathers of the candidate walks, 2 = staged-record
+                             // reads of the bucket waves, as non-temporal loads (streamed once: they
+                             // should not evict the scatter's partially written staging lines from L2)
 };
+
+template <class T>
+__device__ __forceinline__ T ld_nt(const T* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
 
 __device__ __forceinline__ int read_slot(const IterArgs& a, int32_t cx) { return (cx < 0) ? a.sB : a.sA; }
 

@@ -207,13 +207,25 @@ struct ChunkLds {
 // k_probe_lds_rank), phase A takes each record's occurrence index straight from a returning LDS
 // atomic add on its slot's counter -- same-address lanes of one instruction receive the old
 // values in lane order, i.e. stream order -- instead of from ballots over the slot bits.
+// (ph: PPR_DIAG cycle counters of phases A..D at ph[11..14], each phase's LDS traffic waited for
+// before the clock is read; nullptr = no timing)
+__device__ __forceinline__ void diag_lap(unsigned long long* ph, int k, long long& t, const volatile uint32_t* lds) {
+  if (!ph) return;
+  if (*lds == 0xfffffffeu) wave_fence();  // an LDS read in order behind the phase's own
+  const long long t2 = (long long)clock64();
+  ph[k] += (unsigned long long)(t2 - t);
+  t = t2;
+}
+
 template <int NG>
 __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c, int nbits,
                                                  const bool (&valid)[NG], const uint32_t (&slot)[NG],
-                                                 const double (&val)[NG], double factor, bool ordered) {
+                                                 const double (&val)[NG], double factor, bool ordered,
+                                                 unsigned long long* ph = nullptr) {
   const uint64_t lt = lanemask_lt();
   uint32_t occ[NG];
   int nt = 0;
+  long long tph = ph ? (long long)clock64() : 0;
   if (ordered) {
 #pragma unroll
     for (int k = 0; k < NG; k++) {
@@ -250,6 +262,7 @@ __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c,
     occ[k] = base + (uint32_t)__popcll(mm & lt);
     wave_fence();
   }
+  diag_lap(ph, 11, tph, c.cnt);
   // B: offsets of the touched slots (touched order), written over their counts
   int run = 0;
   for (int i0 = 0; i0 < nt; i0 += WAVE) {
@@ -261,11 +274,13 @@ __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c,
   }
   if (lane_id() == 0) c.tof[nt] = (uint16_t)run;
   wave_fence();
+  diag_lap(ph, 12, tph, c.cnt);
   // C: values grouped by slot, stream order inside a slot
 #pragma unroll
   for (int k = 0; k < NG; k++)
     if (valid[k]) c.vals[c.cnt[slot[k]] + occ[k]] = val[k];
   wave_fence();
+  diag_lap(ph, 13, tph, c.cnt);
   // D: one lane per touched slot
   for (int i = lane_id(); i < nt; i += WAVE) {
     const uint32_t sl = c.touched[i];
@@ -284,6 +299,7 @@ __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c,
     c.cnt[sl] = 0;
   }
   wave_fence();
+  diag_lap(ph, 14, tph, c.cnt);
 }
 
 // In-place compaction of occupied slots to the front (keys[0..U), acc[0..U)); returns U.

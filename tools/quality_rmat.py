@@ -1,9 +1,10 @@
-"""Quality of the engine's GRank vs exact PPR at benchmark scale: GRank
-on RMAT-<scale> on the GPU, then the reference harness's measure (benchmarkAlgorithm: top-K Jaccard
-and Kendall against pprSingleSource(g, 100, .85, 1e-4) of sampled non-dangling sources) with the
-exact PPR batched on the GPU.
+"""Quality of the engine vs exact PPR at benchmark scale: GRank (or
+MCCompletePathV2, --algo mc) on RMAT-<scale> on the GPU, then the reference harness's measure
+(benchmarkAlgorithm: top-K Jaccard and Kendall against pprSingleSource(g, 100, .85, 1e-4) of sampled
+non-dangling sources) with the exact PPR batched on the GPU.
 
-    python tools/quality_rmat.py [--scale 22] [--K 64] [--L 128] [--iters 30] [--sources 200]
+    python tools/quality_rmat.py [--algo grank|mc] [--scale 22] [--K 64] [--L 128] [--iters 30] [--sources 200]
+      (mc: --iters = random walks per node R; C5 = --algo mc --K 50 --L 200 --iters 1000)
 """
 import argparse
 import json
@@ -27,10 +28,14 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--sources", type=int, default=200)
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--algo", choices=["grank", "mc"], default="grank")
     a = ap.parse_args()
     t0 = time.time()
     g = ppr.rmat(a.scale, seed=a.seed)
-    r = ppr.grank_csr(g, a.K, a.L, a.iters, 0.85, -1.0, part=g.partitions(), device=0)
+    if a.algo == "mc":
+        r = ppr.mccp2_csr(g, a.K, a.L, a.iters, 0.85, seed=20261016, device=0)
+    else:
+        r = ppr.grank_csr(g, a.K, a.L, a.iters, 0.85, -1.0, part=g.partitions(), device=0)
     t1 = time.time()
     deg = g.degrees()
     rng = np.random.default_rng(2026)
@@ -49,10 +54,12 @@ def main():
         m = int(r.lens[v])
         js.append(ppr.jaccard(r.ids[v, :m].tolist(), eids[i, :min(m, eln[i])].tolist()))
         ks.append(ppr.kendall_correlation(r.scores[v, :m], at[i, :m]))
-    out = {"config": f"grank RMAT-{a.scale} K={a.K} L={a.L} iters={a.iters}", "sources": len(src),
+    what = f"mccompletepathv2 RMAT-{a.scale} K={a.K} L={a.L} R={a.iters}" if a.algo == "mc" else \
+        f"grank RMAT-{a.scale} K={a.K} L={a.L} iters={a.iters}"
+    out = {"config": what, "sources": len(src),
            "jaccard_average": float(np.mean(js)), "jaccard_min": float(np.min(js)),
            "kendall_average": float(np.mean(ks)), "kendall_min": float(np.min(ks)),
-           "exact_ppr_iterations_mean": float(its.mean()), "grank_s": round(t1 - t0, 1),
+           "exact_ppr_iterations_mean": float(its.mean()), "engine_s": round(t1 - t0, 1),
            "exact_ppr_s": round(t2 - t1, 2)}
     print(json.dumps(out))
 
