@@ -521,6 +521,7 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   a.stats = (p->flags & PPR_FLAG_STATS) ? 1u : 0u;
   a.lds_rank = p->lds_rank;
   a.nt = (uint32_t)p->nt_loads;
+  a.whatif = (uint32_t)p->whatif;
   if (unit) { a.sA = 0; a.sB = 0; a.active = -1; return a; }
   a.sA = ((it + 1) / 2) & 1;
   a.sB = (it / 2) & 1;

@@ -488,7 +488,8 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
   BucketWave B;
   B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0, budget);
   if (W.seed >= 0) B.seed(W.seed, W.selfval);
-  const int nb = W.nb;
+  // (PPR_WHATIF 128, timing only: long buckets cut to 2048 records -- what the hot-key chains cost)
+  const int nb = ((a.whatif & 128u) && W.nb > 2048) ? 2048 : W.nb;
   if (ph) { ph[8] = (unsigned long long)clock64(); ph[0] = ph[8] - (unsigned long long)t_start; }
   for (int g0 = 0; g0 < nb; g0 += NG * WAVE) {
     bool cv[NG];

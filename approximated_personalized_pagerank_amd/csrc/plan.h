@@ -64,7 +64,7 @@ struct ppr_plan {
   size_t wg_lds = 0;
   // PPR_WHATIF (timing experiments only; tools/whatif.py): 1 no spill grid, 2 no reduce (k_hub_final
   // selects from the whole list), 4 count twice, 8 scatter twice, 16 an extra dry bucket-wave pass
-  // (no emission), 32 final twice, 64 reduce twice
+  // (no emission), 32 final twice, 64 reduce twice, 128 bucket waves stop after 2048 records
   int whatif = 0;
   int nt_loads = 0;    // PPR_NT (IterArgs::nt): non-temporal candidate gathers (1) / staged-record reads (2)
   int wg_max_passes = 64;  // (WG_MAX_PASSES) PPR_WG_PASSES (tests): workgroup-tier key-bucket passes before overflow

@@ -153,6 +153,7 @@ struct IterArgs {
   uint32_t nt;               // PPR_NT: 1 = basket-row gathers of the candidate walks, 2 = staged-record
                              // reads of the bucket waves, as non-temporal loads (streamed once: they
                              // should not evict the scatter's partially written staging lines from L2)
+  uint32_t whatif;           // PPR_WHATIF bits that act inside kernels (timing experiments, plan.h)
 };
 
 template <class T>
