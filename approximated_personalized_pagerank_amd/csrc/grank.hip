@@ -255,6 +255,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     if (e9b) p->hub_tile_cand = std::max(256, std::min(1 << 20, atoi(e9b)));
     const char* ets = getenv("PPR_TILE_SPLIT_LOGP");  // 12 (HUB_MAX_LOGP): one tile list
     if (ets) p->tile_split_logp = std::max(0, std::min(HUB_MAX_LOGP, atoi(ets)));
+    const char* esp = getenv("PPR_SPEC");
+    if (esp) p->spec_ratio = std::max(0.0, std::min(1.0, atof(esp)));
+    const char* esf = getenv("PPR_SPEC_FROM");
+    if (esf) p->spec_from = std::max(0, atoi(esf));
     const char* ent = getenv("PPR_NT");
     if (ent) p->nt_loads = (int)strtol(ent, nullptr, 0) & 3;
     const char* ewi = getenv("PPR_WHATIF");
@@ -323,22 +327,35 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     }
     p->lds_rank = ok ? 1u : 0u;
   }
-  hipFuncSetAttribute((const void*)k_hub_bucket_w<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_bucket_w<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_bucket_w<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_bucket_w<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_range<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_range<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_range<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_range<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_seg<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_bucket, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_final, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_topk, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_count, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_hot, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipFuncSetAttribute((const void*)k_hub_join, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  // every kernel that may take more than the default 64 KB of dynamic LDS; a refusal (e.g. a
+  // kernel that also declares static LDS) fails the plan instead of surfacing later as a launch error
+  {
+    const std::pair<const void*, const char*> big_lds[] = {
+        {(const void*)k_hub_bucket_w<1>, "k_hub_bucket_w<1>"},
+        {(const void*)k_hub_bucket_w<2>, "k_hub_bucket_w<2>"},
+        {(const void*)k_hub_bucket_w<4>, "k_hub_bucket_w<4>"},
+        {(const void*)k_hub_bucket_w<8>, "k_hub_bucket_w<8>"},
+        {(const void*)k_hub_range<1>, "k_hub_range<1>"},
+        {(const void*)k_hub_range<2>, "k_hub_range<2>"},
+        {(const void*)k_hub_range<4>, "k_hub_range<4>"},
+        {(const void*)k_hub_range<8>, "k_hub_range<8>"},
+        {(const void*)k_hub_seg<4>, "k_hub_seg<4>"},
+        {(const void*)k_hub_bucket, "k_hub_bucket"},
+        {(const void*)k_hub_final, "k_hub_final"},
+        {(const void*)k_topk, "k_topk"},
+        {(const void*)k_hub_count, "k_hub_count"},
+        {(const void*)k_hub_scatter, "k_hub_scatter"},
+        {(const void*)k_hub_hot, "k_hub_hot"},
+        {(const void*)k_hub_join, "k_hub_join"},
+    };
+    for (const auto& k : big_lds)
+      if (hipFuncSetAttribute(k.first, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
+        fprintf(stderr, "ppr_hip: 160 KB dynamic LDS refused for %s\n", k.second);
+        hipGetLastError();
+        plan_free(p);
+        return PPR_ERR_HIP;
+      }
+  }
   *out = p;
   return PPR_OK;
 }
@@ -522,6 +539,8 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   a.lds_rank = p->lds_rank;
   a.nt = (uint32_t)p->nt_loads;
   a.whatif = (uint32_t)p->whatif;
+  a.iter = unit ? -1 : it;
+  a.spec = (unit || p->hot_cap > 0 || it < p->spec_from) ? 0.0 : p->spec_ratio;
   if (unit) { a.sA = 0; a.sB = 0; a.active = -1; return a; }
   a.sA = ((it + 1) / 2) & 1;
   a.sB = (it / 2) & 1;
@@ -719,6 +738,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   size_t off = 0;
   const size_t o_desc = off; off = al(off + sizeof(HubDesc) * nd_all);
   const size_t o_ovl = off;  off = al(off + 4 * (nd_all + 1));
+  const size_t o_rsp = off;  off = al(off + 4 * (nd_all + 1));
   const size_t o_ht = off;   off = al(off + sizeof(HotTask) * (nht + 1));
   const size_t o_hk = off;   off = al(off + 4 * (size_t)L * nht);
   const size_t o_hs = off;   off = al(off + 8 * (size_t)L * nht);
@@ -758,6 +778,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   char* base = (char*)p->d_scratch;
   HubDesc* d_desc_all = (HubDesc*)(base + o_desc);
   int32_t* d_ovl = (int32_t*)(base + o_ovl);     // [0] count, [1..] sources for the HBM-table path
+  int32_t* d_rsp = (int32_t*)(base + o_rsp);     // [0] count, [1..] descriptors whose speculative bound failed
   p->host_plan_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_plan0).count();
   p->host_plan_calls++;
   HIP_OK(hipMemcpyAsync(d_desc_all, desc, sizeof(HubDesc) * nd_all, hipMemcpyHostToDevice, st));
@@ -824,7 +845,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     if (ms && bi >= (size_t)nreg) HIP_OK(hipStreamWaitEvent(st, p->ev_fin[r], 0));  // region free again
     // (k_hub_expand also clears d_sd, d_pc, d_tau, d_oflag, d_lc and, in the first batch, d_ovl[0])
     hipLaunchKernelGGL(k_hub_expand, dim3((unsigned)nd), dim3(256), 0, st, d_desc, d_tile, d_buck, d_rt, d_sg, d_rg,
-                       p->hub_range, d_sd, d_pc, d_tau, d_oflag, d_lc, bi == 0 ? d_ovl : nullptr);
+                       p->hub_range, d_sd, d_pc, d_tau, d_oflag, d_lc, bi == 0 ? d_ovl : nullptr,
+                       bi == 0 ? d_rsp : nullptr);
     HIP_OK(hipGetLastError());
     const int64_t ntiles = b.ntiles;
     const int64_t nbuck = b.nbuck;
@@ -864,7 +886,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     // a batch of sources without successors (init of dangling nodes) has no tiles but still has
     // buckets: the one holding the source's own seed entry
     if (nbuck && p->hub_range == 0) {
-      hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, a, H, d_desc, d_buck,
+      hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, s, a, H, d_desc, d_buck,
                          nbuck, d_cmx, d_sd, d_tau, d_tau_hot, d_bw);
       HIP_OK(hipGetLastError());
     }
@@ -951,7 +973,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     }
     for (int rep = 0; rep < ((p->whatif & 32) ? 2 : 1); rep++) {
       hipLaunchKernelGGL(k_hub_final, dim3((unsigned)nd), dim3(WG_THREADS), p->hub_lds_final, sf, s, a, d_desc,
-                         d_oflag, d_pc, d_pk, d_ps, d_rk, d_rs, fslice, d_ccnt, d_ckey, d_csc, p->Lp, maxdiff, p->d_stats);
+                         d_oflag, d_pc, d_pk, d_ps, d_rk, d_rs, fslice, d_ccnt, d_ckey, d_csc, p->Lp, maxdiff, p->d_stats,
+                         d_rsp, (int32_t)b.d0);
       HIP_OK(hipGetLastError());
     }
     p->merge_launches += 9;
@@ -972,14 +995,33 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     p->ovl_pending = d_ovl;
     return PPR_OK;
   }
-  int32_t novf = 0;
+  int32_t novf = 0, nrsp = 0;
   HIP_OK(hipMemcpyAsync(&novf, d_ovl, 4, hipMemcpyDeviceToHost, st));
+  if (a.spec > 0.0) HIP_OK(hipMemcpyAsync(&nrsp, d_rsp, 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   if (novf) {
     std::vector<int32_t> ov(novf);
     HIP_OK(hipMemcpyAsync(ov.data(), d_ovl + 1, 4 * (size_t)novf, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     fallback.insert(fallback.end(), ov.begin(), ov.end());
+  }
+  if (nrsp) {
+    // sources whose speculative bound k_hub_final could not prove: merged again with the rigorous
+    // bound (their rows were not written), one more hub pass over just them
+    std::vector<int32_t> di(nrsp);
+    HIP_OK(hipMemcpyAsync(di.data(), d_rsp + 1, 4 * (size_t)nrsp, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    std::vector<int32_t> rb(nrsp), rc(2 * (size_t)nrsp);  // sources | candidate counts, out-degrees
+    for (int32_t k = 0; k < nrsp; k++) {
+      const HubDesc& dk = desc[di[k]];
+      rb[k] = dk.v;
+      rc[k] = dk.need;
+      rc[nrsp + k] = (int32_t)(p->h_rp[dk.v + 1] - p->h_rp[dk.v]);
+    }
+    p->spec_redo += nrsp;
+    IterArgs a2 = a;
+    a2.spec = 0.0;
+    return run_hubs(p, a2, rb.data(), rc.data(), (size_t)nrsp, maxdiff, fallback);
   }
   return PPR_OK;
 }

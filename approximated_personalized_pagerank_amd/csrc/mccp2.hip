@@ -176,6 +176,8 @@ extern "C" int ppr_mccp2_plan_combine(ppr_plan* p) {
   a.lds_rank = p->lds_rank;
   a.nt = (uint32_t)p->nt_loads;
   a.whatif = (uint32_t)p->whatif;
+  a.iter = -1;
+  a.spec = 0.0;
   const int64_t nl = (int64_t)p->mc_level_off.size() - 1;
   HIP_OK(hipEventRecord(p->ev_m0, p->stream));
   p->ovl_pending = nullptr;

@@ -90,7 +90,7 @@ struct HubTask { int32_t d; int32_t x; };   // (descriptor, tile or bucket)
 __global__ void __launch_bounds__(256) k_hub_expand(const HubDesc* desc, HubTask* tiles, HubTask* buckets,
                                                     HubTask* rts, HubTask* segs, HubTask* ranges, int krange,
                                                     uint32_t* staged, uint32_t* pt_cnt, unsigned long long* tau,
-                                                    int32_t* oflag, uint32_t* lc, int32_t* ovl) {
+                                                    int32_t* oflag, uint32_t* lc, int32_t* ovl, int32_t* rsp) {
   const int d = blockIdx.x;
   const HubDesc D = desc[d];
   if (threadIdx.x == 0) {
@@ -102,6 +102,7 @@ __global__ void __launch_bounds__(256) k_hub_expand(const HubDesc* desc, HubTask
       lc[0] = 0u;
       lc[1] = 0u;
       if (ovl) ovl[0] = 0;
+      if (rsp) rsp[0] = 0;
     }
   }
   const int P = 1 << D.logP;
@@ -267,7 +268,7 @@ __device__ __forceinline__ double hub_tau(const HubDesc& d, const unsigned long 
   return t;
 }
 
-__global__ void __launch_bounds__(256) k_hub_prep(DevGraph g, IterArgs a, HotSet H, const HubDesc* desc,
+__global__ void __launch_bounds__(256) k_hub_prep(DevGraph g, DevSlab s, IterArgs a, HotSet H, const HubDesc* desc,
                                                   const HubTask* tasks, int64_t ntasks, const int32_t* cm,
                                                   const uint32_t* staged, const unsigned long long* tau_b,
                                                   const unsigned long long* tau_hot, BucketWork* bw) {
@@ -286,7 +287,7 @@ __global__ void __launch_bounds__(256) k_hub_prep(DevGraph g, IterArgs a, HotSet
   w.seed = ((int)hub_digit(d.v, d.logP) == tk.x && !(d.hot >= 0 && H.has(d.v))) ? d.v : -1;
   const int64_t deg = g.rp[d.v + 1] - g.rp[d.v];
   w.factor = merge_factor(a, deg);
-  w.tau = hub_tau(d, tau_b, tk.d, tau_hot, w.factor);
+  w.tau = fmax(hub_tau(d, tau_b, tk.d, tau_hot, w.factor), spec_tau(s, a, d.v));
   w.selfval = self_seed(a, deg);
   w.ts = tie_salt(d.v);
   w.pad = 0;
@@ -937,7 +938,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a,
                                                           const int32_t* red_key, const double* red_sc, int slice,
                                                           uint32_t* cold_cnt, int32_t* cold_key, double* cold_sc,
                                                           int Lp, unsigned long long* maxdiff,
-                                                          unsigned long long* stats) {
+                                                          unsigned long long* stats, int32_t* rsp, int32_t d0) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int di = (int)blockIdx.x;
   const HubDesc d = desc[di];
@@ -963,6 +964,30 @@ __global__ void __launch_bounds__(WG_THREADS) k_hub_final(DevSlab s, IterArgs a,
   }
   const int cnt = hub_select_lds(L, n, Lw, [&](int i) { return pk[i]; }, [&](int i) { return pv[i]; },
                                  tie_salt(d.v));
+  const double ts = spec_tau(s, a, d.v);
+  if (ts > 0.0) {
+    // speculation verified: L selected entries, every one at or above the speculative bound (then
+    // no key left unemitted can reach the top-L); otherwise the row is not written here
+    // (an LDS flag, not __syncthreads_or: that one declares static LDS, and this kernel's launch
+    // attribute already claims all 160 KB as dynamic LDS)
+    if (threadIdx.x == 0) L.misc[M_SPEC] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < cnt; i += WG_THREADS)
+      if (bitsd(L.rv[i]) < ts) L.misc[M_SPEC] = 1;
+    __syncthreads();
+    const bool fail = L.misc[M_SPEC] != 0 || cnt < Lw;
+    if (a.diag && threadIdx.x == 0) {
+      diag_add(a.diag, 180, 1ull);
+      if (fail) {
+        diag_add(a.diag, 181, 1ull);
+        if (a.iter >= 0 && a.iter < 32) diag_add(a.diag, 224 + a.iter, 1ull);
+      }
+    }
+    if (fail) {  // not proven: the source is redone with the rigorous bound (run_hubs, its descriptor index)
+      if (threadIdx.x == 0) rsp[1 + atomicAdd(&rsp[0], 1)] = d0 + di;
+      return;
+    }
+  }
   if (d.hot >= 0) {
     int32_t* ok = cold_key + (int64_t)d.hot * Lw;
     double* os = cold_sc + (int64_t)d.hot * Lw;

@@ -66,7 +66,10 @@ struct ppr_plan {
   // selects from the whole list), 4 count twice, 8 scatter twice, 16 an extra dry bucket-wave pass
   // (no emission), 32 final twice, 64 reduce twice, 128 bucket waves stop after 2048 records
   int whatif = 0;
-  int nt_loads = 0;    // PPR_NT (IterArgs::nt): non-temporal candidate gathers (1) / staged-record reads (2)
+  int nt_loads = 0;
+  double spec_ratio = 0.0;  // PPR_SPEC: speculative hub pruning bound (ppr_common.h spec_tau), 0 = off
+  int spec_from = 6;        // PPR_SPEC_FROM: first iteration that speculates (rows settle after a few)
+  int64_t spec_redo = 0;    // hub sources redone after a failed speculation (PPR_TIMING at destroy)    // PPR_NT (IterArgs::nt): non-temporal candidate gathers (1) / staged-record reads (2)
   int wg_max_passes = 64;  // (WG_MAX_PASSES) PPR_WG_PASSES (tests): workgroup-tier key-bucket passes before overflow
   bool hub_enabled = true;
   unsigned long long* d_maxdiff = nullptr;  // PPR_MAX_ITER_STATS + 1
@@ -210,6 +213,8 @@ inline void plan_free(ppr_plan* p) {
   hipFree(p->d_xsend); hipFree(p->d_xrecv); hipFree(p->d_xsz); hipFree(p->d_xtmp);
   if (p->h_hub_pin) hipHostFree(p->h_hub_pin);
   if (p->h_desc_pin) hipHostFree(p->h_desc_pin);
+  if (getenv("PPR_TIMING") && p->spec_redo)
+    fprintf(stderr, "ppr_timing spec_redo_sources %lld\n", (long long)p->spec_redo);
   if (getenv("PPR_TIMING") && p->host_plan_calls)
     fprintf(stderr, "ppr_timing hub_planning host_s %.4f calls %lld hubs %lld order_s %.4f batches_s %.4f\n",
             p->host_plan_s, (long long)p->host_plan_calls, (long long)p->host_plan_hubs, p->host_plan_part[0],
@@ -241,6 +246,13 @@ inline void plan_free(ppr_plan* p) {
       if (h[150])
         fprintf(stderr, "ppr_diag rows merged %llu, unchanged (norm1 = 0) %llu (%.2f %%)\n", h[150], h[151],
                 100.0 * (double)h[151] / (double)h[150]);
+      if (h[180]) {
+        fprintf(stderr, "ppr_diag speculative bound: %llu hub sources, %llu failed (%.3f %%); failures by iteration:",
+                h[180], h[181], 100.0 * (double)h[181] / (double)h[180]);
+        for (int it = 0; it < 32; it++)
+          if (h[224 + it]) fprintf(stderr, " %d:%llu", it, h[224 + it]);
+        fprintf(stderr, "\n");
+      }
       if (h[166]) {
         const double tot = (double)(h[160] + h[161] + h[162] + h[163] + h[164] + h[165]);
         fprintf(stderr, "ppr_diag bucket_w phases, 1 wave in 8 (%llu waves, %.3e records, %.1f Gcycles): work+setup %.1f %% loads %.1f %% "

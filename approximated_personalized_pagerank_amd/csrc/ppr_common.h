@@ -154,12 +154,26 @@ struct IterArgs {
                              // reads of the bucket waves, as non-temporal loads (streamed once: they
                              // should not evict the scatter's partially written staging lines from L2)
   uint32_t whatif;           // PPR_WHATIF bits that act inside kernels (timing experiments, plan.h)
+  int iter;                  // GRank iteration (diagnostics)
+  double spec;               // speculative pruning ratio (PPR_SPEC; 0 = off): spec_tau below
 };
+
+// Speculative top-L pruning bound of a hub source (GRank iterations): spec x the smallest score of
+// the source's previous row when that row was full. Bucket waves then emit only keys whose exact
+// total reaches it; k_hub_final verifies the speculation (L emitted keys at or above it make it a
+// true lower bound of the L-th largest total, so the top-L is among them) and flags the source
+// for a redo with the rigorous bound otherwise.
 
 template <class T>
 __device__ __forceinline__ T ld_nt(const T* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
 
 __device__ __forceinline__ int read_slot(const IterArgs& a, int32_t cx) { return (cx < 0) ? a.sB : a.sA; }
+
+__device__ __forceinline__ double spec_tau(const DevSlab& s, const IterArgs& a, int v) {
+  if (a.spec <= 0.0 || a.unit || a.mc) return 0.0;
+  const int64_t r = s.lrow((a.active == 1) ? a.sB : a.sA, v);
+  return s.len[r] == s.L ? a.spec * s.rmin[r] : 0.0;
+}
 
 // The hot key set (merge_hot.h): up to a few thousand keys that sit in most successor baskets of
 // the hub sources. A hub's hot keys are accumulated densely by k_hub_hot, its other ("cold") keys

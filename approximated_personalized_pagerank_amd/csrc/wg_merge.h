@@ -102,7 +102,7 @@ __device__ __forceinline__ WgLds wg_carve(unsigned char* base, int T, int Lp, in
 
 // misc slots
 enum { M_FILL = 0, M_OVF = 1, M_PLEN = 2, M_U = 3, M_BIN = 4, M_ABOVE = 5, M_HB = 6, M_TOT = 7,
-       M_LOR0 = 8, M_LOR1 = 9, M_LAND0 = 10, M_LAND1 = 11, M_CNT = 12 };
+       M_LOR0 = 8, M_LOR1 = 9, M_LAND0 = 10, M_LAND1 = 11, M_CNT = 12, M_SPEC = 13 };
 
 // Route one chunk (each lane holds 2 candidates, valid flag) to owner waves, then every wave
 // applies its owner segment in order. Returns false on table overflow.

@@ -200,3 +200,34 @@ def test_gpu_tolerance_stop_beyond_256_iterations():
     r = ppr.grank_csr(csr, 50, 100, 300, 0.85, tol, part=part, device=0)
     assert r.iterations_run == o["iterations_run"]
     assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])
+
+
+@pytest.mark.parametrize("env,want_redo", [
+    ({"PPR_SPEC": "1.0", "PPR_SPEC_FROM": "1"}, True),                         # bound = the previous L-th
+                                                                               # score: proofs fail, sources redone
+    ({"PPR_SPEC": "0.5", "PPR_SPEC_FROM": "0"}, False),                        # from the first iteration
+    ({"PPR_SPEC": "0.9", "PPR_SPEC_FROM": "2", "PPR_HUB_BUDGET": "4096"}, False),  # failures across many batches
+    ({"PPR_SPEC": "0.0"}, False),                                              # off: the rigorous bound only
+])
+def test_gpu_speculative_bound_bit_exact(env, want_redo, monkeypatch, capfd):
+    """speculative hub pruning bound (spec x the source's previous L-th score): bucket waves emit
+    only keys reaching it, k_hub_final proves it (L selected entries at or above it) or the source
+    is merged again with the rigorous bound -- the result never changes (include/grank.h:96-137)"""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("PPR_TIMING", "1")
+    redo = 0
+    for mask, (scale, K, L, it) in [("0x20", (11, 16, 32, 10)), ("0x21", (12, 8, 64, 8)), ("0x2f", (12, 32, 128, 6))]:
+        monkeypatch.setenv("PPR_TIER_MASK", mask)
+        g = ppr.rmat(scale, seed=91 + scale)
+        part = g.partitions()
+        r = ppr.grank_csr(g, K, L, it, 0.85, -1.0, part=part, device=0)
+        o = oracle.grank(g.row_ptr, g.col, part, K, L, it, 0.85, -1.0)
+        assert np.array_equal(r.max_diff, o["max_diff"])
+        assert np.array_equal(r.lens, o["lens"])
+        assert np.array_equal(r.ids, o["ids"])
+        assert np.array_equal(r.scores, o["scores"])
+    err = capfd.readouterr().err
+    redo = sum(int(x.split()[2]) for x in err.splitlines() if x.startswith("ppr_timing spec_redo_sources"))
+    if want_redo:
+        assert redo > 0
