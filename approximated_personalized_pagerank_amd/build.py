@@ -2,7 +2,9 @@
 from __future__ import annotations
 
 import os
+import re
 import subprocess
+import sys
 
 from ._lib import CSRC, CSRC_HEADERS as HEADERS, CSRC_SOURCES as SOURCES, LIB_PATH, PKG_DIR, embedded_digest, \
     source_digest
@@ -33,11 +35,37 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
            "-o", out + ".tmp"] + [os.path.join(src_dir, s) for s in SOURCES
                                   # an older revision (tools/build_variant.py --rev) may predate a source
                                   if csrc is None or os.path.exists(os.path.join(src_dir, s))] + ["-lrccl", "-lpthread"]
+    cmd.append("-Rpass-analysis=kernel-resource-usage")
     if verbose:
         print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    r = subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
+    if r.returncode != 0:
+        print(r.stderr, file=sys.stderr)
+        raise subprocess.CalledProcessError(r.returncode, cmd)
+    check_resources(r.stderr)
     os.replace(out + ".tmp", out)
     return out
+
+
+def check_resources(remarks: str) -> None:
+    """every kernel of the library keeps its state in registers and LDS: private (scratch) memory
+    per lane or register spills would turn into HBM traffic on every wave (an indexable per-lane
+    array cost 3 TB of scratch writes per RMAT-22 job once) -- refuse such a build"""
+    bad, fn = [], None
+    for ln in remarks.splitlines():
+        if "remark:" not in ln:
+            continue
+        m = re.search(r"Function Name: (\S+)", ln)
+        if m:
+            fn = m.group(1)
+            continue
+        if "/rocprim/" in ln or "/hipcub/" in ln:
+            continue
+        m = re.search(r"(ScratchSize \[bytes/lane\]|VGPRs Spill): (\d+)", ln)  # (SGPR spills go to VGPR lanes)
+        if m and int(m.group(2)) > 0:
+            bad.append(f"{fn}: {m.group(1)} {m.group(2)}")
+    if bad:
+        raise RuntimeError("kernels with scratch memory or register spills:\n  " + "\n  ".join(bad))
 
 
 DROPIN_SRC = os.path.join(PKG_DIR, "..", "tests", "cpp", "dropin_test.cc")

@@ -484,8 +484,14 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
   // PPR_DIAG: per-phase cycles of this wave (lane-uniform registers; [8] = last stamp):
   // 0 work record + table setup, 1 record loads, 2 find-or-insert, 3 ordered accumulation,
   // 4 compaction + select, 5 appending atomic; 9 buckets that select (U > L), 10 entries appended
+  // (compiled in only with -DPPR_PHASE_TIMING, tools/build_variant.py: the counters live in private
+  // memory -- 128 B of scratch per lane, 3 TB of scratch writes per RMAT-22 job if always present)
+#if defined(PPR_PHASE_TIMING)
   unsigned long long phv[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // (11-14: chunk phases A-D)
   unsigned long long* ph = (a.diag && (cur & 7) == 0) ? phv : nullptr;  // one wave in 8 (the clock reads cost)
+#else
+  unsigned long long* ph = nullptr;
+#endif
   BucketWave B;
   B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0, budget);
   if (W.seed >= 0) B.seed(W.seed, W.selfval);

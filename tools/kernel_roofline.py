@@ -1,11 +1,11 @@
 """Per-kernel roofline table of one GRank job from a round's profile set (tools/profile_round.sh):
 
-    python tools/kernel_roofline.py STATS.csv FETCH.csv WRITE.csv STEPS [SQ_SUMMARY.txt] > profiles/<r>_kernel_roofline.json
+    python tools/kernel_roofline.py STATS.csv FETCH.csv WRITE.csv TRACE_STEPS PMC_STEPS [SQ_SUMMARY.txt]
 
 STATS.csv  rocprofv3 --kernel-trace --stats summary (TotalDurationNs per kernel)
 FETCH.csv  rocprofv3 --pmc FETCH_SIZE counter collection (KiB; x2 on gfx950, MI355X_MICROARCH.md "HBM")
 WRITE.csv  rocprofv3 --pmc WRITE_SIZE counter collection (KiB)
-STEPS      jobs in the profiled runs (the trace and the PMC passes profile the same bench command)
+TRACE_STEPS / PMC_STEPS  jobs in the traced run and in each PMC run
 SQ_SUMMARY tools/sq_summary.py output: the wave-cycle fractions waiting / issuing (optional)
 
 Per kernel, per job: summed launch durations, HBM bytes (2 x FETCH + WRITE), their rate and the
@@ -51,7 +51,7 @@ def sq(path):
     out, cur = {}, None
     for ln in open(path):
         if not ln.startswith(" "):
-            cur = ln.strip()
+            cur = re.sub(r"<.*", "", ln.strip())
             out[cur] = {}
             continue
         m = re.match(r"\s+(SQ_\w+)\s+([\d.e+]+)(?:\s+\(([\d.]+) of wave cycles\))?", ln)
@@ -61,25 +61,27 @@ def sq(path):
 
 
 def main():
-    stats, fetch, write, steps = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    stats, fetch, write = sys.argv[1], sys.argv[2], sys.argv[3]
+    steps, psteps = int(sys.argv[4]), int(sys.argv[5])
     d, calls = durations(stats)
     f, w = pmc(fetch), pmc(write)
-    q = sq(sys.argv[5]) if len(sys.argv) > 5 else {}
+    q = sq(sys.argv[6]) if len(sys.argv) > 6 else {}
     rows = []
     for k in sorted(d, key=lambda k: -d[k]):
         t = d[k] / steps
         if t < 1e-3:
             continue
-        b = (2 * f.get(k, 0.0) + w.get(k, 0.0)) / steps
+        b = (2 * f.get(k, 0.0) + w.get(k, 0.0)) / psteps
         rate = b / t if t else 0.0
         sqk = q.get(k, {})
         wait, act = sqk.get("SQ_WAIT_ANY"), sqk.get("SQ_ACTIVE_INST_ANY")
         bound = "hbm" if rate >= 0.6 * STREAM_CEIL else ("latency" if (wait or 0) >= 0.5 else "issue")
         rows.append({"kernel": k, "calls_per_job": calls[k] / steps, "time_s_per_job": round(t, 4),
-                     "hbm_bytes_per_job": b, "read_bytes": 2 * f.get(k, 0.0) / steps, "write_bytes": w.get(k, 0.0) / steps,
+                     "hbm_bytes_per_job": b, "read_bytes": 2 * f.get(k, 0.0) / psteps, "write_bytes": w.get(k, 0.0) / psteps,
                      "gbps": round(rate / 1e9, 1), "frac_of_peak": round(rate / PEAK, 4),
                      "sq_wait_frac": wait, "sq_active_frac": act, "bound": bound})
-    json.dump({"note": __doc__.split("\n\n")[2].replace("\n", " "), "steps": steps, "kernels": rows}, sys.stdout,
+    json.dump({"note": __doc__.split("\n\n")[2].replace("\n", " "), "trace_steps": steps, "pmc_steps": psteps,
+               "kernels": rows}, sys.stdout,
               indent=1)
     print()
 
