@@ -24,6 +24,7 @@
 #include <iostream>
 #include <memory>
 #include <thread>
+#include <type_traits>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -64,18 +65,37 @@ struct Flat {
 
 // key -> dense id: open addressing over a mix of std::hash<Key>, filled by all host threads at
 // once (slots claimed by CAS; the graph's keys are unique) -- a serial unordered_map of 4 M keys
-// took most of flatten's time
+// took most of flatten's time. Small trivially copyable keys (integers) are compared against a
+// dense copy instead of through the pointer into the caller's map node (a cache miss per lookup).
+template <typename Key, bool Copy = std::is_trivially_copyable<Key>::value && (sizeof(Key) <= 8)>
+struct KeyStore {  // (generic keys: through the pointer)
+  const std::vector<const Key*>* keys = nullptr;
+  void build(const std::vector<const Key*>& k) { keys = &k; }
+  const Key& at(size_t i) const { return *(*keys)[i]; }
+};
+template <typename Key>
+struct KeyStore<Key, true> {
+  std::vector<Key> copy;
+  void build(const std::vector<const Key*>& k) {
+    copy.resize(k.size());
+    parallel_ranges(k.size(), [&](size_t b, size_t e) {
+      for (size_t i = b; i < e; i++) copy[i] = *k[i];
+    });
+  }
+  const Key& at(size_t i) const { return copy[i]; }
+};
+
 template <typename Key>
 struct KeyIndex {
   std::unique_ptr<std::atomic<int32_t>[]> slot;
   uint64_t mask = 0;
-  const std::vector<const Key*>* keys = nullptr;
+  KeyStore<Key> ks;
   static uint64_t mix(uint64_t x) {  // splitmix64 finaliser: std::hash of integers is the identity
     x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL; x ^= x >> 27; x *= 0x94d049bb133111ebULL; x ^= x >> 31;
     return x;
   }
   void build(const std::vector<const Key*>& k) {
-    keys = &k;
+    ks.build(k);
     uint64_t cap = 16;
     while (cap < 2 * (uint64_t)k.size()) cap <<= 1;
     mask = cap - 1;
@@ -85,7 +105,7 @@ struct KeyIndex {
     });
     parallel_ranges(k.size(), [&](size_t b, size_t e) {
       for (size_t v = b; v < e; v++) {
-        uint64_t h = mix((uint64_t)std::hash<Key>()(*k[v])) & mask;
+        uint64_t h = mix((uint64_t)std::hash<Key>()(ks.at(v))) & mask;
         for (;;) {
           int32_t expect = -1;
           if (slot[h].compare_exchange_strong(expect, (int32_t)v, std::memory_order_relaxed)) break;
@@ -98,7 +118,7 @@ struct KeyIndex {
     uint64_t h = mix((uint64_t)std::hash<Key>()(key)) & mask;
     for (;;) {
       const int32_t s = slot[h].load(std::memory_order_relaxed);
-      if (s < 0 || *(*keys)[(size_t)s] == key) return s;
+      if (s < 0 || ks.at((size_t)s) == key) return s;
       h = (h + 1) & mask;
     }
   }
@@ -107,21 +127,26 @@ struct KeyIndex {
 template <typename Key>
 inline Flat<Key> flatten(const std::unordered_map<Key, std::vector<Key>>& graph) {
   Flat<Key> f;
-  f.keys.reserve(graph.size());
-  for (const auto& kv : graph) f.keys.push_back(&kv.first);
-  KeyIndex<Key> idx;
-  idx.build(f.keys);  // (threads joined: every slot is published to the readers below)
-  const size_t n = f.keys.size();
+  const size_t n = graph.size();
+  // one pass over the map's nodes (each a cache miss): keys and successor lists in iteration
+  // order; everything after it runs on all host threads
+  f.keys.resize(n);
   std::vector<const std::vector<Key>*> succ(n);
-  f.rp.assign(n + 1, 0);
   {
     size_t v = 0;
-    for (const auto& kv : graph) {  // same iteration order as above
+    for (const auto& kv : graph) {
+      f.keys[v] = &kv.first;
       succ[v] = &kv.second;
-      f.rp[v + 1] = f.rp[v] + (int64_t)kv.second.size();
       v++;
     }
   }
+  KeyIndex<Key> idx;
+  idx.build(f.keys);  // (threads joined: every slot is published to the readers below)
+  f.rp.assign(n + 1, 0);
+  parallel_ranges(n, [&](size_t b, size_t e) {
+    for (size_t v = b; v < e; v++) f.rp[v + 1] = (int64_t)succ[v]->size();
+  });
+  for (size_t v = 0; v < n; v++) f.rp[v + 1] += f.rp[v];
   f.col.resize((size_t)f.rp[n]);
   std::atomic<bool> bad(false);
   parallel_ranges(n, [&](size_t b, size_t e) {
