@@ -85,6 +85,25 @@ __global__ void __launch_bounds__(256) k_probe_lds_rank(int* ok, int trials, int
     bad |= act && got != want;
     wave_fence();
   }
+  // the one-shot bucket path (merge_hub.h bucket_oneshot) relies on the same order for the 64-bit
+  // add and for the 64-bit CAS on its slot words (table at offset 0): the lowest lane of a slot
+  // wins the CAS, and every later add returns the count of lower lanes (plus the winner's 1)
+  unsigned long long* w64 = reinterpret_cast<unsigned long long*>(smem + (size_t)wv * wave_bytes);
+  for (int t = 0; t < trials; t++) {
+    const uint32_t r = hash32(t * 7727u + blockIdx.x * 104723u + wv * 37u + 3u);
+    const uint32_t S = 1u << (r % 10);
+    for (int i = l; i < T; i += WAVE) w64[i] = 0xffffffffull;
+    wave_fence();
+    const uint32_t slot = (hash32(r ^ (uint32_t)(l * 2246822519u)) & (S - 1)) % (uint32_t)T;
+    const unsigned long long prev = atomicCAS(&w64[slot], 0xffffffffull, (1ull << 32) | (uint32_t)l);
+    unsigned long long got = 0;
+    if (prev != 0xffffffffull) got = atomicAdd(&w64[slot], 1ull << 32) >> 32;
+    uint32_t below = 0;
+    for (int j = 0; j < l; j++) below += (uint32_t)__shfl((int)slot, j) == slot;
+    if (below == 0) bad |= prev != 0xffffffffull;
+    else bad |= (uint32_t)prev == 0xffffffffu || got != below;
+    wave_fence();
+  }
   if (bad) atomicAnd(ok, 0);
 }
 
@@ -191,8 +210,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   for (int t = 0; t < NT; t++)
     if (p->tierT[t]) {
       const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * WAVES_PER_BLOCK;
-      if (bytes > 64 * 1024)
-        hipFuncSetAttribute((const void*)k_merge_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (bytes > 64 * 1024) {
+        hipFuncSetAttribute((const void*)k_merge_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_merge_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      }
     }
   if (p->tierCap[NT])
     hipFuncSetAttribute((const void*)k_merge_wg, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -283,7 +304,13 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     const char* h4 = getenv("PPR_HOT_MAX");
     if (h4) p->hot_max_need = std::max(0, atoi(h4));
   }
-  p->hub_lds_wave = hub_wave_lds(p->hub_wave_t, p->hub_bw_ng) * p->hub_bw_waves;
+  {
+    // PPR_BW2=0: no one-shot bucket path (merge_hub.h bucket_oneshot); its table shares the wave's LDS
+    const char* e = getenv("PPR_BW2");
+    p->hub_bw2 = !(e && atoi(e) == 0);
+  }
+  p->hub_wave_stride = (int)std::max(hub_wave_lds(p->hub_wave_t, p->hub_bw_ng), p->hub_bw2 ? bw2_lds(p->hub_wave_t) : 0);
+  p->hub_lds_wave = (size_t)p->hub_wave_stride * p->hub_bw_waves;
   if (p->hub_streams == 2) {
     if (hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&p->stream4, hipStreamNonBlocking) != hipSuccess ||
@@ -316,7 +343,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         hipFuncSetAttribute((const void*)k_probe_lds_rank, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipLaunchKernelGGL(k_probe_lds_rank, dim3((unsigned)p->hub_bw_blocks), dim3(64 * p->hub_bw_waves),
                            p->hub_lds_wave, p->stream, d_ok, 64, p->hub_wave_t,
-                           (int)hub_wave_lds(p->hub_wave_t, p->hub_bw_ng));
+                           p->hub_wave_stride);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p->stream) != hipSuccess ||
             hipMemcpy(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
           ok = 0;
@@ -343,8 +370,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         {(const void*)k_hub_bucket, "k_hub_bucket"},
         {(const void*)k_hub_final, "k_hub_final"},
         {(const void*)k_topk, "k_topk"},
-        {(const void*)k_hub_count, "k_hub_count"},
-        {(const void*)k_hub_scatter, "k_hub_scatter"},
+        {(const void*)k_hub_count<false>, "k_hub_count<false>"},
+        {(const void*)k_hub_scatter<false>, "k_hub_scatter<false>"},
+        {(const void*)k_hub_count<true>, "k_hub_count<true>"},
+        {(const void*)k_hub_scatter<true>, "k_hub_scatter<true>"},
         {(const void*)k_hub_hot, "k_hub_hot"},
         {(const void*)k_hub_join, "k_hub_join"},
     };
@@ -538,7 +567,7 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   a.stats = (p->flags & PPR_FLAG_STATS) ? 1u : 0u;
   a.lds_rank = p->lds_rank;
   a.nt = (uint32_t)p->nt_loads;
-  a.whatif = (uint32_t)p->whatif;
+  a.whatif = (uint32_t)p->whatif & 0xffffu;
   a.iter = unit ? -1 : it;
   a.spec = (unit || p->hot_cap > 0 || it < p->spec_from) ? 0.0 : p->spec_ratio;
   if (unit) { a.sA = 0; a.sB = 0; a.active = -1; return a; }
@@ -856,30 +885,39 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       // stranded by the block granularity
       struct TileList { const HubTask* t; int64_t n; int maxP; };
       const TileList tl[2] = {{d_tile, b.ntiles_s, b.maxP_s}, {d_tile + b.ntiles_s, ntiles - b.ntiles_s, maxP}};
-      auto launch_tiles = [&](bool scatter) -> int {
+      auto launch_tiles = [&](bool scatter, const IterArgs& a) -> int {
         for (const TileList& x : tl) {
           if (!x.n) continue;
           const int twpb = x.maxP >= p->tile_wpb_p ? 1 : WAVES_PER_BLOCK;
           const size_t lds_tile = (size_t)twpb * (x.maxP * 4 + HUB_WALK_FLAGS);
           const unsigned tb = (unsigned)((x.n + twpb - 1) / twpb);
+          // (kernels for hot-encoded rows only when the rows are: see DevSlab::keyd)
           if (scatter)
-            hipLaunchKernelGGL(k_hub_scatter, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, x.t, x.n,
-                               x.maxP, d_cmx, d_st);
+            hipLaunchKernelGGL(p->hot_n > 0 ? k_hub_scatter<true> : k_hub_scatter<false>, dim3(tb), dim3(64 * twpb),
+                               lds_tile, st, g, s, a, d_desc, x.t, x.n, x.maxP, d_cmx, d_st);
           else
-            hipLaunchKernelGGL(k_hub_count, dim3(tb), dim3(64 * twpb), lds_tile, st, g, s, a, d_desc, x.t, x.n, x.maxP,
-                               d_cm, d_tau, d_sd);
+            hipLaunchKernelGGL(p->hot_n > 0 ? k_hub_count<true> : k_hub_count<false>, dim3(tb), dim3(64 * twpb),
+                               lds_tile, st, g, s, a, d_desc, x.t, x.n, x.maxP, d_cm, d_tau, d_sd);
           HIP_OK(hipGetLastError());
         }
         return PPR_OK;
       };
       for (int rep = 0; rep < ((p->whatif & 4) ? 2 : 1); rep++) {
         if (rep) HIP_OK(hipMemsetAsync(d_sd, 0, 4 * nd, st));  // (the staged counts are summed)
-        int rc1 = launch_tiles(false);
+        int rc1 = launch_tiles(false, a);
         if (rc1) return rc1;
       }
       HIP_OK(hipcub::DeviceScan::ExclusiveSum(d_tmp, scan_tmp, d_cm, d_cmx, (int)b.cm, st));
       for (int rep = 0; rep < ((p->whatif & 8) ? 2 : 1); rep++) {
-        int rc1 = launch_tiles(true);
+        // (PPR_WHATIF 256: the first of the two scatters stores lane-contiguously, the second,
+        // the real one, rewrites every staged record)
+        IterArgs ar = a;
+        if (rep == 0 && (p->whatif & 256)) ar.whatif |= WI_SCAT_COALESCED;
+        if (rep == 0 && (p->whatif & 4096)) ar.whatif |= WI_SCAT_NOSTORE;
+        if (rep == 0 && (p->whatif & 8192)) ar.whatif |= WI_SCAT_NOSCORE;
+        if (rep == 0 && (p->whatif & 16384)) ar.whatif |= WI_SCAT_COUNT;
+        if (rep == 0 && (p->whatif & 32768)) ar.whatif |= WI_SCAT_WALK;
+        int rc1 = launch_tiles(true, ar);
         if (rc1) return rc1;
       }
     }
@@ -906,6 +944,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       // present in most successor baskets) still has few distinct keys, and its sequential fma
       // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
       const int wpb = p->hub_bw_waves;
+      const int cap2 = (p->hub_bw2 && p->lds_rank) ? BW2_CAP : 0;
       const int64_t blocks = (nbuck + wpb - 1) / wpb;
       const dim3 grid((unsigned)blocks), blk(64 * wpb);
       if (p->hub_range > 0) {
@@ -928,20 +967,20 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
                              p->hub_wave_t, p->hub_bw_budget);
       } else if (p->hub_bw_ng == 1)
         hipLaunchKernelGGL(k_hub_bucket_w<1>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
-                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget, 0);
+                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget, 0, p->hub_wave_stride, cap2);
       else if (p->hub_bw_ng == 2) {
         if (p->whatif & 16)  // timing experiment: a dry pass first (no emission, no spills)
           hipLaunchKernelGGL(k_hub_bucket_w<2>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps,
-                             d_pc, d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget, 1);
+                             d_pc, d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget, 1, p->hub_wave_stride, cap2);
         hipLaunchKernelGGL(k_hub_bucket_w<2>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
-                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget, 0);
+                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget, 0, p->hub_wave_stride, cap2);
       }
       else if (p->hub_bw_ng == 8)
         hipLaunchKernelGGL(k_hub_bucket_w<8>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
-                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget, 0);
+                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget, 0, p->hub_wave_stride, cap2);
       else
         hipLaunchKernelGGL(k_hub_bucket_w<4>, grid, blk, p->hub_lds_wave, sb, s, a, d_bw, nbuck, d_st, d_pk, d_ps, d_pc,
-                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget, 0);
+                           d_gl, d_lc + 1, p->hub_wave_t, p->hub_bw_budget, 0, p->hub_wave_stride, cap2);
       HIP_OK(hipGetLastError());
       // spilled buckets (distinct keys beyond the wave table): persistent workgroups over the spill
       // list, whose length only the device knows
@@ -1186,7 +1225,8 @@ reclassify:
     const int wpb = p->wave_wpb;
     const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * wpb;
     const int64_t blocks = ((int64_t)cnt[t] + wpb - 1) / wpb;
-    hipLaunchKernelGGL(k_merge_lds, dim3((unsigned)blocks), dim3(64 * wpb), bytes, sw, g, s, a,
+    hipLaunchKernelGGL(p->hot_n > 0 ? k_merge_lds<true> : k_merge_lds<false>, dim3((unsigned)blocks), dim3(64 * wpb),
+                       bytes, sw, g, s, a,
                        p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], p->tierT[t], p->Lp,
                        maxdiff, p->d_stats);
     HIP_OK(hipGetLastError());

@@ -148,6 +148,7 @@ __device__ __forceinline__ void hub_tile_walk(const DevGraph& g, const DevSlab& 
   for (int64_t w0 = b; w0 < e; w0 += WAVE) hub_window_walk(g, s, a, w0, min(e, w0 + WAVE), fl, f, succ);
 }
 
+template <bool HK>
 __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterArgs a,
                                                    const HubDesc* desc, const HubTask* tasks,
                                                    int64_t ntasks, int maxP, int32_t* cm,
@@ -173,7 +174,7 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
   // (a source without a hot pass stages every key, decoded)
   const bool hotp = d.hot >= 0;
   hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid, int id, double, bool) {
-    if (valid && (id >= 0 || !hotp)) { atomicAdd(&hist[hub_digit(s.key(id), d.logP)], 1u); nst++; }
+    if (valid && (id >= 0 || !hotp)) { atomicAdd(&hist[hub_digit(s.keyd<HK>(id), d.logP)], 1u); nst++; }
   }, WalkRowMin{&mb, (int)s.L});
   nst = wave_sum(nst);
   if (lane_id() == 0 && nst) {
@@ -189,6 +190,7 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
   for (int i = lane_id(); i < P; i += WAVE) cm[d.cm_off + (int64_t)i * d.T + tk.x] = (int32_t)hist[i];
 }
 
+template <bool HK>
 __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, IterArgs a,
                                                      const HubDesc* desc, const HubTask* tasks,
                                                      int64_t ntasks, int maxP, const int32_t* cm,
@@ -206,8 +208,25 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   // matrix once (one strided gather), so the per-group scatter never waits on global memory
   // (offsets are relative to the source's staging start: they fit 32 bits)
   uint32_t* run = reinterpret_cast<uint32_t*>(smem) + (size_t)wv * maxP;
+  // 16 strided loads per lane in flight at once (a 4096-bucket column is 64 loads per lane)
   const int64_t base0 = cm[d.cm_off];  // the source's first staged record (scanned counts)
-  for (int i = lane_id(); i < P; i += WAVE) run[i] = (uint32_t)(cm[d.cm_off + (int64_t)i * d.T + tk.x] - base0);
+  {
+    const int32_t* col = cm + d.cm_off + tk.x;
+    constexpr int GB = 16;
+    for (int i0 = 0; i0 < P; i0 += WAVE * GB) {
+      int32_t v[GB];
+#pragma unroll
+      for (int k = 0; k < GB; k++) {
+        const int i = i0 + k * WAVE + lane_id();
+        v[k] = i < P ? col[(int64_t)i * d.T] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < GB; k++) {
+        const int i = i0 + k * WAVE + lane_id();
+        if (i < P) run[i] = (uint32_t)(v[k] - base0);
+      }
+    }
+  }
   wave_fence();
   const uint64_t lt = lanemask_lt();
   HubRec* stv = st + base0;
@@ -216,12 +235,25 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   const bool ordered = a.lds_rank != 0;
   hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid0, int id, double sv, bool) {
     const bool valid = valid0 && (id >= 0 || !hotp);  // with a hot pass: cold keys only
-    const int key = valid ? s.key(id) : 0;
+    const int key = valid ? s.keyd<HK>(id) : 0;
     const uint32_t dg = valid ? hub_digit(key, d.logP) : 0u;
+    if (a.whatif & (WI_SCAT_COUNT | WI_SCAT_WALK)) {  // (timing only: non-returning rank atomics / walk only)
+      if (valid && (a.whatif & WI_SCAT_COUNT)) atomicAdd(&run[dg], 1u);
+      if (valid && key == -5 && sv == -1.0) stv[0] = hub_rec(key, sv);
+      return;
+    }
     if (ordered) {
       // lane-ordered LDS atomics (probed per plan, k_probe_lds_rank): same-digit lanes get their
       // run positions in lane order, i.e. stream order -- the stable rank in one instruction
-      if (valid) stv[atomicAdd(&run[dg], 1u)] = hub_rec(key, sv);
+      uint32_t pos = valid ? atomicAdd(&run[dg], 1u) : 0u;
+      if (a.whatif & WI_SCAT_COALESCED) {  // (timing only: the same records stored lane-contiguously)
+        const uint64_t vm = __ballot(valid);
+        if (!vm) return;
+        const uint32_t p0 = (uint32_t)__shfl((int)pos, __ffsll((long long)vm) - 1);
+        pos = min(p0 + (uint32_t)lane_id(), (uint32_t)(d.need - 2));
+      }
+      // (timing only: keeps the loads and ranks, stores nothing)
+      if (valid && (!(a.whatif & WI_SCAT_NOSTORE) || (sv == -1.0 && key == -5))) stv[pos] = hub_rec(key, sv);
       return;
     }
     // lanes holding the same digit: AND of per-bit ballots (stable rank = lower lanes first)
@@ -465,13 +497,199 @@ struct BucketWave {
   }
 };
 
+// ---------------------------------------------------------------------------------------------
+// One-shot bucket (default for buckets of at most BW2_CAP records, with lane-ordered LDS atomics):
+// the whole bucket is loaded into registers at once and accumulated in one pass instead of chunk
+// by chunk, with one 64-bit LDS word per table slot, key | occurrences << 32 | run base << 48:
+//   P1  per group, in stream order: find-or-insert with the occurrence index in the same atomic
+//       (a key's first record claims an empty slot by CAS with count 1, later ones add 1 << 32;
+//       same-address lanes of one instruction are served in lane order -- probed per plan, both
+//       for the 64-bit add and the 64-bit CAS -- and the groups go in order), new slots listed;
+//   P2  exclusive scan of the listed slots' counts -> each slot's run base (into its word);
+//   P3  every record's value to vals[base + occurrence]: the bucket's values grouped by key, in
+//       stream order inside a key;
+//   P4  one lane per listed slot: the key's fma chain over its run, seeded with the source's own
+//       value for the seed key (include/grank.h:103-116 order); the total overwrites the run's
+//       last value;
+//   P5  totals >= tau (at most L by (score desc, tie_w desc)) appended to the source's list.
+// The chunked path needs ~10 dependent LDS round trips per 128 records plus a 512-slot compaction
+// per bucket; this one ~20 per bucket. Buckets it cannot take (more records) use the chunked path.
+constexpr int BW2_GROUPS = 8;
+constexpr int BW2_CAP = BW2_GROUPS * WAVE;  // records
+__host__ __device__ constexpr size_t bw2_lds(int T) {  // words | vals | listed slots | select histogram
+  return ((size_t)T * 8 + (size_t)BW2_CAP * 8 + (size_t)BW2_CAP * 2 + 1024 + 15) & ~(size_t)15;
+}
+
+__device__ __forceinline__ uint32_t bw2_slot(int key, int T) {
+  return (uint32_t)(((unsigned long long)hash32((uint32_t)key) * (uint32_t)T) >> 32);
+}
+
+// returns false when the bucket's distinct keys could exceed `budget` (the caller spills it)
+__device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int budget, const BucketWork& W, int nb,
+                                               const HubRec* st, const IterArgs& a, int Lw, uint32_t* pt_cnt_d,
+                                               int32_t* pt_key, double* pt_sc) {
+  const int l = lane_id();
+  unsigned long long* word = reinterpret_cast<unsigned long long*>(base);
+  double* vals = reinterpret_cast<double*>(base + (size_t)T * 8);
+  uint16_t* listed = reinterpret_cast<uint16_t*>(base + (size_t)T * 8 + (size_t)BW2_CAP * 8);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 8 + (size_t)BW2_CAP * 10);
+  constexpr unsigned long long EMPTYW = 0xffffffffull;  // key EMPTY, count 0
+  constexpr unsigned long long ONE = 1ull << 32;
+  const int ng = (nb + WAVE - 1) / WAVE;  // (uniform) groups holding records
+  int kk[BW2_GROUPS];
+  double cs[BW2_GROUPS];
+#pragma unroll
+  for (int k = 0; k < BW2_GROUPS; k++) {  // every load in flight at once
+    const int q = k * WAVE + l;
+    HubRec r{};
+    if (q < nb) r = st[W.start + q];
+    kk[k] = rec_key(r);
+    cs[k] = rec_sc(r);
+  }
+  for (int i = l; i < T; i += WAVE) word[i] = EMPTYW;
+  wave_fence();
+  int nt = 0;
+  if (W.seed >= 0) {  // the source's own key: listed, no occurrence yet (its chain starts at selfval)
+    if (l == 0) {
+      const uint32_t h = bw2_slot(W.seed, T);
+      word[h] = (unsigned long long)(uint32_t)W.seed;
+      listed[0] = (uint16_t)h;
+    }
+    nt = 1;
+    wave_fence();
+  }
+  const uint64_t lt = lanemask_lt();
+  uint32_t sl[BW2_GROUPS], occ[BW2_GROUPS];
+  unsigned long long c0[BW2_GROUPS];
+#pragma unroll
+  for (int k = 0; k < BW2_GROUPS; k++) {  // first probes up front (a stale EMPTY is caught by the CAS)
+    sl[k] = bw2_slot(kk[k], T);
+    c0[k] = (k < ng && k * WAVE + l < nb) ? word[sl[k]] : EMPTYW;
+  }
+  // P1
+#pragma unroll
+  for (int k = 0; k < BW2_GROUPS; k++) {
+    if (k >= ng) break;  // uniform
+    const bool v = k * WAVE + l < nb;
+    // at most the lanes whose early probe did not show their key bring a new key
+    const int maybe_new = __popcll(__ballot(v && (uint32_t)c0[k] != (uint32_t)kk[k]));
+    if (nt + maybe_new > budget) return false;
+    uint32_t h = sl[k], o = 0;
+    bool fresh = false;
+    if (v) {
+      unsigned long long w = c0[k];
+      for (;;) {
+        const uint32_t wk = (uint32_t)w;
+        if (wk == (uint32_t)kk[k]) { o = (uint32_t)(atomicAdd(&word[h], ONE) >> 32) & 0xffffu; break; }
+        if (wk == 0xffffffffu) {
+          const unsigned long long prev = atomicCAS(&word[h], EMPTYW, ONE | (uint32_t)kk[k]);
+          if (prev == EMPTYW) { fresh = true; break; }  // occurrence 0
+          w = prev;  // taken meanwhile (a lower lane or an earlier group): test the same slot again
+          continue;
+        }
+        h = (h + 1 == (uint32_t)T) ? 0u : h + 1;
+        w = word[h];
+      }
+    }
+    sl[k] = h;
+    occ[k] = o;
+    const uint64_t fm = __ballot(fresh);
+    if (fresh) listed[nt + __popcll(fm & lt)] = (uint16_t)h;
+    nt += __popcll(fm);
+    wave_fence();
+  }
+  // P2: run bases (listed order)
+  int run = 0;
+  for (int i0 = 0; i0 < nt; i0 += WAVE) {
+    const int i = i0 + l;
+    unsigned long long w = 0;
+    int c = 0;
+    if (i < nt) { w = word[listed[i]]; c = (int)((w >> 32) & 0xffffu); }
+    const int incl = wave_incl_scan(c);
+    if (i < nt) word[listed[i]] = (w & 0x0000ffffffffffffull) | ((unsigned long long)(run + incl - c) << 48);
+    run += __builtin_amdgcn_readlane(incl, WAVE - 1);
+  }
+  wave_fence();
+  // P3: values grouped by key
+#pragma unroll
+  for (int k = 0; k < BW2_GROUPS; k++) {
+    if (k >= ng) break;
+    if (k * WAVE + l < nb) vals[(uint32_t)(word[sl[k]] >> 48) + occ[k]] = cs[k];
+  }
+  wave_fence();
+  // P4: one chain per listed slot
+  const double f = W.factor;
+  for (int i0 = 0; i0 < nt; i0 += WAVE) {
+    const int i = i0 + l;
+    if (i < nt) {
+      const unsigned long long w = word[listed[i]];
+      const int c = (int)((w >> 32) & 0xffffu), b = (int)(w >> 48);
+      double x = ((int)(uint32_t)w == W.seed) ? W.selfval : 0.0;
+      int j = b;
+      const int e = b + c;
+      for (; j + 8 <= e; j += 8) {
+        const double v0 = vals[j], v1 = vals[j + 1], v2 = vals[j + 2], v3 = vals[j + 3];
+        const double v4 = vals[j + 4], v5 = vals[j + 5], v6 = vals[j + 6], v7 = vals[j + 7];
+        x = fma(v0, f, x); x = fma(v1, f, x); x = fma(v2, f, x); x = fma(v3, f, x);
+        x = fma(v4, f, x); x = fma(v5, f, x); x = fma(v6, f, x); x = fma(v7, f, x);
+      }
+      for (; j < e; j++) x = fma(vals[j], f, x);
+      if (c > 0) vals[e - 1] = x;  // (a slot without occurrences is the seed key: its total is selfval)
+    }
+  }
+  wave_fence();
+  // P5: keys reaching tau, at most L of them, appended
+  auto total_of = [&](int i) {
+    const unsigned long long w = word[listed[i]];
+    const int c = (int)((w >> 32) & 0xffffu);
+    return c > 0 ? vals[(int)(w >> 48) + c - 1] : W.selfval;
+  };
+  auto key_of = [&](int i) { return (int)(uint32_t)word[listed[i]]; };
+  int kept = 0;
+  for (int i0 = 0; i0 < nt; i0 += WAVE) {
+    const int i = i0 + l;
+    kept += __popcll(__ballot(i < nt && total_of(i) >= W.tau));
+  }
+  if (a.diag && l == 0) {  // distinct keys / kept keys per bucket
+    diag_add(a.diag, 64 + (31 - __clz(nt | 1)), 1ull);
+    diag_add(a.diag, 96 + (31 - __clz(kept | 1)), 1ull);
+  }
+  if (kept == 0) return true;
+  const int cnt = kept <= Lw ? kept : Lw;
+  SelCrit c;
+  const uint32_t ts = W.ts;
+  const double tau = W.tau;
+  if (kept > Lw)  // keys below tau rank as 0 (every kept total is >= tau > 0 here)
+    c = select_top(nt, Lw, key_of, [&](int i) { const double x = total_of(i); return x >= tau ? x : 0.0; }, hist, ts);
+  int at = 0;
+  if (l == 0) at = (int)atomicAdd(pt_cnt_d, (uint32_t)cnt);
+  at = __builtin_amdgcn_readlane(at, 0);
+  int pos0 = 0;
+  for (int i0 = 0; i0 < nt; i0 += WAVE) {
+    const int i = i0 + l;
+    bool sel = false;
+    double x = 0.0;
+    int key = 0;
+    if (i < nt) {
+      x = total_of(i);
+      key = key_of(i);
+      sel = x >= tau && (kept <= Lw || sel_test(c, dbits(x), tie_w(key, ts)));
+    }
+    const uint64_t m = __ballot(sel);
+    if (sel) { const int pos = at + pos0 + __popcll(m & lt); pt_key[pos] = key; pt_sc[pos] = x; }
+    pos0 += __popcll(m);
+  }
+  return true;
+}
+
 // Bucket waves over the staged partition: one wave per bucket, its work record resolved by
 // k_hub_prep; a bucket with more distinct keys than the table holds spills to k_hub_bucket.
 template <int NG>
 __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, const BucketWork* bw,
                                                       int64_t nbuck, const HubRec* st,
                                                       int32_t* pt_key, double* pt_sc, uint32_t* pt_cnt,
-                                                      HubTask* spill, uint32_t* spill_cnt, int T, int budget, int dry) {
+                                                      HubTask* spill, uint32_t* spill_cnt, int T, int budget, int dry,
+                                                      int wbytes, int cap2) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   const int l = lane_id();
@@ -492,11 +710,26 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
 #else
   unsigned long long* ph = nullptr;
 #endif
-  BucketWave B;
-  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0, budget);
-  if (W.seed >= 0) B.seed(W.seed, W.selfval);
   // (PPR_WHATIF 128, timing only: long buckets cut to 2048 records -- what the hot-key chains cost)
   const int nb = ((a.whatif & 128u) && W.nb > 2048) ? 2048 : W.nb;
+  if (nb <= cap2 && !dry && !ph) {  // (cap2 = 0: one-shot path off, or LDS atomics not lane-ordered)
+    if (!bucket_oneshot(smem + (size_t)wv * wbytes, T, budget, W, nb, st, a, s.L, &pt_cnt[W.d], pt_key + W.pt_off,
+                        pt_sc + W.pt_off)) {
+      if (l == 0) { const uint32_t pos = atomicAdd(spill_cnt, 1u); spill[pos] = HubTask{W.d, W.x}; }
+      if (a.diag && l == 0) {
+        diag_add(a.diag, 152, 1ull);
+        diag_add(a.diag, 153, (unsigned long long)nb);
+      }
+    } else if (a.diag && l == 0) {
+      const int bin = 31 - __clz(nb | 1);
+      diag_add(a.diag, bin, 1ull);
+      diag_add(a.diag, 32 + bin, (unsigned long long)((long long)clock64() - t_start));
+    }
+    return;
+  }
+  BucketWave B;
+  B.setup(smem + (size_t)wv * wbytes, T, NG, a.lds_rank != 0, budget);
+  if (W.seed >= 0) B.seed(W.seed, W.selfval);
   if (ph) { ph[8] = (unsigned long long)clock64(); ph[0] = ph[8] - (unsigned long long)t_start; }
   for (int g0 = 0; g0 < nb; g0 += NG * WAVE) {
     bool cv[NG];

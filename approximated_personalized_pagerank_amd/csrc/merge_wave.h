@@ -251,7 +251,7 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
       if (valid) {
         const int64_t r = s.row(sj, uj) + (c - ex);
         key[k] = ld_nt(&s.ids[r], a.nt & 1u);
-        sv[k] = ld_nt(&s.sc[r], a.nt & 1u);
+        sv[k] = (a.whatif & WI_SCAT_NOSCORE) ? 0.5 : ld_nt(&s.sc[r], a.nt & 1u);  // (timing only)
       }
     }
   };
@@ -290,6 +290,7 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
 // flag bytes per wave of hub_window_walk
 constexpr int HUB_WALK_FLAGS = WAVE * HUB_TW_BATCH;
 
+template <bool HK>
 __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterArgs a,
                                                    const int32_t* list, int64_t count, int T,
                                                    int Lp, unsigned long long* maxdiff,
@@ -332,7 +333,7 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
     // the select histogram's LDS is idle until the epilogue: it holds the walk's end flags
     for (int64_t e0 = b; e0 < e; e0 += WAVE)
       hub_window_walk(g, s, a, e0, min(e, e0 + WAVE), reinterpret_cast<uint8_t*>(hist),
-                      [&](bool valid, int id, double sv, bool) { table_apply_own(t, own, valid, s.key(id), sv, factor); },
+                      [&](bool valid, int id, double sv, bool) { table_apply_own(t, own, valid, s.keyd<HK>(id), sv, factor); },
                       WalkRowMin{&mb, (int)s.L});
   }
   wave_fence();

@@ -64,7 +64,10 @@ struct ppr_plan {
   size_t wg_lds = 0;
   // PPR_WHATIF (timing experiments only; tools/whatif.py): 1 no spill grid, 2 no reduce (k_hub_final
   // selects from the whole list), 4 count twice, 8 scatter twice, 16 an extra dry bucket-wave pass
-  // (no emission), 32 final twice, 64 reduce twice, 128 bucket waves stop after 2048 records
+  // (no emission), 32 final twice, 64 reduce twice, 128 bucket waves stop after 2048 records,
+  // 256 (with 8) the first of the two scatters stores lane-contiguously (its scattered stores' cost),
+  // 4096 (with 8) ... stores nothing, 8192 (with 8) ... loads no scores, 16384 (with 8) ... only
+  // counts (non-returning rank atomics), 32768 (with 8) ... only walks
   int whatif = 0;
   int nt_loads = 0;
   double spec_ratio = 0.0;  // PPR_SPEC: speculative hub pruning bound (ppr_common.h spec_tau), 0 = off
@@ -105,6 +108,8 @@ struct ppr_plan {
   bool seg_enabled = false;        // segmented hub buckets (k_hub_seg, PPR_HUB_SEG=1)
   int seg_bucket = 256, seg_t = 512, seg_wpb = 1;
   int hub_bw_ng = 2;               // PPR_BW_NG: groups per chunk (1, 2, 4 or 8)
+  bool hub_bw2 = true;             // PPR_BW2: one-shot path for buckets of <= BW2_CAP records
+  int hub_wave_stride = 0;         // LDS bytes per bucket wave (chunked table or one-shot table)
   int hub_bw_waves = 1;            // PPR_BW_WAVES: waves per block of k_hub_bucket_w
   int hub_range = 0;               // PPR_HUB_RANGE: buckets per k_hub_range wave (0 = k_hub_bucket_w, one each;
                                    // ranges measured no faster: the bucket stage is LDS-latency bound)

@@ -97,6 +97,11 @@ struct DevSlab {
   __device__ __forceinline__ int64_t xrow(int slot, int64_t u) const { return ((int64_t)slot * n + u) * NRANGE; }
   // stored id -> key
   __device__ __forceinline__ int key(int32_t id) const { return id >= 0 ? id : hkeys[(uint32_t)id & 0x7fffffffu]; }
+  // decode for a kernel compiled for one encoding (HK = the rows may hold hot ids, plan hot_n > 0).
+  // Without hot ids no load is emitted: the decode's conditional load (never taken) otherwise costs
+  // an s_waitcnt vmcnt(0) per candidate group after it, which drains the walk's prefetched batch
+  template <bool HK>
+  __device__ __forceinline__ int keyd(int32_t id) const { return HK ? key(id) : id; }
   // key -> stored id
   __device__ __forceinline__ int32_t enc(int key) const {
     if (hn && ((hbits[(uint32_t)key >> 5] >> ((uint32_t)key & 31u)) & 1u)) return (int32_t)(HOT_TAG | hidx[key]);
@@ -153,10 +158,16 @@ struct IterArgs {
   uint32_t nt;               // PPR_NT: 1 = basket-row gathers of the candidate walks, 2 = staged-record
                              // reads of the bucket waves, as non-temporal loads (streamed once: they
                              // should not evict the scatter's partially written staging lines from L2)
-  uint32_t whatif;           // PPR_WHATIF bits that act inside kernels (timing experiments, plan.h)
+  uint32_t whatif;           // PPR_WHATIF bits that act inside kernels (timing experiments, plan.h;
+                             // bits 0-15 as set by the user, WI_* below set per launch by the host)
   int iter;                  // GRank iteration (diagnostics)
   double spec;               // speculative pruning ratio (PPR_SPEC; 0 = off): spec_tau below
 };
+
+// per-launch timing variants of one repeated scatter pass (PPR_WHATIF 256/4096/8192/16384/32768
+// with 8, plan.h): never set from the environment, so the real pass can not inherit them
+constexpr uint32_t WI_SCAT_COALESCED = 1u << 20, WI_SCAT_NOSTORE = 1u << 21, WI_SCAT_NOSCORE = 1u << 22,
+                   WI_SCAT_COUNT = 1u << 23, WI_SCAT_WALK = 1u << 24;
 
 // Speculative top-L pruning bound of a hub source (GRank iterations): spec x the smallest score of
 // the source's previous row when that row was full. Bucket waves then emit only keys whose exact
