@@ -49,6 +49,7 @@ std::unordered_map<Key, std::unordered_map<Key, double>> mccompletepathv2(
   ppr_csr g{(int64_t)n, f.rp.data(), f.col.empty() ? nullptr : f.col.data()};
   std::vector<int32_t> ids(n * K), len(n);
   std::vector<double> sc(n * K);
+  hipdetail::HeapGrowth heap;  // (outer map and inner maps)
   hipdetail::Outer<Key> o;
   std::thread outer([&] { o.build(f); });  // the result's outer map, beside the device call
   const int rc = ppr_mccp2_csr(&g, (uint32_t)K, (uint32_t)L, (uint32_t)iterations, damping, hipdetail::mc_seed(),
