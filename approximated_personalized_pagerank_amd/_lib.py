@@ -22,8 +22,8 @@ LIB_PATH = os.path.join(PKG_DIR, "libppr_hip.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 # every file the library is compiled from (csrc/ plus the public header), in digest order
 CSRC_SOURCES = ["grank.hip", "mccp2.hip", "exact_ppr.hip", "host_graph.cpp"]
-CSRC_HEADERS = ["ppr_device.h", "ppr_common.h", "merge_wave.h", "wg_merge.h", "merge_hub.h", "merge_glb.h",
-                "merge_mc.h", "merge_hot.h", "plan.h", "host_par.h", os.path.join("..", "..", "include", "ppr_hip.h")]
+# every header of csrc/ (a new one can not be left out of the provenance digest) and the C ABI
+CSRC_HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".h")) + [os.path.join("..", "..", "include", "ppr_hip.h")]
 
 
 def source_digest(src_dir: str = CSRC) -> str:
@@ -54,6 +54,7 @@ if os.environ.get("PPR_LIB_VARIANT"):
 
 PPR_MAX_ITER_STATS = 256
 PPR_FLAG_STATS = 1
+PPR_FLAG_CHAIN_SUM = 2  # the reference's in-order fma sums instead of the default exact sum
 
 ERRORS = {
     0: "ok",

@@ -45,6 +45,7 @@
 #include "merge_hub.h"
 #include "merge_glb.h"
 #include "merge_hot.h"
+#include "merge_xs.h"
 
 using namespace pprk;
 
@@ -354,6 +355,49 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     }
     p->lds_rank = ok ? 1u : 0u;
   }
+  // exact-sum GRank (merge_xs.h): the default outside the MC combine; PPR_FLAG_CHAIN_SUM or
+  // PPR_SUM=chain keep the reference's in-order fma chains (and the hub pipeline of merge_hub.h)
+  {
+    p->xsum = !mc && !(p->flags & PPR_FLAG_CHAIN_SUM);
+    const char* es = getenv("PPR_SUM");
+    if (es && !strcmp(es, "chain")) p->xsum = false;
+    if (es && !strcmp(es, "exact") && !mc) p->xsum = true;
+    if (p->xsum) {
+      // the order-bound alternatives of the chain path do not apply: no hot pass, no speculative
+      // bound, no workgroup tier (its overflow would fall to the chain-order HBM table)
+      p->hot_cap = 0;
+      p->spec_ratio = 0.0;
+      p->tierCap[NT] = 0;
+      p->seg_enabled = false;
+      p->hub_range = 0;
+      const char* e1 = getenv("PPR_XR_T");
+      const char* e2 = getenv("PPR_XR_W");
+      const char* e3 = getenv("PPR_XR_RMAX");
+      const char* e4 = getenv("PPR_XR_FILL");
+      if (e1) p->xr_T = std::max(1024, std::min(8192, pow2_at_least(atoi(e1))));
+      if (e2) p->xr_W = std::max(4, std::min(16, atoi(e2)));
+      if (e3) p->xr_rmax = std::max(1, std::min(64, atoi(e3)));
+      if (e4) p->xr_fill = std::max(20, std::min(85, atoi(e4)));
+      const char* e5 = getenv("PPR_XR_DSCALE");
+      if (e5) p->xr_dscale = std::max(1, std::min(1000, atoi(e5)));
+      while (xr_lds_bytes(p->xr_T, p->xr_W, p->Lp) > 160 * 1024 && p->xr_T > 1024) p->xr_T /= 2;
+      if (xr_lds_bytes(p->xr_T, p->xr_W, p->Lp) > 160 * 1024 || xf_lds_bytes(p->Lp, 64) > 160 * 1024) {
+        plan_free(p);
+        return PPR_ERR_RANGE;
+      }
+      p->xf_stage = (int)std::min<size_t>(XF_STAGE, (160 * 1024 - xf_lds_bytes(p->Lp, 0)) / 12) & ~15;
+      for (int t = 0; t < NT; t++)
+        if (p->tierT[t] && lds_wave_bytes_x(p->tierT[t], p->Lp) * p->wave_wpb > 160 * 1024) {
+          p->tierT[t] = 0;
+          p->tierCap[t] = 0;
+        }
+      TRY(dalloc(&p->d_dlast, n));
+      if (hipMemset(p->d_dlast, 0, 4 * (size_t)(n > 0 ? n : 1)) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
+      int32_t caps[NT + 1];
+      for (int t = 0; t <= NT; t++) caps[t] = p->tierCap[t];
+      if (hipMemcpy(p->d_tier_cap, caps, sizeof(caps), hipMemcpyHostToDevice) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
+    }
+  }
   // every kernel that may take more than the default 64 KB of dynamic LDS; a refusal (e.g. a
   // kernel that also declares static LDS) fails the plan instead of surfacing later as a launch error
   {
@@ -376,6 +420,11 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         {(const void*)k_hub_scatter<true>, "k_hub_scatter<true>"},
         {(const void*)k_hub_hot, "k_hub_hot"},
         {(const void*)k_hub_join, "k_hub_join"},
+        {(const void*)k_merge_lds_x, "k_merge_lds_x"},
+        {(const void*)k_xr, "k_xr"},
+        {(const void*)k_xb, "k_xb"},
+        {(const void*)k_xfinal<XDesc>, "k_xfinal<XDesc>"},
+        {(const void*)k_xfinal<HubDesc>, "k_xfinal<HubDesc>"},
     };
     for (const auto& k : big_lds)
       if (hipFuncSetAttribute(k.first, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
@@ -570,6 +619,7 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   a.whatif = (uint32_t)p->whatif & 0xffffu;
   a.iter = unit ? -1 : it;
   a.spec = (unit || p->hot_cap > 0 || it < p->spec_from) ? 0.0 : p->spec_ratio;
+  a.xs = p->xsum ? 1u : 0u;
   if (unit) { a.sA = 0; a.sB = 0; a.active = -1; return a; }
   a.sA = ((it + 1) / 2) & 1;
   a.sB = (it / 2) & 1;
@@ -602,7 +652,7 @@ static int ceil_log2(int64_t x) { return x <= 1 ? 0 : 64 - __builtin_clzll((unsi
 // to `fallback` (HBM-table path) after the last batch (the only host sync here).
 static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
                     const int32_t* cand /* parallel to big, then the out-degrees */, size_t nbig, unsigned long long* maxdiff,
-                    std::vector<int32_t>& fallback) {
+                    std::vector<int32_t>& fallback, const int32_t* dest = nullptr) {
   hipStream_t st = p->stream;
   DevGraph g{p->d_rp, p->d_colx, p->n};
   const DevSlab s = dev_slab(p);
@@ -634,7 +684,14 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     return std::max(1, std::min(HUB_MAX_LOGP, ceil_log2((int64_t)cdiv32((uint32_t)need, hb))));
   };
   std::vector<uint8_t> lpv(nbig);
-  for (size_t i = 0; i < nbig; i++) lpv[i] = (uint8_t)logp_of(cand[i]);
+  if (a.xs) {
+    // exact sum: buckets sized by the expected distinct keys (dest), one workgroup table each
+    const int64_t capb = (int64_t)p->xr_T * p->xr_fill / 100;
+    for (size_t i = 0; i < nbig; i++)
+      lpv[i] = (uint8_t)std::max(1, std::min(HUB_MAX_LOGP, ceil_log2((dest[i] + capb - 1) / capb)));
+  } else {
+    for (size_t i = 0; i < nbig; i++) lpv[i] = (uint8_t)logp_of(cand[i]);
+  }
   // batches mix large and small sources: that hides the long hot-key buckets of the large ones
   // (grouping them by size measured 10 % slower), and it balances the two pipeline stages, whose
   // costs differ by source size (large partitions: count + scatter bound; many small sources:
@@ -797,7 +854,9 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   const size_t o_cnt = off;  off = al(off + 16);
   const size_t o_sd = off;   off = al(off + 4 * maxnd);
   const size_t o_rg = off;   off = al(off + sizeof(HubTask) * (mx.nrange + 1));
-  const size_t o_bw = off;   off = al(off + sizeof(BucketWork) * mx.nbuck);
+  const size_t o_bw = off;   off = al(off + sizeof(BucketWork) * (a.xs ? 1 : mx.nbuck));
+  const size_t o_xt = off;   off = al(off + 8 * maxnd);   // exact sum: sources' list bounds
+  const size_t o_ds = off;   off = al(off + 4 * maxnd);   // exact sum: distinct keys per source
   const size_t region = off;
   // two streams only pay when there is a next batch to overlap with
   const bool ms = p->hub_streams == 2 && batches.size() > 1;
@@ -868,6 +927,8 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     BucketWork* d_bw = (BucketWork*)(rb + o_bw);
     uint32_t* d_sd = (uint32_t*)(rb + o_sd);
     HubTask* d_rg = (HubTask*)(rb + o_rg);
+    unsigned long long* d_xt = (unsigned long long*)(rb + o_xt);
+    uint32_t* d_ds = (uint32_t*)(rb + o_ds);
     const size_t nd = b.d1 - b.d0;
     HubDesc* d_desc = d_desc_all + b.d0;
     const int maxP = b.maxP;
@@ -877,6 +938,9 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
                        p->hub_range, d_sd, d_pc, d_tau, d_oflag, d_lc, bi == 0 ? d_ovl : nullptr,
                        bi == 0 ? d_rsp : nullptr);
     HIP_OK(hipGetLastError());
+    if (a.xs) {  // list bounds and distinct counts (adjacent: one fill)
+      HIP_OK(hipMemsetAsync(d_xt, 0, (size_t)(o_ds - o_xt) + 4 * nd, st));
+    }
     const int64_t ntiles = b.ntiles;
     const int64_t nbuck = b.nbuck;
     if (ntiles) {
@@ -923,7 +987,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     }
     // a batch of sources without successors (init of dangling nodes) has no tiles but still has
     // buckets: the one holding the source's own seed entry
-    if (nbuck && p->hub_range == 0) {
+    if (nbuck && p->hub_range == 0 && !a.xs) {
       hipLaunchKernelGGL(k_hub_prep, dim3((unsigned)((nbuck + 255) / 256)), dim3(256), 0, st, g, s, a, H, d_desc, d_buck,
                          nbuck, d_cmx, d_sd, d_tau, d_tau_hot, d_bw);
       HIP_OK(hipGetLastError());
@@ -938,6 +1002,28 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
                          d_oflag, d_ovl, p->seg_t);
       HIP_OK(hipGetLastError());
       p->merge_launches++;
+    }
+    if (a.xs) {
+      // exact sum: one workgroup per bucket, then one per source over the buckets' lists
+      const int budget = std::min(p->xr_T * 85 / 100, p->xr_T - p->xr_W * WAVE - WAVE);
+      if (nbuck) {
+        hipLaunchKernelGGL(k_xb, dim3((unsigned)nbuck), dim3(64 * p->xr_W), xr_lds_bytes(p->xr_T, p->xr_W, p->Lp), sb, s,
+                           a, d_desc, d_buck, d_cmx, d_sd, d_st, d_tau, p->xr_T, budget, p->Lp, d_xt, d_pk, d_ps, d_pc,
+                           d_ds, d_oflag, d_ovl, p->d_rp);
+        HIP_OK(hipGetLastError());
+        p->merge_launches++;
+      }
+      if (ms) {
+        HIP_OK(hipEventRecord(p->ev_buck[r], sb));
+        HIP_OK(hipStreamWaitEvent(sf, p->ev_buck[r], 0));
+      }
+      hipLaunchKernelGGL(k_xfinal<HubDesc>, dim3((unsigned)nd), dim3(256), xf_lds_bytes(p->Lp, p->xf_stage), sf, s, a,
+                         d_desc, d_xt, d_pk, d_ps, d_pc, d_ds, d_oflag, p->d_dlast, p->Lp, p->xf_stage, maxdiff,
+                         p->d_stats);
+      HIP_OK(hipGetLastError());
+      p->merge_launches++;
+      if (ms) HIP_OK(hipEventRecord(p->ev_fin[r], sf));
+      continue;
     }
     if (nbuck) {
       // every bucket goes to a single wave first: a bucket made long by one hot key (a core node
@@ -1063,6 +1149,224 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     return run_hubs(p, a2, rb.data(), rc.data(), (size_t)nrsp, maxdiff, fallback);
   }
   return PPR_OK;
+}
+
+// Exact-sum merge of the hub sources src[0..n) (candidate counts cand, out-degrees deg, expected
+// distinct keys dest): a source whose keys fit xr_rmax workgroup tables is walked by that many
+// range workgroups (k_xr; one range finishes the source itself, several append to a list that
+// k_xfinal selects from) on the wave-tier stream, the others are partitioned into buckets of one
+// table each (run_hubs: count, scan, scatter, k_xb, k_xfinal) beside them. A table that overflows
+// sends its source back here with a larger estimate.
+static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& src,
+                          const std::vector<int32_t>& cand, const std::vector<int32_t>& deg,
+                          const std::vector<int64_t>& dest, unsigned long long* maxdiff, int depth) {
+  const size_t n = src.size();
+  if (!n) return PPR_OK;
+  if (depth > 12) return PPR_ERR_RANGE;  // (cannot happen: estimates grow 4x per redo up to the candidate count)
+  hipStream_t st = p->stream;
+  hipStream_t sw = p->stream3 ? p->stream3 : st;
+  DevGraph g{p->d_rp, p->d_colx, p->n};
+  const DevSlab s = dev_slab(p);
+  const int64_t L = p->L;
+  // workgroup table classes (slots, waves): 16 waves per CU in each
+  struct Cls { int T, W; };
+  const Cls cls[3] = {{std::min(2048, p->xr_T), std::max(1, p->xr_W / 4)},
+                      {std::min(4096, p->xr_T), std::max(1, p->xr_W / 2)},
+                      {p->xr_T, p->xr_W}};
+  auto cap_of = [&](int T) { return (int64_t)T * p->xr_fill / 100; };
+  std::vector<int32_t> rng;            // ranges per walked source (0: partitioned)
+  std::vector<uint8_t> ci;             // table class of a walked source
+  rng.resize(n);
+  ci.resize(n);
+  std::vector<int32_t> bsrc, bcand;    // partitioned: sources | candidate counts, then degrees
+  std::vector<int32_t> bdest;
+  const int64_t capA = cap_of(p->xr_T);
+  for (size_t i = 0; i < n; i++) {
+    const int64_t R = std::max<int64_t>(1, (dest[i] + capA - 1) / capA);
+    if (R <= p->xr_rmax || !p->hub_enabled) {
+      rng[i] = (int32_t)R;
+      int c = 2;
+      if (R == 1) c = dest[i] <= cap_of(cls[0].T) ? 0 : dest[i] <= cap_of(cls[1].T) ? 1 : 2;
+      ci[i] = (uint8_t)c;
+    } else {
+      rng[i] = 0;
+      bsrc.push_back(src[i]);
+      bdest.push_back((int32_t)std::min<int64_t>(dest[i], INT32_MAX));
+    }
+  }
+  // ranged sources: multi-range ones first (k_xfinal covers descriptors [0, nmulti))
+  std::vector<XDesc> xd;
+  std::vector<XTask> tasks[3];
+  int64_t pt = 0;
+  for (int pass = 0; pass < 2; pass++)
+    for (size_t i = 0; i < n; i++) {
+      if (!rng[i] || (rng[i] > 1) != (pass == 0)) continue;
+      const int32_t d = (int32_t)xd.size();
+      XDesc x;
+      x.v = src[i];
+      x.R = rng[i];
+      x.pt_off = pt;
+      x.factor = p->damping / (double)deg[i];
+      x.selfval = 1.0 - p->damping;
+      if (rng[i] > 1) pt += (int64_t)rng[i] * L;
+      xd.push_back(x);
+      for (int r = 0; r < rng[i]; r++) tasks[ci[i]].push_back(XTask{d, r});
+    }
+  int64_t nmulti = 0;
+  for (const XDesc& x : xd) nmulti += x.R > 1;
+  const size_t nx = xd.size();
+  size_t ntask = 0;
+  for (int c = 0; c < 3; c++) ntask += tasks[c].size();
+  // device scratch: descriptors | tasks | list keys | list scores | pc | dsum | oflag | ovl | xtau
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t off = 0;
+  const size_t o_d = off;  off = al(off + sizeof(XDesc) * (nx + 1));
+  const size_t o_t = off;  off = al(off + sizeof(XTask) * (ntask + 1));
+  const size_t o_k = off;  off = al(off + 4 * (size_t)(pt + 1));
+  const size_t o_s = off;  off = al(off + 8 * (size_t)(pt + 1));
+  const size_t o_z = off;  // zeroed together: pc | dsum | oflag | ovl | xtau
+  const size_t o_pc = off; off = al(off + 4 * (nx + 1));
+  const size_t o_ds = off; off = al(off + 4 * (nx + 1));
+  const size_t o_of = off; off = al(off + 4 * (nx + 1));
+  const size_t o_ov = off; off = al(off + 4 * (nx + 2));
+  const size_t o_xt = off; off = al(off + 8 * (nx + 1));
+  const size_t total = off;
+  std::vector<int32_t> ovl_h;
+  if (nx) {
+    {
+      int rc = ensure_dev(&p->d_xs, &p->xs_bytes, total);
+      if (rc) return rc;
+    }
+    unsigned char* b = p->d_xs;
+    XDesc* d_xd = (XDesc*)(b + o_d);
+    XTask* d_tk = (XTask*)(b + o_t);
+    int32_t* d_pk = (int32_t*)(b + o_k);
+    double* d_ps = (double*)(b + o_s);
+    uint32_t* d_pc = (uint32_t*)(b + o_pc);
+    uint32_t* d_ds = (uint32_t*)(b + o_ds);
+    int32_t* d_of = (int32_t*)(b + o_of);
+    int32_t* d_ov = (int32_t*)(b + o_ov);
+    unsigned long long* d_xt = (unsigned long long*)(b + o_xt);
+    // descriptors and tasks through the pinned staging buffer (one upload)
+    const size_t up = o_t + sizeof(XTask) * ntask;
+    {
+      // (its own pinned buffer: run_hubs below restages h_desc_pin while this upload may be pending;
+      // the previous upload from it completed at the last call's closing sync of sw)
+      int rc = ensure_pinned(&p->h_xs_pin, &p->h_xs_bytes, up);
+      if (rc) return rc;
+    }
+    unsigned char* hb = (unsigned char*)p->h_xs_pin;
+    std::memcpy(hb + o_d, xd.data(), sizeof(XDesc) * nx);
+    size_t tofs[3];
+    {
+      size_t k = 0;
+      for (int c = 0; c < 3; c++) {
+        tofs[c] = k;
+        if (!tasks[c].empty()) std::memcpy(hb + o_t + sizeof(XTask) * k, tasks[c].data(), sizeof(XTask) * tasks[c].size());
+        k += tasks[c].size();
+      }
+    }
+    HIP_OK(hipMemcpyAsync(b, hb, up, hipMemcpyHostToDevice, sw));
+    HIP_OK(hipMemsetAsync(b + o_z, 0, total - o_z, sw));
+    for (int c = 0; c < 3; c++) {
+      if (tasks[c].empty()) continue;
+      const int T = cls[c].T, W = cls[c].W;
+      const int budget = std::min(T * 85 / 100, T - W * WAVE - WAVE);
+      hipLaunchKernelGGL(k_xr, dim3((unsigned)tasks[c].size()), dim3(64 * W), xr_lds_bytes(T, W, p->Lp), sw, g, s, a,
+                         d_xd, d_tk + tofs[c], T, budget, p->Lp, d_xt, d_pk, d_ps, d_pc, d_ds, p->d_dlast, d_of, d_ov,
+                         maxdiff, p->d_stats);
+      HIP_OK(hipGetLastError());
+      p->merge_launches++;
+    }
+    if (nmulti) {
+      hipLaunchKernelGGL(k_xfinal<XDesc>, dim3((unsigned)nmulti), dim3(256), xf_lds_bytes(p->Lp, p->xf_stage), sw, s, a,
+                         d_xd, d_xt, d_pk, d_ps, d_pc, d_ds, d_of, p->d_dlast, p->Lp, p->xf_stage, maxdiff, p->d_stats);
+      HIP_OK(hipGetLastError());
+      p->merge_launches++;
+    }
+  }
+  // partitioned sources beside them
+  std::vector<int32_t> fallback;
+  if (!bsrc.empty()) {
+    const size_t nb = bsrc.size();
+    std::vector<int32_t> cd(2 * nb);
+    {
+      size_t k = 0;
+      for (size_t i = 0; i < n; i++)
+        if (!rng[i]) { cd[k] = cand[i]; cd[nb + k] = deg[i]; k++; }
+    }
+    int rc = run_hubs(p, a, bsrc.data(), cd.data(), nb, maxdiff, fallback, bdest.data());
+    if (rc) return rc;
+  }
+  if (nx) {
+    int32_t novf = 0;
+    HIP_OK(hipMemcpyAsync(&novf, p->d_xs + o_ov, 4, hipMemcpyDeviceToHost, sw));
+    HIP_OK(hipStreamSynchronize(sw));
+    if (novf) {
+      std::vector<int32_t> od(novf);
+      HIP_OK(hipMemcpyAsync(od.data(), p->d_xs + o_ov + 4, 4 * (size_t)novf, hipMemcpyDeviceToHost, sw));
+      HIP_OK(hipStreamSynchronize(sw));
+      for (int32_t d : od) fallback.push_back(xd[d].v);
+    }
+  }
+  if (fallback.empty()) return PPR_OK;
+  // overflowed tables: those sources again, expecting 4x the distinct keys (at most the candidates)
+  p->xr_redo += (int64_t)fallback.size();
+  std::vector<int32_t> rsrc, rcand, rdeg;
+  std::vector<int64_t> rdest;
+  {
+    // index of each overflowed source in this call's list
+    std::vector<std::pair<int32_t, int32_t>> idx(n);
+    for (size_t i = 0; i < n; i++) idx[i] = {src[i], (int32_t)i};
+    std::sort(idx.begin(), idx.end());
+    for (int32_t v : fallback) {
+      auto it = std::lower_bound(idx.begin(), idx.end(), std::make_pair(v, (int32_t)-1));
+      if (it == idx.end() || it->first != v) return PPR_ERR_HIP;
+      const size_t i = (size_t)it->second;
+      rsrc.push_back(src[i]);
+      rcand.push_back(cand[i]);
+      rdeg.push_back(deg[i]);
+      rdest.push_back(std::min<int64_t>((int64_t)cand[i], 4 * dest[i] + 64));
+    }
+  }
+  return run_xhubs_list(p, a, rsrc, rcand, rdeg, rdest, maxdiff, depth + 1);
+}
+
+// the exact-sum merge of the `count` sources of device list `d_list` (hub tier, or any tier the
+// plan leaves without a wave kernel): candidate counts, degrees and last distinct counts gathered
+// on the device, the estimate planned on the host
+static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int64_t count, unsigned long long* maxdiff) {
+  if (count <= 0) return PPR_OK;
+  hipStream_t st = p->stream;
+  const size_t nh = (size_t)count;
+  {
+    size_t capb = p->h_hub_cap * 12;
+    void* ptr = p->h_hub_pin;
+    int r = ensure_pinned(&ptr, &capb, 16 * nh);
+    if (r) return r;
+    p->h_hub_pin = (int32_t*)ptr;
+    p->h_hub_cap = capb / 12;
+  }
+  if (3 * nh > (size_t)p->n) { int r = ensure_dev((unsigned char**)&p->d_gath, &p->gath_bytes, 12 * nh); if (r) return r; }
+  int32_t* d_g = 3 * nh > (size_t)p->n ? p->d_gath : p->d_ovf;
+  int32_t* h = p->h_hub_pin;
+  HIP_OK(hipMemcpyAsync(h, d_list, 4 * nh, hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(k_gather_cand_deg, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_list, (int64_t)nh,
+                     p->d_cand, p->d_rp, d_g, (const int32_t*)p->d_dlast);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(h + nh, d_g, 12 * nh, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  std::vector<int32_t> src(h, h + nh), cand(h + nh, h + 2 * nh), deg(h + 2 * nh, h + 3 * nh);
+  std::vector<int64_t> dest(nh);
+  for (size_t i = 0; i < nh; i++) {
+    // distinct keys expected: the last merge's count (rows change little between updates) plus a
+    // margin, else (first merge) 60 % of the candidates; never more than the candidates + 1
+    const int64_t dl = h[3 * nh + i];
+    const int64_t c = (int64_t)cand[i];
+    dest[i] = std::min<int64_t>(c, dl > 0 ? dl + dl / 8 + 64 : c * 3 / 5 + 64);
+    if (p->xr_dscale != 100) dest[i] = std::max<int64_t>(1, dest[i] * p->xr_dscale / 100);
+  }
+  return run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0);
 }
 
 // classify + launch all tiers for `count` sources of `list`; the span is timed with events on
@@ -1223,14 +1527,31 @@ reclassify:
     if (!cnt[t] || !p->tierT[t]) continue;
     // one wave per block by default: no LDS left unusable by a 4-wave block granularity
     const int wpb = p->wave_wpb;
-    const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * wpb;
     const int64_t blocks = ((int64_t)cnt[t] + wpb - 1) / wpb;
-    hipLaunchKernelGGL(p->hot_n > 0 ? k_merge_lds<true> : k_merge_lds<false>, dim3((unsigned)blocks), dim3(64 * wpb),
-                       bytes, sw, g, s, a,
-                       p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], p->tierT[t], p->Lp,
-                       maxdiff, p->d_stats);
+    if (a.xs) {
+      hipLaunchKernelGGL(k_merge_lds_x, dim3((unsigned)blocks), dim3(64 * wpb), lds_wave_bytes_x(p->tierT[t], p->Lp) * wpb,
+                         sw, g, s, a, p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], p->tierT[t], p->Lp, maxdiff,
+                         p->d_stats, p->d_dlast);
+    } else {
+      const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * wpb;
+      hipLaunchKernelGGL(p->hot_n > 0 ? k_merge_lds<true> : k_merge_lds<false>, dim3((unsigned)blocks), dim3(64 * wpb),
+                         bytes, sw, g, s, a,
+                         p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], p->tierT[t], p->Lp,
+                         maxdiff, p->d_stats);
+    }
     HIP_OK(hipGetLastError());
     p->merge_launches++;
+  }
+  if (a.xs) {
+    // exact sum: every source no wave tier took (the hub tier, tiers the plan left without a
+    // wave kernel) goes through the range / bucket workgroups -- nothing falls to the chain-order
+    // HBM table
+    int r = PPR_OK;
+    for (int t = 0; t < NT && !r; t++)
+      if (cnt[t] && !p->tierT[t]) r = run_xhubs(p, a, p->d_tier_lists + (int64_t)t * p->n, cnt[t], maxdiff);
+    if (!r && cnt[TIER_WG]) r = run_xhubs(p, a, p->d_tier_lists + (int64_t)TIER_WG * p->n, cnt[TIER_WG], maxdiff);
+    if (!r && cnt[TIER_BIG]) r = run_xhubs(p, a, p->d_tier_lists + (int64_t)TIER_BIG * p->n, cnt[TIER_BIG], maxdiff);
+    return r;
   }
   if (cnt[TIER_WG]) {
     hipLaunchKernelGGL(k_merge_wg, dim3(cnt[TIER_WG]), dim3(WG_THREADS), p->wg_lds, st, g, s, a,

@@ -20,12 +20,14 @@ __global__ void __launch_bounds__(256) k_gather_i32(const int32_t* list, int64_t
 // hub planning inputs, gathered so the host walks them sequentially: candidate counts and
 // out-degrees of the listed sources (out[0..count) | out[count..2 count))
 __global__ void __launch_bounds__(256) k_gather_cand_deg(const int32_t* list, int64_t count, const int32_t* cand,
-                                                         const int64_t* rp, int32_t* out) {
+                                                         const int64_t* rp, int32_t* out,
+                                                         const int32_t* dlast = nullptr) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   const int v = list[i];
   out[i] = cand[v];
   out[count + i] = (int32_t)(rp[v + 1] - rp[v]);
+  if (dlast) out[2 * count + i] = dlast[v];  // exact-sum planning: distinct keys of the last merge
 }
 
 // the same gather with the hub count read on the device (at most cap), for the fused small-level

@@ -186,9 +186,13 @@ constexpr int HUB_TW_BATCH = PPR_TW_BATCH;  // candidate groups a walking wave g
 // from the same successor basket (so its keys are distinct; always false in init mode).
 // `succ(ln, rmin_bits)` (optional) sees every lane's successor basket length and row minimum once
 // per window (non-unit mode; invalid lanes report length 0).
+// hub_window_walk_part: the same walk restricted to every nparts-th batch of groups starting at
+// batch `part` (the waves of a workgroup sharing one short successor window, merge_xs.h k_xr);
+// f still sees this wave's candidates in stream order
 template <class F, class S>
-__device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
-                                                int64_t i0, int64_t e, uint8_t* fl, F f, S succ) {
+__device__ __forceinline__ void hub_window_walk_part(const DevGraph& g, const DevSlab& s, const IterArgs& a,
+                                                     int64_t i0, int64_t e, uint8_t* fl, F f, S succ, int part,
+                                                     int nparts) {
   const int64_t i = i0 + lane_id();
   if (a.unit) {  // init: every successor contributes {u: 1.0}
     const bool valid = i < e;
@@ -258,17 +262,25 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
   int key[HUB_TW_BATCH], nkey[HUB_TW_BATCH];
   double sv[HUB_TW_BATCH], nsv[HUB_TW_BATCH];
   bool one[HUB_TW_BATCH], none[HUB_TW_BATCH];
-  if (total > 0) load(0, nkey, nsv, none);
-  for (int g0 = 0; g0 < total; g0 += WAVE * HUB_TW_BATCH) {
+  const int step = WAVE * HUB_TW_BATCH * nparts;
+  const int gs = WAVE * HUB_TW_BATCH * part;
+  if (gs < total) load(gs, nkey, nsv, none);
+  for (int g0 = gs; g0 < total; g0 += step) {
 #pragma unroll
     for (int k = 0; k < HUB_TW_BATCH; k++) { key[k] = nkey[k]; sv[k] = nsv[k]; one[k] = none[k]; }
-    if (g0 + WAVE * HUB_TW_BATCH < total) load(g0 + WAVE * HUB_TW_BATCH, nkey, nsv, none);
+    if (g0 + step < total) load(g0 + step, nkey, nsv, none);
 #pragma unroll
     for (int k = 0; k < HUB_TW_BATCH; k++) {
       if (g0 + k * WAVE >= total) break;  // uniform
       f(g0 + k * WAVE + lane_id() < total, key[k], sv[k], one[k]);
     }
   }
+}
+
+template <class F, class S>
+__device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a,
+                                                int64_t i0, int64_t e, uint8_t* fl, F f, S succ) {
+  hub_window_walk_part(g, s, a, i0, e, fl, f, succ, 0, 1);
 }
 
 struct WalkNoSucc {

@@ -1,0 +1,552 @@
+// merge_xs.h -- the exact-sum basket merge (the plan default for GRank).
+//
+// Every contribution p = fl(s * d/deg) of a successor basket (and the seed 1-d) is added EXACTLY
+// into a fixed-point accumulator of its key, X[k] += floor(p * 2^93) (96 bits: a 64-bit low word
+// and a 32-bit high word), and the basket value is X[k] * 2^-93 rounded to nearest once. Integer
+// addition is associative, so the order of the adds is free: any lane, wave or workgroup adds
+// with LDS atomics, no stable partition, no ordered chains. The result is the exact sum of the
+// rounded products rounded once -- at least as accurate as the reference's in-order fma chain
+// (include/grank.h:107-116), which it matches to a few ulps -- and the same on every run and every
+// GPU count. Restated bit for bit by oracle/grank_oracle.c ("exact" mode). Every basket sums to
+// <= 1, so a key's total stays < 4 (X < 2^95: the high word never reaches the key tag above it).
+//
+//   k_merge_lds_x  one wave per small source (candidates + 1 <= 1536), 16-B LDS slots
+//   k_xr           one workgroup per (hub source, key range): walks the source's successor rows,
+//                  accumulates the keys of its hash range in a shared LDS table (up to 8192
+//                  slots), then either finishes the source (one range) or appends its top-L
+//   k_xb           one workgroup per staged bucket of a partitioned hub source (the partition
+//                  of merge_hub.h: count, scan, scatter), same table and epilogue as k_xr
+//   k_xfinal       one workgroup per listed source: top-L of its ranges' / buckets' lists
+#pragma once
+#include "merge_hub.h"
+
+namespace pprk {
+
+constexpr int XS_F = 93;   // fraction bits of the fixed-point sums (oracle/grank_oracle.c XS_F)
+
+// floor(p * 2^93) of p in [0, 4): lo = low 64 bits, hi = bits 64..94
+__device__ __forceinline__ void xs_conv(double p, unsigned long long& lo, uint32_t& hi) {
+  const unsigned long long b = dbits(p);
+  int e = (int)((b >> 52) & 0x7ffu);
+  unsigned long long m = b & ((1ull << 52) - 1ull);
+  if (e) m |= 1ull << 52; else e = 1;
+  const int sh = e - 1075 + XS_F;
+  if (sh >= 0) {
+    lo = m << sh;
+    hi = sh > 11 ? (uint32_t)(m >> (64 - sh)) : 0u;
+  } else {
+    lo = -sh < 64 ? (m >> -sh) : 0ull;
+    hi = 0u;
+  }
+}
+
+// X * 2^-93 rounded to nearest even: the top 64 bits of X with a sticky bit, one correctly rounded
+// u64 -> f64 conversion, an exact power-of-two scale (oracle_xs_to_double)
+__device__ __forceinline__ double xs_to_double(uint32_t hi, unsigned long long lo) {
+  if (hi == 0u) return ldexp((double)lo, -XS_F);
+  const int n = 32 - __clz(hi);
+  const unsigned long long top = ((unsigned long long)hi << (64 - n)) | (lo >> n);
+  const unsigned long long sticky = (lo & ((1ull << n) - 1ull)) != 0ull ? 1ull : 0ull;
+  return ldexp((double)(top | sticky), n - XS_F);
+}
+
+// value of a single contribution p as the exact path stores it: a lower bound of the total of any
+// key that receives p (totals of nonnegative terms only grow, rounding is monotone)
+__device__ __forceinline__ double xs_single(double p) {
+  unsigned long long lo;
+  uint32_t hi;
+  xs_conv(p, lo, hi);
+  return xs_to_double(hi, lo);
+}
+
+// LDS table of 16-B slots: kh = (key + 1) << 32 | high word (0 = empty), lo = low word.
+struct XTable {
+  unsigned long long* kh;
+  unsigned long long* lo;
+  uint32_t mask;
+};
+
+// find-or-insert `key`, then add X: the low word's returning add yields its carry, which goes
+// with the high word into kh (the tag bits above it never change). Returns true when this lane
+// inserted the key.
+__device__ __forceinline__ bool xt_add(const XTable& t, int key, unsigned long long xlo, uint32_t xhi) {
+  const uint32_t tag = (uint32_t)key + 1u;
+  uint32_t h = hash32((uint32_t)key) & t.mask;
+  bool ins = false;
+  for (;;) {
+    const unsigned long long cur = t.kh[h];
+    if ((uint32_t)(cur >> 32) == tag) break;
+    if (cur == 0ull) {
+      const unsigned long long prev = atomicCAS(&t.kh[h], 0ull, (unsigned long long)tag << 32);
+      if (prev == 0ull) { ins = true; break; }
+      if ((uint32_t)(prev >> 32) == tag) break;
+    }
+    h = (h + 1u) & t.mask;
+  }
+  const unsigned long long old = atomicAdd(&t.lo[h], xlo);
+  const uint32_t up = xhi + ((old + xlo < old) ? 1u : 0u);
+  if (up) atomicAdd(&t.kh[h], (unsigned long long)up);
+  return ins;
+}
+
+__device__ __forceinline__ int xt_key(unsigned long long kh) { return (int)(uint32_t)(kh >> 32) - 1; }
+
+// ---------------------------------------------------------------------------------------------
+// wave tier: layout kh u64[T] | lo u64[T] | rv u64[Lp] | rk i32[Lp] | hist u32[256] | hk i32[2Lp] |
+// hv i32[2Lp] | mf i32[Lp]
+__host__ __device__ constexpr size_t lds_wave_bytes_x(int T, int Lp) {
+  return (size_t)T * 16 + (size_t)Lp * 12 + 1024 + (size_t)Lp * 20;
+}
+
+__global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, IterArgs a, const int32_t* list,
+                                                     int64_t count, int T, int Lp, unsigned long long* maxdiff,
+                                                     unsigned long long* stats, int32_t* dlast) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (w >= count) return;
+  unsigned char* base = smem + (size_t)wv * lds_wave_bytes_x(T, Lp);
+  XTable t;
+  t.kh = reinterpret_cast<unsigned long long*>(base);
+  t.lo = reinterpret_cast<unsigned long long*>(base + (size_t)T * 8);
+  t.mask = (uint32_t)T - 1u;
+  uint64_t* rv = reinterpret_cast<uint64_t*>(base + (size_t)T * 16);
+  int* rk = reinterpret_cast<int*>(base + (size_t)T * 16 + (size_t)Lp * 8);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 16 + (size_t)Lp * 12);
+  int* hk = reinterpret_cast<int*>(base + (size_t)T * 16 + (size_t)Lp * 12 + 1024);
+  int* hv = hk + 2 * Lp;
+  int* mf = hv + 2 * Lp;
+
+  const int v = list[w];
+  const int64_t b = g.rp[v], e = g.rp[v + 1];
+  const double factor = merge_factor(a, e - b);
+  for (int i = lane_id(); i < T; i += WAVE) { t.kh[i] = 0ull; t.lo[i] = 0ull; }
+  wave_fence();
+  if (lane_id() == 0) {
+    unsigned long long lo;
+    uint32_t hi;
+    xs_conv(self_seed(a, e - b), lo, hi);
+    xt_add(t, v, lo, hi);
+  }
+  wave_fence();
+  unsigned long long mb = 0;
+  if (a.unit) {
+    unsigned long long flo;
+    uint32_t fhi;
+    xs_conv(factor, flo, fhi);  // init: every successor contributes 1.0 * d/deg
+    for (int64_t e0 = b; e0 < e; e0 += WAVE) {
+      const int64_t i = e0 + lane_id();
+      if (i < e) xt_add(t, g.colx[i] & 0x7fffffff, flo, fhi);
+    }
+  } else {
+    for (int64_t e0 = b; e0 < e; e0 += WAVE)
+      hub_window_walk(g, s, a, e0, min(e, e0 + WAVE), reinterpret_cast<uint8_t*>(hist),
+                      [&](bool valid, int id, double sv, bool) {
+                        if (valid) {
+                          unsigned long long lo;
+                          uint32_t hi;
+                          xs_conv(sv * factor, lo, hi);
+                          xt_add(t, id, lo, hi);
+                        }
+                      },
+                      WalkRowMin{&mb, (int)s.L});
+  }
+  wave_fence();
+#pragma unroll
+  for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
+  // keys below the pruning bound cannot reach the top-L (a full successor row puts L distinct keys
+  // at >= the single-contribution value of its minimum)
+  const double tau = (!a.unit && mb) ? xs_single(bitsd(mb) * factor) : 0.0;
+  // settle + compact in place: (double value, key) pairs over the front of the table
+  double* vals = reinterpret_cast<double*>(t.kh);
+  int* keys = reinterpret_cast<int*>(t.lo);
+  int U = 0, D = 0;
+  for (int base0 = 0; base0 < T; base0 += WAVE) {
+    const int i = base0 + lane_id();
+    const unsigned long long kh = t.kh[i];
+    const unsigned long long lo = t.lo[i];
+    const bool occ = kh != 0ull;
+    const double x = occ ? xs_to_double((uint32_t)kh, lo) : 0.0;
+    const bool keep = occ && x >= tau;
+    const uint64_t m = __ballot(keep);
+    D += __popcll(__ballot(occ));
+    wave_fence();
+    if (keep) {
+      const int pos = U + __popcll(m & lanemask_lt());
+      vals[pos] = x;
+      keys[pos] = xt_key(kh);
+    }
+    wave_fence();
+    U += __popcll(m);
+  }
+  if (dlast && !a.unit && lane_id() == 0) dlast[v] = D;  // (init counts predict nothing)
+  finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return vals[i]; }, s, a, hist, rv, rk, Lp, hk, hv,
+                mf, maxdiff, stats);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Range / bucket workgroups. LDS: kh u64[T] | lo u64[T] | flags u8[W][HUB_WALK_FLAGS] | hist u32[256] |
+// misc i32[64] | rv u64[Lp] | rk i32[Lp] | hk i32[2Lp] | hv i32[2Lp] | mf i32[Lp]
+__host__ __device__ constexpr size_t xr_lds_bytes(int T, int W, int Lp) {
+  return (size_t)T * 16 + (size_t)W * HUB_WALK_FLAGS + 1024 + 256 + (size_t)Lp * 32;
+}
+
+// one hub source merged by workgroups (k_xr / k_xb): the source, its constants and outputs
+struct XDesc {
+  int32_t v;
+  int32_t R;        // key ranges (k_xr; 1 = one workgroup finishes the source), 0 for a k_xb source
+  int64_t pt_off;   // appended-entry list (R * L, or P * L entries)
+  double factor, selfval;
+};
+
+// misc slots (ints; M_BIN..M_HB = 4..6 belong to wg_radix_kth, 8..9 hold k_xr's row-minimum bound)
+enum { XM_FILL = 0, XM_OVF = 1, XM_CNT = 2, XM_U = 3, XM_MIN = 10 /* u64: 10..11 */ };
+
+struct XrLds {
+  XTable t;
+  uint8_t* fl;
+  WgLds w;  // hist / misc and the row buffers (the select and finish_source scratch)
+};
+
+__device__ __forceinline__ XrLds xr_carve(unsigned char* smem, int T, int W, int Lp) {
+  XrLds x;
+  unsigned char* p = smem;
+  x.t.kh = reinterpret_cast<unsigned long long*>(p); p += (size_t)T * 8;
+  x.t.lo = reinterpret_cast<unsigned long long*>(p); p += (size_t)T * 8;
+  x.t.mask = (uint32_t)T - 1u;
+  x.fl = p; p += (size_t)W * HUB_WALK_FLAGS;
+  x.w = WgLds{};
+  x.w.hist = reinterpret_cast<uint32_t*>(p); p += 1024;
+  x.w.misc = reinterpret_cast<int*>(p); p += 256;
+  x.w.rv = reinterpret_cast<uint64_t*>(p); p += (size_t)Lp * 8;
+  x.w.rk = reinterpret_cast<int*>(p); p += (size_t)Lp * 4;
+  x.w.hk = reinterpret_cast<int*>(p); p += (size_t)Lp * 8;
+  x.w.hv = reinterpret_cast<int*>(p); p += (size_t)Lp * 8;
+  x.w.mf = reinterpret_cast<int*>(p);
+  return x;
+}
+
+__device__ __forceinline__ void xr_clear(const XrLds& x, int T) {
+  for (int i = threadIdx.x; i < T; i += blockDim.x) { x.t.kh[i] = 0ull; x.t.lo[i] = 0ull; }
+  if (threadIdx.x < 64) x.w.misc[threadIdx.x] = 0;
+}
+
+// one accumulated contribution of the calling lane (valid lanes only), with the workgroup's
+// distinct-key budget: a group's new keys are counted by its wave's lowest lane; past the budget
+// the overflow flag stops every wave at its next group (at most W * 64 keys beyond the budget, so
+// a budget <= T - W * 64 - 1 never lets a probe run out of empty slots)
+__device__ __forceinline__ void xr_apply(const XrLds& x, bool valid, int key, double p, int budget) {
+  bool ins = false;
+  if (valid) {
+    unsigned long long lo;
+    uint32_t hi;
+    xs_conv(p, lo, hi);
+    ins = xt_add(x.t, key, lo, hi);
+  }
+  const int n = __popcll(__ballot(ins));
+  if (n && lane_id() == 0) {
+    const int f = atomicAdd(&x.w.misc[XM_FILL], n) + n;
+    if (f > budget) x.w.misc[XM_OVF] = 1;
+  }
+}
+
+// Epilogue of one range / bucket workgroup after its last add (every thread): settle the sums in
+// place (lo := the double value), then
+//   direct: top-L of the table -> the source's row (finish_source on wave 0), dlast[v] = distinct
+//   list:   top-L of the table, keys >= the pruning bound, appended to the source's list; the
+//           range's L-th value (when it has L keys) raises the source's bound xtau[d]
+__device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& s, const IterArgs& a, int Lp,
+                                          const XDesc& xd, int d, bool direct, double tau_rows,
+                                          unsigned long long* xtau, int32_t* pk, double* ps, uint32_t* pc,
+                                          uint32_t* dsum, int32_t* dlast, unsigned long long* maxdiff,
+                                          unsigned long long* stats) {
+  const int L = s.L;
+  const int v = xd.v;
+  for (int i = threadIdx.x; i < T; i += blockDim.x) {
+    const unsigned long long kh = x.t.kh[i];
+    if (kh) x.t.lo[i] = dbits(xs_to_double((uint32_t)kh, x.t.lo[i]));
+  }
+  __syncthreads();
+  const int D = x.w.misc[XM_FILL];
+  const unsigned long long* kh = x.t.kh;
+  const unsigned long long* lo = x.t.lo;
+  auto keyat = [&](int i) { return xt_key(kh[i]); };
+  auto valat = [&](int i) { return bitsd(lo[i]); };
+  const double tau0 = direct ? 0.0 : tau_rows;
+  auto elig = [&](int i) { return kh[i] != 0ull && bitsd(lo[i]) >= tau0; };
+  // eligible count
+  int c = 0;
+  for (int i = threadIdx.x; i < T; i += blockDim.x) c += elig(i) ? 1 : 0;
+  c = wave_sum(c);
+  if (lane_id() == 0 && c) atomicAdd(&x.w.misc[XM_U], c);
+  __syncthreads();
+  const int U = x.w.misc[XM_U];
+  const uint32_t ts = tie_salt(v);
+  SelCrit sc;
+  sc.tie = false; sc.pa = 0; sc.ma = 0; sc.pb = 0; sc.mb = 0;  // (ma = 0: every eligible entry)
+  const bool cut = U > L;
+  if (cut) sc = wg_select_top(x.w, T, L, keyat, valat, elig, ts);
+  // (wg_select_top ends on a barrier)
+  if (direct) {
+    for (int i = threadIdx.x; i < T; i += blockDim.x) {
+      if (!elig(i)) continue;
+      const uint64_t vb = lo[i];
+      const int key = keyat(i);
+      if (cut && !sel_test(sc, vb, tie_w(key, ts))) continue;
+      const int pos = atomicAdd(&x.w.misc[XM_CNT], 1);
+      x.w.rv[pos] = vb;
+      x.w.rk[pos] = key;
+    }
+    __syncthreads();
+    if (threadIdx.x < WAVE) {
+      const int cnt = x.w.misc[XM_CNT];
+      const uint64_t* rv = x.w.rv;
+      const int* rk = x.w.rk;
+      if (dlast && !a.unit && lane_id() == 0) dlast[v] = D;
+      finish_source(v, cnt, [&](int i) { return rk[i]; }, [&](int i) { return bitsd(rv[i]); }, s, a, x.w.hist,
+                    x.w.rv, x.w.rk, Lp, x.w.hk, x.w.hv, x.w.mf, maxdiff, stats);
+    }
+    return;
+  }
+  if (threadIdx.x == 0 && D) atomicAdd(&dsum[d], (uint32_t)D);
+  if (cut) {
+    // the L-th value of this range: the smallest selected value (u64 bits order like the values),
+    // reduced over the whole workgroup before it may raise the source's bound
+    unsigned long long* wmin = reinterpret_cast<unsigned long long*>(&x.w.misc[XM_MIN]);
+    if (threadIdx.x == 0) *wmin = ~0ull;
+    __syncthreads();
+    unsigned long long mn = ~0ull;
+    for (int i = threadIdx.x; i < T; i += blockDim.x)
+      if (elig(i) && sel_test(sc, lo[i], tie_w(keyat(i), ts))) mn = lo[i] < mn ? lo[i] : mn;
+    mn = wave_min_u64(mn);
+    if (lane_id() == 0 && mn != ~0ull) atomicMin(wmin, mn);
+    __syncthreads();
+    if (threadIdx.x == 0 && *wmin != ~0ull) atomicMax(&xtau[d], *wmin);
+    __syncthreads();
+  }
+  const double tb = fmax(tau0, bitsd(__hip_atomic_load(&xtau[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+  for (int i0 = 0; i0 < T; i0 += blockDim.x) {
+    const int i = i0 + threadIdx.x;
+    bool keep = false;
+    if (i < T && elig(i)) {
+      const uint64_t vb = lo[i];
+      keep = bitsd(vb) >= tb && (!cut || sel_test(sc, vb, tie_w(keyat(i), ts)));
+    }
+    const uint64_t m = __ballot(keep);
+    uint32_t base = 0;
+    if (m && lane_id() == 0) base = atomicAdd(&pc[d], (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, 0);
+    if (keep) {
+      const int64_t o = xd.pt_off + base + __popcll(m & lanemask_lt());
+      pk[o] = keyat(i);
+      ps[o] = bitsd(lo[i]);
+    }
+  }
+}
+
+// range r of R of a hub source: key k belongs to range ((hash_b(k) * R) >> 32) -- hash_b orders the
+// stored rows, the table slot hash is hash32, so the two are independent
+__device__ __forceinline__ bool xr_in(int key, int r, int R) {
+  return R == 1 || (int)(((uint64_t)hash_b((uint32_t)key) * (uint32_t)R) >> 32) == r;
+}
+
+struct XTask { int32_t d; int32_t r; };
+
+// One workgroup per (source, range): every wave walks its windows of the source's successor rows
+// (a short successor list: all waves share each window, each taking every W-th batch of groups).
+__global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, const XDesc* xdesc,
+                                             const XTask* tasks, int T, int budget, int Lp, unsigned long long* xtau,
+                                             int32_t* pk, double* ps, uint32_t* pc, uint32_t* dsum, int32_t* dlast,
+                                             int32_t* oflag, int32_t* ovl, unsigned long long* maxdiff,
+                                             unsigned long long* stats) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  const XrLds x = xr_carve(smem, T, W, Lp);
+  const XTask tk = tasks[blockIdx.x];
+  const XDesc xd = xdesc[tk.d];
+  const int v = xd.v, R = xd.R, r = tk.r;
+  xr_clear(x, T);
+  __syncthreads();
+  if (threadIdx.x == 0 && xr_in(v, r, R)) {
+    unsigned long long lo;
+    uint32_t hi;
+    xs_conv(xd.selfval, lo, hi);
+    xt_add(x.t, v, lo, hi);
+    x.w.misc[XM_FILL] = 1;
+  }
+  __syncthreads();
+  const int64_t b = g.rp[v], e = g.rp[v + 1];
+  const double factor = xd.factor;
+  unsigned long long mb = 0;
+  uint8_t* fl = x.fl + (size_t)wv * HUB_WALK_FLAGS;
+  auto fn = [&](bool valid, int id, double sv, bool) {
+    if (x.w.misc[XM_OVF]) return;  // (uniform per wave: one LDS read per group)
+    xr_apply(x, valid && xr_in(id, r, R), id, sv * factor, budget);
+  };
+  if (a.unit) {
+    for (int64_t e0 = b + (int64_t)wv * WAVE; e0 < e; e0 += (int64_t)W * WAVE) {
+      const int64_t i = e0 + lane_id();
+      const int key = i < e ? (g.colx[i] & 0x7fffffff) : 0;
+      if (x.w.misc[XM_OVF]) break;
+      xr_apply(x, i < e && xr_in(key, r, R), key, factor, budget);
+    }
+  } else if (e - b >= (int64_t)W * WAVE) {
+    for (int64_t w0 = b + (int64_t)wv * WAVE; w0 < e; w0 += (int64_t)W * WAVE)
+      hub_window_walk_part(g, s, a, w0, min(e, w0 + WAVE), fl, fn, WalkRowMin{&mb, (int)s.L}, 0, 1);
+  } else {
+    for (int64_t w0 = b; w0 < e; w0 += WAVE)
+      hub_window_walk_part(g, s, a, w0, min(e, w0 + WAVE), fl, fn, WalkRowMin{&mb, (int)s.L}, wv, W);
+  }
+  __syncthreads();
+  if (x.w.misc[XM_OVF]) {
+    if (threadIdx.x == 0 && atomicExch(&oflag[tk.d], 1) == 0) ovl[1 + atomicAdd(&ovl[0], 1)] = tk.d;
+    return;
+  }
+  // pruning bound from the full successor rows (every wave saw every row's minimum)
+#pragma unroll
+  for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
+  if (lane_id() == 0 && mb) atomicMax(reinterpret_cast<unsigned long long*>(&x.w.misc[8]), mb);
+  __syncthreads();
+  const unsigned long long mbb = *reinterpret_cast<unsigned long long*>(&x.w.misc[8]);
+  const double tau_rows = (!a.unit && mbb) ? xs_single(bitsd(mbb) * factor) : 0.0;
+  xr_finish(x, T, s, a, Lp, xd, tk.d, R == 1, tau_rows, xtau, pk, ps, pc, dsum, dlast, maxdiff, stats);
+}
+
+// One workgroup per staged bucket of a partitioned hub source: the bucket's records are
+// contiguous (merge_hub.h k_hub_scatter), W waves take every W-th group of 64.
+constexpr int XB_BATCH = 4;  // groups a wave loads before applying them
+__global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDesc* desc, const HubTask* tasks,
+                                             const int32_t* cm, const uint32_t* staged, const HubRec* st,
+                                             const unsigned long long* tau_b, int T, int budget, int Lp,
+                                             unsigned long long* xtau, int32_t* pk, double* ps, uint32_t* pc,
+                                             uint32_t* dsum, int32_t* oflag, int32_t* ovl, const int64_t* rp) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  const XrLds x = xr_carve(smem, T, W, Lp);
+  const HubTask tk = tasks[blockIdx.x];
+  const HubDesc d = desc[tk.d];
+  int64_t start, nb;
+  hub_bucket_range(d, cm, staged[tk.d], tk.x, start, nb);
+  const int v = d.v;
+  const int64_t deg = rp[v + 1] - rp[v];
+  const double factor = merge_factor(a, deg);
+  xr_clear(x, T);
+  __syncthreads();
+  if (threadIdx.x == 0 && (int)hub_digit(v, d.logP) == tk.x) {
+    unsigned long long lo;
+    uint32_t hi;
+    xs_conv(self_seed(a, deg), lo, hi);
+    xt_add(x.t, v, lo, hi);
+    x.w.misc[XM_FILL] = 1;
+  }
+  __syncthreads();
+  const HubRec* rec = st + start;
+  const int64_t ng = (nb + WAVE - 1) / WAVE;
+  for (int64_t g0 = wv; g0 < ng; g0 += (int64_t)W * XB_BATCH) {
+    int key[XB_BATCH];
+    double sv[XB_BATCH];
+    bool ok[XB_BATCH];
+#pragma unroll
+    for (int k = 0; k < XB_BATCH; k++) {
+      const int64_t q = (g0 + (int64_t)k * W) * WAVE + lane_id();
+      ok[k] = q < nb;
+      key[k] = 0;
+      sv[k] = 0.0;
+      if (ok[k]) { const HubRec hr = rec[q]; key[k] = rec_key(hr); sv[k] = rec_sc(hr); }
+    }
+#pragma unroll
+    for (int k = 0; k < XB_BATCH; k++) {
+      if (x.w.misc[XM_OVF]) break;
+      if ((g0 + (int64_t)k * W) >= ng) break;
+      xr_apply(x, ok[k], key[k], sv[k] * factor, budget);
+    }
+  }
+  __syncthreads();
+  if (x.w.misc[XM_OVF]) {
+    if (threadIdx.x == 0 && atomicExch(&oflag[tk.d], 1) == 0) ovl[1 + atomicAdd(&ovl[0], 1)] = v;
+    return;
+  }
+  const double tau_rows = (!a.unit && tau_b[tk.d]) ? xs_single(bitsd(tau_b[tk.d]) * factor) : 0.0;
+  XDesc xd;
+  xd.v = v; xd.R = 0; xd.pt_off = d.pt_off; xd.factor = factor; xd.selfval = 0.0;
+  xr_finish(x, T, s, a, Lp, xd, tk.d, false, tau_rows, xtau, pk, ps, pc, dsum, nullptr, nullptr, nullptr);
+}
+
+// One workgroup per listed source: top-L of the entries its ranges / buckets appended (keys are
+// disjoint across them) at or above the final bound, then the row, norm1, maxDiff.
+// (Desc: XDesc of a ranged source or HubDesc of a partitioned one: v and pt_off)
+constexpr int XF_STAGE = 4096;  // entries staged in LDS (beyond: the select reads the list in HBM)
+__host__ __device__ constexpr size_t xf_lds_bytes(int Lp, int stage) { return (size_t)stage * 12 + 1024 + 256 + (size_t)Lp * 32; }
+
+template <class Desc>
+__global__ void __launch_bounds__(256) k_xfinal(DevSlab s, IterArgs a, const Desc* desc,
+                                                const unsigned long long* xtau, const int32_t* pk, const double* ps,
+                                                const uint32_t* pc, const uint32_t* dsum, const int32_t* skip,
+                                                int32_t* dlast, int Lp, int stage, unsigned long long* maxdiff,
+                                                unsigned long long* stats) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int d = blockIdx.x;
+  if (skip && skip[d]) return;  // overflowed: redone by the host (uniform: one load per thread, set before this launch)
+  const int v = desc[d].v;
+  const int L = s.L;
+  unsigned char* p = smem;
+  double* sv = reinterpret_cast<double*>(p); p += (size_t)stage * 8;
+  int* sk = reinterpret_cast<int*>(p); p += (size_t)stage * 4;
+  WgLds w = WgLds{};
+  w.hist = reinterpret_cast<uint32_t*>(p); p += 1024;
+  w.misc = reinterpret_cast<int*>(p); p += 256;
+  w.rv = reinterpret_cast<uint64_t*>(p); p += (size_t)Lp * 8;
+  w.rk = reinterpret_cast<int*>(p); p += (size_t)Lp * 4;
+  w.hk = reinterpret_cast<int*>(p); p += (size_t)Lp * 8;
+  w.hv = reinterpret_cast<int*>(p); p += (size_t)Lp * 8;
+  w.mf = reinterpret_cast<int*>(p);
+  const int64_t off = desc[d].pt_off;
+  const int n = (int)pc[d];
+  const double tb = bitsd(xtau[d]);
+  if (threadIdx.x < 64) w.misc[threadIdx.x] = 0;
+  __syncthreads();
+  // stage the entries >= the final bound (the top-L all are: one range alone holds L keys >= it)
+  for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+    const int i = i0 + threadIdx.x;
+    const bool keep = i < n && ps[off + i] >= tb;
+    const uint64_t m = __ballot(keep);
+    int base = 0;
+    if (m && lane_id() == 0) base = atomicAdd(&w.misc[XM_CNT], __popcll(m));
+    base = __shfl(base, 0);
+    const int pos = base + __popcll(m & lanemask_lt());
+    if (keep && pos < stage) { sv[pos] = ps[off + i]; sk[pos] = pk[off + i]; }
+  }
+  __syncthreads();
+  const int U = w.misc[XM_CNT];
+  const uint32_t ts = tie_salt(v);
+  const bool staged = U <= stage;
+  auto keyat = [&](int i) { return staged ? sk[i] : pk[off + i]; };
+  auto valat = [&](int i) { return staged ? sv[i] : ps[off + i]; };
+  const int N = staged ? U : n;
+  auto elig = [&](int i) { return staged || ps[off + i] >= tb; };
+  const bool cut = U > L;
+  SelCrit sc;
+  sc.tie = false; sc.pa = 0; sc.ma = 0; sc.pb = 0; sc.mb = 0;
+  if (cut) sc = wg_select_top(w, N, L, keyat, valat, elig, ts);
+  __syncthreads();
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    if (!elig(i)) continue;
+    const uint64_t vb = dbits(valat(i));
+    const int key = keyat(i);
+    if (cut && !sel_test(sc, vb, tie_w(key, ts))) continue;
+    const int pos = atomicAdd(&w.misc[XM_U], 1);
+    w.rv[pos] = vb;
+    w.rk[pos] = key;
+  }
+  __syncthreads();
+  if (threadIdx.x < WAVE) {
+    const int cnt = w.misc[XM_U];
+    const uint64_t* rv = w.rv;
+    const int* rk = w.rk;
+    if (dlast && !a.unit && lane_id() == 0) dlast[v] = (int32_t)dsum[d];
+    finish_source(v, cnt, [&](int i) { return rk[i]; }, [&](int i) { return bitsd(rv[i]); }, s, a, w.hist, w.rv,
+                  w.rk, Lp, w.hk, w.hv, w.mf, maxdiff, stats);
+  }
+}
+
+}  // namespace pprk

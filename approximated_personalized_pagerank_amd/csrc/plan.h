@@ -174,6 +174,19 @@ struct ppr_plan {
   int32_t* d_indeg = nullptr;         // [n] in-degree (how many sources read the node's row)
   hipStream_t stream5 = nullptr;      // k_hub_hot beside the partition / bucket stages
   hipEvent_t ev_hot0 = nullptr, ev_hot[MAX_REGIONS] = {};
+  // exact-sum GRank (merge_xs.h; PPR_FLAG_CHAIN_SUM / PPR_SUM=chain turn it off)
+  bool xsum = false;
+  int32_t* d_dlast = nullptr;         // [n] distinct keys of each source's last merge (hub planning)
+  int xr_T = 8192, xr_W = 16;         // PPR_XR_T / PPR_XR_W: range / bucket workgroup table slots, waves
+  int xr_rmax = 3;                    // PPR_XR_RMAX: most key ranges a source is walked in (beyond: partition)
+  int xr_fill = 60;                   // PPR_XR_FILL: planned distinct keys per table, % of its slots
+  int xf_stage = 4096;                // k_xfinal entries staged in LDS
+  int xr_dscale = 100;                // PPR_XR_DSCALE (tests): distinct-key estimates scaled, % (forces overflows)
+  unsigned char* d_xs = nullptr;      // range-workgroup scratch (descriptors, tasks, lists)
+  size_t xs_bytes = 0;
+  void* h_xs_pin = nullptr;           // pinned staging of its descriptors and tasks
+  size_t h_xs_bytes = 0;
+  int64_t xr_redo = 0;                // sources redone after a table overflow (PPR_TIMING at destroy)
   // MCCompletePathV2 (mccp2.hip)
   bool mc = false;
   int32_t* d_mc_walk = nullptr;       // walk set W (nodes read before their final basket exists)
@@ -192,7 +205,7 @@ inline void plan_free(ppr_plan* p) {
   hipFree(p->d_rp); hipFree(p->d_colx); hipFree(p->d_part); hipFree(p->d_ids); hipFree(p->d_sc); hipFree(p->d_rix); hipFree(p->d_rmin);
   hipFree(p->d_len); hipFree(p->d_all); hipFree(p->d_act[0]); hipFree(p->d_act[1]);
   hipFree(p->d_cand); hipFree(p->d_tier_lists); hipFree(p->d_tier_cnt); hipFree(p->d_tier_cap); hipFree(p->d_big);
-  hipFree(p->d_ovf); hipFree(p->d_gath);
+  hipFree(p->d_ovf); hipFree(p->d_gath); hipFree(p->d_dlast); hipFree(p->d_xs);
   hipFree(p->d_maxdiff); hipFree(p->d_stats); hipFree(p->d_work); hipFree(p->d_scratch);
   hipFree(p->d_out_ids); hipFree(p->d_out_sc); hipFree(p->d_out_len);
   if (p->ev_a) hipEventDestroy(p->ev_a);
@@ -218,6 +231,9 @@ inline void plan_free(ppr_plan* p) {
   hipFree(p->d_xsend); hipFree(p->d_xrecv); hipFree(p->d_xsz); hipFree(p->d_xtmp);
   if (p->h_hub_pin) hipHostFree(p->h_hub_pin);
   if (p->h_desc_pin) hipHostFree(p->h_desc_pin);
+  if (p->h_xs_pin) hipHostFree(p->h_xs_pin);
+  if (getenv("PPR_TIMING") && p->xr_redo)
+    fprintf(stderr, "ppr_timing xr_redo_sources %lld\n", (long long)p->xr_redo);
   if (getenv("PPR_TIMING") && p->spec_redo)
     fprintf(stderr, "ppr_timing spec_redo_sources %lld\n", (long long)p->spec_redo);
   if (getenv("PPR_TIMING") && p->host_plan_calls)

@@ -160,6 +160,7 @@ struct IterArgs {
                              // should not evict the scatter's partially written staging lines from L2)
   uint32_t whatif;           // PPR_WHATIF bits that act inside kernels (timing experiments, plan.h;
                              // bits 0-15 as set by the user, WI_* below set per launch by the host)
+  uint32_t xs;               // exact-sum GRank merge (merge_xs.h), never in the MC combine
   int iter;                  // GRank iteration (diagnostics)
   double spec;               // speculative pruning ratio (PPR_SPEC; 0 = off): spec_tau below
 };

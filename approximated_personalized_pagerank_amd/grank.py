@@ -65,8 +65,17 @@ def _stats_to(res: GrankResult, st: _lib.PprStats) -> None:
     res.algo_bytes = int(st.algo_bytes)
 
 
+def _flags(stats: bool, sum_mode: Optional[str]) -> int:
+    """sum_mode: None = the library default (exact, or PPR_SUM), "exact", or "chain" (the
+    reference's in-order fma sums, include/grank.h:107-116)"""
+    if sum_mode not in (None, "exact", "chain"):
+        raise ValueError(f"sum_mode must be 'exact' or 'chain', not {sum_mode!r}")
+    return (_lib.PPR_FLAG_STATS if stats else 0) | (_lib.PPR_FLAG_CHAIN_SUM if sum_mode == "chain" else 0)
+
+
 def grank_csr(csr: Csr, K: int, L: int, iterations: int, damping: float, tolerance: float,
-              part: Optional[np.ndarray] = None, device: int = -1, stats: bool = False) -> GrankResult:
+              part: Optional[np.ndarray] = None, device: int = -1, stats: bool = False,
+              sum_mode: Optional[str] = None) -> GrankResult:
     """GRank over a dense CSR graph on one MI355X (synchronous)."""
     _check_params(K, L, iterations, damping)
     n = csr.n
@@ -78,7 +87,7 @@ def grank_csr(csr: Csr, K: int, L: int, iterations: int, damping: float, toleran
         return res
     p = csr.partitions() if part is None else np.ascontiguousarray(part, dtype=np.uint8)
     c = _lib.csr_struct(csr.row_ptr, csr.col)
-    o = _lib.PprOpts(device, _lib.PPR_FLAG_STATS if stats else 0, None)
+    o = _lib.PprOpts(device, _flags(stats, sum_mode), None)
     st = _lib.PprStats()
     rc = _lib.lib().ppr_grank_csr(ctypes.byref(c), _lib.ptr(p), K, L, iterations, damping, tolerance,
                                   ctypes.byref(o), _lib.ptr(ids), _lib.ptr(sc), _lib.ptr(lens),
@@ -110,14 +119,15 @@ class GrankPlan:
     """Device-resident GRank plan (inputs uploaded once; run() is the device phase only)."""
 
     def __init__(self, csr: Csr, K: int, L: int, damping: float, part: Optional[np.ndarray] = None,
-                 device: int = -1, stream: Optional[int] = None, stats: bool = False):
+                 device: int = -1, stream: Optional[int] = None, stats: bool = False,
+                 sum_mode: Optional[str] = None):
         _check_params(K, L, 1, damping)
         self.csr, self.K, self.L = csr, K, L
         self._p = ctypes.c_void_p()
         p = csr.partitions() if part is None else np.ascontiguousarray(part, dtype=np.uint8)
         self.part = p
         c = _lib.csr_struct(csr.row_ptr, csr.col)
-        o = _lib.PprOpts(device, _lib.PPR_FLAG_STATS if stats else 0, stream)
+        o = _lib.PprOpts(device, _flags(stats, sum_mode), stream)
         _lib.check(_lib.lib().ppr_grank_plan_create(ctypes.byref(c), _lib.ptr(p), K, L, damping,
                                                     ctypes.byref(o), ctypes.byref(self._p)), "plan_create")
         self.iterations_run = 0

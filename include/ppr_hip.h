@@ -55,7 +55,12 @@ typedef struct ppr_opts {
 } ppr_opts;
 
 enum {
-  PPR_FLAG_STATS = 1       /* collect candidate counts / algorithmic bytes per iteration */
+  PPR_FLAG_STATS = 1,      /* collect candidate counts / algorithmic bytes per iteration */
+  PPR_FLAG_CHAIN_SUM = 2   /* GRank: sum each key's contributions with the reference's in-order fma
+                              chain (include/grank.h:107-116; bit-identical to it where no top-L tie
+                              is cut). Default: the exact sum -- every contribution fl(s * d/deg)
+                              added exactly, rounded once (order-free). The
+                              environment variable PPR_SUM=chain|exact overrides the default. */
 };
 
 #define PPR_MAX_ITER_STATS 256

@@ -33,6 +33,15 @@
  *   stop rule    include/grank.h:90-94,140   maxDiff[2] = {tol, tol}; loop while
  *                                             i < iterations && max(maxDiff) >= tol
  *   final top-K  include/grank.h:143-147      keepTop(K) of each row by the same rule (row_topk)
+ *
+ * Summation mode (oracle_set_sum; the HIP plan's PPR_FLAG_CHAIN_SUM):
+ *   chain  the reference's own order: acc[k] = fma(s, d/deg, acc[k]) per key in successor order
+ *          (include/grank.h:107-116 under -O3 -march=native)
+ *   exact  (default) every contribution p = fl(s * d/deg) is added EXACTLY into a 128-bit fixed-point
+ *          accumulator X[k] += floor(p * 2^93) (the seed 1-d likewise), and the basket value is
+ *          X[k] * 2^-93 rounded to nearest once: order-free (the GPU sums in any order) and at least
+ *          as accurate as the chain (each key's sum is correctly rounded from the rounded products;
+ *          the 2^-93 truncation is ~1e-28 absolute per term)
  */
 #include <math.h>
 #include <stdint.h>
@@ -66,11 +75,49 @@ static int cmp_sel(const void* a, const void* b) {
   return (x->tie < y->tie) ? -1 : (x->tie > y->tie);
 }
 
+/* ---- summation mode ---- */
+static int g_sum_exact = 1;
+void oracle_set_sum(int exact) { g_sum_exact = exact ? 1 : 0; }
+int oracle_get_sum(void) { return g_sum_exact; }
+
+#define XS_F 93 /* fixed-point fraction bits (approximated_personalized_pagerank_amd/csrc/merge_xs.h) */
+typedef unsigned __int128 xs_t;
+
+/* floor(p * 2^93) of a double p >= 0 (p < 4 in GRank: every basket sums to <= 1) */
+static xs_t xs_conv(double p) {
+  uint64_t b;
+  memcpy(&b, &p, 8);
+  int e = (int)((b >> 52) & 0x7ff);
+  uint64_t m = b & ((1ull << 52) - 1);
+  if (e) m |= 1ull << 52; else e = 1;
+  const int sh = e - 1075 + XS_F;
+  if (sh >= 0) return (xs_t)m << sh;
+  if (-sh >= 64) return 0;
+  return (xs_t)(m >> -sh);
+}
+
+/* X * 2^-93 rounded to nearest even (X < 2^95): the top 64 bits with a sticky bit, one correctly
+ * rounded u64 -> double conversion, an exact power-of-two scale */
+double oracle_xs_to_double(uint64_t hi, uint64_t lo) {
+  if (hi == 0) return ldexp((double)lo, -XS_F);
+  const int n = 64 - __builtin_clzll(hi);
+  const uint64_t top = (hi << (64 - n)) | (lo >> n);
+  const uint64_t sticky = (lo & ((1ull << n) - 1)) != 0;
+  return ldexp((double)(top | sticky), n - XS_F);
+}
+static double xs_to_double(xs_t x) { return oracle_xs_to_double((uint64_t)(x >> 64), (uint64_t)x); }
+void oracle_xs_conv(double p, uint64_t* hi, uint64_t* lo) {
+  const xs_t x = xs_conv(p);
+  *hi = (uint64_t)(x >> 64);
+  *lo = (uint64_t)x;
+}
+
 /* ---- open-addressing accumulator (keys unique, insertion-order independent) ---- */
 typedef struct {
   int64_t cap;
   int32_t* keys;
   double* acc;
+  xs_t* x;        /* exact mode: fixed-point sums */
   int64_t used;
   int64_t* slots; /* occupied slot list, for cheap reset */
 } acc_t;
@@ -84,10 +131,11 @@ static void acc_init(acc_t* a, int64_t need) {
   int64_t cap = 16;
   while (cap < 2 * need + 2) cap <<= 1;
   if (cap > a->cap) {
-    free(a->keys); free(a->acc); free(a->slots);
+    free(a->keys); free(a->acc); free(a->x); free(a->slots);
     a->cap = cap;
     a->keys = (int32_t*)malloc(sizeof(int32_t) * cap);
     a->acc = (double*)malloc(sizeof(double) * cap);
+    a->x = (xs_t*)malloc(sizeof(xs_t) * cap);
     a->slots = (int64_t*)malloc(sizeof(int64_t) * cap);
     for (int64_t i = 0; i < cap; i++) a->keys[i] = -1;
     a->used = 0;
@@ -99,26 +147,50 @@ static void acc_reset(acc_t* a) {
   a->used = 0;
 }
 
-static double* acc_find(acc_t* a, int32_t key) {
+static int64_t acc_slot(acc_t* a, int32_t key) {
   uint64_t mask = (uint64_t)a->cap - 1;
   uint64_t h = mix32((uint32_t)key) & mask;
   for (;;) {
-    if (a->keys[h] == key) return &a->acc[h];
+    if (a->keys[h] == key) return (int64_t)h;
     if (a->keys[h] == -1) {
       a->keys[h] = key;
       a->acc[h] = 0.0;
+      a->x[h] = 0;
       a->slots[a->used++] = (int64_t)h;
-      return &a->acc[h];
+      return (int64_t)h;
     }
     h = (h + 1) & mask;
   }
 }
 
-static void acc_free(acc_t* a) { free(a->keys); free(a->acc); free(a->slots); memset(a, 0, sizeof(*a)); }
+/* the source's seed entry {v: val} (include/grank.h:103-104) */
+static void acc_seed(acc_t* a, int32_t key, double val) {
+  const int64_t h = acc_slot(a, key);
+  if (g_sum_exact) a->x[h] = xs_conv(val); else a->acc[h] = val;
+}
+/* one contribution s of a successor basket to key: acc = fma(s, f, acc) (include/grank.h:114-115),
+ * or exactly X += floor(fl(s * f) * 2^93) */
+static void acc_add(acc_t* a, int32_t key, double s, double f) {
+  const int64_t h = acc_slot(a, key);
+  if (g_sum_exact) a->x[h] += xs_conv(s * f); else a->acc[h] = fma(s, f, a->acc[h]);
+}
+/* init (include/grank.h:73-75): B[v][s] += d/deg, i.e. a contribution 1.0 * f */
+static void acc_add_unit(acc_t* a, int32_t key, double f) {
+  const int64_t h = acc_slot(a, key);
+  if (g_sum_exact) a->x[h] += xs_conv(f); else a->acc[h] = a->acc[h] + f;
+}
+/* exact mode: the basket values from the fixed-point sums (once per merge, before keepTop) */
+static void acc_settle(acc_t* a) {
+  if (!g_sum_exact) return;
+  for (int64_t i = 0; i < a->used; i++) a->acc[a->slots[i]] = xs_to_double(a->x[a->slots[i]]);
+}
+
+static void acc_free(acc_t* a) { free(a->keys); free(a->acc); free(a->x); free(a->slots); memset(a, 0, sizeof(*a)); }
 
 /* keepTop(L) of source v's accumulator: the first L by the selection order, stored by the output
  * order; returns len */
 static int32_t acc_top(acc_t* a, int32_t v, int32_t L, ent_t** buf, int64_t* bufcap, int32_t* ids, double* sc) {
+  acc_settle(a);
   if (a->used > *bufcap) { free(*buf); *bufcap = a->used; *buf = (ent_t*)malloc(sizeof(ent_t) * (*bufcap)); }
   ent_t* e = *buf;
   for (int64_t i = 0; i < a->used; i++) {
@@ -258,11 +330,8 @@ int oracle_grank(int64_t n, const int64_t* rp, const int32_t* col, const uint8_t
     int64_t deg = rp[v + 1] - rp[v];
     double factor = damping / (double)deg;
     acc_init(&a, deg + 1);
-    *acc_find(&a, (int32_t)v) = self;
-    for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
-      double* p = acc_find(&a, col[e]);
-      *p = *p + factor;
-    }
+    acc_seed(&a, (int32_t)v, self);
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) acc_add_unit(&a, col[e], factor);
     cl[v] = acc_top(&a, (int32_t)v, L, &buf, &bufcap, ci + v * L, cs + v * L);
     acc_reset(&a);
   }
@@ -279,15 +348,12 @@ int oracle_grank(int64_t n, const int64_t* rp, const int32_t* col, const uint8_t
       int64_t cand = 1;
       for (int64_t e = rp[v]; e < rp[v + 1]; e++) cand += cl[col[e]];
       acc_init(&a, cand);
-      *acc_find(&a, (int32_t)v) = self;
+      acc_seed(&a, (int32_t)v, self);
       for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
         int32_t u = col[e];
         const int32_t* ui = ci + (int64_t)u * L;
         const double* us = cs + (int64_t)u * L;
-        for (int32_t j = 0; j < cl[u]; j++) {
-          double* p = acc_find(&a, ui[j]);
-          *p = fma(us[j], factor, *p);
-        }
+        for (int32_t j = 0; j < cl[u]; j++) acc_add(&a, ui[j], us[j], factor);
       }
       nl[v] = acc_top(&a, (int32_t)v, L, &buf, &bufcap, ni + v * L, ns + v * L);
       acc_reset(&a);
@@ -325,8 +391,8 @@ int oracle_init_state(int64_t n, const int64_t* rp, const int32_t* col, int32_t 
     int64_t deg = rp[v + 1] - rp[v];
     double factor = damping / (double)deg;
     acc_init(&a, deg + 1);
-    *acc_find(&a, (int32_t)v) = 1.0 - damping;
-    for (int64_t e = rp[v]; e < rp[v + 1]; e++) { double* p = acc_find(&a, col[e]); *p = *p + factor; }
+    acc_seed(&a, (int32_t)v, 1.0 - damping);
+    for (int64_t e = rp[v]; e < rp[v + 1]; e++) acc_add_unit(&a, col[e], factor);
     len[v] = acc_top(&a, (int32_t)v, L, &buf, &bufcap, ids + v * L, sc + v * L);
     acc_reset(&a);
   }
@@ -348,13 +414,10 @@ int oracle_step(int64_t n, const int64_t* rp, const int32_t* col, int32_t L, dou
     int64_t cand = 1;
     for (int64_t e = rp[v]; e < rp[v + 1]; e++) cand += len[col[e]];
     acc_init(&a, cand);
-    *acc_find(&a, v) = 1.0 - damping;
+    acc_seed(&a, v, 1.0 - damping);
     for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
       int32_t u = col[e];
-      for (int32_t j = 0; j < len[u]; j++) {
-        double* p = acc_find(&a, ids[(int64_t)u * L + j]);
-        *p = fma(sc[(int64_t)u * L + j], factor, *p);
-      }
+      for (int32_t j = 0; j < len[u]; j++) acc_add(&a, ids[(int64_t)u * L + j], sc[(int64_t)u * L + j], factor);
     }
     nlen[v] = acc_top(&a, v, L, &buf, &bufcap, nids + (int64_t)v * L, nsc + (int64_t)v * L);
     acc_reset(&a);
@@ -382,13 +445,10 @@ int oracle_step_rows(const int64_t* rp, const int32_t* col, int32_t L, double da
     int64_t cand = 1;
     for (int64_t e = rp[v]; e < rp[v + 1]; e++) cand += len[col[e]];
     acc_init(&a, cand);
-    *acc_find(&a, v) = 1.0 - damping;
+    acc_seed(&a, v, 1.0 - damping);
     for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
       int32_t u = col[e];
-      for (int32_t j = 0; j < len[u]; j++) {
-        double* p = acc_find(&a, ids[(int64_t)u * L + j]);
-        *p = fma(sc[(int64_t)u * L + j], factor, *p);
-      }
+      for (int32_t j = 0; j < len[u]; j++) acc_add(&a, ids[(int64_t)u * L + j], sc[(int64_t)u * L + j], factor);
     }
     nlen[v] = acc_top(&a, v, L, &buf, &bufcap, nids + (int64_t)v * L, nsc + (int64_t)v * L);
     acc_reset(&a);

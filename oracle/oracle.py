@@ -61,12 +61,60 @@ def lib():
         L.oracle_topk_rows.restype = ctypes.c_int
         L.oracle_tie_key.argtypes = [ctypes.c_int32, ctypes.c_int32]
         L.oracle_tie_key.restype = ctypes.c_uint32
+        L.oracle_set_sum.argtypes = [ctypes.c_int]
+        L.oracle_set_sum.restype = None
+        L.oracle_get_sum.argtypes = []
+        L.oracle_get_sum.restype = ctypes.c_int
+        L.oracle_xs_to_double.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_xs_to_double.restype = ctypes.c_double
+        L.oracle_xs_conv.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_xs_conv.restype = None
         _lib = L
     return _lib
 
 
 def _p(a):
     return None if a is None else a.ctypes.data
+
+
+SUM_MODES = ("exact", "chain")
+
+
+def set_sum(mode: str) -> None:
+    """GRank summation mode of every later oracle call (grank_oracle.c header): "exact" (default,
+    the HIP plan's default) or "chain" (the reference's fma order, PPR_FLAG_CHAIN_SUM)."""
+    assert mode in SUM_MODES, mode
+    lib().oracle_set_sum(1 if mode == "exact" else 0)
+
+
+def get_sum() -> str:
+    return "exact" if lib().oracle_get_sum() else "chain"
+
+
+class sum_mode:
+    """with oracle.sum_mode("chain"): ... -- the mode for the block, restored after"""
+
+    def __init__(self, mode: str):
+        self.mode, self.prev = mode, None
+
+    def __enter__(self):
+        self.prev = get_sum()
+        set_sum(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        set_sum(self.prev)
+
+
+def xs_conv(p: float):
+    """floor(p * 2^93) as (hi, lo) 64-bit words"""
+    hi, lo = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    lib().oracle_xs_conv(p, ctypes.byref(hi), ctypes.byref(lo))
+    return hi.value, lo.value
+
+
+def xs_to_double(hi: int, lo: int) -> float:
+    return lib().oracle_xs_to_double(hi, lo)
 
 
 def find_partitions(row_ptr: np.ndarray, col: np.ndarray) -> np.ndarray:

@@ -21,3 +21,24 @@ def _built():
     build.build()
     import oracle
     oracle.build()
+
+
+@pytest.fixture
+def chain_sum(monkeypatch):
+    """The reference's summation order for this test: the HIP plan (PPR_SUM=chain, read at plan
+    creation) and the oracle (oracle.set_sum) both sum each key's contributions with the in-order
+    fma chain of include/grank.h:107-116 -- the mode bit-exact against the compiled reference."""
+    import oracle
+    monkeypatch.setenv("PPR_SUM", "chain")
+    with oracle.sum_mode("chain"):
+        yield
+
+
+@pytest.fixture(params=["exact", "chain"])
+def sum_mode(request, monkeypatch):
+    """Both GRank summation modes (the default exact sum, the reference's fma chain), the HIP plan
+    and the oracle in the same one."""
+    import oracle
+    monkeypatch.setenv("PPR_SUM", request.param)
+    with oracle.sum_mode(request.param):
+        yield request.param

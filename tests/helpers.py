@@ -61,3 +61,29 @@ def tie_aware_recall(ai, asc, al, bi, bsc, bl, tol=1e-12):
             j = np.searchsorted(sa, s - tol)
             hit += j < len(sa) and abs(sa[j] - s) <= tol * max(1.0, abs(s))
     return hit / max(tot, 1)
+
+
+# exact-sum mode vs the reference's fma chain: every score agrees to this relative tolerance
+# (the exact sum of the rounded products, rounded once, against a chain that rounds
+# after every add -- a few ulps apart; 1e-12 leaves a wide margin)
+XSUM_RTOL = 1e-12
+
+
+def rows_close(ai, asc, al, bi, bsc, bl, rtol=XSUM_RTOL):
+    """row by row: same lengths, every key present in both with scores within rtol, and a key in
+    only one row only where its score is within rtol of that row's K-th (a near-tie at the cut
+    that the two summation orders may break differently). Returns the number of such swaps."""
+    swaps = 0
+    assert np.array_equal(al, bl)
+    for v in range(len(al)):
+        n = int(al[v])
+        a = dict(zip(ai[v, :n].tolist(), asc[v, :n].tolist()))
+        b = dict(zip(bi[v, :n].tolist(), bsc[v, :n].tolist()))
+        for k in a.keys() & b.keys():
+            assert abs(a[k] - b[k]) <= rtol * abs(b[k]), (v, k, a[k], b[k])
+        for side, other in ((a, b), (b, a)):
+            for k in side.keys() - other.keys():
+                lo = min(other.values())
+                assert abs(side[k] - lo) <= rtol * abs(lo), (v, k, side[k], lo)
+                swaps += 1
+    return swaps

@@ -26,7 +26,7 @@ from helpers import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-C3_DIGEST = os.path.join(GOLDEN, "c3_rmat22_k64_l128_i30.json")
+C3_DIGESTS = sorted(f for f in os.listdir(GOLDEN) if f.startswith("c3_rmat22_k64_l128_i30") and f.endswith(".json"))
 
 
 def progress(msg):
@@ -41,11 +41,11 @@ def _dig(*arrays):
     return h.hexdigest()
 
 
-@pytest.mark.skipif(not os.path.exists(C3_DIGEST), reason="C3 oracle digest not generated")
-def test_gpu_c4_rmat22_eight_ranks_equal_oracle(monkeypatch):
+@pytest.mark.parametrize("digest", C3_DIGESTS)
+def test_gpu_c4_rmat22_eight_ranks_equal_oracle(digest, monkeypatch):
     from approximated_personalized_pagerank_amd.shard import run_local_group
     monkeypatch.setenv("PPR_HUB_BUDGET", str(1 << 27))
-    with open(C3_DIGEST) as f:
+    with open(os.path.join(GOLDEN, digest)) as f:
         ref = json.load(f)
     world = 8
     t0 = time.time()
@@ -53,7 +53,8 @@ def test_gpu_c4_rmat22_eight_ranks_equal_oracle(monkeypatch):
     part = g.partitions()
     assert (g.n, g.m, _dig(g.col)) == (ref["n"], ref["m"], ref["graph_sha256"])
     K, L, d = ref["K"], ref["L"], ref["damping"]
-    plans = [ppr.GrankPlan(g, K, L, d, part=part, device=0, stats=True) for _ in range(world)]
+    plans = [ppr.GrankPlan(g, K, L, d, part=part, device=0, stats=True, sum_mode=ref.get("sum", "chain"))
+             for _ in range(world)]
     progress(f"graph + {world} plans {time.time() - t0:.1f} s")
     t1 = time.time()
     st = run_local_group(plans, ref["iters"], ref["tol"])

@@ -1,9 +1,11 @@
 """GPU parity: the HIP path (through the C ABI) against the oracle and the reference fixtures.
 
 Contract (DESIGN.md "parity contract"):
-  P1  bit-exact vs the oracle on every config (same fma order, same (score desc, id asc) ties,
-      same norm1 summation pattern -> same iteration count)
-  P2  bit-exact vs the compiled reference where it never cuts a basket at a tie
+  P1  bit-exact vs the oracle on every config, in both summation modes (the default exact sum and
+      the reference's fma chain: same sums, same (score desc, id asc) ties, same norm1 summation
+      pattern -> same iteration count)
+  P2  chain mode: bit-exact vs the compiled reference where it never cuts a basket at a tie;
+      exact mode: the same runs within helpers.XSUM_RTOL
   P3/P4 top-K Jaccard vs the reference on truncating runs (thresholds in helpers.STAT)
 """
 import numpy as np
@@ -11,7 +13,7 @@ import pytest
 
 import approximated_personalized_pagerank_amd as ppr
 import oracle
-from helpers import EXACT, STAT, jaccard_rows, load, ref_rows
+from helpers import EXACT, STAT, jaccard_rows, load, ref_rows, rows_close
 
 pytestmark = pytest.mark.gpu
 
@@ -22,7 +24,7 @@ def run_gpu(f, **kw):
 
 
 @pytest.mark.parametrize("name", EXACT)
-def test_gpu_bit_exact_vs_reference(name):
+def test_gpu_bit_exact_vs_reference(name, chain_sum):
     f = load(name)
     r = run_gpu(f)
     ids, sc, cnt, _ = ref_rows(f)
@@ -31,8 +33,18 @@ def test_gpu_bit_exact_vs_reference(name):
     assert np.array_equal(r.scores, sc)
 
 
+@pytest.mark.parametrize("name", EXACT)
+def test_gpu_exact_sum_vs_reference_within_tolerance(name):
+    f = load(name)
+    r = run_gpu(f)
+    o = oracle.grank(f["rp"], f["col"], f["part"], f["K"], f["L"], f["iters"], f["damping"], f["tol"])
+    assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])
+    ids, sc, cnt, _ = ref_rows(f)
+    rows_close(r.ids, r.scores, r.lens, ids, sc, cnt)
+
+
 @pytest.mark.parametrize("name", sorted(STAT))
-def test_gpu_vs_oracle_and_reference(name):
+def test_gpu_vs_oracle_and_reference(name, sum_mode):
     f = load(name)
     r = run_gpu(f)
     o = oracle.grank(f["rp"], f["col"], f["part"], f["K"], f["L"], f["iters"], f["damping"], f["tol"])
@@ -48,7 +60,7 @@ def test_gpu_vs_oracle_and_reference(name):
 @pytest.mark.parametrize("scale,K,L,it,tol", [(9, 8, 16, 6, -1.0), (10, 16, 32, 8, -1.0),
                                              (11, 32, 64, 10, 1e-4), (12, 64, 128, 7, -1.0),
                                              (10, 5, 100, 9, 1e-3), (8, 3, 700, 5, -1.0)])
-def test_gpu_bit_exact_vs_oracle_rmat(scale, K, L, it, tol):
+def test_gpu_bit_exact_vs_oracle_rmat(scale, K, L, it, tol, sum_mode):
     g = ppr.rmat(scale, seed=scale * 31 + K)
     part = g.partitions()
     r = ppr.grank_csr(g, K, L, it, 0.85, tol, part=part, device=0)
@@ -60,7 +72,7 @@ def test_gpu_bit_exact_vs_oracle_rmat(scale, K, L, it, tol):
     assert np.array_equal(r.scores, o["scores"])
 
 
-def test_gpu_full_slab_vs_oracle():
+def test_gpu_full_slab_vs_oracle(sum_mode):
     g = ppr.rmat(11, seed=3)
     part = g.partitions()
     K, L, it = 16, 48, 7
@@ -100,7 +112,7 @@ def test_gpu_deterministic_and_multi_equal():
     assert m1 == m2
 
 
-def test_gpu_hub_reduce_and_classify_big_bit_exact(monkeypatch):
+def test_gpu_hub_reduce_and_classify_big_bit_exact(monkeypatch, chain_sum):
     """long appended hub lists cut by k_hub_reduce (slice forced small) and long successor lists
     summed by k_classify_big (RMAT-14 hubs exceed 512 successors) match the oracle"""
     monkeypatch.setenv("PPR_HUB_SLICE", "64")
@@ -116,7 +128,7 @@ def test_gpu_hub_reduce_and_classify_big_bit_exact(monkeypatch):
 
 
 @pytest.mark.parametrize("mask", ["0x10", "0x0", "0x11", "0x3", "0x20", "0x21", "0x30"])
-def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
+def test_gpu_tier_paths_bit_exact(mask, monkeypatch, sum_mode):
     """every merge path alone (wave tiers 0x1-0x8, workgroup tier 0x10, hub pipeline 0x20, HBM-table
     path 0x0) and mixes of them match the oracle bit for bit"""
     monkeypatch.setenv("PPR_TIER_MASK", mask)
@@ -166,7 +178,7 @@ def test_gpu_tier_paths_bit_exact(mask, monkeypatch):
     {"PPR_HOT_N": "64", "PPR_HOT_AT": "0", "PPR_HOT_MAX": "3000"},          # large hubs without a hot pass
                                                                             # (tagged ids decoded in the partition)
 ])
-def test_gpu_hub_bucket_variants_bit_exact(seg_env, monkeypatch):
+def test_gpu_hub_bucket_variants_bit_exact(seg_env, monkeypatch, chain_sum):
     """every hub bucket engine -- staged buckets on one wave each (k_hub_bucket_w), spills to the
     workgroup kernel (k_hub_bucket), hash-range segments of the successor rows (k_hub_seg) --
     matches the oracle bit for bit, alone (hub tier only, 0x20) and mixed with the wave tiers"""
@@ -184,7 +196,7 @@ def test_gpu_hub_bucket_variants_bit_exact(seg_env, monkeypatch):
         assert np.array_equal(r.scores, o["scores"])
 
 
-def test_gpu_tolerance_stop_beyond_256_iterations():
+def test_gpu_tolerance_stop_beyond_256_iterations(sum_mode):
     """iterations >= PPR_MAX_ITER_STATS share one maxDiff slot, zeroed per iteration: a tolerance
     that is first met after iteration 256 stops the run where the oracle stops
     (include/grank.h:90-94,140)"""
@@ -209,7 +221,7 @@ def test_gpu_tolerance_stop_beyond_256_iterations():
     ({"PPR_SPEC": "0.9", "PPR_SPEC_FROM": "2", "PPR_HUB_BUDGET": "4096"}, False),  # failures across many batches
     ({"PPR_SPEC": "0.0"}, False),                                              # off: the rigorous bound only
 ])
-def test_gpu_speculative_bound_bit_exact(env, want_redo, monkeypatch, capfd):
+def test_gpu_speculative_bound_bit_exact(env, want_redo, monkeypatch, capfd, chain_sum):
     """speculative hub pruning bound (spec x the source's previous L-th score): bucket waves emit
     only keys reaching it, k_hub_final proves it (L selected entries at or above it) or the source
     is merged again with the rigorous bound -- the result never changes (include/grank.h:96-137)"""
@@ -231,3 +243,60 @@ def test_gpu_speculative_bound_bit_exact(env, want_redo, monkeypatch, capfd):
     redo = sum(int(x.split()[2]) for x in err.splitlines() if x.startswith("ppr_timing spec_redo_sources"))
     if want_redo:
         assert redo > 0
+
+
+@pytest.mark.parametrize("xenv", [
+    {},                                                           # defaults
+    {"PPR_XR_RMAX": "1"},                                         # every multi-table source partitioned
+    {"PPR_XR_RMAX": "64", "PPR_XR_FILL": "20"},                   # many key ranges per source
+    {"PPR_XR_T": "1024", "PPR_XR_W": "4", "PPR_XR_FILL": "20"},   # small tables: more ranges / buckets
+    {"PPR_XR_DSCALE": "5"},                                       # estimates 20x too low: table overflows,
+                                                                  # sources redone with larger estimates
+    {"PPR_XR_DSCALE": "5", "PPR_XR_RMAX": "1"},                   # ... in the bucket workgroups
+    {"PPR_XR_RMAX": "1", "PPR_HUB_BUDGET": "4096"},               # many partition batches, three regions
+    {"PPR_XR_RMAX": "1", "PPR_HUB_BUDGET": "4096", "PPR_HUB_STREAMS": "1"},  # ... on one stream
+    {"PPR_XR_RMAX": "1", "PPR_XR_FILL": "20", "PPR_HUB_MIX": "0"},  # many buckets, list order
+    {"PPR_TIER_MASK": "0x0"},                                     # no wave tier: every source in workgroups
+    {"PPR_TIER_MASK": "0xf"},                                     # no partition: ranges only
+    {"PPR_WAVE_WPB": "4"},                                        # 4-wave blocks in the wave tier
+])
+def test_gpu_exact_sum_paths_bit_exact(xenv, monkeypatch):
+    """the exact-sum engines (merge_xs.h: wave tier, range workgroups, bucket workgroups, list
+    finals, the overflow redo) match the oracle's exact mode bit for bit, alone and mixed"""
+    for k, v in xenv.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("PPR_TIMING", "1")
+    for mask, (scale, K, L, it) in [(None, (10, 16, 32, 5)), ("0x21", (11, 8, 64, 4)), ("0x20", (12, 8, 128, 3)),
+                                    (None, (13, 32, 128, 4))]:
+        if mask and "PPR_TIER_MASK" not in xenv:
+            monkeypatch.setenv("PPR_TIER_MASK", mask)
+        elif "PPR_TIER_MASK" not in xenv:
+            monkeypatch.delenv("PPR_TIER_MASK", raising=False)
+        g = ppr.rmat(scale, seed=91 + scale)
+        part = g.partitions()
+        r = ppr.grank_csr(g, K, L, it, 0.85, -1.0, part=part, device=0)
+        o = oracle.grank(g.row_ptr, g.col, part, K, L, it, 0.85, -1.0)
+        assert np.array_equal(r.max_diff, o["max_diff"])
+        assert np.array_equal(r.lens, o["lens"])
+        assert np.array_equal(r.ids, o["ids"])
+        assert np.array_equal(r.scores, o["scores"])
+
+
+def test_gpu_exact_sum_init_hubs_and_damping():
+    """init of sources with more successors than the wave tiers take (range workgroups in unit
+    mode), damping at the ends of [0, 1]"""
+    g = ppr.rmat(12, seed=4)
+    part = g.partitions()
+    for d in (0.0, 0.5, 1.0):
+        r = ppr.grank_csr(g, 8, 16, 2, d, -1.0, part=part, device=0)
+        o = oracle.grank(g.row_ptr, g.col, part, 8, 16, 2, d, -1.0)
+        assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])
+    # a star with a hub of 3000 successors: its init basket needs more than the largest wave table
+    n = 3001
+    d = {0: list(range(1, n))}
+    d.update({i: [0] for i in range(1, n)})
+    csr = ppr.Csr.from_dict(d)
+    part = csr.partitions()
+    r = ppr.grank_csr(csr, 16, 64, 4, 0.85, -1.0, part=part, device=0)
+    o = oracle.grank(csr.row_ptr, csr.col, part, 16, 64, 4, 0.85, -1.0)
+    assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])

@@ -46,15 +46,21 @@ def sample_sources(cand, rng, top=20, per_class=300, bounds=(0, 1536, 16384, 262
     return np.unique(np.concatenate(pick))
 
 
-def test_gpu_c2_rmat18_whole_run_digest():
-    with open(os.path.join(GOLDEN, "c2_rmat18_k32_l64_i20.json")) as f:
+C2_DIGESTS = sorted(f for f in os.listdir(GOLDEN) if f.startswith("c2_rmat18_k32_l64_i20") and f.endswith(".json"))
+
+
+@pytest.mark.parametrize("digest", C2_DIGESTS)
+def test_gpu_c2_rmat18_whole_run_digest(digest):
+    """digests of the oracle's whole run in the summation mode they record ("sum": chain when absent)"""
+    with open(os.path.join(GOLDEN, digest)) as f:
         ref = json.load(f)
     g = ppr.rmat(ref["scale"], seed=ref["seed"])
     import hashlib
     dig = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()  # noqa: E731
     assert (g.n, g.m, dig(g.col)) == (ref["n"], ref["m"], ref["graph_sha256"])
     t = time.time()
-    r = ppr.grank_csr(g, ref["K"], ref["L"], ref["iters"], ref["damping"], ref["tol"], part=g.partitions(), device=0)
+    r = ppr.grank_csr(g, ref["K"], ref["L"], ref["iters"], ref["damping"], ref["tol"], part=g.partitions(), device=0,
+                      sum_mode=ref.get("sum", "chain"))
     progress(f"C2 RMAT-18 K32/L64/20 it: {time.time() - t:.2f} s incl. plan creation")
     assert r.iterations_run == ref["iterations_run"]
     assert [float(x).hex() for x in r.max_diff] == ref["max_diff"]
@@ -63,7 +69,7 @@ def test_gpu_c2_rmat18_whole_run_digest():
     assert dig(r.scores) == ref["scores_sha256"]
 
 
-C3_DIGEST = os.path.join(GOLDEN, "c3_rmat22_k64_l128_i30.json")
+C3_DIGESTS = sorted(f for f in os.listdir(GOLDEN) if f.startswith("c3_rmat22_k64_l128_i30") and f.endswith(".json"))
 
 
 def _dig(*arrays):
@@ -74,19 +80,19 @@ def _dig(*arrays):
     return h.hexdigest()
 
 
-@pytest.mark.skipif(not os.path.exists(C3_DIGEST), reason="C3 oracle digest not generated")
-def test_gpu_c3_rmat22_whole_run_vs_oracle_digest():
+@pytest.mark.parametrize("digest", C3_DIGESTS)
+def test_gpu_c3_rmat22_whole_run_vs_oracle_digest(digest):
     """the headline workload end to end, bit for bit against the CPU oracle: final rows, the
     whole slab after an early (1, partition 1) and a late partition-0 iteration (28), and every
     iteration's maxDiff (include/grank.h:96-147)"""
-    with open(C3_DIGEST) as f:
+    with open(os.path.join(GOLDEN, digest)) as f:
         ref = json.load(f)
     t0 = time.time()
     g = ppr.rmat(ref["scale"], seed=ref["seed"])
     part = g.partitions()
     assert (g.n, g.m, _dig(g.col), _dig(part)) == (ref["n"], ref["m"], ref["graph_sha256"], ref["part_sha256"])
     K, L, d = ref["K"], ref["L"], ref["damping"]
-    plan = ppr.GrankPlan(g, K, L, d, part=part, device=0)
+    plan = ppr.GrankPlan(g, K, L, d, part=part, device=0, sum_mode=ref.get("sum", "chain"))
     for it in (1, 28):  # state after iteration `it` = after it + 1 iterations
         plan.run(it + 1, -1.0)
         ids, sc, ln = plan.fetch_slab(it + 1)

@@ -33,7 +33,9 @@ def profile_drift(ai, asc, al, bi, bsc, bl):
 
 
 @pytest.mark.parametrize("it", [3, 8])
-def test_single_step_from_reference_state_differs_by_ties_only(it):
+def test_single_step_from_reference_state_differs_by_ties_only(it, chain_sum):
+    """(in the reference's summation order, PPR_FLAG_CHAIN_SUM; the default exact sum is a few ulps
+    from it, tests/test_oracle_golden.py test_oracle_exact_sum_within_tolerance)"""
     z = np.load(f"{GOLDEN}/r1_rmat12_l32.npz")
     rp, col, part = z["rp"], z["col"], z["part"]
     L = int(z["params"][1])

@@ -8,7 +8,8 @@ SHA-256 digests -- final rows, the full L-slab after every iteration, the maxDif
 the bit-exact targets of tests/test_gpu_scale.py (C3, one GPU) and tests/test_gpu_c4.py (C4, the
 source-sharded loop with 8 ranks).
 
-    python tools/make_c3_digest.py [--threads 8]  -> tests/golden/c3_rmat22_k64_l128_i30.json
+    python tools/make_c3_digest.py [--threads 8] [--sum exact|chain]
+        -> tests/golden/c3_rmat22_k64_l128_i30.json (chain), c3_rmat22_k64_l128_i30_exact.json (exact)
 """
 import argparse
 import hashlib
@@ -48,8 +49,13 @@ def main():
     ap.add_argument("--L", type=int, default=128)
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
-    ap.add_argument("--out", default=os.path.join(ROOT, "tests", "golden", "c3_rmat22_k64_l128_i30.json"))
+    ap.add_argument("--sum", choices=["exact", "chain"], default="chain", help="GRank summation mode (oracle.set_sum)")
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
+    oracle.set_sum(a.sum)
+    if a.out is None:
+        a.out = os.path.join(ROOT, "tests", "golden",
+                             "c3_rmat22_k64_l128_i30" + ("_exact" if a.sum == "exact" else "") + ".json")
     d, seed, tol = 0.85, 42, -1.0
     t0 = time.time()
     g = ppr.rmat(a.scale, seed=seed)
@@ -80,7 +86,7 @@ def main():
            "iterations_run": a.iters, "max_diff": [float(x).hex() for x in md],
            "ids_sha256": digest(out[0]), "scores_sha256": digest(out[1]), "lens_sha256": digest(out[2]),
            "slab_after_iteration_sha256": slabs,
-           "oracle_seconds": round(time.time() - t0, 1), "oracle_threads": a.threads}
+           "oracle_seconds": round(time.time() - t0, 1), "oracle_threads": a.threads, "sum": a.sum}
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
     print(a.out, res["oracle_seconds"], "s")

@@ -2,7 +2,8 @@
 CPU oracle (oracle/grank_oracle.c): C2 = RMAT-18 K32/L64/20 iterations (BASELINE.json configs[1]).
 The whole result is too large to commit; its SHA-256 digests are bit-exact targets.
 
-    python tools/make_scale_digests.py   -> tests/golden/c2_rmat18_k32_l64_i20.json
+    python tools/make_scale_digests.py [exact|chain]
+        -> tests/golden/c2_rmat18_k32_l64_i20.json (chain), c2_rmat18_k32_l64_i20_exact.json (exact)
 """
 import hashlib
 import json
@@ -25,6 +26,8 @@ def digest(a: np.ndarray) -> str:
 
 
 def main():
+    mode = sys.argv[1] if len(sys.argv) > 1 else "chain"
+    oracle.set_sum(mode)
     scale, K, L, it, d, tol, seed = 18, 32, 64, 20, 0.85, -1.0, 42
     g = ppr.rmat(scale, seed=seed)
     part = g.partitions()
@@ -36,8 +39,8 @@ def main():
            "iterations_run": int(o["iterations_run"]),
            "max_diff": [float(x).hex() for x in o["max_diff"]],
            "ids_sha256": digest(o["ids"]), "scores_sha256": digest(o["scores"]), "lens_sha256": digest(o["lens"]),
-           "oracle_seconds": round(time.time() - t, 1)}
-    path = os.path.join(ROOT, "tests", "golden", "c2_rmat18_k32_l64_i20.json")
+           "oracle_seconds": round(time.time() - t, 1), "sum": mode}
+    path = os.path.join(ROOT, "tests", "golden", "c2_rmat18_k32_l64_i20" + ("_exact" if mode == "exact" else "") + ".json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(path, out["oracle_seconds"], "s")
