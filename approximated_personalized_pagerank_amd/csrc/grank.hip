@@ -371,16 +371,16 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       p->seg_enabled = false;
       p->hub_range = 0;
       const char* e1 = getenv("PPR_XR_T");
-      const char* e2 = getenv("PPR_XR_W");
       const char* e3 = getenv("PPR_XR_RMAX");
       const char* e4 = getenv("PPR_XR_FILL");
       if (e1) p->xr_T = std::max(1024, std::min(8192, pow2_at_least(atoi(e1))));
-      if (e2) p->xr_W = std::max(4, std::min(16, atoi(e2)));
+      p->xr_W = p->xr_T / (8 * WAVE);  // every thread settles 8 table slots (merge_xs.h XR_SLOTS)
       if (e3) p->xr_rmax = std::max(1, std::min(64, atoi(e3)));
       if (e4) p->xr_fill = std::max(20, std::min(85, atoi(e4)));
       const char* e5 = getenv("PPR_XR_DSCALE");
       if (e5) p->xr_dscale = std::max(1, std::min(1000, atoi(e5)));
-      while (xr_lds_bytes(p->xr_T, p->xr_W, p->Lp) > 160 * 1024 && p->xr_T > 1024) p->xr_T /= 2;
+      while (xr_lds_bytes(p->xr_T, p->xr_T / (8 * WAVE), p->Lp) > 160 * 1024 && p->xr_T > 1024) p->xr_T /= 2;
+      p->xr_W = p->xr_T / (8 * WAVE);
       if (xr_lds_bytes(p->xr_T, p->xr_W, p->Lp) > 160 * 1024 || xf_lds_bytes(p->Lp, 64) > 160 * 1024) {
         plan_free(p);
         return PPR_ERR_RANGE;
@@ -1170,9 +1170,10 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
   const int64_t L = p->L;
   // workgroup table classes (slots, waves): 16 waves per CU in each
   struct Cls { int T, W; };
-  const Cls cls[3] = {{std::min(2048, p->xr_T), std::max(1, p->xr_W / 4)},
-                      {std::min(4096, p->xr_T), std::max(1, p->xr_W / 2)},
-                      {p->xr_T, p->xr_W}};
+  // (T / 512 waves: the epilogue settles XR_SLOTS = 8 slots per thread)
+  const Cls cls[3] = {{std::min(2048, p->xr_T), std::min(2048, p->xr_T) / 512},
+                      {std::min(4096, p->xr_T), std::min(4096, p->xr_T) / 512},
+                      {p->xr_T, p->xr_T / 512}};
   auto cap_of = [&](int T) { return (int64_t)T * p->xr_fill / 100; };
   std::vector<int32_t> rng;            // ranges per walked source (0: partitioned)
   std::vector<uint8_t> ci;             // table class of a walked source
@@ -1208,7 +1209,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       x.pt_off = pt;
       x.factor = p->damping / (double)deg[i];
       x.selfval = 1.0 - p->damping;
-      if (rng[i] > 1) pt += (int64_t)rng[i] * L;
+      pt += (int64_t)rng[i] * L;  // every range appends at most L entries (one range: the whole top-L)
       xd.push_back(x);
       for (int r = 0; r < rng[i]; r++) tasks[ci[i]].push_back(XTask{d, r});
     }
@@ -1273,14 +1274,19 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       const int T = cls[c].T, W = cls[c].W;
       const int budget = std::min(T * 85 / 100, T - W * WAVE - WAVE);
       hipLaunchKernelGGL(k_xr, dim3((unsigned)tasks[c].size()), dim3(64 * W), xr_lds_bytes(T, W, p->Lp), sw, g, s, a,
-                         d_xd, d_tk + tofs[c], T, budget, p->Lp, d_xt, d_pk, d_ps, d_pc, d_ds, p->d_dlast, d_of, d_ov,
-                         maxdiff, p->d_stats);
+                         d_xd, d_tk + tofs[c], T, budget, p->Lp, d_xt, d_pk, d_ps, d_pc, d_ds, d_of, d_ov);
       HIP_OK(hipGetLastError());
       p->merge_launches++;
     }
     if (nmulti) {
       hipLaunchKernelGGL(k_xfinal<XDesc>, dim3((unsigned)nmulti), dim3(256), xf_lds_bytes(p->Lp, p->xf_stage), sw, s, a,
                          d_xd, d_xt, d_pk, d_ps, d_pc, d_ds, d_of, p->d_dlast, p->Lp, p->xf_stage, maxdiff, p->d_stats);
+      HIP_OK(hipGetLastError());
+      p->merge_launches++;
+    }
+    if ((int64_t)nx > nmulti) {
+      hipLaunchKernelGGL(k_xfin1, dim3((unsigned)((int64_t)nx - nmulti)), dim3(64), xf1_lds_bytes(p->Lp), sw, s, a, d_xd,
+                         (int)nmulti, d_pk, d_ps, d_pc, d_ds, d_of, p->d_dlast, p->Lp, maxdiff, p->d_stats);
       HIP_OK(hipGetLastError());
       p->merge_launches++;
     }

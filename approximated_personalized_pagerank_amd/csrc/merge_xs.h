@@ -226,15 +226,21 @@ __device__ __forceinline__ XrLds xr_carve(unsigned char* smem, int T, int W, int
   return x;
 }
 
+// PPR_DIAG: cycles since the last lap into counter `slot` (thread 0 only)
+__device__ __forceinline__ void xr_lap(const IterArgs& a, int slot, long long& t) {
+  if (!a.diag || threadIdx.x != 0) return;
+  const long long now = (long long)clock64();
+  diag_add(a.diag, slot, (unsigned long long)(now - t));
+  t = now;
+}
+
 __device__ __forceinline__ void xr_clear(const XrLds& x, int T) {
   for (int i = threadIdx.x; i < T; i += blockDim.x) { x.t.kh[i] = 0ull; x.t.lo[i] = 0ull; }
   if (threadIdx.x < 64) x.w.misc[threadIdx.x] = 0;
 }
 
-// one accumulated contribution of the calling lane (valid lanes only), with the workgroup's
-// distinct-key budget: a group's new keys are counted by its wave's lowest lane; past the budget
-// the overflow flag stops every wave at its next group (at most W * 64 keys beyond the budget, so
-// a budget <= T - W * 64 - 1 never lets a probe run out of empty slots)
+// one accumulated contribution of the calling lane (valid lanes only); a group's new keys are
+// counted by its wave's lowest lane (the workgroup's distinct-key budget, xr_stop)
 __device__ __forceinline__ void xr_apply(const XrLds& x, bool valid, int key, double p, int budget) {
   bool ins = false;
   if (valid) {
@@ -244,104 +250,142 @@ __device__ __forceinline__ void xr_apply(const XrLds& x, bool valid, int key, do
     ins = xt_add(x.t, key, lo, hi);
   }
   const int n = __popcll(__ballot(ins));
-  if (n && lane_id() == 0) {
-    const int f = atomicAdd(&x.w.misc[XM_FILL], n) + n;
-    if (f > budget) x.w.misc[XM_OVF] = 1;
-  }
+  if (n && lane_id() == 0) atomicAdd(&x.w.misc[XM_FILL], n);  // (no return: xr_stop reads the count)
+}
+// every wave checks the shared count before each group: once it passes the budget no wave starts
+// another group, so the table holds at most budget + W * 64 keys (a budget <= T - W * 64 - 1 never
+// lets a probe run out of empty slots)
+__device__ __forceinline__ bool xr_stop(const XrLds& x, int budget) {
+  return __hip_atomic_load(&x.w.misc[XM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget;
 }
 
-// Epilogue of one range / bucket workgroup after its last add (every thread): settle the sums in
-// place (lo := the double value), then
-//   direct: top-L of the table -> the source's row (finish_source on wave 0), dlast[v] = distinct
-//   list:   top-L of the table, keys >= the pruning bound, appended to the source's list; the
-//           range's L-th value (when it has L keys) raises the source's bound xtau[d]
-__device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& s, const IterArgs& a, int Lp,
-                                          const XDesc& xd, int d, bool direct, double tau_rows,
+// Epilogue of one range / bucket workgroup after its last add (every thread):
+//   settle  each thread turns its (at most XR_SLOTS) occupied slots into (key, double) pairs and
+//           keeps those at or above the pruning bound tau0 (no other key can reach the top-L);
+//   compact the kept pairs to a dense array over the front of the table (after a barrier, so no
+//           slot is overwritten before it was read);
+//   select  top-L of the dense array when it holds more than L (radix select over U entries, not T);
+//   emit    the selected pairs -> the source's list; with `publish` (several ranges / buckets per
+//           source) the range's L-th value first raises the source's bound xtau[d] and only pairs at
+//           or above the current bound are appended.
+// The row itself is written by k_xfin1 / k_xfinal from the list.
+constexpr int XR_SLOTS = 8;  // table slots per thread (T <= 8 * blockDim: T / W = 512 in every class)
+__device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& s, const IterArgs& a,
+                                          const XDesc& xd, int d, bool publish, double tau0,
                                           unsigned long long* xtau, int32_t* pk, double* ps, uint32_t* pc,
-                                          uint32_t* dsum, int32_t* dlast, unsigned long long* maxdiff,
-                                          unsigned long long* stats) {
+                                          uint32_t* dsum, long long* tph = nullptr, int slot = 0) {
   const int L = s.L;
   const int v = xd.v;
-  for (int i = threadIdx.x; i < T; i += blockDim.x) {
-    const unsigned long long kh = x.t.kh[i];
-    if (kh) x.t.lo[i] = dbits(xs_to_double((uint32_t)kh, x.t.lo[i]));
+  int kk[XR_SLOTS];
+  double kv[XR_SLOTS];
+  bool keep[XR_SLOTS];
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < XR_SLOTS; j++) {
+    const int i = threadIdx.x + j * (int)blockDim.x;
+    keep[j] = false;
+    kk[j] = 0;
+    kv[j] = 0.0;
+    if (i < T) {
+      const unsigned long long kh = x.t.kh[i];
+      if (kh) {
+        kv[j] = xs_to_double((uint32_t)kh, x.t.lo[i]);
+        kk[j] = xt_key(kh);
+        keep[j] = kv[j] >= tau0;
+      }
+    }
+    c += keep[j] ? 1 : 0;
   }
+  // wave-aggregated positions in the dense array
+  const int incl = wave_incl_scan(c);
+  int base = 0;
+  if (lane_id() == WAVE - 1 && incl) base = atomicAdd(&x.w.misc[XM_U], incl);
+  base = __builtin_amdgcn_readlane(base, WAVE - 1) + incl - c;
+  __syncthreads();  // every slot read
+  int* dk = reinterpret_cast<int*>(x.t.kh);
+  double* dv = reinterpret_cast<double*>(x.t.lo);
+#pragma unroll
+  for (int j = 0; j < XR_SLOTS; j++)
+    if (keep[j]) { dk[base] = kk[j]; dv[base] = kv[j]; base++; }
   __syncthreads();
   const int D = x.w.misc[XM_FILL];
-  const unsigned long long* kh = x.t.kh;
-  const unsigned long long* lo = x.t.lo;
-  auto keyat = [&](int i) { return xt_key(kh[i]); };
-  auto valat = [&](int i) { return bitsd(lo[i]); };
-  const double tau0 = direct ? 0.0 : tau_rows;
-  auto elig = [&](int i) { return kh[i] != 0ull && bitsd(lo[i]) >= tau0; };
-  // eligible count
-  int c = 0;
-  for (int i = threadIdx.x; i < T; i += blockDim.x) c += elig(i) ? 1 : 0;
-  c = wave_sum(c);
-  if (lane_id() == 0 && c) atomicAdd(&x.w.misc[XM_U], c);
-  __syncthreads();
   const int U = x.w.misc[XM_U];
-  const uint32_t ts = tie_salt(v);
-  SelCrit sc;
-  sc.tie = false; sc.pa = 0; sc.ma = 0; sc.pb = 0; sc.mb = 0;  // (ma = 0: every eligible entry)
-  const bool cut = U > L;
-  if (cut) sc = wg_select_top(x.w, T, L, keyat, valat, elig, ts);
-  // (wg_select_top ends on a barrier)
-  if (direct) {
-    for (int i = threadIdx.x; i < T; i += blockDim.x) {
-      if (!elig(i)) continue;
-      const uint64_t vb = lo[i];
-      const int key = keyat(i);
-      if (cut && !sel_test(sc, vb, tie_w(key, ts))) continue;
-      const int pos = atomicAdd(&x.w.misc[XM_CNT], 1);
-      x.w.rv[pos] = vb;
-      x.w.rk[pos] = key;
-    }
-    __syncthreads();
-    if (threadIdx.x < WAVE) {
-      const int cnt = x.w.misc[XM_CNT];
-      const uint64_t* rv = x.w.rv;
-      const int* rk = x.w.rk;
-      if (dlast && !a.unit && lane_id() == 0) dlast[v] = D;
-      finish_source(v, cnt, [&](int i) { return rk[i]; }, [&](int i) { return bitsd(rv[i]); }, s, a, x.w.hist,
-                    x.w.rv, x.w.rk, Lp, x.w.hk, x.w.hv, x.w.mf, maxdiff, stats);
-    }
-    return;
-  }
   if (threadIdx.x == 0 && D) atomicAdd(&dsum[d], (uint32_t)D);
-  if (cut) {
-    // the L-th value of this range: the smallest selected value (u64 bits order like the values),
-    // reduced over the whole workgroup before it may raise the source's bound
-    unsigned long long* wmin = reinterpret_cast<unsigned long long*>(&x.w.misc[XM_MIN]);
-    if (threadIdx.x == 0) *wmin = ~0ull;
-    __syncthreads();
-    unsigned long long mn = ~0ull;
-    for (int i = threadIdx.x; i < T; i += blockDim.x)
-      if (elig(i) && sel_test(sc, lo[i], tie_w(keyat(i), ts))) mn = lo[i] < mn ? lo[i] : mn;
-    mn = wave_min_u64(mn);
-    if (lane_id() == 0 && mn != ~0ull) atomicMin(wmin, mn);
-    __syncthreads();
-    if (threadIdx.x == 0 && *wmin != ~0ull) atomicMax(&xtau[d], *wmin);
-    __syncthreads();
+  const uint32_t ts = tie_salt(v);
+  auto keyat = [&](int i) { return dk[i]; };
+  auto valat = [&](int i) { return dv[i]; };
+  SelCrit sc;
+  sc.tie = false; sc.pa = 0; sc.ma = 0; sc.pb = 0; sc.mb = 0;
+  const bool cut = U > L;
+  if (tph) xr_lap(a, slot, *tph);  // settle + compact
+  if (cut) sc = wg_select_top(x.w, U, L, keyat, valat, [](int) { return true; }, ts);
+  // (wg_select_top ends on a barrier)
+  if (tph) xr_lap(a, slot + 1, *tph);  // select
+  double tb = tau0;
+  if (publish) {
+    if (cut) {
+      // the L-th value of this range: the smallest selected value (u64 bits order like the values),
+      // reduced over the whole workgroup before it may raise the source's bound
+      unsigned long long* wmin = reinterpret_cast<unsigned long long*>(&x.w.misc[XM_MIN]);
+      if (threadIdx.x == 0) *wmin = ~0ull;
+      __syncthreads();
+      unsigned long long mn = ~0ull;
+      for (int i = threadIdx.x; i < U; i += blockDim.x) {
+        const unsigned long long vb = dbits(dv[i]);
+        if (sel_test(sc, vb, tie_w(dk[i], ts))) mn = vb < mn ? vb : mn;
+      }
+      mn = wave_min_u64(mn);
+      if (lane_id() == 0 && mn != ~0ull) atomicMin(wmin, mn);
+      __syncthreads();
+      if (threadIdx.x == 0 && *wmin != ~0ull) atomicMax(&xtau[d], *wmin);
+      __syncthreads();
+    }
+    tb = fmax(tb, bitsd(__hip_atomic_load(&xtau[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
   }
-  const double tb = fmax(tau0, bitsd(__hip_atomic_load(&xtau[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-  for (int i0 = 0; i0 < T; i0 += blockDim.x) {
+  for (int i0 = 0; i0 < U; i0 += blockDim.x) {
     const int i = i0 + threadIdx.x;
-    bool keep = false;
-    if (i < T && elig(i)) {
-      const uint64_t vb = lo[i];
-      keep = bitsd(vb) >= tb && (!cut || sel_test(sc, vb, tie_w(keyat(i), ts)));
+    bool k = false;
+    if (i < U) {
+      const uint64_t vb = dbits(dv[i]);
+      k = dv[i] >= tb && (!cut || sel_test(sc, vb, tie_w(dk[i], ts)));
     }
-    const uint64_t m = __ballot(keep);
-    uint32_t base = 0;
-    if (m && lane_id() == 0) base = atomicAdd(&pc[d], (uint32_t)__popcll(m));
-    base = (uint32_t)__shfl((int)base, 0);
-    if (keep) {
-      const int64_t o = xd.pt_off + base + __popcll(m & lanemask_lt());
-      pk[o] = keyat(i);
-      ps[o] = bitsd(lo[i]);
+    const uint64_t m = __ballot(k);
+    uint32_t b0 = 0;
+    if (m && lane_id() == 0) b0 = atomicAdd(&pc[d], (uint32_t)__popcll(m));
+    b0 = (uint32_t)__shfl((int)b0, 0);
+    if (k) {
+      const int64_t o = xd.pt_off + b0 + __popcll(m & lanemask_lt());
+      pk[o] = dk[i];
+      ps[o] = dv[i];
     }
   }
+  if (tph) xr_lap(a, slot + 2, *tph);  // emission
+}
+
+// The row of a one-range source (k_xr emitted at most L entries, its whole top-L): one wave per
+// source copies the list and runs finish_source (row in hash order, range index, norm1, maxDiff)
+// -- the big-table workgroup is gone by then, so the row work runs at full occupancy.
+__host__ __device__ constexpr size_t xf1_lds_bytes(int Lp) { return (size_t)Lp * 12 + 1024 + (size_t)Lp * 20; }
+__global__ void __launch_bounds__(64) k_xfin1(DevSlab s, IterArgs a, const XDesc* xdesc, int d0, const int32_t* pk,
+                                              const double* ps, const uint32_t* pc, const uint32_t* dsum,
+                                              const int32_t* skip, int32_t* dlast, int Lp,
+                                              unsigned long long* maxdiff, unsigned long long* stats) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int d = d0 + (int)blockIdx.x;
+  if (skip[d]) return;  // overflowed: redone by the host
+  const XDesc xd = xdesc[d];
+  uint64_t* rv = reinterpret_cast<uint64_t*>(smem);
+  int* rk = reinterpret_cast<int*>(smem + (size_t)Lp * 8);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + (size_t)Lp * 12);
+  int* hk = reinterpret_cast<int*>(smem + (size_t)Lp * 12 + 1024);
+  int* hv = hk + 2 * Lp;
+  int* mf = hv + 2 * Lp;
+  const int n = (int)pc[d];
+  for (int i = lane_id(); i < n; i += WAVE) { rk[i] = pk[xd.pt_off + i]; rv[i] = dbits(ps[xd.pt_off + i]); }
+  wave_fence();
+  if (dlast && !a.unit && lane_id() == 0) dlast[xd.v] = (int32_t)dsum[d];
+  finish_source(xd.v, n, [&](int i) { return rk[i]; }, [&](int i) { return bitsd(rv[i]); }, s, a, hist, rv, rk, Lp,
+                hk, hv, mf, maxdiff, stats);
 }
 
 // range r of R of a hub source: key k belongs to range ((hash_b(k) * R) >> 32) -- hash_b orders the
@@ -356,15 +400,15 @@ struct XTask { int32_t d; int32_t r; };
 // (a short successor list: all waves share each window, each taking every W-th batch of groups).
 __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, const XDesc* xdesc,
                                              const XTask* tasks, int T, int budget, int Lp, unsigned long long* xtau,
-                                             int32_t* pk, double* ps, uint32_t* pc, uint32_t* dsum, int32_t* dlast,
-                                             int32_t* oflag, int32_t* ovl, unsigned long long* maxdiff,
-                                             unsigned long long* stats) {
+                                             int32_t* pk, double* ps, uint32_t* pc, uint32_t* dsum,
+                                             int32_t* oflag, int32_t* ovl) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
   const XrLds x = xr_carve(smem, T, W, Lp);
   const XTask tk = tasks[blockIdx.x];
   const XDesc xd = xdesc[tk.d];
   const int v = xd.v, R = xd.R, r = tk.r;
+  long long tph = a.diag ? (long long)clock64() : 0;  // PPR_DIAG phase cycles (thread 0, between barriers)
   xr_clear(x, T);
   __syncthreads();
   if (threadIdx.x == 0 && xr_in(v, r, R)) {
@@ -375,19 +419,20 @@ __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, 
     x.w.misc[XM_FILL] = 1;
   }
   __syncthreads();
+  xr_lap(a, 183, tph);
   const int64_t b = g.rp[v], e = g.rp[v + 1];
   const double factor = xd.factor;
   unsigned long long mb = 0;
   uint8_t* fl = x.fl + (size_t)wv * HUB_WALK_FLAGS;
   auto fn = [&](bool valid, int id, double sv, bool) {
-    if (x.w.misc[XM_OVF]) return;  // (uniform per wave: one LDS read per group)
+    if (xr_stop(x, budget)) return;  // (uniform per wave: one LDS read per group)
     xr_apply(x, valid && xr_in(id, r, R), id, sv * factor, budget);
   };
   if (a.unit) {
     for (int64_t e0 = b + (int64_t)wv * WAVE; e0 < e; e0 += (int64_t)W * WAVE) {
       const int64_t i = e0 + lane_id();
       const int key = i < e ? (g.colx[i] & 0x7fffffff) : 0;
-      if (x.w.misc[XM_OVF]) break;
+      if (xr_stop(x, budget)) break;
       xr_apply(x, i < e && xr_in(key, r, R), key, factor, budget);
     }
   } else if (e - b >= (int64_t)W * WAVE) {
@@ -398,7 +443,13 @@ __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, 
       hub_window_walk_part(g, s, a, w0, min(e, w0 + WAVE), fl, fn, WalkRowMin{&mb, (int)s.L}, wv, W);
   }
   __syncthreads();
-  if (x.w.misc[XM_OVF]) {
+  xr_lap(a, 184, tph);
+  if (a.diag && threadIdx.x == 0) {
+    diag_add(a.diag, 182, 1ull);
+    diag_add(a.diag, 188, (unsigned long long)(xd.R > 0 ? (e - b) : 0));
+    diag_add(a.diag, 189, (unsigned long long)x.w.misc[XM_FILL]);
+  }
+  if (x.w.misc[XM_FILL] > budget) {
     if (threadIdx.x == 0 && atomicExch(&oflag[tk.d], 1) == 0) ovl[1 + atomicAdd(&ovl[0], 1)] = tk.d;
     return;
   }
@@ -409,7 +460,7 @@ __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, 
   __syncthreads();
   const unsigned long long mbb = *reinterpret_cast<unsigned long long*>(&x.w.misc[8]);
   const double tau_rows = (!a.unit && mbb) ? xs_single(bitsd(mbb) * factor) : 0.0;
-  xr_finish(x, T, s, a, Lp, xd, tk.d, R == 1, tau_rows, xtau, pk, ps, pc, dsum, dlast, maxdiff, stats);
+  xr_finish(x, T, s, a, xd, tk.d, R > 1, tau_rows, xtau, pk, ps, pc, dsum, a.diag ? &tph : nullptr, 185);
 }
 
 // One workgroup per staged bucket of a partitioned hub source: the bucket's records are
@@ -430,6 +481,7 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
   const int v = d.v;
   const int64_t deg = rp[v + 1] - rp[v];
   const double factor = merge_factor(a, deg);
+  long long tph = a.diag ? (long long)clock64() : 0;
   xr_clear(x, T);
   __syncthreads();
   if (threadIdx.x == 0 && (int)hub_digit(v, d.logP) == tk.x) {
@@ -446,30 +498,37 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
     int key[XB_BATCH];
     double sv[XB_BATCH];
     bool ok[XB_BATCH];
+    // (clamped, unconditional loads: a load under a branch ends in its own vmcnt(0) wait, which
+    // serialised the batch)
 #pragma unroll
     for (int k = 0; k < XB_BATCH; k++) {
       const int64_t q = (g0 + (int64_t)k * W) * WAVE + lane_id();
       ok[k] = q < nb;
-      key[k] = 0;
-      sv[k] = 0.0;
-      if (ok[k]) { const HubRec hr = rec[q]; key[k] = rec_key(hr); sv[k] = rec_sc(hr); }
+      const HubRec hr = rec[ok[k] ? q : nb - 1];
+      key[k] = rec_key(hr);
+      sv[k] = rec_sc(hr);
     }
 #pragma unroll
     for (int k = 0; k < XB_BATCH; k++) {
-      if (x.w.misc[XM_OVF]) break;
+      if (xr_stop(x, budget)) break;
       if ((g0 + (int64_t)k * W) >= ng) break;
       xr_apply(x, ok[k], key[k], sv[k] * factor, budget);
     }
   }
   __syncthreads();
-  if (x.w.misc[XM_OVF]) {
+  xr_lap(a, 155, tph);
+  if (a.diag && threadIdx.x == 0) {
+    diag_add(a.diag, 154, 1ull);
+    diag_add(a.diag, 159, (unsigned long long)nb);
+  }
+  if (x.w.misc[XM_FILL] > budget) {
     if (threadIdx.x == 0 && atomicExch(&oflag[tk.d], 1) == 0) ovl[1 + atomicAdd(&ovl[0], 1)] = v;
     return;
   }
   const double tau_rows = (!a.unit && tau_b[tk.d]) ? xs_single(bitsd(tau_b[tk.d]) * factor) : 0.0;
   XDesc xd;
   xd.v = v; xd.R = 0; xd.pt_off = d.pt_off; xd.factor = factor; xd.selfval = 0.0;
-  xr_finish(x, T, s, a, Lp, xd, tk.d, false, tau_rows, xtau, pk, ps, pc, dsum, nullptr, nullptr, nullptr);
+  xr_finish(x, T, s, a, xd, tk.d, true, tau_rows, xtau, pk, ps, pc, dsum, a.diag ? &tph : nullptr, 156);
 }
 
 // One workgroup per listed source: top-L of the entries its ranges / buckets appended (keys are

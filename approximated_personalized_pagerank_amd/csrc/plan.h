@@ -177,7 +177,7 @@ struct ppr_plan {
   // exact-sum GRank (merge_xs.h; PPR_FLAG_CHAIN_SUM / PPR_SUM=chain turn it off)
   bool xsum = false;
   int32_t* d_dlast = nullptr;         // [n] distinct keys of each source's last merge (hub planning)
-  int xr_T = 8192, xr_W = 16;         // PPR_XR_T / PPR_XR_W: range / bucket workgroup table slots, waves
+  int xr_T = 8192, xr_W = 16;         // PPR_XR_T: range / bucket workgroup table slots (waves = T / 512)
   int xr_rmax = 3;                    // PPR_XR_RMAX: most key ranges a source is walked in (beyond: partition)
   int xr_fill = 60;                   // PPR_XR_FILL: planned distinct keys per table, % of its slots
   int xf_stage = 4096;                // k_xfinal entries staged in LDS
@@ -287,6 +287,14 @@ inline void plan_free(ppr_plan* p) {
                   "C value placement %.1f %% D per-slot chains %.1f %%\n", 100.0 * h[172] / acc, 100.0 * h[173] / acc,
                   100.0 * h[174] / acc, 100.0 * h[175] / acc);
       }
+      if (h[182])
+        fprintf(stderr, "ppr_diag k_xr: %llu workgroups, %.3e successor edges walked, %.3e distinct keys; Gcycles "
+                "(thread 0) setup %.2f accumulate %.2f settle %.2f select %.2f finish %.2f\n", h[182], (double)h[188],
+                (double)h[189], h[183] / 1e9, h[184] / 1e9, h[185] / 1e9, h[186] / 1e9, h[187] / 1e9);
+      if (h[154])
+        fprintf(stderr, "ppr_diag k_xb: %llu workgroups, %.3e records (%.0f per bucket); Gcycles (thread 0) setup+accumulate "
+                "%.2f settle %.2f select %.2f emit %.2f\n", h[154], (double)h[159], (double)h[159] / (double)h[154],
+                h[155] / 1e9, h[156] / 1e9, h[157] / 1e9, h[158] / 1e9);
       if (h[170]) {
         fprintf(stderr, "ppr_diag hub final: %llu sources, appended entries %.3e (%.1f per source, %.1f x L); by log2(entries):",
                 h[170], (double)h[171], (double)h[171] / (double)h[170], (double)h[171] / (double)h[170] / (double)p->L);

@@ -249,7 +249,7 @@ def test_gpu_speculative_bound_bit_exact(env, want_redo, monkeypatch, capfd, cha
     {},                                                           # defaults
     {"PPR_XR_RMAX": "1"},                                         # every multi-table source partitioned
     {"PPR_XR_RMAX": "64", "PPR_XR_FILL": "20"},                   # many key ranges per source
-    {"PPR_XR_T": "1024", "PPR_XR_W": "4", "PPR_XR_FILL": "20"},   # small tables: more ranges / buckets
+    {"PPR_XR_T": "1024", "PPR_XR_FILL": "20"},                    # small tables: more ranges / buckets
     {"PPR_XR_DSCALE": "5"},                                       # estimates 20x too low: table overflows,
                                                                   # sources redone with larger estimates
     {"PPR_XR_DSCALE": "5", "PPR_XR_RMAX": "1"},                   # ... in the bucket workgroups
