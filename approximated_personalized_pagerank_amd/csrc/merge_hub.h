@@ -117,21 +117,24 @@ __global__ void __launch_bounds__(256) k_hub_expand(const HubDesc* desc, HubTask
   for (int x = threadIdx.x; x < D.nsl; x += blockDim.x) rts[D.rt_off + x] = HubTask{d, x};
 }
 
-// one staged candidate: key and score packed in 12 bytes (dword aligned, one dwordx3 store /
+// one staged candidate: score and key packed in 12 bytes (dword aligned, one dwordx3 store /
 // load), so a scattered store touches one partial line instead of two (separate key / score
-// arrays); measured as fast as a padded 16-B record, with 3/4 of its staging memory
+// arrays); measured as fast as a padded 16-B record, with 3/4 of its staging memory. The score
+// comes first: a dwordx3 load lands in an even-aligned register triple, so the score is an
+// aligned 64-bit pair as loaded (key first, the compiler re-aligned it with moves that waited for
+// the load)
 struct HubRec {
   uint32_t w[3];
 };
 __device__ __forceinline__ HubRec hub_rec(int key, double sc) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(sc);
   HubRec r{};
-  r.w[0] = (uint32_t)key; r.w[1] = (uint32_t)b; r.w[2] = (uint32_t)(b >> 32);
+  r.w[0] = (uint32_t)b; r.w[1] = (uint32_t)(b >> 32); r.w[2] = (uint32_t)key;
   return r;
 }
-__device__ __forceinline__ int rec_key(const HubRec& r) { return (int)r.w[0]; }
+__device__ __forceinline__ int rec_key(const HubRec& r) { return (int)r.w[2]; }
 __device__ __forceinline__ double rec_sc(const HubRec& r) {
-  return __longlong_as_double((long long)(((unsigned long long)r.w[2] << 32) | r.w[1]));
+  return __longlong_as_double((long long)(((unsigned long long)r.w[1] << 32) | r.w[0]));
 }
 
 __device__ __forceinline__ uint32_t hub_digit(int key, int logP) {

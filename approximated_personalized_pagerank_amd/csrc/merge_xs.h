@@ -59,40 +59,58 @@ __device__ __forceinline__ double xs_single(double p) {
   return xs_to_double(hi, lo);
 }
 
-// LDS table of 16-B slots: kh = (key + 1) << 32 | high word (0 = empty), lo = low word.
+// LDS table of 16-B slots in three arrays: keys u32 (key + 1, 0 = empty), lo u64 (low word of the
+// sum), hi u32 (high word). Slots are probed in aligned groups of four keys, one ds_read_b128 per
+// step: the longest probe among a group's 64 lanes (the wave waits for it) stays short at fills
+// where single-slot linear probing ran long chains.
 struct XTable {
-  unsigned long long* kh;
+  uint32_t* keys;
   unsigned long long* lo;
+  uint32_t* hi;
   uint32_t mask;
 };
 
 // find-or-insert `key`, then add X: the low word's returning add yields its carry, which goes
-// with the high word into kh (the tag bits above it never change). Returns true when this lane
-// inserted the key.
+// with the high word into hi. Returns true when this lane inserted the key.
 __device__ __forceinline__ bool xt_add(const XTable& t, int key, unsigned long long xlo, uint32_t xhi) {
   const uint32_t tag = (uint32_t)key + 1u;
-  uint32_t h = hash32((uint32_t)key) & t.mask;
+  uint32_t g = hash32((uint32_t)key) & t.mask & ~3u;
   bool ins = false;
+  uint32_t h;
   for (;;) {
-    const unsigned long long cur = t.kh[h];
-    if ((uint32_t)(cur >> 32) == tag) break;
-    if (cur == 0ull) {
-      const unsigned long long prev = atomicCAS(&t.kh[h], 0ull, (unsigned long long)tag << 32);
-      if (prev == 0ull) { ins = true; break; }
-      if ((uint32_t)(prev >> 32) == tag) break;
+    const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g);
+    if (q.x == tag) { h = g; break; }
+    if (q.y == tag) { h = g + 1; break; }
+    if (q.z == tag) { h = g + 2; break; }
+    if (q.w == tag) { h = g + 3; break; }
+    const int e = q.x == 0u ? 0 : q.y == 0u ? 1 : q.z == 0u ? 2 : q.w == 0u ? 3 : -1;
+    if (e >= 0) {
+      const uint32_t prev = atomicCAS(&t.keys[g + e], 0u, tag);
+      if (prev == 0u) { h = g + e; ins = true; break; }
+      if (prev == tag) { h = g + e; break; }
+      continue;  // another key took it: read the group again
     }
-    h = (h + 1u) & t.mask;
+    g = (g + 4u) & t.mask;
   }
   const unsigned long long old = atomicAdd(&t.lo[h], xlo);
   const uint32_t up = xhi + ((old + xlo < old) ? 1u : 0u);
-  if (up) atomicAdd(&t.kh[h], (unsigned long long)up);
+  if (up) atomicAdd(&t.hi[h], up);
   return ins;
 }
 
-__device__ __forceinline__ int xt_key(unsigned long long kh) { return (int)(uint32_t)(kh >> 32) - 1; }
+__host__ __device__ constexpr size_t xt_bytes(int T) { return (size_t)T * 16; }
+// carve a T-slot table at p (16-B aligned)
+__device__ __forceinline__ XTable xt_carve(unsigned char* p, int T) {
+  XTable t;
+  t.keys = reinterpret_cast<uint32_t*>(p);
+  t.lo = reinterpret_cast<unsigned long long*>(p + (size_t)T * 4);
+  t.hi = reinterpret_cast<uint32_t*>(p + (size_t)T * 12);
+  t.mask = (uint32_t)T - 1u;
+  return t;
+}
 
 // ---------------------------------------------------------------------------------------------
-// wave tier: layout kh u64[T] | lo u64[T] | rv u64[Lp] | rk i32[Lp] | hist u32[256] | hk i32[2Lp] |
+// wave tier: layout table (16 T) | rv u64[Lp] | rk i32[Lp] | hist u32[256] | hk i32[2Lp] |
 // hv i32[2Lp] | mf i32[Lp]
 __host__ __device__ constexpr size_t lds_wave_bytes_x(int T, int Lp) {
   return (size_t)T * 16 + (size_t)Lp * 12 + 1024 + (size_t)Lp * 20;
@@ -106,10 +124,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (w >= count) return;
   unsigned char* base = smem + (size_t)wv * lds_wave_bytes_x(T, Lp);
-  XTable t;
-  t.kh = reinterpret_cast<unsigned long long*>(base);
-  t.lo = reinterpret_cast<unsigned long long*>(base + (size_t)T * 8);
-  t.mask = (uint32_t)T - 1u;
+  const XTable t = xt_carve(base, T);
   uint64_t* rv = reinterpret_cast<uint64_t*>(base + (size_t)T * 16);
   int* rk = reinterpret_cast<int*>(base + (size_t)T * 16 + (size_t)Lp * 8);
   uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 16 + (size_t)Lp * 12);
@@ -120,7 +135,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   const int v = list[w];
   const int64_t b = g.rp[v], e = g.rp[v + 1];
   const double factor = merge_factor(a, e - b);
-  for (int i = lane_id(); i < T; i += WAVE) { t.kh[i] = 0ull; t.lo[i] = 0ull; }
+  for (int i = lane_id(); i < T; i += WAVE) { t.keys[i] = 0u; t.lo[i] = 0ull; t.hi[i] = 0u; }
   wave_fence();
   if (lane_id() == 0) {
     unsigned long long lo;
@@ -158,15 +173,15 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   // at >= the single-contribution value of its minimum)
   const double tau = (!a.unit && mb) ? xs_single(bitsd(mb) * factor) : 0.0;
   // settle + compact in place: (double value, key) pairs over the front of the table
-  double* vals = reinterpret_cast<double*>(t.kh);
-  int* keys = reinterpret_cast<int*>(t.lo);
+  double* vals = reinterpret_cast<double*>(t.lo);
+  int* keys = reinterpret_cast<int*>(t.keys);
   int U = 0, D = 0;
   for (int base0 = 0; base0 < T; base0 += WAVE) {
     const int i = base0 + lane_id();
-    const unsigned long long kh = t.kh[i];
+    const uint32_t kt = t.keys[i];
     const unsigned long long lo = t.lo[i];
-    const bool occ = kh != 0ull;
-    const double x = occ ? xs_to_double((uint32_t)kh, lo) : 0.0;
+    const bool occ = kt != 0u;
+    const double x = occ ? xs_to_double(t.hi[i], lo) : 0.0;
     const bool keep = occ && x >= tau;
     const uint64_t m = __ballot(keep);
     D += __popcll(__ballot(occ));
@@ -174,7 +189,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
     if (keep) {
       const int pos = U + __popcll(m & lanemask_lt());
       vals[pos] = x;
-      keys[pos] = xt_key(kh);
+      keys[pos] = (int)kt - 1;
     }
     wave_fence();
     U += __popcll(m);
@@ -185,7 +200,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
 }
 
 // ---------------------------------------------------------------------------------------------
-// Range / bucket workgroups. LDS: kh u64[T] | lo u64[T] | flags u8[W][HUB_WALK_FLAGS] | hist u32[256] |
+// Range / bucket workgroups. LDS: table (16 T) | flags u8[W][HUB_WALK_FLAGS] | hist u32[256] |
 // misc i32[64] | rv u64[Lp] | rk i32[Lp] | hk i32[2Lp] | hv i32[2Lp] | mf i32[Lp]
 __host__ __device__ constexpr size_t xr_lds_bytes(int T, int W, int Lp) {
   return (size_t)T * 16 + (size_t)W * HUB_WALK_FLAGS + 1024 + 256 + (size_t)Lp * 32;
@@ -211,9 +226,7 @@ struct XrLds {
 __device__ __forceinline__ XrLds xr_carve(unsigned char* smem, int T, int W, int Lp) {
   XrLds x;
   unsigned char* p = smem;
-  x.t.kh = reinterpret_cast<unsigned long long*>(p); p += (size_t)T * 8;
-  x.t.lo = reinterpret_cast<unsigned long long*>(p); p += (size_t)T * 8;
-  x.t.mask = (uint32_t)T - 1u;
+  x.t = xt_carve(p, T); p += xt_bytes(T);
   x.fl = p; p += (size_t)W * HUB_WALK_FLAGS;
   x.w = WgLds{};
   x.w.hist = reinterpret_cast<uint32_t*>(p); p += 1024;
@@ -235,7 +248,7 @@ __device__ __forceinline__ void xr_lap(const IterArgs& a, int slot, long long& t
 }
 
 __device__ __forceinline__ void xr_clear(const XrLds& x, int T) {
-  for (int i = threadIdx.x; i < T; i += blockDim.x) { x.t.kh[i] = 0ull; x.t.lo[i] = 0ull; }
+  for (int i = threadIdx.x; i < T; i += blockDim.x) { x.t.keys[i] = 0u; x.t.lo[i] = 0ull; x.t.hi[i] = 0u; }
   if (threadIdx.x < 64) x.w.misc[threadIdx.x] = 0;
 }
 
@@ -287,10 +300,10 @@ __device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& 
     kk[j] = 0;
     kv[j] = 0.0;
     if (i < T) {
-      const unsigned long long kh = x.t.kh[i];
-      if (kh) {
-        kv[j] = xs_to_double((uint32_t)kh, x.t.lo[i]);
-        kk[j] = xt_key(kh);
+      const uint32_t kt = x.t.keys[i];
+      if (kt) {
+        kv[j] = xs_to_double(x.t.hi[i], x.t.lo[i]);
+        kk[j] = (int)kt - 1;
         keep[j] = kv[j] >= tau0;
       }
     }
@@ -302,7 +315,7 @@ __device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& 
   if (lane_id() == WAVE - 1 && incl) base = atomicAdd(&x.w.misc[XM_U], incl);
   base = __builtin_amdgcn_readlane(base, WAVE - 1) + incl - c;
   __syncthreads();  // every slot read
-  int* dk = reinterpret_cast<int*>(x.t.kh);
+  int* dk = reinterpret_cast<int*>(x.t.keys);
   double* dv = reinterpret_cast<double*>(x.t.lo);
 #pragma unroll
   for (int j = 0; j < XR_SLOTS; j++)
@@ -494,26 +507,82 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
   __syncthreads();
   const HubRec* rec = st + start;
   const int64_t ng = (nb + WAVE - 1) / WAVE;
-  for (int64_t g0 = wv; g0 < ng; g0 += (int64_t)W * XB_BATCH) {
-    int key[XB_BATCH];
-    double sv[XB_BATCH];
-    bool ok[XB_BATCH];
-    // (clamped, unconditional loads: a load under a branch ends in its own vmcnt(0) wait, which
-    // serialised the batch)
+  // a batch of XB_BATCH groups per wave (groups wv, wv + W, ...), the next batch's loads issued
+  // before the current one is applied (clamped, unconditional loads: a load under a branch ends
+  // in its own vmcnt(0) wait)
+  struct Batch { HubRec r[XB_BATCH]; };
+  auto load = [&](int64_t g0, Batch& hr) {
 #pragma unroll
     for (int k = 0; k < XB_BATCH; k++) {
       const int64_t q = (g0 + (int64_t)k * W) * WAVE + lane_id();
-      ok[k] = q < nb;
-      const HubRec hr = rec[ok[k] ? q : nb - 1];
-      key[k] = rec_key(hr);
-      sv[k] = rec_sc(hr);
+      hr.r[k] = rec[q < nb ? q : nb - 1];
     }
+  };
+  // (no early exits inside a batch: a break there made the compiler shuffle the prefetched
+  // registers, which waits for the prefetch)
+  // Hot key of the wave: a bucket holding one of the source's core keys has that key in a third
+  // or more of its records (one per successor row), and same-address LDS atomics serialise lane by
+  // lane. Each wave picks the most frequent of 8 sampled keys of its first group (when it fills
+  // >= 1/8 of the group) and sums that key's contributions in a per-lane register accumulator --
+  // exact 96-bit adds, order-free like the table -- added to the table once per lane at the end.
+  int hk = -1;
+  unsigned long long hlo = 0ull;
+  uint32_t hhi = 0u;
+  auto apply = [&](int64_t g0, const Batch& hr) {
 #pragma unroll
     for (int k = 0; k < XB_BATCH; k++) {
-      if (xr_stop(x, budget)) break;
-      if ((g0 + (int64_t)k * W) >= ng) break;
-      xr_apply(x, ok[k], key[k], sv[k] * factor, budget);
+      const int64_t gk = g0 + (int64_t)k * W;
+      if (gk < ng && !xr_stop(x, budget)) {
+        const int64_t q = gk * WAVE + lane_id();
+        const int key = rec_key(hr.r[k]);
+        const double p = rec_sc(hr.r[k]) * factor;
+        bool valid = q < nb;
+        if (valid && key == hk) {
+          unsigned long long lo;
+          uint32_t hi;
+          xs_conv(p, lo, hi);
+          const unsigned long long nl = hlo + lo;
+          hhi += hi + (nl < hlo ? 1u : 0u);
+          hlo = nl;
+          valid = false;
+        }
+        xr_apply(x, valid, key, p, budget);
+      }
     }
+  };
+  Batch ba, bb;
+  const int64_t step = (int64_t)W * XB_BATCH;
+  if (wv < ng) {
+    load(wv, ba);
+    // (the first group only: its lanes are valid up to nb)
+    const bool v0 = (int64_t)wv * WAVE + lane_id() < nb;
+    const int k0 = rec_key(ba.r[0]);
+    int best = 0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const int cand = __builtin_amdgcn_readlane(k0, c * 8);
+      const int n = __popcll(__ballot(v0 && k0 == cand));
+      if (n > best && __builtin_amdgcn_readlane((int)v0, c * 8)) { best = n; hk = cand; }
+    }
+    if (best < 8) hk = -1;
+  }
+  // (sched_barrier: the scheduler otherwise pulls the next batch's first uses up into the current
+  // batch, waiting for the prefetch right after issuing it)
+  for (int64_t g0 = wv; g0 < ng; g0 += 2 * step) {
+    load(g0 + step < ng ? g0 + step : g0, bb);  // (unconditional: past the end it reloads a batch)
+    __builtin_amdgcn_sched_barrier(0);
+    apply(g0, ba);
+    __builtin_amdgcn_sched_barrier(0);
+    if (g0 + step >= ng) break;
+    load(g0 + 2 * step < ng ? g0 + 2 * step : g0, ba);
+    __builtin_amdgcn_sched_barrier(0);
+    apply(g0 + step, bb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // the hot key's register sums (a lane's sum stays below the key's total < 2^95): once per lane
+  if (hk >= 0 && (hlo | hhi)) {
+    const bool ins = xt_add(x.t, hk, hlo, hhi);
+    if (ins) atomicAdd(&x.w.misc[XM_FILL], 1);
   }
   __syncthreads();
   xr_lap(a, 155, tph);
