@@ -283,31 +283,47 @@ __device__ __forceinline__ bool xr_stop(const XrLds& x, int budget) {
 //           or above the current bound are appended.
 // The row itself is written by k_xfin1 / k_xfinal from the list.
 constexpr int XR_SLOTS = 8;  // table slots per thread (T <= 8 * blockDim: T / W = 512 in every class)
+constexpr double XR_SPEC = 0.9;  // speculative bound of a one-range source: this x its previous L-th score
 __device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& s, const IterArgs& a,
-                                          const XDesc& xd, int d, bool publish, double tau0,
+                                          const XDesc& xd, int d, bool publish, double tau0, double tau_spec,
                                           unsigned long long* xtau, int32_t* pk, double* ps, uint32_t* pc,
                                           uint32_t* dsum, long long* tph = nullptr, int slot = 0) {
   const int L = s.L;
   const int v = xd.v;
+  // a list range may already filter by the bound the source's other ranges published
+  if (publish) tau0 = fmax(tau0, bitsd(__hip_atomic_load(&xtau[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+  // speculative bound (one-range sources): kept only when at least L keys reach it -- then the
+  // top-L lies among them, so the result never depends on it
+  const double ts_hi = fmax(tau0, tau_spec);
   int kk[XR_SLOTS];
   double kv[XR_SLOTS];
-  bool keep[XR_SLOTS];
-  int c = 0;
+  int c = 0, c_hi = 0;
 #pragma unroll
   for (int j = 0; j < XR_SLOTS; j++) {
     const int i = threadIdx.x + j * (int)blockDim.x;
-    keep[j] = false;
-    kk[j] = 0;
+    kk[j] = -1;
     kv[j] = 0.0;
     if (i < T) {
       const uint32_t kt = x.t.keys[i];
       if (kt) {
         kv[j] = xs_to_double(x.t.hi[i], x.t.lo[i]);
-        kk[j] = (int)kt - 1;
-        keep[j] = kv[j] >= tau0;
+        if (kv[j] >= tau0) kk[j] = (int)kt - 1;
       }
     }
-    c += keep[j] ? 1 : 0;
+    c += kk[j] >= 0 ? 1 : 0;
+    c_hi += (kk[j] >= 0 && kv[j] >= ts_hi) ? 1 : 0;
+  }
+  if (tau_spec > tau0) {
+    const int w_hi = wave_sum(c_hi);
+    if (lane_id() == 0 && w_hi) atomicAdd(&x.w.misc[XM_CNT], w_hi);
+    __syncthreads();
+    if (x.w.misc[XM_CNT] >= L) {  // (uniform)
+      tau0 = ts_hi;
+      c = c_hi;
+#pragma unroll
+      for (int j = 0; j < XR_SLOTS; j++)
+        if (kk[j] >= 0 && kv[j] < ts_hi) kk[j] = -1;
+    }
   }
   // wave-aggregated positions in the dense array
   const int incl = wave_incl_scan(c);
@@ -319,7 +335,7 @@ __device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& 
   double* dv = reinterpret_cast<double*>(x.t.lo);
 #pragma unroll
   for (int j = 0; j < XR_SLOTS; j++)
-    if (keep[j]) { dk[base] = kk[j]; dv[base] = kv[j]; base++; }
+    if (kk[j] >= 0) { dk[base] = kk[j]; dv[base] = kv[j]; base++; }
   __syncthreads();
   const int D = x.w.misc[XM_FILL];
   const int U = x.w.misc[XM_U];
@@ -473,7 +489,14 @@ __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, 
   __syncthreads();
   const unsigned long long mbb = *reinterpret_cast<unsigned long long*>(&x.w.misc[8]);
   const double tau_rows = (!a.unit && mbb) ? xs_single(bitsd(mbb) * factor) : 0.0;
-  xr_finish(x, T, s, a, xd, tk.d, R > 1, tau_rows, xtau, pk, ps, pc, dsum, a.diag ? &tph : nullptr, 185);
+  // one-range source: its previous L-th score (row minimum of a full current row) x XR_SPEC as a
+  // speculative bound (scores move little between updates; the check in xr_finish keeps it exact)
+  double tau_spec = 0.0;
+  if (R == 1 && !a.unit && !a.mc) {
+    const int64_t cr = s.lrow((a.active == 1) ? a.sB : a.sA, v);
+    if (s.len[cr] == s.L) tau_spec = XR_SPEC * s.rmin[cr];
+  }
+  xr_finish(x, T, s, a, xd, tk.d, R > 1, tau_rows, tau_spec, xtau, pk, ps, pc, dsum, a.diag ? &tph : nullptr, 185);
 }
 
 // One workgroup per staged bucket of a partitioned hub source: the bucket's records are
@@ -597,7 +620,7 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
   const double tau_rows = (!a.unit && tau_b[tk.d]) ? xs_single(bitsd(tau_b[tk.d]) * factor) : 0.0;
   XDesc xd;
   xd.v = v; xd.R = 0; xd.pt_off = d.pt_off; xd.factor = factor; xd.selfval = 0.0;
-  xr_finish(x, T, s, a, xd, tk.d, true, tau_rows, xtau, pk, ps, pc, dsum, a.diag ? &tph : nullptr, 156);
+  xr_finish(x, T, s, a, xd, tk.d, true, tau_rows, 0.0, xtau, pk, ps, pc, dsum, a.diag ? &tph : nullptr, 156);
 }
 
 // One workgroup per listed source: top-L of the entries its ranges / buckets appended (keys are
