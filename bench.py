@@ -40,16 +40,23 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 PROFILES = os.path.join(ROOT, "profiles")
 
 
-def pmc_traffic(tag):
-    """HBM bytes per step of the merge phase from the committed rocprofv3 PMC summary of this
-    workload (tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, separate passes), or None."""
+def sum_mode():
+    """the GRank summation mode the plans of this process use (include/ppr_hip.h PPR_FLAG_CHAIN_SUM;
+    PPR_SUM overrides the default, the exact sum)"""
+    return "chain" if os.environ.get("PPR_SUM") == "chain" else "exact"
+
+
+def pmc_traffic(tag, mode):
+    """HBM bytes per step of the merge phase from the newest committed rocprofv3 PMC summary of this
+    workload in this summation mode (tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, separate
+    passes; a summary without a "sum" field predates the exact sum: chain), or None."""
     import glob
-    hits = sorted(glob.glob(os.path.join(PROFILES, f"*_{tag}_pmc.json")))
-    if not hits:
-        return None, None
-    with open(hits[-1]) as f:
-        d = json.load(f)
-    return d.get("merge_phase_traffic_bytes"), os.path.relpath(hits[-1], ROOT)
+    for path in sorted(glob.glob(os.path.join(PROFILES, f"*_{tag}_pmc.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("sum", "chain") == mode:
+            return d.get("merge_phase_traffic_bytes"), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def mc_cpu_baseline(scale, K, L, walks, damping, seed):
@@ -398,7 +405,7 @@ def main():
     achieved = stats["algo_bytes"] / 1e9 / (stats["merge_ms"] / 1e3) if stats["merge_ms"] > 0 else 0.0
     traffic, traffic_src = (None, None)
     if (args.scale, args.K, args.L, args.iters) == (22, 64, 128, 30):
-        traffic, traffic_src = pmc_traffic(f"grank_rmat22_k64_l128")
+        traffic, traffic_src = pmc_traffic("grank_rmat22_k64_l128", sum_mode())
     line = {
         "metric": f"source-nodes/sec grank K={args.K} L={args.L} on RMAT-{args.scale}; 1/2/4/8 MI355X + HBM GB/s",
         "value": value,
@@ -415,9 +422,13 @@ def main():
         "config": {"workload": f"grank RMAT-{args.scale} K={args.K} L={args.L} iters={args.iters} "
                                f"damping={args.damping} tol={args.tol}",
                    "nodes": g.n, "edges": g.m, "iterations_run": stats["iterations"],
-                   "parallelism": f"source-shard x{world}" if world > 1 else "1 GPU"},
+                   "parallelism": f"source-shard x{world}" if world > 1 else "1 GPU",
+                   "sum": sum_mode()},
         "roofline": {"bound": "hbm",
-                     "kernel": ("basket-merge phase: k_classify + k_merge_lds (wave tiers) + hub pipeline "
+                     "kernel": ("basket-merge phase, exact sum: k_classify + k_merge_lds_x (wave tier) + k_xr "
+                                "(range workgroups) + partition (k_hub_count, device scan, k_hub_scatter) + k_xb "
+                                "(bucket workgroups) + k_xfin1 / k_xfinal" if sum_mode() == "exact" else
+                                "basket-merge phase, chain sum: k_classify + k_merge_lds (wave tiers) + hub pipeline "
                                 "(k_hub_count, device scan, k_hub_scatter, k_hub_bucket_w, k_hub_final)"),
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,

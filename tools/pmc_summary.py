@@ -18,7 +18,8 @@ import csv
 import json
 import sys
 
-MERGE_KERNELS = ("k_classify", "k_merge_lds", "k_merge_wg", "k_merge_glb", "k_hub_", "rocprim", "k_stat")
+MERGE_KERNELS = ("k_classify", "k_merge_lds", "k_merge_wg", "k_merge_glb", "k_hub_", "rocprim", "k_stat", "k_xr", "k_xb",
+                 "k_xfin", "k_gather")
 
 
 def per_kernel(path):
@@ -31,7 +32,7 @@ def per_kernel(path):
     return acc, calls
 
 
-def main(fetch_csv, write_csv, steps):
+def main(fetch_csv, write_csv, steps, mode="chain"):
     f, calls = per_kernel(fetch_csv)
     w, _ = per_kernel(write_csv)
     kernels = {}
@@ -44,6 +45,7 @@ def main(fetch_csv, write_csv, steps):
                  "this engine's access patterns, profiles/r02_pmc_calibration.json); KiB -> bytes"),
         "merge_phase_traffic_bytes": sum(kernels[k]["fetch_bytes"] + kernels[k]["write_bytes"] for k in merge),
         "merge_kernels": merge,
+        "sum": mode,
         "kernels": kernels,
     }
     json.dump(out, sys.stdout, indent=1)
@@ -51,4 +53,5 @@ def main(fetch_csv, write_csv, steps):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1)
+    # (4th argument: the GRank summation mode the profiled run used, exact | chain)
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1, sys.argv[4] if len(sys.argv) > 4 else "chain")
