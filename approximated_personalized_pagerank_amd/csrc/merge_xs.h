@@ -23,6 +23,7 @@
 namespace pprk {
 
 constexpr int XS_F = 93;   // fraction bits of the fixed-point sums (oracle/grank_oracle.c XS_F)
+constexpr double XR_SPEC = 0.9;  // speculative bound of a whole-source table: this x its previous L-th score
 
 // floor(p * 2^93) of p in [0, 4): lo = low 64 bits, hi = bits 64..94
 __device__ __forceinline__ void xs_conv(double p, unsigned long long& lo, uint32_t& hi) {
@@ -96,6 +97,30 @@ __device__ __forceinline__ bool xt_add(const XTable& t, int key, unsigned long l
   const uint32_t up = xhi + ((old + xlo < old) ? 1u : 0u);
   if (up) atomicAdd(&t.hi[h], up);
   return ins;
+}
+
+// the slot of `key` within a loaded group of four (or -1)
+__device__ __forceinline__ int xt_match(const uint4& q, uint32_t g, uint32_t tag) {
+  return q.x == tag ? (int)g : q.y == tag ? (int)g + 1 : q.z == tag ? (int)g + 2 : q.w == tag ? (int)g + 3 : -1;
+}
+// find-or-insert only (xt_add's probe loop); returns the slot, `ins` when this lane inserted
+__device__ __forceinline__ uint32_t xt_slot(const XTable& t, int key, bool& ins) {
+  const uint32_t tag = (uint32_t)key + 1u;
+  uint32_t g = hash32((uint32_t)key) & t.mask & ~3u;
+  ins = false;
+  for (;;) {
+    const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g);
+    const int m = xt_match(q, g, tag);
+    if (m >= 0) return (uint32_t)m;
+    const int e = q.x == 0u ? 0 : q.y == 0u ? 1 : q.z == 0u ? 2 : q.w == 0u ? 3 : -1;
+    if (e >= 0) {
+      const uint32_t prev = atomicCAS(&t.keys[g + e], 0u, tag);
+      if (prev == 0u) { ins = true; return g + e; }
+      if (prev == tag) return g + e;
+      continue;
+    }
+    g = (g + 4u) & t.mask;
+  }
 }
 
 __host__ __device__ constexpr size_t xt_bytes(int T) { return (size_t)T * 16; }
@@ -175,7 +200,14 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   // settle + compact in place: (double value, key) pairs over the front of the table
   double* vals = reinterpret_cast<double*>(t.lo);
   int* keys = reinterpret_cast<int*>(t.keys);
-  int U = 0, D = 0;
+  // speculative bound: 0.9 x the source's previous L-th score (a full current row's minimum), kept
+  // only when at least L keys reach it -- the top-L then lies among them (exact either way)
+  double tspec = 0.0;
+  if (!a.unit && !a.mc) {
+    const int64_t cr = s.lrow((a.active == 1) ? a.sB : a.sA, v);
+    if (s.len[cr] == s.L) tspec = fmax(tau, XR_SPEC * s.rmin[cr]);
+  }
+  int U = 0, D = 0, Uhi = 0;
   for (int base0 = 0; base0 < T; base0 += WAVE) {
     const int i = base0 + lane_id();
     const uint32_t kt = t.keys[i];
@@ -185,6 +217,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
     const bool keep = occ && x >= tau;
     const uint64_t m = __ballot(keep);
     D += __popcll(__ballot(occ));
+    Uhi += __popcll(__ballot(keep && x >= tspec));
     wave_fence();
     if (keep) {
       const int pos = U + __popcll(m & lanemask_lt());
@@ -193,6 +226,22 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
     }
     wave_fence();
     U += __popcll(m);
+  }
+  if (tspec > tau && Uhi >= (int)s.L && Uhi < U) {
+    // keep only the entries at or above the speculative bound (in place, order kept)
+    int U2 = 0;
+    for (int i0 = 0; i0 < U; i0 += WAVE) {
+      const int i = i0 + lane_id();
+      const double x = i < U ? vals[i] : 0.0;
+      const int k = i < U ? keys[i] : 0;
+      const bool keep = i < U && x >= tspec;
+      const uint64_t m = __ballot(keep);
+      wave_fence();
+      if (keep) { const int pos = U2 + __popcll(m & lanemask_lt()); vals[pos] = x; keys[pos] = k; }
+      wave_fence();
+      U2 += __popcll(m);
+    }
+    U = U2;
   }
   if (dlast && !a.unit && lane_id() == 0) dlast[v] = D;  // (init counts predict nothing)
   finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return vals[i]; }, s, a, hist, rv, rk, Lp, hk, hv,
@@ -283,7 +332,6 @@ __device__ __forceinline__ bool xr_stop(const XrLds& x, int budget) {
 //           or above the current bound are appended.
 // The row itself is written by k_xfin1 / k_xfinal from the list.
 constexpr int XR_SLOTS = 8;  // table slots per thread (T <= 8 * blockDim: T / W = 512 in every class)
-constexpr double XR_SPEC = 0.9;  // speculative bound of a one-range source: this x its previous L-th score
 __device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& s, const IterArgs& a,
                                           const XDesc& xd, int d, bool publish, double tau0, double tau_spec,
                                           unsigned long long* xtau, int32_t* pk, double* ps, uint32_t* pc,
@@ -464,12 +512,14 @@ __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, 
       if (xr_stop(x, budget)) break;
       xr_apply(x, i < e && xr_in(key, r, R), key, factor, budget);
     }
-  } else if (e - b >= (int64_t)W * WAVE) {
-    for (int64_t w0 = b + (int64_t)wv * WAVE; w0 < e; w0 += (int64_t)W * WAVE)
-      hub_window_walk_part(g, s, a, w0, min(e, w0 + WAVE), fl, fn, WalkRowMin{&mb, (int)s.L}, 0, 1);
   } else {
-    for (int64_t w0 = b; w0 < e; w0 += WAVE)
-      hub_window_walk_part(g, s, a, w0, min(e, w0 + WAVE), fl, fn, WalkRowMin{&mb, (int)s.L}, wv, W);
+    // each wave walks its own contiguous share of the successor list (one window setup per 64
+    // successors, every wave busy at once); sharing each window among the waves cost every wave
+    // the window's dependent setup loads once per window, one window after another
+    const int64_t chunk = (e - b + W - 1) / W;
+    const int64_t c0 = b + (int64_t)wv * chunk, c1 = min(e, c0 + chunk);
+    for (int64_t w0 = c0; w0 < c1; w0 += WAVE)
+      hub_window_walk(g, s, a, w0, min(c1, w0 + WAVE), fl, fn, WalkRowMin{&mb, (int)s.L});
   }
   __syncthreads();
   xr_lap(a, 184, tph);
@@ -551,27 +601,79 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
   int hk = -1;
   unsigned long long hlo = 0ull;
   uint32_t hhi = 0u;
+  // A batch's XB_BATCH groups are applied together: their group-of-four probe reads issued back
+  // to back, then the rare misses (new keys, longer probes) resolved one group after another,
+  // then all returning low-word adds, then the high-word adds -- a few dependent LDS round trips
+  // per batch instead of per group (the waves sat 59 % of their cycles waiting).
+  // below budget_fast (W * XB_BATCH * 64 keys of slack) the batch goes at once; past it, group by
+  // group with the per-group budget check (a probe must always find an empty slot)
+  const int budget_fast = T - W * WAVE * XB_BATCH - WAVE;
   auto apply = [&](int64_t g0, const Batch& hr) {
+    if (xr_stop(x, budget_fast)) {
+#pragma unroll
+      for (int k = 0; k < XB_BATCH; k++) {
+        const int64_t gk = g0 + (int64_t)k * W;
+        if (gk < ng && !xr_stop(x, budget)) {
+          bool valid = gk * WAVE + lane_id() < nb;
+          const int key = rec_key(hr.r[k]);
+          const double p = rec_sc(hr.r[k]) * factor;
+          if (valid && key == hk) {
+            unsigned long long lo;
+            uint32_t hi;
+            xs_conv(p, lo, hi);
+            const unsigned long long nl = hlo + lo;
+            hhi += hi + (nl < hlo ? 1u : 0u);
+            hlo = nl;
+            valid = false;
+          }
+          xr_apply(x, valid, key, p, budget);
+        }
+      }
+      return;
+    }
+    bool v[XB_BATCH];
+    int key[XB_BATCH];
+    unsigned long long lo[XB_BATCH];
+    uint32_t hi[XB_BATCH], g[XB_BATCH];
+    uint4 q[XB_BATCH];
 #pragma unroll
     for (int k = 0; k < XB_BATCH; k++) {
       const int64_t gk = g0 + (int64_t)k * W;
-      if (gk < ng && !xr_stop(x, budget)) {
-        const int64_t q = gk * WAVE + lane_id();
-        const int key = rec_key(hr.r[k]);
-        const double p = rec_sc(hr.r[k]) * factor;
-        bool valid = q < nb;
-        if (valid && key == hk) {
-          unsigned long long lo;
-          uint32_t hi;
-          xs_conv(p, lo, hi);
-          const unsigned long long nl = hlo + lo;
-          hhi += hi + (nl < hlo ? 1u : 0u);
-          hlo = nl;
-          valid = false;
-        }
-        xr_apply(x, valid, key, p, budget);
+      key[k] = rec_key(hr.r[k]);
+      v[k] = gk < ng && gk * WAVE + lane_id() < nb;
+      xs_conv(rec_sc(hr.r[k]) * factor, lo[k], hi[k]);
+      if (v[k] && key[k] == hk) {
+        const unsigned long long nl = hlo + lo[k];
+        hhi += hi[k] + (nl < hlo ? 1u : 0u);
+        hlo = nl;
+        v[k] = false;
+      }
+      g[k] = hash32((uint32_t)key[k]) & x.t.mask & ~3u;
+    }
+#pragma unroll
+    for (int k = 0; k < XB_BATCH; k++) q[k] = *reinterpret_cast<const uint4*>(x.t.keys + g[k]);
+    int h[XB_BATCH];
+    int nins = 0;
+#pragma unroll
+    for (int k = 0; k < XB_BATCH; k++) {
+      h[k] = xt_match(q[k], g[k], (uint32_t)key[k] + 1u);
+      if (__ballot(v[k] && h[k] < 0)) {
+        bool ins = false;
+        if (v[k] && h[k] < 0) h[k] = (int)xt_slot(x.t, key[k], ins);
+        nins += __popcll(__ballot(ins));
       }
     }
+    // (unconditional atomics -- an idle lane adds 0 to slot 0 -- so the four returning adds are in
+    // flight together: under a per-lane branch each one ended in its own wait)
+    unsigned long long old[XB_BATCH];
+#pragma unroll
+    for (int k = 0; k < XB_BATCH; k++) {
+      if (!v[k]) { h[k] = 0; lo[k] = 0ull; hi[k] = 0u; }
+      old[k] = atomicAdd(&x.t.lo[h[k]], lo[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < XB_BATCH; k++) atomicAdd(&x.t.hi[h[k]], hi[k] + ((old[k] + lo[k] < old[k]) ? 1u : 0u));
+    if (nins && lane_id() == 0) atomicAdd(&x.w.misc[XM_FILL], nins);
   };
   Batch ba, bb;
   const int64_t step = (int64_t)W * XB_BATCH;
