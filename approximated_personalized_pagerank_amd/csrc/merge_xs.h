@@ -605,32 +605,13 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
   // to back, then the rare misses (new keys, longer probes) resolved one group after another,
   // then all returning low-word adds, then the high-word adds -- a few dependent LDS round trips
   // per batch instead of per group (the waves sat 59 % of their cycles waiting).
-  // below budget_fast (W * XB_BATCH * 64 keys of slack) the batch goes at once; past it, group by
-  // group with the per-group budget check (a probe must always find an empty slot)
-  const int budget_fast = T - W * WAVE * XB_BATCH - WAVE;
+  // Budget: before a group inserts new keys its wave checks the shared count (an LDS read) and
+  // adds the group's inserts to it right after, before its next check, so at most one group per
+  // wave (64 keys) is ever uncounted and the table holds at most budget + W * 64 keys. (A batch
+  // that checked once for its four groups let the other waves' checks miss up to 4 * 64 keys of
+  // each batch in flight: a table could fill up and a probe run forever.) Past the budget a
+  // wave drops its new keys: the source overflows and is merged again.
   auto apply = [&](int64_t g0, const Batch& hr) {
-    if (xr_stop(x, budget_fast)) {
-#pragma unroll
-      for (int k = 0; k < XB_BATCH; k++) {
-        const int64_t gk = g0 + (int64_t)k * W;
-        if (gk < ng && !xr_stop(x, budget)) {
-          bool valid = gk * WAVE + lane_id() < nb;
-          const int key = rec_key(hr.r[k]);
-          const double p = rec_sc(hr.r[k]) * factor;
-          if (valid && key == hk) {
-            unsigned long long lo;
-            uint32_t hi;
-            xs_conv(p, lo, hi);
-            const unsigned long long nl = hlo + lo;
-            hhi += hi + (nl < hlo ? 1u : 0u);
-            hlo = nl;
-            valid = false;
-          }
-          xr_apply(x, valid, key, p, budget);
-        }
-      }
-      return;
-    }
     bool v[XB_BATCH];
     int key[XB_BATCH];
     unsigned long long lo[XB_BATCH];
@@ -653,14 +634,18 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
 #pragma unroll
     for (int k = 0; k < XB_BATCH; k++) q[k] = *reinterpret_cast<const uint4*>(x.t.keys + g[k]);
     int h[XB_BATCH];
-    int nins = 0;
 #pragma unroll
     for (int k = 0; k < XB_BATCH; k++) {
       h[k] = xt_match(q[k], g[k], (uint32_t)key[k] + 1u);
       if (__ballot(v[k] && h[k] < 0)) {
-        bool ins = false;
-        if (v[k] && h[k] < 0) h[k] = (int)xt_slot(x.t, key[k], ins);
-        nins += __popcll(__ballot(ins));
+        if (xr_stop(x, budget)) {
+          if (h[k] < 0) v[k] = false;
+        } else {
+          bool ins = false;
+          if (v[k] && h[k] < 0) h[k] = (int)xt_slot(x.t, key[k], ins);
+          const int nins = __popcll(__ballot(ins));
+          if (nins && lane_id() == 0) atomicAdd(&x.w.misc[XM_FILL], nins);
+        }
       }
     }
     // (unconditional atomics -- an idle lane adds 0 to slot 0 -- so the four returning adds are in
@@ -673,7 +658,6 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
     }
 #pragma unroll
     for (int k = 0; k < XB_BATCH; k++) atomicAdd(&x.t.hi[h[k]], hi[k] + ((old[k] + lo[k] < old[k]) ? 1u : 0u));
-    if (nins && lane_id() == 0) atomicAdd(&x.w.misc[XM_FILL], nins);
   };
   Batch ba, bb;
   const int64_t step = (int64_t)W * XB_BATCH;
