@@ -1162,7 +1162,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
                           const std::vector<int64_t>& dest, unsigned long long* maxdiff, int depth) {
   const size_t n = src.size();
   if (!n) return PPR_OK;
-  if (depth > 12) return PPR_ERR_RANGE;  // (cannot happen: estimates grow 4x per redo up to the candidate count)
+  if (depth > 12) return PPR_ERR_RANGE;  // (cannot happen: estimates grow 4x per redo)
   hipStream_t st = p->stream;
   hipStream_t sw = p->stream3 ? p->stream3 : st;
   DevGraph g{p->d_rp, p->d_colx, p->n};
@@ -1316,7 +1316,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
     }
   }
   if (fallback.empty()) return PPR_OK;
-  // overflowed tables: those sources again, expecting 4x the distinct keys (at most the candidates)
+  // overflowed tables: those sources again, expecting 4x the distinct keys
   p->xr_redo += (int64_t)fallback.size();
   std::vector<int32_t> rsrc, rcand, rdeg;
   std::vector<int64_t> rdest;
@@ -1332,7 +1332,10 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       rsrc.push_back(src[i]);
       rcand.push_back(cand[i]);
       rdeg.push_back(deg[i]);
-      rdest.push_back(std::min<int64_t>((int64_t)cand[i], 4 * dest[i] + 64));
+      // (an estimate already at the candidate count still grows: with the fill target near the
+      // budget a range or bucket can overflow by hash variance alone, and only more of them help)
+      const int64_t grown = 4 * dest[i] + 64;
+      rdest.push_back(dest[i] >= (int64_t)cand[i] ? grown : std::min<int64_t>((int64_t)cand[i], grown));
     }
   }
   return run_xhubs_list(p, a, rsrc, rcand, rdeg, rdest, maxdiff, depth + 1);

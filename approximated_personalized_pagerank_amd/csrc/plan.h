@@ -179,7 +179,7 @@ struct ppr_plan {
   int32_t* d_dlast = nullptr;         // [n] distinct keys of each source's last merge (hub planning)
   int xr_T = 8192, xr_W = 16;         // PPR_XR_T: range / bucket workgroup table slots (waves = T / 512)
   int xr_rmax = 3;                    // PPR_XR_RMAX: most key ranges a source is walked in (beyond: partition)
-  int xr_fill = 60;                   // PPR_XR_FILL: planned distinct keys per table, % of its slots
+  int xr_fill = 80;                   // PPR_XR_FILL: planned distinct keys per table, % of its slots
   int xf_stage = 4096;                // k_xfinal entries staged in LDS
   int xr_dscale = 100;                // PPR_XR_DSCALE (tests): distinct-key estimates scaled, % (forces overflows)
   unsigned char* d_xs = nullptr;      // range-workgroup scratch (descriptors, tasks, lists)
