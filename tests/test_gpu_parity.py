@@ -256,6 +256,8 @@ def test_gpu_speculative_bound_bit_exact(env, want_redo, monkeypatch, capfd, cha
     {"PPR_XR_RMAX": "1", "PPR_HUB_BUDGET": "4096"},               # many partition batches, three regions
     {"PPR_XR_RMAX": "1", "PPR_HUB_BUDGET": "4096", "PPR_HUB_STREAMS": "1"},  # ... on one stream
     {"PPR_XR_RMAX": "1", "PPR_XR_FILL": "20", "PPR_HUB_MIX": "0"},  # many buckets, list order
+    {"PPR_XR_FILL": "85"},                                        # tables planned at the budget: overflows by
+    {"PPR_XR_FILL": "85", "PPR_XR_RMAX": "1"},                    # hash variance, redone past the candidate count
     {"PPR_TIER_MASK": "0x0"},                                     # no wave tier: every source in workgroups
     {"PPR_TIER_MASK": "0xf"},                                     # no partition: ranges only
     {"PPR_WAVE_WPB": "4"},                                        # 4-wave blocks in the wave tier
