@@ -43,7 +43,11 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
         print(r.stderr, file=sys.stderr)
         raise subprocess.CalledProcessError(r.returncode, cmd)
     if not any(str(d).startswith("PPR_PHASE_TIMING") for d in defines):  # (diagnostic variants keep counters in scratch)
-        check_resources(r.stderr)
+        try:
+            check_resources(r.stderr)
+        except RuntimeError:
+            os.remove(out + ".tmp")  # (the library in place stays the last accepted build)
+            raise
     os.replace(out + ".tmp", out)
     return out
 
