@@ -346,18 +346,22 @@ __device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& 
   int kk[XR_SLOTS];
   double kv[XR_SLOTS];
   int c = 0, c_hi = 0;
+  // (all slot reads issued unconditionally and back to back -- a read under `if (key)` waited on
+  // its own; an index past T re-reads slot T - 1 and is dropped)
+  uint32_t kt[XR_SLOTS], kh[XR_SLOTS];
+  unsigned long long kl[XR_SLOTS];
 #pragma unroll
   for (int j = 0; j < XR_SLOTS; j++) {
-    const int i = threadIdx.x + j * (int)blockDim.x;
-    kk[j] = -1;
-    kv[j] = 0.0;
-    if (i < T) {
-      const uint32_t kt = x.t.keys[i];
-      if (kt) {
-        kv[j] = xs_to_double(x.t.hi[i], x.t.lo[i]);
-        if (kv[j] >= tau0) kk[j] = (int)kt - 1;
-      }
-    }
+    const int i = min(T - 1, (int)threadIdx.x + j * (int)blockDim.x);
+    kt[j] = x.t.keys[i];
+    kl[j] = x.t.lo[i];
+    kh[j] = x.t.hi[i];
+  }
+#pragma unroll
+  for (int j = 0; j < XR_SLOTS; j++) {
+    const bool in = (int)threadIdx.x + j * (int)blockDim.x < T;
+    kv[j] = xs_to_double(kh[j], kl[j]);
+    kk[j] = (in && kt[j] && kv[j] >= tau0) ? (int)kt[j] - 1 : -1;
     c += kk[j] >= 0 ? 1 : 0;
     c_hi += (kk[j] >= 0 && kv[j] >= ts_hi) ? 1 : 0;
   }
