@@ -46,6 +46,7 @@
 #include "merge_glb.h"
 #include "merge_hot.h"
 #include "merge_xs.h"
+#include "merge_sv.h"
 
 using namespace pprk;
 
@@ -396,6 +397,23 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       int32_t caps[NT + 1];
       for (int t = 0; t <= NT; t++) caps[t] = p->tierCap[t];
       if (hipMemcpy(p->d_tier_cap, caps, sizeof(caps), hipMemcpyHostToDevice) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
+      // the sieve (merge_sv.h) for the wide sources: its prev table takes 2 Lp <= one slot per thread
+      const char* s0 = getenv("PPR_SV");
+      p->sv_enabled = !(s0 && atoi(s0) == 0) && 2 * p->Lp <= SV_THREADS && sv_lds_bytes(p->Lp) <= 160 * 1024 &&
+                      svf_lds_bytes(p->Lp) <= 160 * 1024;
+      const char* s1 = getenv("PPR_SV_SLICE");
+      const char* s2 = getenv("PPR_SV_MIN");
+      if (s1) p->sv_slice = std::max<int64_t>(64, atoll(s1));
+      if (s2) p->sv_min = std::max<int64_t>(0, atoll(s2));
+      const char* s3 = getenv("PPR_SV_BUDGET");
+      if (s3) p->sv_budget = std::max(0, std::min(SV_XT_BUDGET, atoi(s3)));
+      if (p->sv_enabled &&
+          (hipStreamCreateWithFlags(&p->stream_sv, hipStreamNonBlocking) != hipSuccess ||
+           hipStreamCreateWithFlags(&p->stream_sv2, hipStreamNonBlocking) != hipSuccess ||
+           hipEventCreateWithFlags(&p->ev_sv, hipEventDisableTiming) != hipSuccess)) {
+        plan_free(p);
+        return PPR_ERR_HIP;
+      }
     }
   }
   // every kernel that may take more than the default 64 KB of dynamic LDS; a refusal (e.g. a
@@ -425,6 +443,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         {(const void*)k_xb, "k_xb"},
         {(const void*)k_xfinal<XDesc>, "k_xfinal<XDesc>"},
         {(const void*)k_xfinal<HubDesc>, "k_xfinal<HubDesc>"},
+        {(const void*)k_sv1, "k_sv1"},
+        {(const void*)k_svA, "k_svA"},
+        {(const void*)k_svB, "k_svB"},
+        {(const void*)k_svF, "k_svF"},
     };
     for (const auto& k : big_lds)
       if (hipFuncSetAttribute(k.first, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
@@ -1341,9 +1363,144 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
   return run_xhubs_list(p, a, rsrc, rcand, rdeg, rdest, maxdiff, depth + 1);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The sieve (merge_sv.h) for sources `src` (candidate counts `cand`): one-slice sources by k_sv1 on
+// stream_sv2 (largest first), multi-slice sources by k_svA -> k_svB -> k_svF on stream_sv. The
+// launches are asynchronous; sieve_collect waits and returns the sources handed back.
+struct SvRun {
+  std::vector<int32_t> v;   // source of each descriptor
+  size_t o_ovl = 0;         // offset of the overflow list in d_sv
+  bool live = false;
+};
+
+static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& src,
+                        const std::vector<int32_t>& cand, const std::vector<int32_t>& deg, unsigned long long* maxdiff,
+                        SvRun& run) {
+  const size_t n = src.size();
+  run.live = false;
+  if (!n) return PPR_OK;
+  DevGraph g{p->d_rp, p->d_colx, p->n};
+  const DevSlab s = dev_slab(p);
+  const int Lp = p->Lp;
+  // multi-slice sources first (descriptors [0, nm)), then the one-slice ones by candidates, descending
+  std::vector<size_t> multi, one;
+  for (size_t i = 0; i < n; i++) ((int64_t)cand[i] > p->sv_slice ? multi : one).push_back(i);
+  std::stable_sort(one.begin(), one.end(), [&](size_t x, size_t y) { return cand[x] > cand[y]; });
+  const size_t nm = multi.size(), nx = n;
+  std::vector<SvDesc> desc;
+  std::vector<SvTask> tasks;
+  desc.reserve(nx);
+  run.v.clear();
+  int64_t tg_total = 0;
+  for (size_t k = 0; k < nm; k++) {
+    const size_t i = multi[k];
+    SvDesc d{};
+    d.v = src[i];
+    d.S = (int32_t)std::min<int64_t>(((int64_t)cand[i] + p->sv_slice - 1) / p->sv_slice, std::max<int32_t>(1, deg[i]));
+    d.factor = p->damping / (double)deg[i];
+    d.gsk = (int64_t)k * SV_R * SV_W;
+    d.gpt = (int64_t)k * 2 * Lp;
+    // every slice flushes at most its table's keys: half-full global table at worst
+    d.tg = pow2_at_least(std::min<int64_t>(2 * (int64_t)d.S * (SV_XT_BUDGET + SV_WAVES * WAVE + 1),
+                                           2 * (int64_t)cand[i] + 64));
+    d.gxt = tg_total;
+    tg_total += d.tg;
+    for (int s2 = 0; s2 < d.S; s2++) tasks.push_back(SvTask{(int32_t)k, s2});
+    desc.push_back(d);
+    run.v.push_back(d.v);
+  }
+  for (size_t i : one) {
+    SvDesc d{};
+    d.v = src[i];
+    d.S = 1;
+    d.factor = p->damping / (double)deg[i];
+    desc.push_back(d);
+    run.v.push_back(d.v);
+  }
+  const size_t nt = tasks.size();
+  // d_sv: desc | tasks | zeroed: ovl[1 + nx] | oflag[nm] | gpt | gsk | gkeys | ga | gb
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t off = 0;
+  const size_t o_d = off; off = al(off + sizeof(SvDesc) * nx);
+  const size_t o_t = off; off = al(off + sizeof(SvTask) * (nt + 1));
+  const size_t o_z = off;
+  const size_t o_ov = off; off = al(off + 4 * (1 + nx));
+  const size_t o_of = off; off = al(off + 4 * (nm + 1));
+  const size_t o_pt = off; off = al(off + 8 * 2 * (size_t)Lp * nm);
+  const size_t o_sk = off; off = al(off + 4 * (size_t)SV_R * SV_W * nm);
+  const size_t o_gk = off; off = al(off + 4 * (size_t)tg_total);
+  const size_t o_ga = off; off = al(off + 8 * (size_t)tg_total);
+  const size_t o_gb = off; off = al(off + 8 * (size_t)tg_total);
+  const size_t total = off;
+  { int r = ensure_dev(&p->d_sv, &p->sv_bytes, total); if (r) return r; }
+  const size_t up = o_t + sizeof(SvTask) * nt;
+  { int r = ensure_pinned(&p->h_sv_pin, &p->h_sv_bytes, up); if (r) return r; }
+  unsigned char* hb = (unsigned char*)p->h_sv_pin;
+  std::memcpy(hb + o_d, desc.data(), sizeof(SvDesc) * nx);
+  if (nt) std::memcpy(hb + o_t, tasks.data(), sizeof(SvTask) * nt);
+  unsigned char* b = p->d_sv;
+  hipStream_t s1 = p->stream_sv, s2 = p->stream_sv2;
+  HIP_OK(hipMemcpyAsync(b, hb, up, hipMemcpyHostToDevice, s1));
+  HIP_OK(hipMemsetAsync(b + o_z, 0, total - o_z, s1));
+  // the one-slice stream starts once the descriptors are up and the overflow list is zeroed
+  HIP_OK(hipEventRecord(p->ev_sv, s1));
+  HIP_OK(hipStreamWaitEvent(s2, p->ev_sv, 0));
+  const SvDesc* d_d = (const SvDesc*)(b + o_d);
+  const SvTask* d_t = (const SvTask*)(b + o_t);
+  int32_t* d_ov = (int32_t*)(b + o_ov);
+  int32_t* d_of = (int32_t*)(b + o_of);
+  unsigned long long* d_pt = (unsigned long long*)(b + o_pt);
+  uint32_t* d_sk = (uint32_t*)(b + o_sk);
+  uint32_t* d_gk = (uint32_t*)(b + o_gk);
+  unsigned long long* d_ga = (unsigned long long*)(b + o_ga);
+  unsigned long long* d_gb = (unsigned long long*)(b + o_gb);
+  const size_t lds = sv_lds_bytes(Lp);
+  if (nx > nm) {
+    hipLaunchKernelGGL(k_sv1, dim3((unsigned)(nx - nm)), dim3(SV_THREADS), lds, s2, g, s, a, d_d, (int)nm, Lp, p->sv_budget,
+                       maxdiff, p->d_stats, d_ov);
+    HIP_OK(hipGetLastError());
+    p->merge_launches++;
+  }
+  if (nm) {
+    hipLaunchKernelGGL(k_svA, dim3((unsigned)nt), dim3(SV_THREADS), lds, s1, g, s, a, d_d, d_t, Lp, d_sk, d_pt);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(k_svB, dim3((unsigned)nt), dim3(SV_THREADS), lds, s1, g, s, a, d_d, d_t, Lp, p->sv_budget, d_sk,
+                       d_pt, d_gk, d_ga, d_gb, d_of);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(k_svF, dim3((unsigned)nm), dim3(256), svf_lds_bytes(Lp), s1, s, a, d_d, Lp, d_pt, d_gk, d_ga,
+                       d_gb, d_of, d_ov, maxdiff, p->d_stats);
+    HIP_OK(hipGetLastError());
+    p->merge_launches += 3;
+  }
+  p->sv_sources += (int64_t)nx;
+  run.o_ovl = o_ov;
+  run.live = true;
+  return PPR_OK;
+}
+
+// wait for the sieve, append the sources it handed back (table overflows) to `back`
+static int sieve_collect(ppr_plan* p, SvRun& run, std::vector<int32_t>& back) {
+  if (!run.live) return PPR_OK;
+  run.live = false;
+  HIP_OK(hipEventRecord(p->ev_sv, p->stream_sv2));
+  HIP_OK(hipStreamWaitEvent(p->stream_sv, p->ev_sv, 0));
+  int32_t novf = 0;
+  HIP_OK(hipMemcpyAsync(&novf, p->d_sv + run.o_ovl, 4, hipMemcpyDeviceToHost, p->stream_sv));
+  HIP_OK(hipStreamSynchronize(p->stream_sv));
+  if (!novf) return PPR_OK;
+  std::vector<int32_t> od(novf);
+  HIP_OK(hipMemcpyAsync(od.data(), p->d_sv + run.o_ovl + 4, 4 * (size_t)novf, hipMemcpyDeviceToHost, p->stream_sv));
+  HIP_OK(hipStreamSynchronize(p->stream_sv));
+  for (int32_t d : od) back.push_back(run.v[(size_t)d]);
+  p->sv_redo += novf;
+  return PPR_OK;
+}
+
 // the exact-sum merge of the `count` sources of device list `d_list` (hub tier, or any tier the
-// plan leaves without a wave kernel): candidate counts, degrees and last distinct counts gathered
-// on the device, the estimate planned on the host
+// plan leaves without a wave kernel): candidate counts, degrees, last distinct counts and current
+// row lengths gathered on the device; sources with a full current row go through the sieve
+// (merge_sv.h), the others -- and any the sieve hands back -- through the range / partition
+// engines with the distinct-key estimate planned on the host
 static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int64_t count, unsigned long long* maxdiff) {
   if (count <= 0) return PPR_OK;
   hipStream_t st = p->stream;
@@ -1351,29 +1508,66 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
   {
     size_t capb = p->h_hub_cap * 12;
     void* ptr = p->h_hub_pin;
-    int r = ensure_pinned(&ptr, &capb, 16 * nh);
+    int r = ensure_pinned(&ptr, &capb, 20 * nh);
     if (r) return r;
     p->h_hub_pin = (int32_t*)ptr;
     p->h_hub_cap = capb / 12;
   }
-  if (3 * nh > (size_t)p->n) { int r = ensure_dev((unsigned char**)&p->d_gath, &p->gath_bytes, 12 * nh); if (r) return r; }
-  int32_t* d_g = 3 * nh > (size_t)p->n ? p->d_gath : p->d_ovf;
+  if (4 * nh > (size_t)p->n) { int r = ensure_dev((unsigned char**)&p->d_gath, &p->gath_bytes, 16 * nh); if (r) return r; }
+  int32_t* d_g = 4 * nh > (size_t)p->n ? p->d_gath : p->d_ovf;
   int32_t* h = p->h_hub_pin;
   HIP_OK(hipMemcpyAsync(h, d_list, 4 * nh, hipMemcpyDeviceToHost, st));
-  hipLaunchKernelGGL(k_gather_cand_deg, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_list, (int64_t)nh,
-                     p->d_cand, p->d_rp, d_g, (const int32_t*)p->d_dlast);
+  hipLaunchKernelGGL(k_gather_sv, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, d_list, (int64_t)nh,
+                     p->d_cand, p->d_rp, (const int32_t*)p->d_dlast, dev_slab(p), a, d_g);
   HIP_OK(hipGetLastError());
-  HIP_OK(hipMemcpyAsync(h + nh, d_g, 12 * nh, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(h + nh, d_g, 16 * nh, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
-  std::vector<int32_t> src(h, h + nh), cand(h + nh, h + 2 * nh), deg(h + 2 * nh, h + 3 * nh);
-  std::vector<int64_t> dest(nh);
-  for (size_t i = 0; i < nh; i++) {
-    // distinct keys expected: the last merge's count (rows change little between updates) plus a
-    // margin, else (first merge) 60 % of the candidates; never more than the candidates + 1
+  std::vector<int32_t> hcopy(h, h + 5 * nh);  // (the pinned buffer is restaged by later calls)
+  h = hcopy.data();
+  const bool sieve = p->sv_enabled && a.xs && !a.unit && !a.mc && p->hot_n == 0;
+  std::vector<int32_t> src, cand, deg, ssrc, scand, sdeg;
+  std::vector<int64_t> dest;
+  // distinct keys expected: the last merge's count (rows change little between updates) plus a
+  // margin, else (first merge) 60 % of the candidates; never more than the candidates + 1
+  auto estimate = [&](size_t i) {
     const int64_t dl = h[3 * nh + i];
-    const int64_t c = (int64_t)cand[i];
-    dest[i] = std::min<int64_t>(c, dl > 0 ? dl + dl / 8 + 64 : c * 3 / 5 + 64);
-    if (p->xr_dscale != 100) dest[i] = std::max<int64_t>(1, dest[i] * p->xr_dscale / 100);
+    const int64_t c = (int64_t)h[nh + i];
+    int64_t x = std::min<int64_t>(c, dl > 0 ? dl + dl / 8 + 64 : c * 3 / 5 + 64);
+    if (p->xr_dscale != 100) x = std::max<int64_t>(1, x * p->xr_dscale / 100);
+    return x;
+  };
+  for (size_t i = 0; i < nh; i++) {
+    const int32_t c = h[nh + i];
+    if (sieve && h[4 * nh + i] == (int32_t)p->L && c >= p->sv_min && c < (1 << 30)) {
+      ssrc.push_back(h[i]);
+      scand.push_back(c);
+      sdeg.push_back(h[2 * nh + i]);
+    } else {
+      src.push_back(h[i]);
+      cand.push_back(c);
+      deg.push_back(h[2 * nh + i]);
+      dest.push_back(estimate(i));
+    }
+  }
+  SvRun run;
+  if (!ssrc.empty()) { int r = sieve_launch(p, a, ssrc, scand, sdeg, maxdiff, run); if (r) return r; }
+  if (!src.empty()) { int r = run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0); if (r) return r; }
+  std::vector<int32_t> back;
+  { int r = sieve_collect(p, run, back); if (r) return r; }
+  if (back.empty()) return PPR_OK;
+  // handed back: the range / partition engines, with the usual estimate
+  std::vector<std::pair<int32_t, size_t>> idx(nh);
+  for (size_t i = 0; i < nh; i++) idx[i] = {h[i], i};
+  std::sort(idx.begin(), idx.end());
+  src.clear(); cand.clear(); deg.clear(); dest.clear();
+  for (int32_t v : back) {
+    auto it = std::lower_bound(idx.begin(), idx.end(), std::make_pair(v, (size_t)0));
+    if (it == idx.end() || it->first != v) return PPR_ERR_HIP;
+    const size_t i = it->second;
+    src.push_back(v);
+    cand.push_back(h[nh + i]);
+    deg.push_back(h[2 * nh + i]);
+    dest.push_back(estimate(i));
   }
   return run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0);
 }

@@ -69,10 +69,10 @@ struct ppr_plan {
   // 4096 (with 8) ... stores nothing, 8192 (with 8) ... loads no scores, 16384 (with 8) ... only
   // counts (non-returning rank atomics), 32768 (with 8) ... only walks
   int whatif = 0;
-  int nt_loads = 0;
+  int nt_loads = 0;         // PPR_NT (IterArgs::nt): non-temporal candidate gathers (1) / staged-record reads (2)
   double spec_ratio = 0.0;  // PPR_SPEC: speculative hub pruning bound (ppr_common.h spec_tau), 0 = off
   int spec_from = 6;        // PPR_SPEC_FROM: first iteration that speculates (rows settle after a few)
-  int64_t spec_redo = 0;    // hub sources redone after a failed speculation (PPR_TIMING at destroy)    // PPR_NT (IterArgs::nt): non-temporal candidate gathers (1) / staged-record reads (2)
+  int64_t spec_redo = 0;    // hub sources redone after a failed speculation (PPR_TIMING at destroy)
   int wg_max_passes = 64;  // (WG_MAX_PASSES) PPR_WG_PASSES (tests): workgroup-tier key-bucket passes before overflow
   bool hub_enabled = true;
   unsigned long long* d_maxdiff = nullptr;  // PPR_MAX_ITER_STATS + 1
@@ -187,6 +187,18 @@ struct ppr_plan {
   void* h_xs_pin = nullptr;           // pinned staging of its descriptors and tasks
   size_t h_xs_bytes = 0;
   int64_t xr_redo = 0;                // sources redone after a table overflow (PPR_TIMING at destroy)
+  // sieve merge of the wide exact-sum sources (merge_sv.h): PPR_SV=0 turns it off
+  bool sv_enabled = false;
+  int64_t sv_slice = 1LL << 18;       // PPR_SV_SLICE: candidates per slice workgroup
+  int64_t sv_min = 0;                 // PPR_SV_MIN: sources with fewer candidates keep the range engines
+  int sv_budget = 2457;               // PPR_SV_BUDGET (tests): passing keys a table takes (<= SV_XT_BUDGET)
+  hipStream_t stream_sv = nullptr, stream_sv2 = nullptr;  // multi-slice chain | one-slice sources
+  hipEvent_t ev_sv = nullptr;
+  unsigned char* d_sv = nullptr;      // descriptors, tasks, overflow list, global sketches / tables
+  size_t sv_bytes = 0;
+  void* h_sv_pin = nullptr;           // pinned staging of descriptors and tasks, overflow count
+  size_t h_sv_bytes = 0;
+  int64_t sv_sources = 0, sv_redo = 0;  // sieved sources, handed back after an overflow (PPR_TIMING)
   // MCCompletePathV2 (mccp2.hip)
   bool mc = false;
   int32_t* d_mc_walk = nullptr;       // walk set W (nodes read before their final basket exists)
@@ -232,6 +244,13 @@ inline void plan_free(ppr_plan* p) {
   if (p->h_hub_pin) hipHostFree(p->h_hub_pin);
   if (p->h_desc_pin) hipHostFree(p->h_desc_pin);
   if (p->h_xs_pin) hipHostFree(p->h_xs_pin);
+  hipFree(p->d_sv);
+  if (p->h_sv_pin) hipHostFree(p->h_sv_pin);
+  if (p->stream_sv) hipStreamDestroy(p->stream_sv);
+  if (p->stream_sv2) hipStreamDestroy(p->stream_sv2);
+  if (p->ev_sv) hipEventDestroy(p->ev_sv);
+  if (getenv("PPR_TIMING") && p->sv_sources)
+    fprintf(stderr, "ppr_timing sieve_sources %lld sieve_redo %lld\n", (long long)p->sv_sources, (long long)p->sv_redo);
   if (getenv("PPR_TIMING") && p->xr_redo)
     fprintf(stderr, "ppr_timing xr_redo_sources %lld\n", (long long)p->xr_redo);
   if (getenv("PPR_TIMING") && p->spec_redo)
@@ -291,6 +310,11 @@ inline void plan_free(ppr_plan* p) {
         fprintf(stderr, "ppr_diag k_xr: %llu workgroups, %.3e successor edges walked, %.3e distinct keys; Gcycles "
                 "(thread 0) setup %.2f accumulate %.2f settle %.2f select %.2f finish %.2f\n", h[182], (double)h[188],
                 (double)h[189], h[183] / 1e9, h[184] / 1e9, h[185] / 1e9, h[186] / 1e9, h[187] / 1e9);
+      if (h[135] || h[149])
+        fprintf(stderr, "ppr_diag sieve: %llu one-slice sources (%llu handed back), %llu multi-slice; passing keys %.3e "
+                "(candidates %.3e), entries beside the prev keys at the select %.3e; one-slice Gcycles (thread 0) "
+                "pass1 %.2f bound+bitmap %.2f pass2 %.2f select+row %.2f\n", h[135], h[137], h[149], (double)h[136],
+                (double)h[138], (double)h[139], h[145] / 1e9, h[146] / 1e9, h[147] / 1e9, h[148] / 1e9);
       if (h[154])
         fprintf(stderr, "ppr_diag k_xb: %llu workgroups, %.3e records (%.0f per bucket); Gcycles (thread 0) setup+accumulate "
                 "%.2f settle %.2f select %.2f emit %.2f\n", h[154], (double)h[159], (double)h[159] / (double)h[154],

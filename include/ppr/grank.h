@@ -10,8 +10,14 @@
 //   2. ppr_grank_csr(): BFS partitions (include/internal/pprInternal.h:29-99), upload, init,
 //      iterations, final top-K on the device, download;
 //   3. the top-K rows are materialised back into unordered_map<Key, unordered_map<Key,double>>.
+// Results vs the reference (INTEGRATION.md "Numerical contract"):
+//   default (exact sum)  every score within 1e-12 relative of the reference's: each basket value is
+//                        the exact sum of the rounded products, rounded once (the reference rounds
+//                        after every add of its fma chain, include/grank.h:114-115)
+//   PPR_SUM=chain        the reference's in-order fma chain: bit-identical scores wherever the
+//                        reference never cuts a basket at a tie
 // Which keys survive among those tied at a top-L/top-K cut: a per-source hash of the key (the
-// reference leaves it to its hash-map history); untied results are bit-identical.
+// reference leaves it to its hash-map history).
 #ifndef PPR_HIP_DROPIN_GRANK_H
 #define PPR_HIP_DROPIN_GRANK_H
 
@@ -38,36 +44,54 @@
 namespace ppr {
 namespace hipdetail {
 
-// While the result maps are built (~130 M node allocations at RMAT-22, from every host thread):
-// glibc grows each thread's malloc heap 64 MB at a time instead of 128 KB (M_TOP_PAD). Every
-// growth step is an mprotect that takes the process's mmap lock exclusively against the other
-// threads' page faults; with the default step the fill ran 3-5x slower (8 threads: 6-10 s vs
-// 1.8-2.5 s). The previous setting (MALLOC_TOP_PAD_, else glibc's 128 KB) is restored after.
+// While the result maps are built (~130 M node allocations at RMAT-22, from every host thread),
+// glibc grows each thread's malloc heap M_TOP_PAD bytes at a time (default 128 KB). Every growth
+// step is an mprotect that takes the process's mmap lock exclusively against the other threads'
+// page faults; with the default step the fill ran 3-5x slower (8 threads: 6-10 s vs 1.8-2.5 s at
+// 64 MB). mallopt is process-wide, so this is OPT-IN: PPR_HEAP_PAD=<MB> sets M_TOP_PAD for the
+// duration of the calls that are materialising results; the last of several concurrent calls to
+// finish sets it back to MALLOC_TOP_PAD_ (else glibc's 128 KB) -- glibc has no getter for a value
+// the application may have set itself, so an application that sets M_TOP_PAD should leave
+// PPR_HEAP_PAD unset (INTEGRATION.md "Host threads and memory").
 struct HeapGrowth {
 #if defined(__GLIBC__)
-  HeapGrowth() { mallopt(M_TOP_PAD, 64 << 20); }
+  static std::atomic<int>& active() {
+    static std::atomic<int> n(0);
+    return n;
+  }
+  bool on = false;
+  HeapGrowth() {
+    const char* e = getenv("PPR_HEAP_PAD");
+    const int mb = e && *e ? atoi(e) : 0;
+    if (mb <= 0) return;
+    on = true;
+    active().fetch_add(1);
+    mallopt(M_TOP_PAD, (mb > 1024 ? 1024 : mb) << 20);
+  }
   ~HeapGrowth() {
+    if (!on || active().fetch_sub(1) != 1) return;
     const char* e = getenv("MALLOC_TOP_PAD_");
     mallopt(M_TOP_PAD, e && *e ? atoi(e) : 128 * 1024);
   }
 #endif
 };
 
-// run f(begin, end) over [0, n) on the host's hardware threads (the map <-> CSR conversions
-// dominate end-to-end time once the device phase takes seconds)
-// host threads: PPR_HOST_THREADS, else OMP_NUM_THREADS (set to the CPU share on shared hosts,
-// where hardware_concurrency() reports every CPU of the machine), else hardware_concurrency()
-inline size_t host_threads() {
+// host threads of one call: the caller's count (ppr::grankMulti's nThreads), else PPR_HOST_THREADS,
+// else OMP_NUM_THREADS (set to the CPU share on shared hosts, where hardware_concurrency() reports
+// every CPU of the machine), else hardware_concurrency()
+inline size_t host_threads(size_t requested = 0) {
+  if (requested > 0) return requested;
   const char* e = getenv("PPR_HOST_THREADS");
   if (!e || !*e) e = getenv("OMP_NUM_THREADS");
   if (e && *e && atoi(e) > 0) return (size_t)atoi(e);
   return std::max<size_t>(1, std::thread::hardware_concurrency());
 }
 
+// run f(begin, end) over [0, n) on up to nt host threads (the map <-> CSR conversions dominate
+// end-to-end time once the device phase takes seconds)
 template <class F>
-inline void parallel_ranges(size_t n, F f) {
-  size_t nt = host_threads();
-  nt = std::min<size_t>(nt, std::max<size_t>(1, n / 4096));
+inline void parallel_ranges(size_t n, size_t nt, F f) {
+  nt = std::min<size_t>(std::max<size_t>(1, nt), std::max<size_t>(1, n / 4096));
   if (nt <= 1) { f((size_t)0, n); return; }
   std::vector<std::thread> th;
   th.reserve(nt);
@@ -89,15 +113,15 @@ struct Flat {
 template <typename Key, bool Copy = std::is_trivially_copyable<Key>::value && (sizeof(Key) <= 8)>
 struct KeyStore {  // (generic keys: through the pointer)
   const std::vector<const Key*>* keys = nullptr;
-  void build(const std::vector<const Key*>& k) { keys = &k; }
+  void build(const std::vector<const Key*>& k, size_t) { keys = &k; }
   const Key& at(size_t i) const { return *(*keys)[i]; }
 };
 template <typename Key>
 struct KeyStore<Key, true> {
   std::vector<Key> copy;
-  void build(const std::vector<const Key*>& k) {
+  void build(const std::vector<const Key*>& k, size_t nt) {
     copy.resize(k.size());
-    parallel_ranges(k.size(), [&](size_t b, size_t e) {
+    parallel_ranges(k.size(), nt, [&](size_t b, size_t e) {
       for (size_t i = b; i < e; i++) copy[i] = *k[i];
     });
   }
@@ -113,16 +137,16 @@ struct KeyIndex {
     x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL; x ^= x >> 27; x *= 0x94d049bb133111ebULL; x ^= x >> 31;
     return x;
   }
-  void build(const std::vector<const Key*>& k) {
-    ks.build(k);
+  void build(const std::vector<const Key*>& k, size_t nt) {
+    ks.build(k, nt);
     uint64_t cap = 16;
     while (cap < 2 * (uint64_t)k.size()) cap <<= 1;
     mask = cap - 1;
     slot.reset(new std::atomic<int32_t>[cap]);
-    parallel_ranges((size_t)cap, [&](size_t b, size_t e) {
+    parallel_ranges((size_t)cap, nt, [&](size_t b, size_t e) {
       for (size_t i = b; i < e; i++) slot[i].store(-1, std::memory_order_relaxed);
     });
-    parallel_ranges(k.size(), [&](size_t b, size_t e) {
+    parallel_ranges(k.size(), nt, [&](size_t b, size_t e) {
       for (size_t v = b; v < e; v++) {
         uint64_t h = mix((uint64_t)std::hash<Key>()(ks.at(v))) & mask;
         for (;;) {
@@ -143,32 +167,79 @@ struct KeyIndex {
   }
 };
 
+// The graph's nodes in iteration order (dense id = position), on nt threads. Node-based hash maps
+// (libstdc++, libc++) keep each bucket's nodes contiguous in their one iteration list, so the list
+// is the buckets' node runs in some bucket order: per bucket (threads) its node count and where
+// the list continues after its last node (++ of find(last key)); the bucket chain from begin()
+// gives every run's dense offset (one serial pass over non-empty buckets, not over nodes); the
+// nodes are then written run by run (threads). Any inconsistency (a library that does not keep
+// runs contiguous) falls back to one serial walk of the list.
 template <typename Key>
-inline Flat<Key> flatten(const std::unordered_map<Key, std::vector<Key>>& graph) {
-  Flat<Key> f;
+inline void iteration_order(const std::unordered_map<Key, std::vector<Key>>& graph, size_t nt,
+                            std::vector<const Key*>& keys, std::vector<const std::vector<Key>*>& succ) {
   const size_t n = graph.size();
-  // one pass over the map's nodes (each a cache miss): keys and successor lists in iteration
-  // order; everything after it runs on all host threads
-  f.keys.resize(n);
-  std::vector<const std::vector<Key>*> succ(n);
-  {
+  keys.resize(n);
+  succ.resize(n);
+  auto serial = [&] {
     size_t v = 0;
     for (const auto& kv : graph) {
-      f.keys[v] = &kv.first;
+      keys[v] = &kv.first;
       succ[v] = &kv.second;
       v++;
     }
+  };
+  const size_t B = graph.bucket_count();
+  if (nt <= 1 || n < (1u << 16) || B == 0) { serial(); return; }
+  std::vector<int64_t> cnt(B), nxt(B), start(B, -1);
+  parallel_ranges(B, nt, [&](size_t b0, size_t b1) {
+    for (size_t b = b0; b < b1; b++) {
+      int64_t c = 0;
+      const Key* last = nullptr;
+      for (auto it = graph.begin(b); it != graph.end(b); ++it) { c++; last = &it->first; }
+      cnt[b] = c;
+      nxt[b] = -1;
+      if (c) {
+        auto it = graph.find(*last);
+        ++it;
+        nxt[b] = it == graph.end() ? -2 : (int64_t)graph.bucket(it->first);
+      }
+    }
+  });
+  size_t off = 0, runs = 0;
+  for (int64_t b = (int64_t)graph.bucket(graph.begin()->first); b >= 0 && runs < B; b = nxt[(size_t)b], runs++) {
+    if (start[(size_t)b] >= 0 || !cnt[(size_t)b]) { off = n + 1; break; }  // (a bucket twice: not runs)
+    start[(size_t)b] = (int64_t)off;
+    off += (size_t)cnt[(size_t)b];
   }
+  if (off != n) { serial(); return; }
+  parallel_ranges(B, nt, [&](size_t b0, size_t b1) {
+    for (size_t b = b0; b < b1; b++) {
+      if (!cnt[b]) continue;
+      size_t v = (size_t)start[b];
+      for (auto it = graph.begin(b); it != graph.end(b); ++it, v++) {
+        keys[v] = &it->first;
+        succ[v] = &it->second;
+      }
+    }
+  });
+}
+
+template <typename Key>
+inline Flat<Key> flatten(const std::unordered_map<Key, std::vector<Key>>& graph, size_t nt) {
+  Flat<Key> f;
+  const size_t n = graph.size();
+  std::vector<const std::vector<Key>*> succ;
+  iteration_order(graph, nt, f.keys, succ);
   KeyIndex<Key> idx;
-  idx.build(f.keys);  // (threads joined: every slot is published to the readers below)
+  idx.build(f.keys, nt);  // (threads joined: every slot is published to the readers below)
   f.rp.assign(n + 1, 0);
-  parallel_ranges(n, [&](size_t b, size_t e) {
+  parallel_ranges(n, nt, [&](size_t b, size_t e) {
     for (size_t v = b; v < e; v++) f.rp[v + 1] = (int64_t)succ[v]->size();
   });
   for (size_t v = 0; v < n; v++) f.rp[v + 1] += f.rp[v];
   f.col.resize((size_t)f.rp[n]);
   std::atomic<bool> bad(false);
-  parallel_ranges(n, [&](size_t b, size_t e) {
+  parallel_ranges(n, nt, [&](size_t b, size_t e) {
     for (size_t v = b; v < e; v++) {
       int64_t o = f.rp[v];
       for (const Key& s : *succ[v]) {
@@ -215,8 +286,8 @@ struct Outer {
 // inner maps from the device's top-K rows (independent per source: all host threads)
 template <typename Key>
 inline void materialize_rows(const Flat<Key>& f, Outer<Key>& o, size_t K, const std::vector<int32_t>& ids,
-                             const std::vector<double>& sc, const std::vector<int32_t>& len) {
-  parallel_ranges(f.keys.size(), [&](size_t b, size_t e) {
+                             const std::vector<double>& sc, const std::vector<int32_t>& len, size_t nt) {
+  parallel_ranges(f.keys.size(), nt, [&](size_t b, size_t e) {
     for (size_t v = b; v < e; v++) {
       std::unordered_map<Key, double>& m = *o.row[v];
       m.reserve((size_t)len[v]);
@@ -228,11 +299,12 @@ inline void materialize_rows(const Flat<Key>& f, Outer<Key>& o, size_t K, const 
 template <typename Key>
 inline std::unordered_map<Key, std::unordered_map<Key, double>> grank_device(
     const std::unordered_map<Key, std::vector<Key>>& graph, size_t K, size_t L, size_t iterations,
-    double damping, double tolerance) {
+    double damping, double tolerance, size_t nthreads = 0) {
   if (graph.empty()) return {};
   if (K > 0xffffffffu || L > 0xffffffffu || iterations > 0xffffffffu) fail(PPR_ERR_RANGE);
+  const size_t nt = host_threads(nthreads);
   const auto t0 = std::chrono::steady_clock::now();
-  Flat<Key> f = flatten(graph);
+  Flat<Key> f = flatten(graph, nt);
   const size_t n = f.keys.size();
   ppr_csr g{(int64_t)n, f.rp.data(), f.col.empty() ? nullptr : f.col.data()};
   std::vector<int32_t> ids(n * K), len(n);
@@ -253,7 +325,7 @@ inline std::unordered_map<Key, std::unordered_map<Key, double>> grank_device(
   outer.join();
   if (rc != PPR_OK) fail(rc);
   const auto t2b = std::chrono::steady_clock::now();
-  materialize_rows(f, o, K, ids, sc, len);
+  materialize_rows(f, o, K, ids, sc, len, nt);
   if (getenv("PPR_TIMING")) {  // phase breakdown of one call (stderr)
     const auto t3 = std::chrono::steady_clock::now();
     auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {

@@ -44,7 +44,8 @@ std::unordered_map<Key, std::unordered_map<Key, double>> mccompletepathv2(
   hipdetail::check_params(K, L, iterations, damping);
   if (graph.empty()) return {};
   if (K > 0xffffffffu || L > 0xffffffffu || iterations > 0xffffffffu) hipdetail::fail(PPR_ERR_RANGE);
-  hipdetail::Flat<Key> f = hipdetail::flatten(graph);
+  const size_t nt = hipdetail::host_threads();
+  hipdetail::Flat<Key> f = hipdetail::flatten(graph, nt);
   const size_t n = f.keys.size();
   ppr_csr g{(int64_t)n, f.rp.data(), f.col.empty() ? nullptr : f.col.data()};
   std::vector<int32_t> ids(n * K), len(n);
@@ -56,7 +57,7 @@ std::unordered_map<Key, std::unordered_map<Key, double>> mccompletepathv2(
                                nullptr, ids.data(), sc.data(), len.data(), nullptr);
   outer.join();
   if (rc != PPR_OK) hipdetail::fail(rc);
-  hipdetail::materialize_rows(f, o, K, ids, sc, len);
+  hipdetail::materialize_rows(f, o, K, ids, sc, len, nt);
   return std::move(o.out);
 }
 

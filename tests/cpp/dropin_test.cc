@@ -9,11 +9,16 @@
 //                                    to end (PPR_TIMING=1: flatten / device / materialise split on stderr)
 //   dropin_test e2echeck <scale> <iters> <stride>  the same call; every stride-th result row compared
 //                                    with the device rows of ppr_grank_csr on the same CSR, bit for bit
+//   dropin_test multieq <scale> <iters>  grankMulti(..., 1) == grankMulti(..., 8) == grank(...) maps
+//   dropin_test order <n> <seed>     (host only) the threaded iteration-order walk of flatten equals the
+//                                    map's own iteration order, for int and string keys, after inserts,
+//                                    erasures and rehashes
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -26,6 +31,20 @@ using namespace std;
 static int check(bool c, const char* what) {
   if (!c) { fprintf(stderr, "FAILED: %s\n", what); return 1; }
   return 0;
+}
+
+// flatten's threaded iteration-order walk == the map's own order (1 = mismatch)
+template <typename K>
+static int same_order(const unordered_map<K, vector<K>>& g, const char* what) {
+  vector<const K*> k1, k2;
+  vector<const vector<K>*> s1, s2;
+  ppr::hipdetail::iteration_order(g, 1, k1, s1);
+  ppr::hipdetail::iteration_order(g, 8, k2, s2);
+  int bad = check(k1.size() == g.size() && k1 == k2 && s1 == s2, what);
+  size_t v = 0;
+  for (typename unordered_map<K, vector<K>>::const_iterator it = g.begin(); it != g.end(); ++it, ++v)
+    if (v >= k1.size() || k1[v] != &it->first) return bad + check(false, what);
+  return bad;
 }
 
 int main(int argc, char** argv) {
@@ -123,7 +142,7 @@ int main(int argc, char** argv) {
     const size_t K = 64, L = 128;
     auto res = ppr::grank(graph, K, L, iters, 0.85, -1.0);
     // the same call through the C ABI on the same flattening (dense id = graph iteration order)
-    ppr::hipdetail::Flat<int> f = ppr::hipdetail::flatten(graph);
+    ppr::hipdetail::Flat<int> f = ppr::hipdetail::flatten(graph, ppr::hipdetail::host_threads());
     ppr_csr g{(int64_t)f.keys.size(), f.rp.data(), f.col.data()};
     std::vector<int32_t> ids(f.keys.size() * K), len(f.keys.size());
     std::vector<double> sc(f.keys.size() * K);
@@ -144,6 +163,42 @@ int main(int argc, char** argv) {
       entries += len[v];
     }
     printf("{\"rows_checked\": %lld, \"entries_checked\": %lld, \"bad\": %d}\n", (long long)rows, (long long)entries, bad);
+    return bad ? 1 : 0;
+  }
+  if (mode == "multieq") {
+    const int scale = atoi(argv[2]);
+    const int iters = atoi(argv[3]);
+    const int64_t n = 1LL << scale;
+    std::vector<int64_t> rp(n + 1);
+    const int64_t m = ppr_rmat_generate(scale, 16, 0.57, 0.19, 0.19, 7, rp.data(), nullptr, 0);
+    std::vector<int32_t> col(m);
+    ppr_rmat_generate(scale, 16, 0.57, 0.19, 0.19, 7, rp.data(), col.data(), m);
+    for (int64_t v = 0; v < n; v++) graph[(int)v].assign(col.begin() + rp[v], col.begin() + rp[v + 1]);
+    auto a = ppr::grankMulti(graph, 32, 64, iters, 0.85, 1e-4, 1);
+    auto b = ppr::grankMulti(graph, 32, 64, iters, 0.85, 1e-4, 8);
+    auto c = ppr::grank(graph, 32, 64, iters, 0.85, 1e-4);
+    int bad = check(a == b, "grankMulti 1 thread == 8 threads") + check(a == c, "grankMulti == grank");
+    return bad ? 1 : 0;
+  }
+  if (mode == "order") {
+    const size_t n = (size_t)atoll(argv[2]);
+    uint64_t s = (uint64_t)atoll(argv[3]) * 0x9E3779B97F4A7C15ull + 1;
+    auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+    int bad = 0;
+    auto same = [&](int r, const char*) { bad += r; };
+    unordered_map<int, vector<int>> gi;
+    for (size_t i = 0; i < n; i++) gi[(int)(rnd() % (4 * n))].push_back((int)i);
+    same(same_order(gi, "int keys"), "");
+    for (size_t i = 0; i < n / 3; i++) gi.erase((int)(rnd() % (4 * n)));
+    same(same_order(gi, "int keys after erasures"), "");
+    gi.rehash(gi.bucket_count() * 4);
+    same(same_order(gi, "int keys after a rehash"), "");
+    gi.max_load_factor(4.0f);
+    gi.rehash(1);
+    same(same_order(gi, "int keys, load factor 4"), "");
+    unordered_map<string, vector<string>> gs;
+    for (size_t i = 0; i < n / 2; i++) gs["k" + to_string(rnd() % (2 * n))].push_back("x");
+    same(same_order(gs, "string keys"), "");
     return bad ? 1 : 0;
   }
   if (mode == "empty") {

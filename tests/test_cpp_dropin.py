@@ -41,6 +41,22 @@ def test_mc_known_answers_cpp(dropin):
     assert p.returncode == 0, p.stderr
 
 
+@pytest.mark.parametrize("n,seed", [(70000, 1), (300000, 2), (1000, 3)])
+def test_flatten_iteration_order_threaded(dropin, n, seed):
+    """flatten's threaded walk of the map (per-bucket node runs chained in list order) yields the
+    map's own iteration order -- the dense ids the reference's partitions depend on"""
+    p = subprocess.run([dropin, "order", str(n), str(seed)], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+
+
+@pytest.mark.gpu
+def test_grank_multi_threads_equal_grank(dropin):
+    """ppr::grankMulti(..., 1) == grankMulti(..., 8) == ppr::grank maps (nThreads sizes the host work
+    only, header-only/grankMulti.h:289-304; test/grankMultiThreadTest.cc:384-576)"""
+    p = subprocess.run([dropin, "multieq", "13", "6"], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+
+
 def test_empty_graph(dropin):
     assert subprocess.run([dropin, "empty"]).returncode == 0
 

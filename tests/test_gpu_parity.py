@@ -302,3 +302,41 @@ def test_gpu_exact_sum_init_hubs_and_damping():
     r = ppr.grank_csr(csr, 16, 64, 4, 0.85, -1.0, part=part, device=0)
     o = oracle.grank(csr.row_ptr, csr.col, part, 16, 64, 4, 0.85, -1.0)
     assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])
+
+
+@pytest.mark.parametrize("senv,want", [
+    ({}, "sieve"),                                            # defaults
+    ({"PPR_TIER_MASK": "0x0"}, "sieve"),                      # every source with a full row sieved
+    ({"PPR_SV_SLICE": "256"}, "sieve"),                       # multi-slice sources (k_svA / k_svB / k_svF)
+    ({"PPR_SV_SLICE": "300", "PPR_TIER_MASK": "0x0"}, "sieve"),
+    ({"PPR_SV_BUDGET": "2"}, "redo"),                         # passing keys overflow the table: sources
+    ({"PPR_SV_BUDGET": "2", "PPR_SV_SLICE": "512"}, "redo"),  # handed back to the range / partition engines
+    ({"PPR_SV_MIN": "20000"}, "sieve"),                       # only the widest sources sieved
+    ({"PPR_SV": "0"}, None),                                  # off: range / partition engines only
+])
+def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):
+    """the sieve merge of the wide sources (merge_sv.h: exact prev-key sums + count-min sketch,
+    exact second pass for the keys the sketch cannot rule out) equals the oracle's exact sum bit for
+    bit -- one-slice and multi-slice sources, table overflows handed back, mixed with every tier"""
+    for k, v in senv.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("PPR_TIMING", "1")
+    for scale, K, L, it in [(11, 16, 32, 8), (12, 32, 128, 6), (13, 64, 128, 5)]:
+        g = ppr.rmat(scale, seed=191 + scale)
+        part = g.partitions()
+        r = ppr.grank_csr(g, K, L, it, 0.85, -1.0, part=part, device=0)
+        o = oracle.grank(g.row_ptr, g.col, part, K, L, it, 0.85, -1.0)
+        assert np.array_equal(r.max_diff, o["max_diff"])
+        assert np.array_equal(r.lens, o["lens"])
+        assert np.array_equal(r.ids, o["ids"])
+        assert np.array_equal(r.scores, o["scores"])
+    err = capfd.readouterr().err
+    lines = [x.split() for x in err.splitlines() if x.startswith("ppr_timing sieve_sources")]
+    sieved = sum(int(x[2]) for x in lines)
+    redo = sum(int(x[4]) for x in lines)
+    if want:
+        assert sieved > 0
+    else:
+        assert sieved == 0
+    if want == "redo":
+        assert redo > 0
