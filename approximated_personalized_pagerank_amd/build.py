@@ -90,3 +90,26 @@ def build_dropin(force: bool = False) -> str:
                     "-L", PKG_DIR, "-lppr_hip", f"-Wl,-rpath,{PKG_DIR}"], check=True)
     os.replace(DROPIN_BIN + ".tmp", DROPIN_BIN)
     return DROPIN_BIN
+
+
+HOST_ASAN_SRC = os.path.join(PKG_DIR, "..", "tests", "cpp", "host_asan_test.cc")
+HOST_ASAN_BIN = os.path.join(PKG_DIR, "..", "tests", "cpp", "_host_asan_test")
+
+
+def build_host_asan(force: bool = False) -> str:
+    """The engine's host code (csrc/host_graph.cpp and include/ppr/grank.h's flatten / KeyIndex /
+    materialisation) under g++ -fsanitize=address,undefined, driven by tests/cpp/host_asan_test.cc
+    (SURVEY.md s5). The sanitized host_graph.cpp symbols interpose over the library's copies;
+    libppr_hip.so supplies only ppr_strerror. No device code is involved."""
+    lib = build()
+    inc = os.path.join(PKG_DIR, "..", "include")
+    hg = os.path.join(CSRC, "host_graph.cpp")
+    deps = [HOST_ASAN_SRC, hg, lib, os.path.join(inc, "ppr", "grank.h"), os.path.join(CSRC, "host_par.h")]
+    if (not force and os.path.exists(HOST_ASAN_BIN)
+            and os.path.getmtime(HOST_ASAN_BIN) > max(os.path.getmtime(d) for d in deps)):
+        return HOST_ASAN_BIN
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                    "-fno-sanitize-recover=undefined", "-I", inc, HOST_ASAN_SRC, hg, "-o", HOST_ASAN_BIN + ".tmp",
+                    "-pthread", "-L", PKG_DIR, "-lppr_hip", f"-Wl,-rpath,{PKG_DIR}"], check=True)
+    os.replace(HOST_ASAN_BIN + ".tmp", HOST_ASAN_BIN)
+    return HOST_ASAN_BIN

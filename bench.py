@@ -111,14 +111,17 @@ def end_to_end(scale, iters, K, L):
         return None
     from approximated_personalized_pagerank_amd import build as _build
     binary = _build.build_dropin()
-    env = dict(os.environ, PPR_TIMING="1")
+    # PPR_HEAP_PAD: the result maps' malloc heaps grow 64 MB at a time (include/ppr/grank.h HeapGrowth,
+    # opt-in because mallopt is process-wide; this program sets nothing else)
+    env = dict(os.environ, PPR_TIMING="1", PPR_HEAP_PAD=os.environ.get("PPR_HEAP_PAD", "64"))
     p = subprocess.run([binary, "e2e", str(scale), str(iters)], capture_output=True, text=True, env=env,
                        check=True, timeout=900)
     d = json.loads(p.stdout.strip().splitlines()[-1])
     split = parse_ppr_timing(p.stderr)
     out = {"total_s": d["total_s"], "graph": "RMAT-%d as unordered_map<int, vector<int>> (%d nodes, %d edges)"
            % (scale, d["nodes"], d["edges"]), "result_entries": d["entries"],
-           "call": f"ppr::grank(graph, K={K}, L={L}, {iters}, 0.85, nThreads, -1) via include/ppr/grank.h"}
+           "call": f"ppr::grank(graph, K={K}, L={L}, {iters}, 0.85, -1) via include/ppr/grank.h",
+           "env": {"PPR_HEAP_PAD": env["PPR_HEAP_PAD"]}}
     if split:
         out.update(flatten_s=split.get("flatten_s"), device_s=split.get("device_s"),
                    plan_and_upload_s=split["csr_call_s"] - split["device_s"] if "csr_call_s" in split else None,
