@@ -286,6 +286,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     if (ent) p->nt_loads = (int)strtol(ent, nullptr, 0) & 3;
     const char* ewi = getenv("PPR_WHATIF");
     if (ewi) p->whatif = (int)strtol(ewi, nullptr, 0);
+    const char* exr = getenv("PPR_XROUTE");
+    if (exr && atoi(exr) == 0) p->xroute = false;
     const char* e9e = getenv("PPR_WG_PASSES");  // tests: force workgroup-tier overflows
     if (e9e) p->wg_max_passes = std::max(1, std::min(WG_MAX_PASSES, atoi(e9e)));
     const char* e9d = getenv("PPR_FUSED_MAX");
@@ -2056,8 +2058,42 @@ static int xrange(ppr_plan* p, int32_t it, int64_t begin, int64_t end, XRange* x
   return PPR_OK;
 }
 
-// compact block of a range into buf (capacity cap >= 8 + cnt * row_bytes); the block's size is
-// also written to the device int64 *d_total when given. Asynchronous on the plan's stream.
+// compact block of `cnt` rows (node ids `list`, slot `nxt`) into buf (capacity >= 8 + cnt * row
+// bytes); the block's size is also written to the device int64 *d_total when given. Asynchronous
+// on the plan's stream.
+static int xpack_nodes(ppr_plan* p, int nxt, const int32_t* list, int64_t cnt, unsigned char* buf, int64_t* d_total) {
+  hipStream_t st = p->stream;
+  int64_t* off = reinterpret_cast<int64_t*>(buf);
+  if (cnt == 0) {
+    HIP_OK(hipMemsetAsync(buf, 0, 8, st));
+    if (d_total) hipLaunchKernelGGL(k_xtotal, dim3(1), dim3(64), 0, st, (const int64_t*)off, (int64_t)0, d_total);
+    HIP_OK(hipGetLastError());
+    return PPR_OK;
+  }
+  const DevSlab s = dev_slab(p);
+  // row sizes into the payload area (free until the pack), scanned into the offset header
+  int64_t* sz = reinterpret_cast<int64_t*>(buf + 8 * (cnt + 1));
+  hipLaunchKernelGGL(k_xsize, dim3((unsigned)((cnt + 256) / 256)), dim3(256), 0, st, s, nxt, list, cnt, sz);
+  size_t tmp = 0;
+  HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, sz, off, (int)(cnt + 1), st));
+  int rc = ensure_dev(&p->d_xtmp, &p->xtmp_bytes, tmp);
+  if (rc) return rc;
+  HIP_OK(hipcub::DeviceScan::ExclusiveSum(p->d_xtmp, tmp, sz, off, (int)(cnt + 1), st));
+  hipLaunchKernelGGL(k_xpack, dim3((unsigned)((cnt + 3) / 4)), dim3(256), 0, st, s, nxt, list, cnt, buf);
+  if (d_total) hipLaunchKernelGGL(k_xtotal, dim3(1), dim3(64), 0, st, (const int64_t*)off, cnt, d_total);
+  HIP_OK(hipGetLastError());
+  return PPR_OK;
+}
+
+static int xunpack_nodes(ppr_plan* p, int nxt, const int32_t* list, int64_t cnt, const unsigned char* buf) {
+  if (cnt == 0) return PPR_OK;
+  hipLaunchKernelGGL(k_xunpack, dim3((unsigned)((cnt + 3) / 4)), dim3(256), 0, p->stream, dev_slab(p), nxt, list, cnt,
+                     buf);
+  HIP_OK(hipGetLastError());
+  return PPR_OK;
+}
+
+// compact block of a range of iteration it's active list (the rows it wrote)
 static int xpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, unsigned char* buf, int64_t cap,
                  int64_t* d_total) {
   XRange x;
@@ -2067,27 +2103,7 @@ static int xpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, unsigned c
   ppr_grank_plan_row_bytes(p, &rb);
   if (!buf || cap < 8 + x.cnt * rb) return PPR_ERR_ARG;
   HIP_OK(hipSetDevice(p->device));
-  hipStream_t st = p->stream;
-  int64_t* off = reinterpret_cast<int64_t*>(buf);
-  if (x.cnt == 0) {
-    HIP_OK(hipMemsetAsync(buf, 0, 8, st));
-    if (d_total) hipLaunchKernelGGL(k_xtotal, dim3(1), dim3(64), 0, st, (const int64_t*)off, (int64_t)0, d_total);
-    HIP_OK(hipGetLastError());
-    return PPR_OK;
-  }
-  const DevSlab s = dev_slab(p);
-  // row sizes into the payload area (free until the pack), scanned into the offset header
-  int64_t* sz = reinterpret_cast<int64_t*>(buf + 8 * (x.cnt + 1));
-  hipLaunchKernelGGL(k_xsize, dim3((unsigned)((x.cnt + 256) / 256)), dim3(256), 0, st, s, x.nxt, x.list, x.cnt, sz);
-  size_t tmp = 0;
-  HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, sz, off, (int)(x.cnt + 1), st));
-  rc = ensure_dev(&p->d_xtmp, &p->xtmp_bytes, tmp);
-  if (rc) return rc;
-  HIP_OK(hipcub::DeviceScan::ExclusiveSum(p->d_xtmp, tmp, sz, off, (int)(x.cnt + 1), st));
-  hipLaunchKernelGGL(k_xpack, dim3((unsigned)((x.cnt + 3) / 4)), dim3(256), 0, st, s, x.nxt, x.list, x.cnt, buf);
-  if (d_total) hipLaunchKernelGGL(k_xtotal, dim3(1), dim3(64), 0, st, (const int64_t*)off, x.cnt, d_total);
-  HIP_OK(hipGetLastError());
-  return PPR_OK;
+  return xpack_nodes(p, x.nxt, x.list, x.cnt, buf, d_total);
 }
 
 static int xunpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const unsigned char* buf) {
@@ -2097,10 +2113,7 @@ static int xunpack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, const un
   if (x.cnt == 0) return PPR_OK;
   if (!buf) return PPR_ERR_ARG;
   HIP_OK(hipSetDevice(p->device));
-  hipLaunchKernelGGL(k_xunpack, dim3((unsigned)((x.cnt + 3) / 4)), dim3(256), 0, p->stream, dev_slab(p), x.nxt,
-                     x.list, x.cnt, buf);
-  HIP_OK(hipGetLastError());
-  return PPR_OK;
+  return xunpack_nodes(p, x.nxt, x.list, x.cnt, buf);
 }
 
 extern "C" int ppr_grank_plan_pack(ppr_plan* p, int32_t it, int64_t begin, int64_t end, void* dev_buf,
@@ -2219,7 +2232,10 @@ struct LocalGroup {
   bool failed = false;
   std::vector<unsigned char*> bufs;
   std::vector<unsigned long long> md;
-  explicit LocalGroup(int n_) : n(n_), bufs(n_), md(n_) {}
+  std::vector<std::vector<unsigned char*>> pbufs;  // routed blocks: [sender][receiver]
+  std::vector<std::vector<int64_t>> psz;
+  explicit LocalGroup(int n_)
+      : n(n_), bufs(n_), md(n_), pbufs(n_, std::vector<unsigned char*>(n_)), psz(n_, std::vector<int64_t>(n_)) {}
   bool barrier() {
     std::unique_lock<std::mutex> lk(mu);
     if (failed) return false;
@@ -2275,6 +2291,191 @@ static int x_allreduce_max(ppr_plan* p, unsigned long long* mdp, hipStream_t s) 
   return PPR_OK;
 }
 
+// the broadcast exchange of iteration it: this rank's whole range to every rank (bounds b)
+static int x_exchange_bulk(ppr_plan* p, uint32_t it, const std::vector<int64_t>& b) {
+  hipStream_t s = p->stream;
+  int64_t rb = 0;
+  ppr_grank_plan_row_bytes(p, &rb);
+  // all-gather of compact blocks (merge_glb.h): only the entries travel; every rank broadcasts its
+  // block from its send buffer (grouped; the root broadcasts in place, so it copies nothing) and
+  // unpacks the others'. Every block travels at its bound, 8 + rows * row_bytes (the offset header
+  // inside says where each row ends): the bounds are known on every host, so no size exchange and
+  // no host sync before the broadcasts.
+  const int64_t mine = b[p->rank + 1] - b[p->rank];
+  int rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, (size_t)(8 + mine * rb));
+  if (rc) return rc;
+  rc = xpack(p, (int32_t)it, b[p->rank], b[p->rank + 1], p->d_xsend, (int64_t)p->xsend_bytes, nullptr);
+  if (rc) return rc;
+  std::vector<int64_t> sz(p->nranks);
+  for (int r = 0; r < p->nranks; r++) sz[r] = 8 + (b[r + 1] - b[r]) * rb;
+  std::vector<size_t> xo(p->nranks + 1, 0);
+  for (int r = 0; r < p->nranks; r++) xo[r + 1] = xo[r] + (r == p->rank ? 0 : (size_t)sz[r]);
+  rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, std::max<size_t>(8, xo[p->nranks]));
+  if (rc) return rc;
+  p->x_bytes += (int64_t)xo[p->nranks];
+  p->x_rows_sent += mine;
+  rc = x_blocks(p, b, sz, xo, s);
+  if (rc) return rc;
+  for (int r = 0; r < p->nranks; r++) {
+    if (r == p->rank || b[r + 1] == b[r]) continue;
+    rc = xunpack(p, (int32_t)it, b[r], b[r + 1], p->d_xrecv + xo[r]);
+    if (rc) return rc;
+  }
+  return PPR_OK;
+}
+
+// Consumer routing: per partition q, the rows of this rank's range that each peer d reads (send
+// lists) and the rows of each peer r's range that this rank reads (receive lists), node ids in
+// list order. Both sides derive a list from the same mask and bounds, so they agree on it without
+// exchanging it.
+struct XRoute {
+  std::vector<int64_t> scnt[2], rcnt[2];   // [world] rows
+  std::vector<size_t> soff[2], roff[2];    // [world] int offsets into d_xlists
+};
+
+static int xroute_build(ppr_plan* p, const std::vector<int64_t> (&bd)[2], XRoute& xr) {
+  const int W = p->nranks, me = p->rank;
+  const int64_t n = p->n;
+  hipStream_t s = p->stream;
+  int rc = PPR_OK;
+  if (!p->d_xowner) { rc = dalloc(&p->d_xowner, n); if (rc) return rc; }
+  if (!p->d_xcmask) { rc = dalloc(&p->d_xcmask, n); if (rc) return rc; }
+  HIP_OK(hipMemsetAsync(p->d_xowner, 0xff, (size_t)n, s));
+  HIP_OK(hipMemsetAsync(p->d_xcmask, 0, 4 * (size_t)n, s));
+  for (int q = 0; q < 2; q++) {
+    if (!p->nact[q]) continue;
+    XBounds xb{};
+    xb.world = W;
+    for (int r = 0; r <= W; r++) xb.b[r] = bd[q][r];
+    hipLaunchKernelGGL(k_xowner, dim3((unsigned)((p->nact[q] + 255) / 256)), dim3(256), 0, s, p->d_act[q], p->nact[q],
+                       xb, p->d_xowner);
+  }
+  hipLaunchKernelGGL(k_xcmask, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, p->d_rp, p->d_colx, n, p->d_xowner,
+                     p->d_xcmask);
+  HIP_OK(hipGetLastError());
+  size_t total = 0;
+  for (int q = 0; q < 2; q++) {
+    xr.scnt[q].assign(W, 0); xr.rcnt[q].assign(W, 0);
+    xr.soff[q].assign(W, 0); xr.roff[q].assign(W, 0);
+    const int64_t mine = bd[q][me + 1] - bd[q][me];
+    for (int d = 0; d < W; d++) {
+      if (d == me) continue;
+      xr.soff[q][d] = total; total += (size_t)mine;
+      xr.roff[q][d] = total; total += (size_t)(bd[q][d + 1] - bd[q][d]);
+    }
+  }
+  rc = ensure_dev((unsigned char**)&p->d_xlists, &p->xlists_cap, 4 * std::max<size_t>(1, total) + 8 * 4 * (size_t)W);
+  if (rc) return rc;
+  int32_t* nsel = reinterpret_cast<int32_t*>(p->d_xlists + std::max<size_t>(1, total));  // [2][2][W] counts
+  HIP_OK(hipMemsetAsync(nsel, 0, 4 * 4 * (size_t)W, s));
+  size_t tmp = 0, need = 0;
+  for (int q = 0; q < 2; q++)
+    for (int r = 0; r < W; r++) {
+      const int64_t cnt = bd[q][r + 1] - bd[q][r];
+      if (!cnt) continue;
+      HIP_OK(hipcub::DeviceSelect::If(nullptr, tmp, p->d_act[q], p->d_xlists, nsel, (int)cnt,
+                                      XConsumedBy{p->d_xcmask, 1u}, s));
+      need = std::max(need, tmp);
+    }
+  rc = ensure_dev(&p->d_xtmp, &p->xtmp_bytes, std::max<size_t>(need, 1));
+  if (rc) return rc;
+  for (int q = 0; q < 2; q++)
+    for (int d = 0; d < W; d++) {
+      if (d == me) continue;
+      const int64_t ms = bd[q][me + 1] - bd[q][me], rs = bd[q][d + 1] - bd[q][d];
+      tmp = p->xtmp_bytes;
+      if (ms) HIP_OK(hipcub::DeviceSelect::If(p->d_xtmp, tmp, p->d_act[q] + bd[q][me], p->d_xlists + xr.soff[q][d],
+                                              nsel + (q * 2 + 0) * W + d, (int)ms, XConsumedBy{p->d_xcmask, 1u << d}, s));
+      tmp = p->xtmp_bytes;
+      if (rs) HIP_OK(hipcub::DeviceSelect::If(p->d_xtmp, tmp, p->d_act[q] + bd[q][d], p->d_xlists + xr.roff[q][d],
+                                              nsel + (q * 2 + 1) * W + d, (int)rs, XConsumedBy{p->d_xcmask, 1u << me},
+                                              s));
+    }
+  std::vector<int32_t> h(4 * (size_t)W);
+  HIP_OK(hipMemcpyAsync(h.data(), nsel, 4 * h.size(), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  for (int q = 0; q < 2; q++)
+    for (int d = 0; d < W; d++) {
+      xr.scnt[q][d] = h[(q * 2 + 0) * W + d];
+      xr.rcnt[q][d] = h[(q * 2 + 1) * W + d];
+    }
+  return PPR_OK;
+}
+
+// the routed exchange of iteration it: per peer, the rows it reads; exact block sizes (one 8-byte
+// send / receive per peer first), then the blocks, then the unpacks
+static int x_exchange_routed(ppr_plan* p, uint32_t it, const XRoute& xr) {
+  const int W = p->nranks, me = p->rank, q = (int)(it & 1);
+  hipStream_t s = p->stream;
+  int64_t rb = 0;
+  ppr_grank_plan_row_bytes(p, &rb);
+  const int nxt = ((iter_args(p, (int)it, false).active == 1) ? iter_args(p, (int)it, false).sB
+                                                               : iter_args(p, (int)it, false).sA) ^ 1;
+  std::vector<size_t> so(W + 1, 0), ro(W + 1, 0);
+  for (int d = 0; d < W; d++) {
+    so[d + 1] = so[d] + (xr.scnt[q][d] ? (size_t)(8 + xr.scnt[q][d] * rb) : 0);
+    ro[d + 1] = ro[d] + (xr.rcnt[q][d] ? (size_t)(8 + xr.rcnt[q][d] * rb) : 0);
+  }
+  int rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, std::max<size_t>(8, so[W]));
+  if (rc) return rc;
+  rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, std::max<size_t>(8, ro[W]));
+  if (rc) return rc;
+  rc = ensure_dev(&p->d_xsz, &p->xsz_bytes, 16 * (size_t)W);
+  if (rc) return rc;
+  int64_t* tx = reinterpret_cast<int64_t*>(p->d_xsz);
+  int64_t* rx = tx + W;
+  for (int d = 0; d < W; d++) {
+    if (!xr.scnt[q][d]) continue;
+    rc = xpack_nodes(p, nxt, p->d_xlists + xr.soff[q][d], xr.scnt[q][d], p->d_xsend + so[d], tx + d);
+    if (rc) return rc;
+    p->x_rows_sent += xr.scnt[q][d];
+  }
+  std::vector<int64_t> hsz(2 * (size_t)W, 0);
+  if (p->lgroup) {
+    LocalGroup& G = *p->lgroup;
+    HIP_OK(hipMemcpyAsync(hsz.data(), tx, 8 * (size_t)W, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));  // this rank's blocks are complete
+    for (int d = 0; d < W; d++) { G.pbufs[me][d] = p->d_xsend + so[d]; G.psz[me][d] = xr.scnt[q][d] ? hsz[d] : 0; }
+    if (!G.barrier()) return PPR_ERR_HIP;
+    for (int r = 0; r < W; r++) {
+      if (r == me || !xr.rcnt[q][r]) continue;
+      const int64_t z = G.psz[r][me];
+      if (z < 8 || (size_t)z > ro[r + 1] - ro[r]) return PPR_ERR_HIP;  // (lists disagree)
+      hsz[W + r] = z;
+      HIP_OK(hipMemcpyAsync(p->d_xrecv + ro[r], G.pbufs[r][me], (size_t)z, hipMemcpyDeviceToDevice, s));
+    }
+    HIP_OK(hipStreamSynchronize(s));
+    if (!G.barrier()) return PPR_ERR_HIP;  // no rank reuses its send buffer before all copied
+  } else {
+    NCCL_OK(ncclGroupStart());
+    for (int d = 0; d < W; d++) {
+      if (d == me) continue;
+      if (xr.scnt[q][d]) NCCL_OK(ncclSend(tx + d, 1, ncclInt64, d, p->comm, s));
+      if (xr.rcnt[q][d]) NCCL_OK(ncclRecv(rx + d, 1, ncclInt64, d, p->comm, s));
+    }
+    NCCL_OK(ncclGroupEnd());
+    HIP_OK(hipMemcpyAsync(hsz.data(), tx, 16 * (size_t)W, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    NCCL_OK(ncclGroupStart());
+    for (int d = 0; d < W; d++) {
+      if (d == me) continue;
+      if (xr.scnt[q][d]) NCCL_OK(ncclSend(p->d_xsend + so[d], (size_t)hsz[d], ncclUint8, d, p->comm, s));
+      if (xr.rcnt[q][d]) {
+        if (hsz[W + d] < 8 || (size_t)hsz[W + d] > ro[d + 1] - ro[d]) return PPR_ERR_HIP;
+        NCCL_OK(ncclRecv(p->d_xrecv + ro[d], (size_t)hsz[W + d], ncclUint8, d, p->comm, s));
+      }
+    }
+    NCCL_OK(ncclGroupEnd());
+  }
+  for (int r = 0; r < W; r++) {
+    if (r == me || !xr.rcnt[q][r]) continue;
+    p->x_bytes += hsz[W + r];
+    rc = xunpack_nodes(p, nxt, p->d_xlists + xr.roff[q][r], xr.rcnt[q][r], p->d_xrecv + ro[r]);
+    if (rc) return rc;
+  }
+  return PPR_OK;
+}
+
 extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance,
                                           ppr_stats* st) {
   if (!p) return PPR_ERR_ARG;
@@ -2287,14 +2488,19 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
   p->merge_launches = 0;
   p->merge_ms = 0.0;
   p->x_bytes = 0;
+  p->x_rows_sent = 0;
   HIP_OK(hipEventRecord(p->ev_a, s));
   int rc = ppr_grank_plan_init(p);
   if (rc) return rc;
   std::vector<int64_t> bd[2];
   shard_bounds(p->work[0], p->nranks, bd[0]);
   shard_bounds(p->work[1], p->nranks, bd[1]);
-  int64_t rb = 0;
-  ppr_grank_plan_row_bytes(p, &rb);
+  // consumer routing: during the run a row goes only to the ranks that read it; the result rows of
+  // both partitions are broadcast once after the last iteration, so every rank ends with the
+  // whole slab (ppr_grank_plan_finish's top-K reads every row)
+  const bool route = p->nranks > 1 && p->nranks <= 32 && p->xroute;
+  XRoute xr;
+  if (route) { rc = xroute_build(p, bd, xr); if (rc) return rc; }
   double md[2] = {tolerance, tolerance};
   uint32_t it = 0;
   for (; it < iterations && std::max(md[0], md[1]) >= tolerance; it++) {
@@ -2303,32 +2509,8 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
     if (rc) return rc;
     unsigned long long* mdp = p->d_maxdiff + (it < PPR_MAX_ITER_STATS ? it : PPR_MAX_ITER_STATS);
     if (p->nranks > 1) {
-      // all-gather of compact blocks (merge_glb.h): only the entries travel; every rank
-      // broadcasts its block from its send buffer (grouped; the root broadcasts in place, so it
-      // copies nothing) and unpacks the others'.
-      const int64_t mine = b[p->rank + 1] - b[p->rank];
-      rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, (size_t)(8 + mine * rb));
+      rc = route ? x_exchange_routed(p, it, xr) : x_exchange_bulk(p, it, bd[it & 1]);
       if (rc) return rc;
-      rc = xpack(p, (int32_t)it, b[p->rank], b[p->rank + 1], p->d_xsend, (int64_t)p->xsend_bytes, nullptr);
-      if (rc) return rc;
-      // every block travels at its bound, 8 + rows * row_bytes (the offset header inside says
-      // where each row ends): the bounds are known on every host, so no size all-gather and no
-      // host sync before the broadcasts -- active rows are nearly full at L = 128, the bound
-      // costs < 1 % more bytes than the exact sizes
-      std::vector<int64_t> sz(p->nranks);
-      for (int r = 0; r < p->nranks; r++) sz[r] = 8 + (b[r + 1] - b[r]) * rb;
-      std::vector<size_t> xo(p->nranks + 1, 0);
-      for (int r = 0; r < p->nranks; r++) xo[r + 1] = xo[r] + (r == p->rank ? 0 : (size_t)sz[r]);
-      rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, std::max<size_t>(8, xo[p->nranks]));
-      if (rc) return rc;
-      p->x_bytes += xo[p->nranks];
-      rc = x_blocks(p, b, sz, xo, s);
-      if (rc) return rc;
-      for (int r = 0; r < p->nranks; r++) {
-        if (r == p->rank || b[r + 1] == b[r]) continue;
-        rc = xunpack(p, (int32_t)it, b[r], b[r + 1], p->d_xrecv + xo[r]);
-        if (rc) return rc;
-      }
       rc = x_allreduce_max(p, mdp, s);
       if (rc) return rc;
     }
@@ -2340,6 +2522,13 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
       std::swap(md[0], md[1]);
     }
   }
+  if (route)
+    for (int q = 0; q < 2; q++) {  // each partition's rows as its last iteration wrote them
+      const int64_t last = (int64_t)it - 1 - (((int64_t)it - 1 - q) & 1);
+      if (last < 0 || (last & 1) != q) continue;
+      rc = x_exchange_bulk(p, (uint32_t)last, bd[q]);
+      if (rc) return rc;
+    }
   rc = ppr_grank_plan_finish(p, (int32_t)it);
   if (rc) return rc;
   HIP_OK(hipEventRecord(p->ev_b, s));
@@ -2359,6 +2548,13 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
     st->algo_bytes = (int64_t)sv[1];
     st->merge_launches = p->merge_launches;
   }
+  return PPR_OK;
+}
+
+extern "C" int ppr_grank_plan_exchange_bytes(ppr_plan* p, int64_t* recv_bytes, int64_t* rows_sent) {
+  if (!p) return PPR_ERR_ARG;
+  if (recv_bytes) *recv_bytes = p->x_bytes;
+  if (rows_sent) *rows_sent = p->x_rows_sent;
   return PPR_OK;
 }
 

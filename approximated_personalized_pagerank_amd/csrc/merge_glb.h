@@ -234,6 +234,41 @@ __global__ void k_xunpack(DevSlab s, int nxt, const int32_t* list, int64_t count
   }
 }
 
+// ---- consumer routing of the sharded loop's rows (grank.hip xroute_build) ----
+// work-balanced range bounds of one partition's active list (at most 32 ranks: a u32 mask per node)
+struct XBounds {
+  int64_t b[33];
+  int32_t world;
+};
+// owner rank of every active node of one partition's list
+__global__ void k_xowner(const int32_t* act, int64_t cnt, XBounds xb, int8_t* owner) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cnt) return;
+  int r = 0;
+  while (r + 1 < xb.world && xb.b[r + 1] <= i) r++;
+  owner[act[i]] = (int8_t)r;
+}
+// bit r of cmask[u]: some source merged by rank r (in either partition) reads u's row. One wave per
+// source; a bit already set is not or-ed again (a popular row would otherwise serialise millions
+// of atomics on one address).
+__global__ void k_xcmask(const int64_t* rp, const int32_t* colx, int64_t n, const int8_t* owner, uint32_t* cmask) {
+  const int64_t v = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
+  if (v >= n) return;
+  const int r = owner[v];
+  if (r < 0) return;
+  const uint32_t bit = 1u << r;
+  for (int64_t e = rp[v] + lane_id(); e < rp[v + 1]; e += WAVE) {
+    const int u = colx[e] & 0x7fffffff;
+    if (!(__hip_atomic_load(&cmask[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(&cmask[u], bit);
+  }
+}
+// hipcub::DeviceSelect::If predicate: the node's row is read by rank `bit`
+struct XConsumedBy {
+  const uint32_t* m;
+  uint32_t bit;
+  __host__ __device__ bool operator()(const int32_t& v) const { return (m[v] & bit) != 0u; }
+};
+
 __global__ void k_zero_u64(unsigned long long* p, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 0ull;

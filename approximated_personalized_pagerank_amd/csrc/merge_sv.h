@@ -48,6 +48,7 @@ constexpr int SV_BM_WORDS = SV_R * SV_W / 64;  // sieve bitmap (u64 words)
 constexpr size_t SV_SKETCH_BYTES = (size_t)SV_R * SV_W * 4;
 constexpr size_t SV_REGION = SV_SKETCH_BYTES > (size_t)SV_XT * 20 ? SV_SKETCH_BYTES : (size_t)SV_XT * 20;
 constexpr int SVF_CAP = 4096;                 // k_svF: dense entries at or above the bound
+constexpr uint32_t WI_SV_P1WALK = 1u << 11;   // PPR_WHATIF 2048: sieve pass 1 through hub_window_walk (A/B)
 
 // ---------------------------------------------------------------------------------------------
 // split exact accumulators (keys u32 | A u64 | B u64: 20 B a slot)
@@ -267,32 +268,166 @@ __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, co
   });
 }
 
+// The candidates of successors [i0, e) (<= 64) like hub_window_walk, a batch of HUB_TW_BATCH
+// groups at a time (the next batch's loads in flight): fb(valid[], key[], ridx[], score[]) with each
+// candidate's slab index; scores are loaded only with kScores (pass 2 loads a score only for a
+// candidate that passes).
+template <bool kScores, class FB>
+__device__ __forceinline__ void sv_window(const DevGraph& g, const DevSlab& s, const IterArgs& a, int64_t i0,
+                                          int64_t e, uint8_t* fl, FB fb) {
+  constexpr int NB = HUB_TW_BATCH;
+  const int64_t i = i0 + lane_id();
+  int u = 0, sl = 0, ln = 0;
+  if (i < e) {
+    const int32_t cx = g.colx[i];
+    u = cx & 0x7fffffff;
+    sl = read_slot(a, cx);
+    ln = s.len[s.lrow(sl, u)];
+  }
+  const int incl = wave_incl_scan(ln);
+  const int total = __builtin_amdgcn_readlane(incl, WAVE - 1);
+  const bool flags = !__ballot(i < e && ln == 0);
+  auto load = [&](int g0, int (&key)[NB], int64_t (&ri)[NB], double (&sv)[NB]) {
+    if (flags) {
+#pragma unroll
+      for (int q = 0; q < NB / 4; q++) reinterpret_cast<uint32_t*>(fl)[q * WAVE + lane_id()] = 0u;
+      wave_fence();
+      if (incl > g0 && incl < g0 + WAVE * NB) fl[incl - g0] = 1;
+      wave_fence();
+    }
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      const int c = g0 + k * WAVE + lane_id();
+      int j = 0;
+      if (flags) {
+        const int G = g0 + k * WAVE;
+        const uint64_t ends = __ballot(fl[k * WAVE + lane_id()] != 0) & ~1ull;
+        j = __popcll(__ballot(incl <= G)) + __popcll(ends & (lanemask_lt() | (1ull << lane_id())));
+      } else {
+#pragma unroll
+        for (int step = 32; step; step >>= 1) {
+          const int pv = __shfl(incl, j + step - 1);
+          if (pv <= c) j += step;
+        }
+      }
+      const int jj = j < WAVE ? j : WAVE - 1;
+      const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
+      const int ex = jj > 0 ? exv : 0;
+      const int uj = __shfl(u, jj);
+      const int sj = __shfl(sl, jj);
+      key[k] = 0;
+      ri[k] = 0;
+      sv[k] = 0.0;
+      if (c < total) {
+        ri[k] = s.row(sj, uj) + (c - ex);
+        key[k] = ld_nt(&s.ids[ri[k]], a.nt & 1u);
+        if (kScores) sv[k] = ld_nt(&s.sc[ri[k]], a.nt & 1u);
+      }
+    }
+  };
+  int key[NB], nkey[NB];
+  int64_t ri[NB], nri[NB];
+  double sv[NB], nsv[NB];
+  if (total > 0) load(0, nkey, nri, nsv);
+  for (int g0 = 0; g0 < total; g0 += WAVE * NB) {
+    bool valid[NB];
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+      key[k] = nkey[k];
+      ri[k] = nri[k];
+      sv[k] = nsv[k];
+      valid[k] = g0 + k * WAVE + lane_id() < total;
+    }
+    if (g0 + WAVE * NB < total) load(g0 + WAVE * NB, nkey, nri, nsv);
+    fb(valid, key, ri, sv);
+  }
+}
+
+// pass 1, one batch at a time: the first PT group of every candidate read at once, the rare
+// longer probes after, then the exact PT adds or the sketch adds
+__device__ __forceinline__ void sv_pass1b(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
+                                          int64_t b0, int64_t b1, double factor, uint32_t* sk) {
+  constexpr int NB = HUB_TW_BATCH;
+  const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  const int64_t chunk = (b1 - b0 + W - 1) / W;
+  const int64_t c0 = b0 + (int64_t)wv * chunk, c1 = min(b1, c0 + chunk);
+  uint8_t* fl = x.fl + (size_t)wv * HUB_WALK_FLAGS;
+  for (int64_t w0 = c0; w0 < c1; w0 += WAVE)
+    sv_window<true>(g, s, a, w0, min(c1, w0 + WAVE), fl, [&](const bool (&valid)[NB], const int (&key)[NB],
+                                                            const int64_t (&)[NB], const double (&sv)[NB]) {
+      uint4 q[NB];
+      uint32_t g0[NB];
+#pragma unroll
+      for (int k = 0; k < NB; k++) {
+        g0[k] = hash32((uint32_t)key[k]) & x.pt.mask & ~3u;
+        q[k] = *reinterpret_cast<const uint4*>(x.pt.keys + g0[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < NB; k++) {
+        if (!valid[k]) continue;
+        int h = xt_match(q[k], g0[k], (uint32_t)key[k] + 1u);
+        if (h < 0 && q[k].x && q[k].y && q[k].z && q[k].w) h = x2_find(x.pt, key[k]);  // (a full group: probe on)
+        const double p = sv[k] * factor;
+        if (h >= 0) {
+          unsigned long long lo;
+          uint32_t hi;
+          xs_conv(p, lo, hi);
+          x2_add(x.pt, h, lo, hi);
+        } else {
+          sv_sketch_add(sk, key[k], sv_units(p));
+        }
+      }
+    });
+}
+
 // pass 2 over successors [b0, b1): keys outside PT that pass the sieve, exactly into XT (budget
-// checked before every group that inserts; past it the workgroup only flags the overflow)
+// checked before every group that inserts; past it the workgroup only flags the overflow). Per
+// batch: the sieve tests of all its groups, then the passing candidates' scores (loads in flight
+// together), then the inserts.
 __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
                                          const X2Table& xt, int64_t b0, int64_t b1, double factor, int budget) {
-  sv_walk(g, s, a, x, b0, b1, [&](bool valid, int id, double sv, bool) {
-    bool want = valid && sv_passes(x.bm, id);
-    if (want) want = x2_find(x.pt, id) < 0;
-    if (!__ballot(want)) return;
-    if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
-      if (lane_id() == 0) x.misc[SVM_OVF] = 1;
-      return;
-    }
-    bool ins = false;
-    int h = -1;
-    if (want) h = x2_slot(xt, id, ins);
-    const int nins = __popcll(__ballot(ins));
-    if (nins && lane_id() == 0) atomicAdd(&x.misc[SVM_FILL], nins);
-    if (__ballot(want && h < 0) && lane_id() == 0) x.misc[SVM_OVF] = 1;
-    if (h >= 0) {
-      unsigned long long lo;
-      uint32_t hi;
-      xs_conv(sv * factor, lo, hi);
-      x2_add(xt, h, lo, hi);
-    }
-    if (a.diag && lane_id() == 0) diag_add(a.diag, 138, (unsigned long long)__popcll(__ballot(want)));
-  });
+  constexpr int NB = HUB_TW_BATCH;
+  const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  const int64_t chunk = (b1 - b0 + W - 1) / W;
+  const int64_t c0 = b0 + (int64_t)wv * chunk, c1 = min(b1, c0 + chunk);
+  uint8_t* fl = x.fl + (size_t)wv * HUB_WALK_FLAGS;
+  for (int64_t w0 = c0; w0 < c1; w0 += WAVE)
+    sv_window<false>(g, s, a, w0, min(c1, w0 + WAVE), fl, [&](const bool (&valid)[NB], const int (&key)[NB],
+                                                             const int64_t (&ri)[NB], const double (&)[NB]) {
+      bool want[NB];
+      bool any = false;
+#pragma unroll
+      for (int k = 0; k < NB; k++) {
+        want[k] = valid[k] && sv_passes(x.bm, key[k]);
+        if (want[k]) want[k] = x2_find(x.pt, key[k]) < 0;
+        any = any || want[k];
+      }
+      if (!__ballot(any)) return;
+      double sv[NB];
+#pragma unroll
+      for (int k = 0; k < NB; k++) sv[k] = want[k] ? ld_nt(&s.sc[ri[k]], a.nt & 1u) : 0.0;
+#pragma unroll
+      for (int k = 0; k < NB; k++) {
+        if (!__ballot(want[k])) continue;
+        if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
+          if (lane_id() == 0) x.misc[SVM_OVF] = 1;
+          return;
+        }
+        bool ins = false;
+        int h = -1;
+        if (want[k]) h = x2_slot(xt, key[k], ins);
+        const int nins = __popcll(__ballot(ins));
+        if (nins && lane_id() == 0) atomicAdd(&x.misc[SVM_FILL], nins);
+        if (__ballot(want[k] && h < 0) && lane_id() == 0) x.misc[SVM_OVF] = 1;
+        if (h >= 0) {
+          unsigned long long lo;
+          uint32_t hi;
+          xs_conv(sv[k] * factor, lo, hi);
+          x2_add(xt, h, lo, hi);
+        }
+        if (a.diag && lane_id() == 0) diag_add(a.diag, 138, (unsigned long long)__popcll(__ballot(want[k])));
+      }
+    });
 }
 
 // the self seed (1 - d) of v: into PT when v is a prev key, else into the sketch (pass 1)
@@ -375,7 +510,8 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
     sv_seed1(x, v, 1.0 - a.damping, sk);
   }
   const int64_t b = g.rp[v], e = g.rp[v + 1];
-  sv_pass1(g, s, a, x, b, e, sd.factor, sk);
+  if (a.whatif & WI_SV_P1WALK) sv_pass1(g, s, a, x, b, e, sd.factor, sk);
+  else sv_pass1b(g, s, a, x, b, e, sd.factor, sk);
   __syncthreads();
   sv_lap(a, 145, tph);
   // bound: the smallest exact total of the L prev keys
@@ -467,7 +603,8 @@ __global__ void __launch_bounds__(SV_THREADS) k_svA(DevGraph g, DevSlab s, IterA
   if (tk.k == 0 && threadIdx.x == 0) sv_seed1(x, v, 1.0 - a.damping, sk);
   int64_t b0, b1;
   sv_slice(g.rp[v], g.rp[v + 1], tk.k, sd.S, b0, b1);
-  sv_pass1(g, s, a, x, b0, b1, sd.factor, sk);
+  if (a.whatif & WI_SV_P1WALK) sv_pass1(g, s, a, x, b0, b1, sd.factor, sk);
+  else sv_pass1b(g, s, a, x, b0, b1, sd.factor, sk);
   __syncthreads();
   uint32_t* gs = gsk + sd.gsk;
   for (int c = threadIdx.x; c < SV_R * SV_W; c += blockDim.x) {

@@ -131,6 +131,14 @@ struct ppr_plan {
   double host_plan_part[2] = {0.0, 0.0};     // ordering, batch/descriptor loop  // the last hub pass: sources, largest candidate count
   int32_t* ovl_pending = nullptr;     // MC combine: a level's hub overflow list not yet read (run_hubs)
   int64_t x_bytes = 0;                // block bytes received by this rank in the last sharded run
+  // consumer routing (grank.hip xroute_build): a row goes only to the ranks whose sources read it;
+  // PPR_XROUTE=0 sends every row to every rank (the broadcast exchange)
+  bool xroute = true;
+  int8_t* d_xowner = nullptr;         // [n] rank merging each active node (-1: dangling)
+  uint32_t* d_xcmask = nullptr;       // [n] ranks reading each node's row
+  int32_t* d_xlists = nullptr;        // per partition: send lists to each peer, receive lists from each peer
+  size_t xlists_cap = 0;
+  int64_t x_rows_sent = 0;            // rows this rank sent in the last sharded run
   int64_t merge_launches = 0;
   double merge_ms = 0.0;           // sum of merge-phase spans (classify .. last merge kernel)
   hipEvent_t ev_a = nullptr, ev_b = nullptr, ev_m0 = nullptr, ev_m1 = nullptr;
@@ -241,6 +249,7 @@ inline void plan_free(ppr_plan* p) {
   if (p->stream4) hipStreamDestroy(p->stream4);
   if (p->comm) ncclCommDestroy(p->comm);
   hipFree(p->d_xsend); hipFree(p->d_xrecv); hipFree(p->d_xsz); hipFree(p->d_xtmp);
+  hipFree(p->d_xowner); hipFree(p->d_xcmask); hipFree(p->d_xlists);
   if (p->h_hub_pin) hipHostFree(p->h_hub_pin);
   if (p->h_desc_pin) hipHostFree(p->h_desc_pin);
   if (p->h_xs_pin) hipHostFree(p->h_xs_pin);

@@ -220,6 +220,15 @@ def run_local_group(plans, iterations: int, tolerance: float):
     return list(st)
 
 
+def exchange_bytes(plan):
+    """(block bytes this rank received, rows it sent) in the plan's last sharded run"""
+    import ctypes
+    from . import _lib
+    rb, rs = ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(_lib.lib().ppr_grank_plan_exchange_bytes(plan._p, ctypes.byref(rb), ctypes.byref(rs)), "exchange_bytes")
+    return int(rb.value), int(rs.value)
+
+
 def device_count() -> int:
     import ctypes
     from . import _lib

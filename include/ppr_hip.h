@@ -152,18 +152,29 @@ int ppr_grank_plan_active_list(ppr_plan* p, int32_t it, int32_t* out);
 int ppr_grank_plan_fold_maxdiff(ppr_plan* p, int32_t it, double maxdiff);
 
 /* ---- source sharding over RCCL (one process per GPU) ----
+ * Replaces the reference's per-iteration thread fan-out (header-only/grankMulti.h:376-396).
  * Rank 0 creates a 128-byte RCCL unique id, the caller broadcasts it (any channel), and every rank
  * calls ppr_grank_plan_comm_init. ppr_grank_plan_run_sharded then runs the whole job like
  * ppr_grank_plan_run, but each rank merges only its work-balanced range of every iteration's
- * active list (ppr_grank_plan_shard_bounds) and the written rows are exchanged as compact blocks:
- * an ncclAllGather of the block sizes, then one grouped set of ncclBroadcast calls (an
- * all-gather of variable-size blocks, no padding) on the plan's stream; maxDiff is combined with ncclAllReduce(MAX) so every rank
- * applies the reference's stopping rule to the same value. Results equal the 1-GPU run. */
+ * active list (ppr_grank_plan_shard_bounds) and the rows it wrote travel as compact blocks on the
+ * plan's stream:
+ *   routed (default, up to 32 ranks): a row goes only to the ranks whose sources read it (its
+ *     consumers, computed once per run from the CSR and the fixed bounds); per iteration one
+ *     grouped ncclSend/ncclRecv of the exact 8-byte block sizes, then one of the blocks; after
+ *     the last iteration each partition's final rows are broadcast once, so every rank ends with
+ *     the whole slab;
+ *   PPR_XROUTE=0: every rank's block to every rank (grouped ncclBroadcast at the block's bound,
+ *     8 + rows * ppr_grank_plan_row_bytes, no size exchange).
+ * maxDiff is combined with ncclAllReduce(MAX) on its IEEE bits, so every rank applies the
+ * reference's stopping rule to the same value. Results equal the 1-GPU run bit for bit.
+ * ppr_grank_plan_exchange_bytes: block bytes this rank received and rows it sent in its last
+ * sharded run (no reference counterpart: measurement). */
 int ppr_device_count(int32_t* count);
 int ppr_comm_unique_id(void* id128);
 int ppr_grank_plan_comm_init(ppr_plan* p, const void* id128, int32_t nranks, int32_t rank);
 int ppr_grank_plan_shard_bounds(ppr_plan* p, int32_t it, int32_t nranks, int64_t* bounds);
 int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance, ppr_stats* st);
+int ppr_grank_plan_exchange_bytes(ppr_plan* p, int64_t* recv_bytes, int64_t* rows_sent);
 /* Tests: the same native loop with n plans of this process as the ranks (one thread each, block
  * exchange by device copies instead of RCCL: RCCL refuses two ranks on one GPU). st: n stats or
  * null. Every plan must be built on the same graph and parameters. */

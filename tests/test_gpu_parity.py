@@ -312,6 +312,7 @@ def test_gpu_exact_sum_init_hubs_and_damping():
     ({"PPR_SV_BUDGET": "2"}, "redo"),                         # passing keys overflow the table: sources
     ({"PPR_SV_BUDGET": "2", "PPR_SV_SLICE": "512"}, "redo"),  # handed back to the range / partition engines
     ({"PPR_SV_MIN": "20000"}, "sieve"),                       # only the widest sources sieved
+    ({"PPR_WHATIF": "2048", "PPR_SV_SLICE": "700"}, "sieve"),  # pass 1 through hub_window_walk
     ({"PPR_SV": "0"}, None),                                  # off: range / partition engines only
 ])
 def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):

@@ -173,3 +173,29 @@ def test_gpu_local_group_more_ranks_than_sources_past_256_iterations(hot, monkey
         assert np.array_equal(r.lens, ref.lens) and np.array_equal(r.ids, ref.ids)
         assert np.array_equal(r.scores.view(np.uint64), ref.scores.view(np.uint64))
         pl.close()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gpu_routed_exchange_bit_exact_and_smaller(world, monkeypatch):
+    """consumer routing (a row goes only to the ranks whose sources read it; exact block sizes; the
+    final rows broadcast once) ends every rank with the single-GPU result bit for bit, tolerance
+    stop included, and moves fewer bytes than the broadcast exchange (PPR_XROUTE=0)"""
+    import approximated_personalized_pagerank_amd as ppr
+    from approximated_personalized_pagerank_amd.shard import exchange_bytes, run_local_group
+    g = ppr.rmat(14, seed=17)
+    part = g.partitions()
+    K, L, iters, tol = 32, 64, 9, 1e-5
+    ref = ppr.grank_csr(g, K, L, iters, 0.85, tol, part=part, device=0)
+    got = {}
+    for route in ("1", "0"):
+        monkeypatch.setenv("PPR_XROUTE", route)
+        plans = [ppr.GrankPlan(g, K, L, 0.85, part=part, device=0) for _ in range(world)]
+        st = run_local_group(plans, iters, tol)
+        got[route] = max(exchange_bytes(pl)[0] for pl in plans)
+        for pl, s in zip(plans, st):
+            assert int(s.iterations_run) == ref.iterations_run
+            r = pl.fetch()
+            assert np.array_equal(r.lens, ref.lens) and np.array_equal(r.ids, ref.ids)
+            assert np.array_equal(r.scores.view(np.uint64), ref.scores.view(np.uint64))
+            pl.close()
+    assert got["1"] < got["0"], got
