@@ -165,6 +165,7 @@ def lib() -> ctypes.CDLL:
         "ppr_grank_plan_shard_bounds": (ctypes.c_int, [vp, i32, i32, vp]),
         "ppr_grank_plan_run_sharded": (ctypes.c_int, [vp, u32, f64, vp]),
         "ppr_grank_plan_exchange_bytes": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
+        "ppr_grank_plan_kernel_stats": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp]),
         "ppr_grank_plan_run_local_group": (ctypes.c_int, [vp, i32, u32, f64, vp]),
         "ppr_grank_plan_pack_host": (ctypes.c_int, [vp, i32, i64, i64, vp, i64, ctypes.POINTER(i64)]),
         "ppr_grank_plan_unpack_host": (ctypes.c_int, [vp, i32, i64, i64, vp, i64]),

@@ -185,7 +185,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   TRY(dalloc(&p->d_tier_cap, NT + 1));
   TRY(dalloc(&p->d_ovf, n));
   TRY(dalloc(&p->d_maxdiff, PPR_MAX_ITER_STATS + 1));
-  TRY(dalloc(&p->d_stats, 2));
+  TRY(dalloc(&p->d_stats, PPR_NSTATS));
   TRY(dalloc(&p->d_out_ids, (size_t)n * K));
   TRY(dalloc(&p->d_out_sc, (size_t)n * K));
   TRY(dalloc(&p->d_out_len, n));
@@ -401,18 +401,25 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       if (hipMemcpy(p->d_tier_cap, caps, sizeof(caps), hipMemcpyHostToDevice) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
       // the sieve (merge_sv.h) for the wide sources: its prev table takes 2 Lp <= one slot per thread
       const char* s0 = getenv("PPR_SV");
-      p->sv_enabled = !(s0 && atoi(s0) == 0) && 2 * p->Lp <= SV_THREADS && sv_lds_bytes(p->Lp) <= 160 * 1024 &&
-                      svf_lds_bytes(p->Lp) <= 160 * 1024;
+      p->sv_enabled = !(s0 && atoi(s0) == 0) && 2 * p->Lp <= SV_THREADS &&
+                      sv_lds_bytes(p->Lp, SV_LARGE) <= 160 * 1024 && svf_lds_bytes(p->Lp) <= 160 * 1024;
       const char* s1 = getenv("PPR_SV_SLICE");
       const char* s2 = getenv("PPR_SV_MIN");
       if (s1) p->sv_slice = std::max<int64_t>(64, atoll(s1));
       if (s2) p->sv_min = std::max<int64_t>(0, atoll(s2));
+      const char* s5 = getenv("PPR_SV_SMALL");
+      const char* s6 = getenv("PPR_SV_MID");
+      if (s5) p->sv_small = std::max<int64_t>(0, atoll(s5));
+      if (s6) p->sv_mid = std::max<int64_t>(0, atoll(s6));
       const char* s3 = getenv("PPR_SV_BUDGET");
       if (s3) p->sv_budget = std::max(0, std::min(SV_XT_BUDGET, atoi(s3)));
-      if (p->sv_enabled &&
-          (hipStreamCreateWithFlags(&p->stream_sv, hipStreamNonBlocking) != hipSuccess ||
-           hipStreamCreateWithFlags(&p->stream_sv2, hipStreamNonBlocking) != hipSuccess ||
-           hipEventCreateWithFlags(&p->ev_sv, hipEventDisableTiming) != hipSuccess)) {
+      // the sieve's streams are the hub pipeline's (idle in the exact sum once the sieve takes the
+      // wide sources): more streams than the process's 4 hardware queues would share queues with
+      // the wave tier's stream3 and serialise behind it
+      p->stream_sv = p->stream2 ? p->stream2 : p->stream;
+      p->stream_sv2 = p->stream4 ? p->stream4 : p->stream;
+      p->stream_sv3 = p->stream5 ? p->stream5 : p->stream;
+      if (p->sv_enabled && hipEventCreateWithFlags(&p->ev_sv, hipEventDisableTiming) != hipSuccess) {
         plan_free(p);
         return PPR_ERR_HIP;
       }
@@ -1369,6 +1376,36 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
 // The sieve (merge_sv.h) for sources `src` (candidate counts `cand`): one-slice sources by k_sv1 on
 // stream_sv2 (largest first), multi-slice sources by k_svA -> k_svB -> k_svF on stream_sv. The
 // launches are asynchronous; sieve_collect waits and returns the sources handed back.
+// per-kernel roofline bookkeeping (plan.h NKST groups): events around a group's launches on its
+// stream; kst_fold reads the pair once the stream has been synchronised
+static void kst_reset(ppr_plan* p) {
+  for (int g = 0; g < ppr_plan::NKST; g++) {
+    p->kst_ms[g] = 0.0; p->kst_bytes[g] = 0.0; p->kst_pend_bytes[g] = 0.0;
+    p->kst_launches[g] = 0; p->kst_live[g] = false;
+  }
+}
+static void kst_begin(ppr_plan* p, int g, hipStream_t s) {
+  if (!p->ev_k[2 * g] && hipEventCreate(&p->ev_k[2 * g]) != hipSuccess) return;
+  if (!p->ev_k[2 * g + 1] && hipEventCreate(&p->ev_k[2 * g + 1]) != hipSuccess) return;
+  hipEventRecord(p->ev_k[2 * g], s);
+}
+static void kst_end(ppr_plan* p, int g, hipStream_t s, double bytes) {
+  if (!p->ev_k[2 * g + 1]) return;
+  hipEventRecord(p->ev_k[2 * g + 1], s);
+  p->kst_live[g] = true;
+  p->kst_pend_bytes[g] = bytes;
+}
+static void kst_fold(ppr_plan* p, int g) {
+  if (!p->kst_live[g]) return;
+  p->kst_live[g] = false;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, p->ev_k[2 * g], p->ev_k[2 * g + 1]) == hipSuccess) {
+    p->kst_ms[g] += ms;
+    p->kst_bytes[g] += p->kst_pend_bytes[g];
+    p->kst_launches[g]++;
+  }
+}
+
 struct SvRun {
   std::vector<int32_t> v;   // source of each descriptor
   size_t o_ovl = 0;         // offset of the overflow list in d_sv
@@ -1384,11 +1421,26 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   DevGraph g{p->d_rp, p->d_colx, p->n};
   const DevSlab s = dev_slab(p);
   const int Lp = p->Lp;
-  // multi-slice sources first (descriptors [0, nm)), then the one-slice ones by candidates, descending
+  // multi-slice sources first (descriptors [0, nm)), then the one-slice ones by size class (large,
+  // mid, small), each by candidates, descending
   std::vector<size_t> multi, one;
   for (size_t i = 0; i < n; i++) ((int64_t)cand[i] > p->sv_slice ? multi : one).push_back(i);
   std::stable_sort(one.begin(), one.end(), [&](size_t x, size_t y) { return cand[x] > cand[y]; });
   const size_t nm = multi.size(), nx = n;
+  // SURVEY s8d bytes of a sieved source: row pointer, its successors' ids and lengths, their rows,
+  // its own old row (full: L) and the new one, the length
+  auto sv_algo_bytes = [&](size_t i) {
+    return 8.0 + 8.0 * deg[i] + 12.0 * ((double)cand[i] - 1.0) + 24.0 * (double)p->L + 4.0;
+  };
+  size_t cls_end[3] = {0, 0, 0};  // one-slice class boundaries (indices into `one`): large | mid | small
+  {
+    size_t k = 0;
+    while (k < one.size() && (int64_t)cand[one[k]] >= p->sv_mid) k++;
+    cls_end[0] = k;
+    while (k < one.size() && (int64_t)cand[one[k]] >= p->sv_small) k++;
+    cls_end[1] = k;
+    cls_end[2] = one.size();
+  }
   std::vector<SvDesc> desc;
   std::vector<SvTask> tasks;
   desc.reserve(nx);
@@ -1400,10 +1452,10 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
     d.v = src[i];
     d.S = (int32_t)std::min<int64_t>(((int64_t)cand[i] + p->sv_slice - 1) / p->sv_slice, std::max<int32_t>(1, deg[i]));
     d.factor = p->damping / (double)deg[i];
-    d.gsk = (int64_t)k * SV_R * SV_W;
+    d.gsk = (int64_t)k * SV_R * (1 << SV_LARGE.wlog);
     d.gpt = (int64_t)k * 2 * Lp;
     // every slice flushes at most its table's keys: half-full global table at worst
-    d.tg = pow2_at_least(std::min<int64_t>(2 * (int64_t)d.S * (SV_XT_BUDGET + SV_WAVES * WAVE + 1),
+    d.tg = pow2_at_least(std::min<int64_t>(2 * (int64_t)d.S * (SV_LARGE.budget + SV_LARGE.threads() + 1),
                                            2 * (int64_t)cand[i] + 64));
     d.gxt = tg_total;
     tg_total += d.tg;
@@ -1420,16 +1472,20 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
     run.v.push_back(d.v);
   }
   const size_t nt = tasks.size();
-  // d_sv: desc | tasks | zeroed: ovl[1 + nx] | oflag[nm] | gpt | gsk | gkeys | ga | gb
+  // d_sv: desc | tasks | one-slice selections (keys, values) | zeroed: ovl[1 + nx] | selected
+  // counts[nx] | oflag[nm] | gpt | gsk | gkeys | ga | gb
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   size_t off = 0;
   const size_t o_d = off; off = al(off + sizeof(SvDesc) * nx);
   const size_t o_t = off; off = al(off + sizeof(SvTask) * (nt + 1));
+  const size_t o_sk = off; off = al(off + 4 * (size_t)Lp * nx);
+  const size_t o_sv = off; off = al(off + 8 * (size_t)Lp * nx);
   const size_t o_z = off;
   const size_t o_ov = off; off = al(off + 4 * (1 + nx));
+  const size_t o_sn = off; off = al(off + 4 * nx);
   const size_t o_of = off; off = al(off + 4 * (nm + 1));
   const size_t o_pt = off; off = al(off + 8 * 2 * (size_t)Lp * nm);
-  const size_t o_sk = off; off = al(off + 4 * (size_t)SV_R * SV_W * nm);
+  const size_t o_gs = off; off = al(off + 4 * (size_t)SV_R * ((size_t)1 << SV_LARGE.wlog) * nm);
   const size_t o_gk = off; off = al(off + 4 * (size_t)tg_total);
   const size_t o_ga = off; off = al(off + 8 * (size_t)tg_total);
   const size_t o_gb = off; off = al(off + 8 * (size_t)tg_total);
@@ -1444,26 +1500,52 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   hipStream_t s1 = p->stream_sv, s2 = p->stream_sv2;
   HIP_OK(hipMemcpyAsync(b, hb, up, hipMemcpyHostToDevice, s1));
   HIP_OK(hipMemsetAsync(b + o_z, 0, total - o_z, s1));
-  // the one-slice stream starts once the descriptors are up and the overflow list is zeroed
+  // the one-slice streams start once the descriptors are up and the overflow list is zeroed
   HIP_OK(hipEventRecord(p->ev_sv, s1));
   HIP_OK(hipStreamWaitEvent(s2, p->ev_sv, 0));
+  HIP_OK(hipStreamWaitEvent(p->stream_sv3, p->ev_sv, 0));
   const SvDesc* d_d = (const SvDesc*)(b + o_d);
   const SvTask* d_t = (const SvTask*)(b + o_t);
   int32_t* d_ov = (int32_t*)(b + o_ov);
   int32_t* d_of = (int32_t*)(b + o_of);
   unsigned long long* d_pt = (unsigned long long*)(b + o_pt);
-  uint32_t* d_sk = (uint32_t*)(b + o_sk);
+  uint32_t* d_sk = (uint32_t*)(b + o_gs);
+  int32_t* d_ok = (int32_t*)(b + o_sk);
+  double* d_ovv = (double*)(b + o_sv);
+  int32_t* d_on = (int32_t*)(b + o_sn);
   uint32_t* d_gk = (uint32_t*)(b + o_gk);
   unsigned long long* d_ga = (unsigned long long*)(b + o_ga);
   unsigned long long* d_gb = (unsigned long long*)(b + o_gb);
-  const size_t lds = sv_lds_bytes(Lp);
-  if (nx > nm) {
-    hipLaunchKernelGGL(k_sv1, dim3((unsigned)(nx - nm)), dim3(SV_THREADS), lds, s2, g, s, a, d_d, (int)nm, Lp, p->sv_budget,
-                       maxdiff, p->d_stats, d_ov);
-    HIP_OK(hipGetLastError());
-    p->merge_launches++;
+  const size_t lds = sv_lds_bytes(Lp, SV_LARGE);
+  {
+    // one-slice classes beside the multi-slice chain (stream_sv): large then small on stream_sv2,
+    // mid on stream_sv3, so each class's tail overlaps another's work
+    const SvGeom geo[3] = {SV_LARGE, SV_MID, SV_SMALL};
+    hipStream_t cs[3] = {s2, p->stream_sv3, s2};
+    size_t c0 = 0;
+    for (int c = 0; c < 3; c++) {
+      const size_t cnt = cls_end[c] - c0;
+      const int d0 = (int)(nm + c0);
+      double bytes = 0.0;
+      for (size_t k = c0; k < cls_end[c]; k++) bytes += sv_algo_bytes(one[k]);
+      c0 = cls_end[c];
+      if (!cnt) continue;
+      const SvGeom G = geo[c];
+      kst_begin(p, 1 + c, cs[c]);
+      hipLaunchKernelGGL(k_sv1, dim3((unsigned)cnt), dim3(G.threads()), sv_lds_bytes(Lp, G), cs[c], g, s, a, d_d, d0, Lp,
+                         G, std::min(p->sv_budget, G.budget), d_ov, d_ok, d_ovv, d_on);
+      HIP_OK(hipGetLastError());
+      hipLaunchKernelGGL(k_svfin, dim3((unsigned)cnt), dim3(64), svfin_lds_bytes(Lp), cs[c], s, a, d_d, d0, d_ok, d_ovv,
+                         d_on, Lp, maxdiff, p->d_stats);
+      HIP_OK(hipGetLastError());
+      kst_end(p, 1 + c, cs[c], bytes);
+      p->merge_launches += 2;
+    }
   }
   if (nm) {
+    double bytes = 0.0;
+    for (size_t i : multi) bytes += sv_algo_bytes(i);
+    kst_begin(p, 4, s1);
     hipLaunchKernelGGL(k_svA, dim3((unsigned)nt), dim3(SV_THREADS), lds, s1, g, s, a, d_d, d_t, Lp, d_sk, d_pt);
     HIP_OK(hipGetLastError());
     hipLaunchKernelGGL(k_svB, dim3((unsigned)nt), dim3(SV_THREADS), lds, s1, g, s, a, d_d, d_t, Lp, p->sv_budget, d_sk,
@@ -1472,6 +1554,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
     hipLaunchKernelGGL(k_svF, dim3((unsigned)nm), dim3(256), svf_lds_bytes(Lp), s1, s, a, d_d, Lp, d_pt, d_gk, d_ga,
                        d_gb, d_of, d_ov, maxdiff, p->d_stats);
     HIP_OK(hipGetLastError());
+    kst_end(p, 4, s1, bytes);
     p->merge_launches += 3;
   }
   p->sv_sources += (int64_t)nx;
@@ -1486,9 +1569,12 @@ static int sieve_collect(ppr_plan* p, SvRun& run, std::vector<int32_t>& back) {
   run.live = false;
   HIP_OK(hipEventRecord(p->ev_sv, p->stream_sv2));
   HIP_OK(hipStreamWaitEvent(p->stream_sv, p->ev_sv, 0));
+  HIP_OK(hipEventRecord(p->ev_sv, p->stream_sv3));
+  HIP_OK(hipStreamWaitEvent(p->stream_sv, p->ev_sv, 0));
   int32_t novf = 0;
   HIP_OK(hipMemcpyAsync(&novf, p->d_sv + run.o_ovl, 4, hipMemcpyDeviceToHost, p->stream_sv));
   HIP_OK(hipStreamSynchronize(p->stream_sv));
+  for (int g = 1; g < ppr_plan::NKST; g++) kst_fold(p, g);
   if (!novf) return PPR_OK;
   std::vector<int32_t> od(novf);
   HIP_OK(hipMemcpyAsync(od.data(), p->d_sv + run.o_ovl + 4, 4 * (size_t)novf, hipMemcpyDeviceToHost, p->stream_sv));
@@ -1589,6 +1675,7 @@ int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count
   if (rc || a.mc) return rc;
   HIP_OK(hipEventRecord(p->ev_m1, p->stream));
   HIP_OK(hipEventSynchronize(p->ev_m1));
+  kst_fold(p, 0);
   float ms = 0.f;
   HIP_OK(hipEventElapsedTime(&ms, p->ev_m0, p->ev_m1));
   if (!a.unit) p->merge_ms += ms;
@@ -1728,8 +1815,10 @@ reclassify:
   }
   // the classification is complete (host sync): the wave tiers need no event to start on stream3
   hipStream_t sw = p->stream3 ? p->stream3 : st;
+  bool wave_ev = false;
   for (int t = 0; t < NT; t++) {
     if (!cnt[t] || !p->tierT[t]) continue;
+    if (!wave_ev && !a.unit && !a.mc) { kst_begin(p, 0, sw); wave_ev = true; }
     // one wave per block by default: no LDS left unusable by a 4-wave block granularity
     const int wpb = p->wave_wpb;
     const int64_t blocks = ((int64_t)cnt[t] + wpb - 1) / wpb;
@@ -1747,6 +1836,7 @@ reclassify:
     HIP_OK(hipGetLastError());
     p->merge_launches++;
   }
+  if (wave_ev) kst_end(p, 0, sw, 0.0);  // (bytes: the device counter, read at the end of the run)
   if (a.xs) {
     // exact sum: every source no wave tier took (the hub tier, tiers the plan left without a
     // wave kernel) goes through the range / bucket workgroups -- nothing falls to the chain-order
@@ -1926,9 +2016,10 @@ extern "C" int ppr_grank_plan_run(ppr_plan* p, uint32_t iterations, double toler
   HIP_OK(hipSetDevice(p->device));
   hipStream_t s = p->stream;
   HIP_OK(hipMemsetAsync(p->d_maxdiff, 0, 8 * (PPR_MAX_ITER_STATS + 1), s));
-  HIP_OK(hipMemsetAsync(p->d_stats, 0, 16, s));
+  HIP_OK(hipMemsetAsync(p->d_stats, 0, 8 * PPR_NSTATS, s));
   p->merge_launches = 0;
   p->merge_ms = 0.0;
+  kst_reset(p);
   HIP_OK(hipEventRecord(p->ev_a, s));
   int rc = ppr_grank_plan_init(p);
   if (rc) return rc;
@@ -1961,12 +2052,23 @@ extern "C" int ppr_grank_plan_run(ppr_plan* p, uint32_t iterations, double toler
     st->iterations_run = (int32_t)it;
     st->device_ms = ms;
     st->merge_ms = p->merge_ms;
-    unsigned long long sv[2];
-    HIP_OK(hipMemcpyAsync(sv, p->d_stats, 16, hipMemcpyDeviceToHost, s));
+    unsigned long long sv[3];
+    HIP_OK(hipMemcpyAsync(sv, p->d_stats, 24, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     st->candidates = (int64_t)sv[0];
     st->algo_bytes = (int64_t)sv[1];
     st->merge_launches = p->merge_launches;
+    p->kst_bytes[0] = (double)sv[2];
+  }
+  return PPR_OK;
+}
+
+extern "C" int ppr_grank_plan_kernel_stats(ppr_plan* p, int32_t n, double* bytes, double* ms, int64_t* launches) {
+  if (!p || n < 0) return PPR_ERR_ARG;
+  for (int g = 0; g < n && g < ppr_plan::NKST; g++) {
+    if (bytes) bytes[g] = p->kst_bytes[g];
+    if (ms) ms[g] = p->kst_ms[g];
+    if (launches) launches[g] = p->kst_launches[g];
   }
   return PPR_OK;
 }
@@ -2484,7 +2586,7 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
   HIP_OK(hipSetDevice(p->device));
   hipStream_t s = p->stream;
   HIP_OK(hipMemsetAsync(p->d_maxdiff, 0, 8 * (PPR_MAX_ITER_STATS + 1), s));
-  HIP_OK(hipMemsetAsync(p->d_stats, 0, 16, s));
+  HIP_OK(hipMemsetAsync(p->d_stats, 0, 8 * PPR_NSTATS, s));
   p->merge_launches = 0;
   p->merge_ms = 0.0;
   p->x_bytes = 0;

@@ -217,7 +217,7 @@ extern "C" int ppr_mccp2_plan_run(ppr_plan* p, uint32_t walks, uint64_t seed, pp
   if (walks == 0) return PPR_ERR_ITERS;
   HIP_OK(hipSetDevice(p->device));
   hipStream_t s = p->stream;
-  HIP_OK(hipMemsetAsync(p->d_stats, 0, 16, s));
+  HIP_OK(hipMemsetAsync(p->d_stats, 0, 8 * PPR_NSTATS, s));
   p->merge_launches = 0;
   p->merge_ms = 0.0;
   p->mc_walk_ms = 0.0;

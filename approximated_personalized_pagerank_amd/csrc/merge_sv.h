@@ -37,16 +37,30 @@
 namespace pprk {
 
 constexpr int SV_R = 3;                       // sketch rows
-constexpr int SV_WLOG = 13;                   // counters per row = 2^SV_WLOG
-constexpr int SV_W = 1 << SV_WLOG;
 constexpr int SV_UNIT_LOG = 31;               // a counter unit is 2^-31 (GRank totals are <= 1)
-constexpr int SV_WAVES = 16;
-constexpr int SV_THREADS = SV_WAVES * WAVE;
-constexpr int SV_XT = 4096;                   // pass-2 table slots
-constexpr int SV_XT_BUDGET = SV_XT * 85 / 100 - SV_WAVES * WAVE;  // distinct passing keys before overflow
-constexpr int SV_BM_WORDS = SV_R * SV_W / 64;  // sieve bitmap (u64 words)
-constexpr size_t SV_SKETCH_BYTES = (size_t)SV_R * SV_W * 4;
-constexpr size_t SV_REGION = SV_SKETCH_BYTES > (size_t)SV_XT * 20 ? SV_SKETCH_BYTES : (size_t)SV_XT * 20;
+constexpr int SV_XS = 4;                      // pass-2 table slots per thread in every size class
+// Size classes of the one-slice workgroups (host: sieve_launch): the widest sources take 16 waves
+// and a 3 x 8192 sketch (one workgroup per CU), narrower ones 8 waves / 3 x 4096 (two per CU) or
+// 4 waves / 3 x 2048 (four per CU) -- a narrow source's few batches per wave cannot hide their HBM
+// latencies unless several sources share the CU. Multi-slice sources use the widest class.
+struct SvGeom {
+  int wlog;     // counters per sketch row = 2^wlog
+  int waves;
+  int xt;       // pass-2 table slots (= SV_XS * threads)
+  int budget;   // distinct passing keys before the table overflows
+  __host__ __device__ constexpr int threads() const { return waves * WAVE; }
+  __host__ __device__ constexpr int bm_words() const { return SV_R * (1 << wlog) / 64; }
+  __host__ __device__ constexpr size_t sketch_bytes() const { return (size_t)SV_R * ((size_t)1 << wlog) * 4; }
+  __host__ __device__ constexpr size_t region() const {
+    return sketch_bytes() > (size_t)xt * 20 ? sketch_bytes() : (size_t)xt * 20;
+  }
+};
+__host__ __device__ constexpr SvGeom sv_geom(int wlog, int waves) {
+  return SvGeom{wlog, waves, SV_XS * waves * WAVE, SV_XS * waves * WAVE * 85 / 100 - waves * WAVE};
+}
+constexpr SvGeom SV_LARGE = sv_geom(13, 16), SV_MID = sv_geom(12, 8), SV_SMALL = sv_geom(11, 4);
+constexpr int SV_THREADS = 16 * WAVE;         // the widest class (multi-slice kernels)
+constexpr int SV_XT_BUDGET = SV_LARGE.budget;
 constexpr int SVF_CAP = 4096;                 // k_svF: dense entries at or above the bound
 constexpr uint32_t WI_SV_P1WALK = 1u << 11;   // PPR_WHATIF 2048: sieve pass 1 through hub_window_walk (A/B)
 
@@ -128,8 +142,8 @@ __device__ __forceinline__ uint64_t sv_mix(uint32_t k) {
   x ^= x >> 32;
   return x;
 }
-__device__ __forceinline__ uint32_t sv_cell(uint64_t x, int j) {
-  return (uint32_t)j * SV_W + ((uint32_t)(x >> (SV_WLOG * j)) & (uint32_t)(SV_W - 1));
+__device__ __forceinline__ uint32_t sv_cell(uint64_t x, int j, int wlog) {
+  return ((uint32_t)j << wlog) + ((uint32_t)(x >> (wlog * j)) & ((1u << wlog) - 1u));
 }
 // ceil(p * 2^31): an upper bound of the contribution in counter units
 __device__ __forceinline__ uint32_t sv_units(double p) {
@@ -143,18 +157,18 @@ __device__ __forceinline__ uint32_t sv_thr(double theta) {
   const double x = floor(ldexp(theta, SV_UNIT_LOG) * (1.0 - 0x1p-40));
   return x <= 0.0 ? 0u : x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
 }
-__device__ __forceinline__ void sv_sketch_add(uint32_t* sk, int key, uint32_t u) {
+__device__ __forceinline__ void sv_sketch_add(uint32_t* sk, int key, uint32_t u, int wlog) {
   const uint64_t x = sv_mix((uint32_t)key);
 #pragma unroll
-  for (int j = 0; j < SV_R; j++) atomicAdd(&sk[sv_cell(x, j)], u);
+  for (int j = 0; j < SV_R; j++) atomicAdd(&sk[sv_cell(x, j, wlog)], u);
 }
 // every counter of `key` at or above the threshold (bitmap of the counters that are)
-__device__ __forceinline__ bool sv_passes(const uint64_t* bm, int key) {
+__device__ __forceinline__ bool sv_passes(const uint64_t* bm, int key, int wlog) {
   const uint64_t x = sv_mix((uint32_t)key);
   uint64_t w[SV_R];
   uint32_t c[SV_R];
 #pragma unroll
-  for (int j = 0; j < SV_R; j++) { c[j] = sv_cell(x, j); w[j] = bm[c[j] >> 6]; }
+  for (int j = 0; j < SV_R; j++) { c[j] = sv_cell(x, j, wlog); w[j] = bm[c[j] >> 6]; }
   bool ok = true;
 #pragma unroll
   for (int j = 0; j < SV_R; j++) ok = ok && ((w[j] >> (c[j] & 63u)) & 1ull);
@@ -167,7 +181,7 @@ struct SvDesc {
   int32_t v;
   int32_t S;          // slices (1: k_sv1)
   double factor;      // d / deg
-  int64_t gsk;        // multi: u32 offset of its global sketch (SV_R * SV_W)
+  int64_t gsk;        // multi: u32 offset of its global sketch (SV_LARGE: SV_R * 8192)
   int64_t gpt;        // multi: offset of its PT sums (Lp pairs of u64: A, B by prev-row position)
   int64_t gxt;        // multi: slot offset of its global table
   int32_t tg;         // multi: global table slots (power of two)
@@ -177,12 +191,12 @@ struct SvTask { int32_t d; int32_t k; };
 
 // LDS of the slice / single-source workgroups:
 //   region (sketch in pass 1; XT in pass 2; dense (value, key) list in the select)
-//   PT (2 Lp slots) | pti i32[2 Lp] (prev-row position of a PT slot) | bitmap u64[SV_BM_WORDS] |
-//   walk flags u8[SV_WAVES][HUB_WALK_FLAGS] | misc i32[64] | finish_source scratch
+//   PT (2 Lp slots) | pti i32[2 Lp] (prev-row position of a PT slot) | bitmap u64[bm_words] |
+//   walk flags u8[waves][HUB_WALK_FLAGS] | misc i32[64] | hist u32[256] (block select)
 enum { SVM_FILL = 0, SVM_OVF = 1, SVM_U = 2, SVM_PT = 3, SVM_THETA = 8 /* u64: 8..9 */ };
-__host__ __device__ constexpr size_t sv_lds_bytes(int Lp) {
-  return SV_REGION + x2_bytes(2 * Lp) + (size_t)8 * Lp + (size_t)SV_BM_WORDS * 8 +
-         (size_t)SV_WAVES * HUB_WALK_FLAGS + 256 + 1024 + (size_t)Lp * 32;
+__host__ __device__ constexpr size_t sv_lds_bytes(int Lp, SvGeom G) {
+  return G.region() + x2_bytes(2 * Lp) + (size_t)8 * Lp + (size_t)G.bm_words() * 8 +
+         (size_t)G.waves * HUB_WALK_FLAGS + 256 + 1024;
 }
 struct SvLds {
   unsigned char* region;
@@ -192,27 +206,21 @@ struct SvLds {
   uint8_t* fl;
   int* misc;
   uint32_t* hist;
-  uint64_t* rv;
-  int* rk;
-  int* hk;
-  int* hv;
-  int* mf;
+  int wlog;
+  int bm_words;
 };
-__device__ __forceinline__ SvLds sv_carve(unsigned char* smem, int Lp) {
+__device__ __forceinline__ SvLds sv_carve(unsigned char* smem, int Lp, SvGeom G) {
   SvLds x;
   unsigned char* p = smem;
-  x.region = p; p += SV_REGION;
+  x.region = p; p += G.region();
   x.pt = x2_carve(p, 2 * Lp); p += x2_bytes(2 * Lp);
   x.pti = reinterpret_cast<int*>(p); p += (size_t)8 * Lp;
-  x.bm = reinterpret_cast<uint64_t*>(p); p += (size_t)SV_BM_WORDS * 8;
-  x.fl = p; p += (size_t)SV_WAVES * HUB_WALK_FLAGS;
+  x.bm = reinterpret_cast<uint64_t*>(p); p += (size_t)G.bm_words() * 8;
+  x.fl = p; p += (size_t)G.waves * HUB_WALK_FLAGS;
   x.misc = reinterpret_cast<int*>(p); p += 256;
-  x.hist = reinterpret_cast<uint32_t*>(p); p += 1024;
-  x.rv = reinterpret_cast<uint64_t*>(p); p += (size_t)Lp * 8;
-  x.rk = reinterpret_cast<int*>(p); p += (size_t)Lp * 4;
-  x.hk = reinterpret_cast<int*>(p); p += (size_t)Lp * 8;
-  x.hv = reinterpret_cast<int*>(p); p += (size_t)Lp * 8;
-  x.mf = reinterpret_cast<int*>(p);
+  x.hist = reinterpret_cast<uint32_t*>(p);
+  x.wlog = G.wlog;
+  x.bm_words = G.bm_words();
   return x;
 }
 
@@ -263,7 +271,7 @@ __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, co
       xs_conv(p, lo, hi);
       x2_add(x.pt, h, lo, hi);
     } else {
-      sv_sketch_add(sk, id, sv_units(p));
+      sv_sketch_add(sk, id, sv_units(p), x.wlog);
     }
   });
 }
@@ -374,7 +382,7 @@ __device__ __forceinline__ void sv_pass1b(const DevGraph& g, const DevSlab& s, c
           xs_conv(p, lo, hi);
           x2_add(x.pt, h, lo, hi);
         } else {
-          sv_sketch_add(sk, key[k], sv_units(p));
+          sv_sketch_add(sk, key[k], sv_units(p), x.wlog);
         }
       }
     });
@@ -398,7 +406,7 @@ __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, co
       bool any = false;
 #pragma unroll
       for (int k = 0; k < NB; k++) {
-        want[k] = valid[k] && sv_passes(x.bm, key[k]);
+        want[k] = valid[k] && sv_passes(x.bm, key[k], x.wlog);
         if (want[k]) want[k] = x2_find(x.pt, key[k]) < 0;
         any = any || want[k];
       }
@@ -439,12 +447,12 @@ __device__ __forceinline__ void sv_seed1(const SvLds& x, int v, double seed, uin
     xs_conv(seed, lo, hi);
     x2_add(x.pt, h, lo, hi);
   } else {
-    sv_sketch_add(sk, v, sv_units(seed));
+    sv_sketch_add(sk, v, sv_units(seed), x.wlog);
   }
 }
 // ... and into XT in pass 2 when v is not a prev key and passes
 __device__ __forceinline__ void sv_seed2(const SvLds& x, const X2Table& xt, int v, double seed) {
-  if (x2_find(x.pt, v) >= 0 || !sv_passes(x.bm, v)) return;
+  if (x2_find(x.pt, v) >= 0 || !sv_passes(x.bm, v, x.wlog)) return;
   bool ins;
   const int h = x2_slot(xt, v, ins);
   if (h < 0) { x.misc[SVM_OVF] = 1; return; }
@@ -459,7 +467,7 @@ __device__ __forceinline__ void sv_seed2(const SvLds& x, const X2Table& xt, int 
 template <class Get>
 __device__ __forceinline__ void sv_bitmap(const SvLds& x, uint32_t thr, Get get) {
   const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
-  for (int w = wv; w < SV_BM_WORDS; w += W) {
+  for (int w = wv; w < x.bm_words; w += W) {
     const uint64_t m = __ballot(get(w * 64 + lane_id()) >= thr);
     if (lane_id() == 0) x.bm[w] = m;
   }
@@ -487,10 +495,10 @@ __device__ __forceinline__ void sv_clear_region(const SvLds& x, size_t bytes) {
 
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterArgs a, const SvDesc* desc, int d0,
-                                                    int Lp, int budget, unsigned long long* maxdiff,
-                                                    unsigned long long* stats, int32_t* ovl) {
+                                                    int Lp, SvGeom G, int budget, int32_t* ovl, int32_t* out_k,
+                                                    double* out_v, int32_t* out_n) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const SvLds x = sv_carve(smem, Lp);
+  const SvLds x = sv_carve(smem, Lp, G);
   const int d = d0 + (int)blockIdx.x;
   const SvDesc sd = desc[d];
   const int v = sd.v;
@@ -502,7 +510,7 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
   }
   long long tph = a.diag ? (long long)clock64() : 0;
   uint32_t* sk = reinterpret_cast<uint32_t*>(x.region);
-  sv_clear_region(x, SV_SKETCH_BYTES);
+  sv_clear_region(x, G.sketch_bytes());
   sv_build_pt(x, s, a, v, Lp);
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -522,52 +530,54 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
   const uint32_t thr = sv_thr(theta);
   sv_bitmap(x, thr, [&](int c) { return sk[c]; });
   __syncthreads();
-  const X2Table xt = x2_carve(x.region, SV_XT);
-  sv_clear_region(x, x2_bytes(SV_XT));
+  const X2Table xt = x2_carve(x.region, G.xt);
+  sv_clear_region(x, x2_bytes(G.xt));
   __syncthreads();
   sv_lap(a, 146, tph);
   if (threadIdx.x == 0) sv_seed2(x, xt, v, 1.0 - a.damping);
   sv_pass2(g, s, a, x, xt, b, e, sd.factor, budget);
   __syncthreads();
   sv_lap(a, 147, tph);
-  if (x.misc[SVM_OVF] || x.misc[SVM_FILL] > budget + SV_WAVES * WAVE) {
+  if (x.misc[SVM_OVF] || x.misc[SVM_FILL] > budget + G.waves * WAVE) {
     if (threadIdx.x == 0) ovl[1 + atomicAdd(&ovl[0], 1)] = d;
     if (a.diag && threadIdx.x == 0) diag_add(a.diag, 137, 1ull);
     return;
   }
-  // dense (value, key) list of PT u {XT keys >= theta}: slot values into registers, then written
-  // over the front of the region after every slot was read
-  constexpr int XS = SV_XT / SV_THREADS;
-  double xv[XS + 1];
-  int xk[XS + 1];
+  // dense (value, key) list of PT u {XT keys >= theta}: the table's slot values into registers
+  // (SV_XS per thread), then written over the front of the region after every slot was read; the
+  // PT entries (outside the region) after them
+  double xv[SV_XS];
+  int xk[SV_XS];
   int c = 0;
 #pragma unroll
-  for (int j = 0; j < XS; j++) {
-    const int i = (int)threadIdx.x + j * SV_THREADS;
+  for (int j = 0; j < SV_XS; j++) {
+    const int i = (int)threadIdx.x + j * (int)blockDim.x;
     const uint32_t kt = xt.keys[i];
     const double val = kt ? x2_value(xt.a[i], xt.b[i]) : 0.0;
     xk[j] = (kt && val >= theta) ? (int)kt - 1 : -1;
     xv[j] = val;
     c += xk[j] >= 0;
   }
-  xk[XS] = -1;
-  xv[XS] = 0.0;
-  if ((int)threadIdx.x < Tpt && x.pt.keys[threadIdx.x]) {
-    xk[XS] = (int)x.pt.keys[threadIdx.x] - 1;
-    xv[XS] = x2_value(x.pt.a[threadIdx.x], x.pt.b[threadIdx.x]);
-    c++;
-  }
   const int incl = wave_incl_scan(c);
   int base = 0;
   if (lane_id() == WAVE - 1 && incl) base = atomicAdd(&x.misc[SVM_U], incl);
   base = __builtin_amdgcn_readlane(base, WAVE - 1) + incl - c;
   __syncthreads();  // every slot read
-  const int cap = SV_XT + Lp;
+  const int cap = G.xt + Lp;
   double* dv = reinterpret_cast<double*>(x.region);
   int* dk = reinterpret_cast<int*>(x.region + (size_t)cap * 8);
 #pragma unroll
-  for (int j = 0; j <= XS; j++)
+  for (int j = 0; j < SV_XS; j++)
     if (xk[j] >= 0) { dv[base] = xv[j]; dk[base] = xk[j]; base++; }
+  for (int i0 = 0; i0 < Tpt; i0 += blockDim.x) {
+    const int i = i0 + (int)threadIdx.x;
+    const bool has = i < Tpt && x.pt.keys[i] != 0u;
+    const uint64_t m = __ballot(has);
+    int b0 = 0;
+    if (m && lane_id() == 0) b0 = atomicAdd(&x.misc[SVM_U], __popcll(m));
+    b0 = __shfl(b0, 0) + __popcll(m & lanemask_lt());
+    if (has) { dv[b0] = x2_value(x.pt.a[i], x.pt.b[i]); dk[b0] = (int)x.pt.keys[i] - 1; }
+  }
   __syncthreads();
   const int U = x.misc[SVM_U];
   if (a.diag && threadIdx.x == 0) {
@@ -575,10 +585,63 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
     diag_add(a.diag, 136, (unsigned long long)x.misc[SVM_FILL]);
     diag_add(a.diag, 139, (unsigned long long)(U - L));
   }
-  if (threadIdx.x < WAVE)
-    finish_source(v, U, [&](int i) { return dk[i]; }, [&](int i) { return dv[i]; }, s, a, x.hist, x.rv, x.rk, Lp,
-                  x.hk, x.hv, x.mf, maxdiff, stats);
+  // top-L of the dense list (every thread: a block radix select when U > L), emitted for k_svfin,
+  // which writes the row at full occupancy once this LDS-heavy workgroup is gone
+  const uint32_t ts = tie_salt(v);
+  SelCrit sc;
+  sc.tie = false; sc.pa = 0; sc.ma = 0; sc.pb = 0; sc.mb = 0;
+  const bool cut = U > L;
+  if (cut) {
+    WgLds w = WgLds{};
+    w.hist = x.hist;
+    w.misc = x.misc;
+    sc = wg_select_top(w, U, L, [&](int i) { return dk[i]; }, [&](int i) { return dv[i]; }, [](int) { return true; }, ts);
+  }
+  if (threadIdx.x == 0) x.misc[SVM_PT] = 0;
+  __syncthreads();
+  int32_t* ok = out_k + (int64_t)d * Lp;
+  double* ov = out_v + (int64_t)d * Lp;
+  for (int i0 = 0; i0 < U; i0 += blockDim.x) {
+    const int i = i0 + threadIdx.x;
+    const bool sel = i < U && (!cut || sel_test(sc, dbits(dv[i]), tie_w(dk[i], ts)));
+    const uint64_t m = __ballot(sel);
+    int b0 = 0;
+    if (m && lane_id() == 0) b0 = atomicAdd(&x.misc[SVM_PT], __popcll(m));
+    b0 = __shfl(b0, 0);
+    if (sel) {
+      const int pos = b0 + __popcll(m & lanemask_lt());
+      ok[pos] = dk[i];
+      ov[pos] = dv[i];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) out_n[d] = x.misc[SVM_PT];
   if (threadIdx.x == 0) sv_lap(a, 148, tph);
+}
+
+// the row of a one-slice source from its selected entries (k_sv1): one wave per source -- sort in
+// hash order, write, range index, norm1 against the old row, maxDiff (finish_source)
+__host__ __device__ constexpr size_t svfin_lds_bytes(int Lp) { return (size_t)Lp * 12 + 1024 + (size_t)Lp * 20; }
+__global__ void __launch_bounds__(64) k_svfin(DevSlab s, IterArgs a, const SvDesc* desc, int d0, const int32_t* in_k,
+                                              const double* in_v, const int32_t* in_n, int Lp,
+                                              unsigned long long* maxdiff, unsigned long long* stats) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int d = d0 + (int)blockIdx.x;
+  const int n = in_n[d];
+  if (n <= 0) return;  // handed back (a written source has L >= 1 entries)
+  const int v = desc[d].v;
+  uint64_t* rv = reinterpret_cast<uint64_t*>(smem);
+  int* rk = reinterpret_cast<int*>(smem + (size_t)Lp * 8);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + (size_t)Lp * 12);
+  int* hk = reinterpret_cast<int*>(smem + (size_t)Lp * 12 + 1024);
+  int* hv = hk + 2 * Lp;
+  int* mf = hv + 2 * Lp;
+  const int32_t* ik = in_k + (int64_t)d * Lp;
+  const double* iv = in_v + (int64_t)d * Lp;
+  for (int i = lane_id(); i < n; i += WAVE) { rk[i] = ik[i]; rv[i] = dbits(iv[i]); }
+  wave_fence();
+  finish_source(v, n, [&](int i) { return rk[i]; }, [&](int i) { return bitsd(rv[i]); }, s, a, hist, rv, rk, Lp, hk, hv,
+                mf, maxdiff, stats);
 }
 
 // slice k of S of the successor list [b, e)
@@ -592,12 +655,13 @@ __global__ void __launch_bounds__(SV_THREADS) k_svA(DevGraph g, DevSlab s, IterA
                                                     const SvTask* tasks, int Lp, uint32_t* gsk,
                                                     unsigned long long* gpt) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const SvLds x = sv_carve(smem, Lp);
+  constexpr SvGeom G = SV_LARGE;
+  const SvLds x = sv_carve(smem, Lp, G);
   const SvTask tk = tasks[blockIdx.x];
   const SvDesc sd = desc[tk.d];
   const int v = sd.v;
   uint32_t* sk = reinterpret_cast<uint32_t*>(x.region);
-  sv_clear_region(x, SV_SKETCH_BYTES);
+  sv_clear_region(x, G.sketch_bytes());
   sv_build_pt(x, s, a, v, Lp);
   __syncthreads();
   if (tk.k == 0 && threadIdx.x == 0) sv_seed1(x, v, 1.0 - a.damping, sk);
@@ -607,7 +671,7 @@ __global__ void __launch_bounds__(SV_THREADS) k_svA(DevGraph g, DevSlab s, IterA
   else sv_pass1b(g, s, a, x, b0, b1, sd.factor, sk);
   __syncthreads();
   uint32_t* gs = gsk + sd.gsk;
-  for (int c = threadIdx.x; c < SV_R * SV_W; c += blockDim.x) {
+  for (int c = threadIdx.x; c < SV_R * (1 << G.wlog); c += blockDim.x) {
     const uint32_t u = sk[c];
     if (u) atomicAdd(&gs[c], u);
   }
@@ -642,7 +706,8 @@ __global__ void __launch_bounds__(SV_THREADS) k_svB(DevGraph g, DevSlab s, IterA
                                                     const unsigned long long* gpt, uint32_t* gkeys,
                                                     unsigned long long* ga, unsigned long long* gb, int32_t* oflag) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const SvLds x = sv_carve(smem, Lp);
+  constexpr SvGeom G = SV_LARGE;
+  const SvLds x = sv_carve(smem, Lp, G);
   const SvTask tk = tasks[blockIdx.x];
   const SvDesc sd = desc[tk.d];
   const int v = sd.v;
@@ -656,15 +721,15 @@ __global__ void __launch_bounds__(SV_THREADS) k_svB(DevGraph g, DevSlab s, IterA
   const uint32_t thr = sv_thr(theta);
   const uint32_t* gs = gsk + sd.gsk;
   sv_bitmap(x, thr, [&](int c) { return gs[c]; });
-  const X2Table xt = x2_carve(x.region, SV_XT);
-  sv_clear_region(x, x2_bytes(SV_XT));
+  const X2Table xt = x2_carve(x.region, G.xt);
+  sv_clear_region(x, x2_bytes(G.xt));
   __syncthreads();
   if (tk.k == 0 && threadIdx.x == 0) sv_seed2(x, xt, v, 1.0 - a.damping);
   int64_t b0, b1;
   sv_slice(g.rp[v], g.rp[v + 1], tk.k, sd.S, b0, b1);
   sv_pass2(g, s, a, x, xt, b0, b1, sd.factor, budget);
   __syncthreads();
-  if (x.misc[SVM_OVF] || x.misc[SVM_FILL] > budget + SV_WAVES * WAVE) {
+  if (x.misc[SVM_OVF] || x.misc[SVM_FILL] > budget + G.waves * WAVE) {
     if (threadIdx.x == 0) oflag[tk.d] = 1;
     return;
   }
@@ -673,7 +738,7 @@ __global__ void __launch_bounds__(SV_THREADS) k_svB(DevGraph g, DevSlab s, IterA
   unsigned long long* gA = ga + sd.gxt;
   unsigned long long* gB = gb + sd.gxt;
   bool full = false;
-  for (int i = threadIdx.x; i < SV_XT; i += blockDim.x) {
+  for (int i = threadIdx.x; i < G.xt; i += blockDim.x) {
     const uint32_t kt = xt.keys[i];
     if (!kt) continue;
     const int64_t h = sv_gslot(gk, sd.tg, (int)kt - 1);

@@ -54,9 +54,9 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
   __shared__ int s_tier[CLS_PER_BLOCK];
   __shared__ int s_src[CLS_PER_BLOCK];
   __shared__ uint32_t s_base[NLISTS];
-  __shared__ unsigned long long s_red[2][WAVES_PER_BLOCK];
+  __shared__ unsigned long long s_red[3][WAVES_PER_BLOCK];
   const int wv = threadIdx.x >> 6;
-  unsigned long long my_c = 0, my_b = 0;
+  unsigned long long my_c = 0, my_b = 0, my_w = 0;
   for (int k = 0; k < per_wave; k++) {
     const int slot = wv * per_wave + k;
     const int64_t idx = (int64_t)blockIdx.x * per_block + slot;
@@ -89,6 +89,7 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
       const int ownlen = (a.unit || a.mc) ? 0 : s.len[s.lrow(a.active == 0 ? a.sA : a.sB, v)];
       my_c += (unsigned long long)c;
       my_b += (unsigned long long)(8 + 8 * (e - b) + 12 * c + 12 * ownlen);
+      if (t < NT) my_w += (unsigned long long)(8 + 8 * (e - b) + 12 * c + 12 * ownlen);  // (wave-tier share)
     }
   }
   __syncthreads();
@@ -97,7 +98,7 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
     for (int i = 0; i < per_block; i++) n += s_tier[i] == (int)threadIdx.x;
     s_base[threadIdx.x] = n ? atomicAdd(&tier_cnt[threadIdx.x], n) : 0u;
   }
-  if (a.stats && lane_id() == 0) { s_red[0][wv] = my_c; s_red[1][wv] = my_b; }
+  if (a.stats && lane_id() == 0) { s_red[0][wv] = my_c; s_red[1][wv] = my_b; s_red[2][wv] = my_w; }
   __syncthreads();
   if ((int)threadIdx.x < per_block) {
     const int t = s_tier[threadIdx.x];
@@ -108,10 +109,11 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
     }
   }
   if (a.stats && threadIdx.x == 0) {
-    unsigned long long sc = 0, sb = 0;
-    for (int i = 0; i < WAVES_PER_BLOCK; i++) { sc += s_red[0][i]; sb += s_red[1][i]; }
+    unsigned long long sc = 0, sb = 0, sw = 0;
+    for (int i = 0; i < WAVES_PER_BLOCK; i++) { sc += s_red[0][i]; sb += s_red[1][i]; sw += s_red[2][i]; }
     if (sc) atomicAdd(&stats[0], sc);
     if (sb) atomicAdd(&stats[1], sb);
+    if (sw) atomicAdd(&stats[2], sw);
   }
 }
 
@@ -144,6 +146,7 @@ __global__ void __launch_bounds__(CLS_BIG_THREADS) k_classify_big(DevGraph g, De
         const int ownlen = a.mc ? 0 : s.len[s.lrow(a.active == 0 ? a.sA : a.sB, v)];
         atomicAdd(&stats[0], (unsigned long long)c);
         atomicAdd(&stats[1], (unsigned long long)(8 + 8 * (e - b) + 12 * c + 12 * ownlen));
+        if (t < NT) atomicAdd(&stats[2], (unsigned long long)(8 + 8 * (e - b) + 12 * c + 12 * ownlen));
       }
     }
     __syncthreads();

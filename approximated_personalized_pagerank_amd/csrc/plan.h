@@ -79,7 +79,14 @@ struct ppr_plan {
   // iterations >= PPR_MAX_ITER_STATS share the last maxDiff slot: it is zeroed at the first
   // ppr_grank_plan_iterate call of each such iteration (a sharded iteration may call it per range)
   int32_t md_shared_it = -1;
-  unsigned long long* d_stats = nullptr;    // 2
+  unsigned long long* d_stats = nullptr;    // PPR_NSTATS: candidates, algorithmic bytes, wave-tier bytes
+  // per-kernel roofline (ppr_grank_plan_kernel_stats): HIP events around each kernel group on the
+  // stream it runs on, algorithmic bytes of the sources it merged (SURVEY s8d per source)
+  static constexpr int NKST = 5;      // wave tier | sieve large | sieve mid | sieve small | sieve multi-slice
+  hipEvent_t ev_k[2 * NKST] = {};
+  bool kst_live[NKST] = {};
+  double kst_ms[NKST] = {}, kst_bytes[NKST] = {}, kst_pend_bytes[NKST] = {};
+  int64_t kst_launches[NKST] = {};
   GlbWork* d_work = nullptr;
   int64_t work_cap = 0;
   void* d_scratch = nullptr;
@@ -200,7 +207,9 @@ struct ppr_plan {
   int64_t sv_slice = 1LL << 18;       // PPR_SV_SLICE: candidates per slice workgroup
   int64_t sv_min = 0;                 // PPR_SV_MIN: sources with fewer candidates keep the range engines
   int sv_budget = 2457;               // PPR_SV_BUDGET (tests): passing keys a table takes (<= SV_XT_BUDGET)
-  hipStream_t stream_sv = nullptr, stream_sv2 = nullptr;  // multi-slice chain | one-slice sources
+  int64_t sv_small = 16384, sv_mid = 65536;  // PPR_SV_SMALL / PPR_SV_MID: one-slice size classes by candidates
+  hipStream_t stream_sv = nullptr, stream_sv2 = nullptr, stream_sv3 = nullptr;  // large + multi-slice | mid | small
+                                      // (borrowed: stream2 / stream4 / stream5, not owned)
   hipEvent_t ev_sv = nullptr;
   unsigned char* d_sv = nullptr;      // descriptors, tasks, overflow list, global sketches / tables
   size_t sv_bytes = 0;
@@ -238,6 +247,8 @@ inline void plan_free(ppr_plan* p) {
     if (p->ev_fin[i]) hipEventDestroy(p->ev_fin[i]);
   }
   if (p->ev_wave) hipEventDestroy(p->ev_wave);
+  for (int i = 0; i < 2 * ppr_plan::NKST; i++)
+    if (p->ev_k[i]) hipEventDestroy(p->ev_k[i]);
   if (p->ev_hot0) hipEventDestroy(p->ev_hot0);
   for (int i = 0; i < ppr_plan::MAX_REGIONS; i++)
     if (p->ev_hot[i]) hipEventDestroy(p->ev_hot[i]);
@@ -255,8 +266,6 @@ inline void plan_free(ppr_plan* p) {
   if (p->h_xs_pin) hipHostFree(p->h_xs_pin);
   hipFree(p->d_sv);
   if (p->h_sv_pin) hipHostFree(p->h_sv_pin);
-  if (p->stream_sv) hipStreamDestroy(p->stream_sv);
-  if (p->stream_sv2) hipStreamDestroy(p->stream_sv2);
   if (p->ev_sv) hipEventDestroy(p->ev_sv);
   if (getenv("PPR_TIMING") && p->sv_sources)
     fprintf(stderr, "ppr_timing sieve_sources %lld sieve_redo %lld\n", (long long)p->sv_sources, (long long)p->sv_redo);

@@ -23,6 +23,7 @@ constexpr int TIER_BIG = NT + 1;      // hub pipeline
 constexpr int NLISTS = NT + 2;
 constexpr int MAX_L = 4096;           // widest basket the kernels accept
 constexpr int WAVES_PER_BLOCK = 4;
+constexpr int PPR_NSTATS = 8;         // device counters: candidates, algorithmic bytes, wave-tier bytes
 // PPR_DIAG counters (u64, printed at plan destruction, plan.h): PPR_DIAG_BASE counters, plus as
 // many per shard -- per-wave counters go to a shard picked by block and wave, so hundreds of
 // millions of waves do not serialise on a few addresses (that contention distorted the timings)

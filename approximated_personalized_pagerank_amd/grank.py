@@ -153,6 +153,22 @@ class GrankPlan:
         self.iterations_run = int(st.iterations_run)
         return st
 
+    KERNEL_GROUPS = ("wave tier k_merge_lds_x", "sieve large k_sv1+k_svfin (16 waves)",
+                     "sieve mid k_sv1+k_svfin (8 waves)", "sieve small k_sv1+k_svfin (4 waves)",
+                     "sieve multi-slice k_svA+k_svB+k_svF")
+
+    def kernel_stats(self):
+        """per kernel group of the last run(): SURVEY s8d algorithmic bytes of the sources it merged,
+        HIP event milliseconds on its stream, event pairs (include/ppr_hip.h ppr_grank_plan_kernel_stats)"""
+        n = len(self.KERNEL_GROUPS)
+        b = np.zeros(n)
+        ms = np.zeros(n)
+        la = np.zeros(n, dtype=np.int64)
+        _lib.check(_lib.lib().ppr_grank_plan_kernel_stats(self._p, n, _lib.ptr(b), _lib.ptr(ms), _lib.ptr(la)),
+                   "kernel_stats")
+        return {name: {"algo_bytes": float(b[i]), "ms": float(ms[i]), "launches": int(la[i])}
+                for i, name in enumerate(self.KERNEL_GROUPS)}
+
     # step-level API (source sharding)
     def init(self):
         _lib.check(_lib.lib().ppr_grank_plan_init(self._p), "plan_init")

@@ -376,6 +376,7 @@ def main():
             plan.run(args.iters, args.tol)
         merge_ms = algo = dev_ms = 0.0
         launches = 0
+        kst = {}
         t0 = time.perf_counter()
         for _ in range(args.steps):
             st = plan.run(args.iters, args.tol)  # synchronous: ends with an event sync
@@ -383,9 +384,13 @@ def main():
             algo += st.algo_bytes
             dev_ms += st.device_ms
             launches += st.merge_launches
+            for k, v in plan.kernel_stats().items():  # (host reads of counters the run already holds)
+                d = kst.setdefault(k, {"algo_bytes": 0.0, "ms": 0.0, "launches": 0})
+                for f in d:
+                    d[f] += v[f]
         elapsed = time.perf_counter() - t0
         stats = dict(merge_ms=merge_ms, algo_bytes=algo, device_ms=dev_ms, iterations=st.iterations_run,
-                     launches=launches)
+                     launches=launches, kernels=kst)
         cpu = e2e = None
         if not args.no_cpu_baseline:
             try:
@@ -406,6 +411,14 @@ def main():
     steps = args.steps
     value = g.n * steps / elapsed
     achieved = stats["algo_bytes"] / 1e9 / (stats["merge_ms"] / 1e3) if stats["merge_ms"] > 0 else 0.0
+    kernels = {}
+    for k, v in stats.get("kernels", {}).items():
+        if v["ms"] <= 0:
+            continue
+        gbs = v["algo_bytes"] / 1e9 / (v["ms"] / 1e3)
+        kernels[k] = {"algo_bytes_per_step": v["algo_bytes"] / steps, "ms_per_step": v["ms"] / steps,
+                      "launches_per_step": v["launches"] / steps, "achieved": gbs, "frac": gbs / HBM_PEAK_GBS}
+    dominant = max(kernels, key=lambda k: kernels[k]["ms_per_step"]) if kernels else None
     traffic, traffic_src = (None, None)
     if (args.scale, args.K, args.L, args.iters) == (22, 64, 128, 30):
         traffic, traffic_src = pmc_traffic("grank_rmat22_k64_l128", sum_mode())
@@ -428,9 +441,10 @@ def main():
                    "parallelism": f"source-shard x{world}" if world > 1 else "1 GPU",
                    "sum": sum_mode()},
         "roofline": {"bound": "hbm",
-                     "kernel": ("basket-merge phase, exact sum: k_classify + k_merge_lds_x (wave tier) + k_xr "
-                                "(range workgroups) + partition (k_hub_count, device scan, k_hub_scatter) + k_xb "
-                                "(bucket workgroups) + k_xfin1 / k_xfinal" if sum_mode() == "exact" else
+                     "kernel": ("basket-merge phase, exact sum: k_classify + k_merge_lds_x (wave tier) + sieve "
+                                "(k_sv1 + k_svfin in three size classes, k_svA + k_svB + k_svF for multi-slice "
+                                "sources; range / partition engines for the sources it hands back)"
+                                if sum_mode() == "exact" else
                                 "basket-merge phase, chain sum: k_classify + k_merge_lds (wave tiers) + hub pipeline "
                                 "(k_hub_count, device scan, k_hub_scatter, k_hub_bucket_w, k_hub_final)"),
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -438,7 +452,9 @@ def main():
                      "algo_bytes_per_step": stats["algo_bytes"] / steps,
                      "merge_ms_per_step": stats["merge_ms"] / steps,
                      "merge_launches_per_step": stats["launches"] / steps,
-                     "traffic": traffic, "traffic_source": traffic_src},
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "dominant_kernel": dominant,
+                     "kernels": kernels},
         "cpu_baseline": cpu,
         "end_to_end": e2e,
     }

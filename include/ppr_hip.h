@@ -175,6 +175,13 @@ int ppr_grank_plan_comm_init(ppr_plan* p, const void* id128, int32_t nranks, int
 int ppr_grank_plan_shard_bounds(ppr_plan* p, int32_t it, int32_t nranks, int64_t* bounds);
 int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance, ppr_stats* st);
 int ppr_grank_plan_exchange_bytes(ppr_plan* p, int64_t* recv_bytes, int64_t* rows_sent);
+/* Per-kernel roofline of the last ppr_grank_plan_run (no reference counterpart: measurement).
+ * Kernel groups, in this order: 0 wave tier (k_merge_lds_x), 1 sieve large (k_sv1 + k_svfin, 16
+ * waves), 2 sieve mid (8 waves), 3 sieve small (4 waves), 4 sieve multi-slice (k_svA + k_svB +
+ * k_svF). bytes: SURVEY s8d algorithmic bytes of the sources the group merged (the wave tier's
+ * without the written rows); ms: HIP event time of the group's launches on its stream; launches:
+ * event pairs summed. Up to n groups are written. */
+int ppr_grank_plan_kernel_stats(ppr_plan* p, int32_t n, double* bytes, double* ms, int64_t* launches);
 /* Tests: the same native loop with n plans of this process as the ranks (one thread each, block
  * exchange by device copies instead of RCCL: RCCL refuses two ranks on one GPU). st: n stats or
  * null. Every plan must be built on the same graph and parameters. */

@@ -313,6 +313,9 @@ def test_gpu_exact_sum_init_hubs_and_damping():
     ({"PPR_SV_BUDGET": "2", "PPR_SV_SLICE": "512"}, "redo"),  # handed back to the range / partition engines
     ({"PPR_SV_MIN": "20000"}, "sieve"),                       # only the widest sources sieved
     ({"PPR_WHATIF": "2048", "PPR_SV_SLICE": "700"}, "sieve"),  # pass 1 through hub_window_walk
+    ({"PPR_SV_SMALL": "0", "PPR_SV_MID": "0", "PPR_TIER_MASK": "0x0"}, "sieve"),  # every one-slice source 16 waves
+    ({"PPR_SV_SMALL": "1000000000", "PPR_SV_MID": "1000000000"}, "sieve"),        # ... 4 waves
+    ({"PPR_SV_SMALL": "0", "PPR_SV_MID": "1000000000", "PPR_SV_BUDGET": "40"}, "redo"),  # ... 8 waves
     ({"PPR_SV": "0"}, None),                                  # off: range / partition engines only
 ])
 def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):
