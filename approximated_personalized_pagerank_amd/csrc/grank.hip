@@ -328,6 +328,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
           hipEventCreateWithFlags(&p->ev_fin[i], hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&p->ev_hot[i], hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
   }
+  p->stream_wave = p->stream3;
   {
     hipDeviceProp_t prop;
     p->num_cus = hipGetDeviceProperties(&prop, p->device) == hipSuccess ? prop.multiProcessorCount : 256;
@@ -413,12 +414,19 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       if (s6) p->sv_mid = std::max<int64_t>(0, atoll(s6));
       const char* s3 = getenv("PPR_SV_BUDGET");
       if (s3) p->sv_budget = std::max(0, std::min(SV_XT_BUDGET, atoi(s3)));
-      // the sieve's streams are the hub pipeline's (idle in the exact sum once the sieve takes the
-      // wide sources): more streams than the process's 4 hardware queues would share queues with
-      // the wave tier's stream3 and serialise behind it
+      // Streams of the exact sum: a process has 4 hardware queues (HIP's default), and streams
+      // beyond them share queues -- a kernel then waits behind another stream's kernel. The hot
+      // pass's stream5 is unused here (no hot pass), so it goes, and each of the 4 remaining streams
+      // gets its own queue: the plan stream (classification, then the sieve's mid class), stream2
+      // (the wave tier, then the multi-slice chain: the wave tier is heavy in the partition with
+      // many small sources, the multi-slice sources live in the other), stream4 (the sieve's large
+      // and small classes) and stream3 (the range engines for the sources the sieve does not take
+      // or hands back)
+      if (p->stream5) { hipStreamDestroy(p->stream5); p->stream5 = nullptr; }
+      if (p->sv_enabled && p->stream2) p->stream_wave = p->stream2;
       p->stream_sv = p->stream2 ? p->stream2 : p->stream;
       p->stream_sv2 = p->stream4 ? p->stream4 : p->stream;
-      p->stream_sv3 = p->stream5 ? p->stream5 : p->stream;
+      p->stream_sv3 = p->stream;
       if (p->sv_enabled && hipEventCreateWithFlags(&p->ev_sv, hipEventDisableTiming) != hipSuccess) {
         plan_free(p);
         return PPR_ERR_HIP;
@@ -1497,13 +1505,14 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   std::memcpy(hb + o_d, desc.data(), sizeof(SvDesc) * nx);
   if (nt) std::memcpy(hb + o_t, tasks.data(), sizeof(SvTask) * nt);
   unsigned char* b = p->d_sv;
-  hipStream_t s1 = p->stream_sv, s2 = p->stream_sv2;
-  HIP_OK(hipMemcpyAsync(b, hb, up, hipMemcpyHostToDevice, s1));
-  HIP_OK(hipMemsetAsync(b + o_z, 0, total - o_z, s1));
-  // the one-slice streams start once the descriptors are up and the overflow list is zeroed
-  HIP_OK(hipEventRecord(p->ev_sv, s1));
-  HIP_OK(hipStreamWaitEvent(s2, p->ev_sv, 0));
-  HIP_OK(hipStreamWaitEvent(p->stream_sv3, p->ev_sv, 0));
+  hipStream_t s1 = p->stream_sv, s2 = p->stream_sv2, s3 = p->stream_sv3;
+  // descriptors up and the zeroed region cleared on the mid class's stream (the plan stream: idle
+  // once the classification is read), the other sieve streams wait for it
+  HIP_OK(hipMemcpyAsync(b, hb, up, hipMemcpyHostToDevice, s3));
+  HIP_OK(hipMemsetAsync(b + o_z, 0, total - o_z, s3));
+  HIP_OK(hipEventRecord(p->ev_sv, s3));
+  if (s1 != s3) HIP_OK(hipStreamWaitEvent(s1, p->ev_sv, 0));
+  if (s2 != s3) HIP_OK(hipStreamWaitEvent(s2, p->ev_sv, 0));
   const SvDesc* d_d = (const SvDesc*)(b + o_d);
   const SvTask* d_t = (const SvTask*)(b + o_t);
   int32_t* d_ov = (int32_t*)(b + o_ov);
@@ -1521,7 +1530,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
     // one-slice classes beside the multi-slice chain (stream_sv): large then small on stream_sv2,
     // mid on stream_sv3, so each class's tail overlaps another's work
     const SvGeom geo[3] = {SV_LARGE, SV_MID, SV_SMALL};
-    hipStream_t cs[3] = {s2, p->stream_sv3, s2};
+    hipStream_t cs[3] = {s2, s3, s2};
     size_t c0 = 0;
     for (int c = 0; c < 3; c++) {
       const size_t cnt = cls_end[c] - c0;
@@ -1567,10 +1576,14 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
 static int sieve_collect(ppr_plan* p, SvRun& run, std::vector<int32_t>& back) {
   if (!run.live) return PPR_OK;
   run.live = false;
-  HIP_OK(hipEventRecord(p->ev_sv, p->stream_sv2));
-  HIP_OK(hipStreamWaitEvent(p->stream_sv, p->ev_sv, 0));
-  HIP_OK(hipEventRecord(p->ev_sv, p->stream_sv3));
-  HIP_OK(hipStreamWaitEvent(p->stream_sv, p->ev_sv, 0));
+  if (p->stream_sv2 != p->stream_sv) {
+    HIP_OK(hipEventRecord(p->ev_sv, p->stream_sv2));
+    HIP_OK(hipStreamWaitEvent(p->stream_sv, p->ev_sv, 0));
+  }
+  if (p->stream_sv3 != p->stream_sv) {
+    HIP_OK(hipEventRecord(p->ev_sv, p->stream_sv3));
+    HIP_OK(hipStreamWaitEvent(p->stream_sv, p->ev_sv, 0));
+  }
   int32_t novf = 0;
   HIP_OK(hipMemcpyAsync(&novf, p->d_sv + run.o_ovl, 4, hipMemcpyDeviceToHost, p->stream_sv));
   HIP_OK(hipStreamSynchronize(p->stream_sv));
@@ -1668,8 +1681,8 @@ int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count
   // MC combine levels are timed as a whole by the caller: no per-level event sync
   if (!a.mc) HIP_OK(hipEventRecord(p->ev_m0, p->stream));
   int rc = run_merge_impl(p, a, list, count, maxdiff);
-  if (p->stream3) {  // the wave tiers ran on stream3
-    HIP_OK(hipEventRecord(p->ev_wave, p->stream3));
+  if (p->stream_wave && p->stream_wave != p->stream) {  // the wave tiers ran on their own stream
+    HIP_OK(hipEventRecord(p->ev_wave, p->stream_wave));
     HIP_OK(hipStreamWaitEvent(p->stream, p->ev_wave, 0));
   }
   if (rc || a.mc) return rc;
@@ -1813,8 +1826,8 @@ reclassify:
     HIP_OK(hipMemcpyAsync(cnt, p->d_tier_cnt, sizeof(cnt), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
   }
-  // the classification is complete (host sync): the wave tiers need no event to start on stream3
-  hipStream_t sw = p->stream3 ? p->stream3 : st;
+  // the classification is complete (host sync): the wave tiers need no event to start on their stream
+  hipStream_t sw = p->stream_wave ? p->stream_wave : st;
   bool wave_ev = false;
   for (int t = 0; t < NT; t++) {
     if (!cnt[t] || !p->tierT[t]) continue;

@@ -62,7 +62,6 @@ constexpr SvGeom SV_LARGE = sv_geom(13, 16), SV_MID = sv_geom(12, 8), SV_SMALL =
 constexpr int SV_THREADS = 16 * WAVE;         // the widest class (multi-slice kernels)
 constexpr int SV_XT_BUDGET = SV_LARGE.budget;
 constexpr int SVF_CAP = 4096;                 // k_svF: dense entries at or above the bound
-constexpr uint32_t WI_SV_P1WALK = 1u << 11;   // PPR_WHATIF 2048: sieve pass 1 through hub_window_walk (A/B)
 
 // ---------------------------------------------------------------------------------------------
 // split exact accumulators (keys u32 | A u64 | B u64: 20 B a slot)
@@ -134,21 +133,34 @@ __device__ __forceinline__ int x2_slot(const X2Table& t, int key, bool& ins) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// count-min sketch: SV_R counters per key from one 64-bit mix (independent of hash32 / hash_b)
-__device__ __forceinline__ uint64_t sv_mix(uint32_t k) {
-  uint64_t x = (uint64_t)k * 0x9E3779B97F4A7C15ull;
-  x ^= x >> 29;
-  x *= 0xBF58476D1CE4E5B9ull;
-  x ^= x >> 32;
-  return x;
+// One hash per key: hash32 (a bijection, so distinct keys never share it), which also places the
+// key in PT; a cheap derived word for the third sketch row and the PT prefilter. (Independent of
+// hash_b, which orders the stored rows.)
+struct SvHash {
+  uint32_t h, h2;
+};
+__device__ __forceinline__ SvHash sv_hash(int key) {
+  SvHash r;
+  r.h = hash32((uint32_t)key);
+  r.h2 = r.h * 0x85EBCA77u + 0x27D4EB2Fu;
+  r.h2 ^= r.h2 >> 15;
+  return r;
 }
-__device__ __forceinline__ uint32_t sv_cell(uint64_t x, int j, int wlog) {
-  return ((uint32_t)j << wlog) + ((uint32_t)(x >> (wlog * j)) & ((1u << wlog) - 1u));
+// sketch cell of row j (rows of 2^wlog counters, wlog <= 13)
+__device__ __forceinline__ uint32_t sv_cell(const SvHash& k, int j, int wlog) {
+  const uint32_t m = (1u << wlog) - 1u;
+  const uint32_t c = j == 0 ? (k.h & m) : j == 1 ? ((k.h >> 13) & m) : (k.h2 >> (32 - wlog));
+  return ((uint32_t)j << wlog) + c;
 }
-// ceil(p * 2^31): an upper bound of the contribution in counter units
+// PT prefilter: one of 4096 bits per key; a clear bit proves the key is not a prev key
+constexpr int SV_BLOOM_WORDS = 128;
+__device__ __forceinline__ uint32_t sv_bloom_bit(const SvHash& k) { return (k.h2 >> 4) & 4095u; }
+// an upper bound of p * 2^31 in counter units: fl(p) is within 2^-24 relative of p, the factor
+// 2^31 (1 + 2^-20) -- exact in single precision -- and the +1 after the truncation cover that and
+// the product's rounding (f >= p 2^31 (1 + 2^-20)(1 - 2^-24)^2 > p 2^31)
 __device__ __forceinline__ uint32_t sv_units(double p) {
-  const double x = ceil(ldexp(p, SV_UNIT_LOG));
-  return x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
+  const float f = (float)p * 2147485696.0f;
+  return f >= 4294967040.0f ? 0xffffffffu : (uint32_t)f + 1u;
 }
 // counter threshold of the bound theta: a key whose total reaches theta has every counter >=
 // 2^31 * theta * (1 - 2^-52) (its stored value rounds up by at most half an ulp); the margin
@@ -157,22 +169,30 @@ __device__ __forceinline__ uint32_t sv_thr(double theta) {
   const double x = floor(ldexp(theta, SV_UNIT_LOG) * (1.0 - 0x1p-40));
   return x <= 0.0 ? 0u : x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
 }
-__device__ __forceinline__ void sv_sketch_add(uint32_t* sk, int key, uint32_t u, int wlog) {
-  const uint64_t x = sv_mix((uint32_t)key);
+__device__ __forceinline__ void sv_sketch_add(uint32_t* sk, const SvHash& k, uint32_t u, int wlog) {
 #pragma unroll
-  for (int j = 0; j < SV_R; j++) atomicAdd(&sk[sv_cell(x, j, wlog)], u);
+  for (int j = 0; j < SV_R; j++) atomicAdd(&sk[sv_cell(k, j, wlog)], u);
 }
-// every counter of `key` at or above the threshold (bitmap of the counters that are)
-__device__ __forceinline__ bool sv_passes(const uint64_t* bm, int key, int wlog) {
-  const uint64_t x = sv_mix((uint32_t)key);
-  uint64_t w[SV_R];
-  uint32_t c[SV_R];
+// every counter of the key at or above the threshold (bitmap of the counters that are; the three
+// words are read together)
+__device__ __forceinline__ bool sv_passes(const uint32_t* bm, const SvHash& k, int wlog) {
+  uint32_t w[SV_R], c[SV_R];
 #pragma unroll
-  for (int j = 0; j < SV_R; j++) { c[j] = sv_cell(x, j, wlog); w[j] = bm[c[j] >> 6]; }
-  bool ok = true;
-#pragma unroll
-  for (int j = 0; j < SV_R; j++) ok = ok && ((w[j] >> (c[j] & 63u)) & 1ull);
-  return ok;
+  for (int j = 0; j < SV_R; j++) { c[j] = sv_cell(k, j, wlog); w[j] = bm[c[j] >> 5]; }
+  return ((w[0] >> (c[0] & 31u)) & (w[1] >> (c[1] & 31u)) & (w[2] >> (c[2] & 31u)) & 1u) != 0u;
+}
+// PT membership: the prefilter bit, then the probe from the key's hash
+__device__ __forceinline__ int x2_find_h(const X2Table& t, int key, uint32_t h) {
+  const uint32_t tag = (uint32_t)key + 1u;
+  uint32_t g = h & t.mask & ~3u;
+  for (uint32_t n = 0; n <= t.mask; n += 4) {
+    const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g);
+    const int m = xt_match(q, g, tag);
+    if (m >= 0) return m;
+    if (q.x == 0u || q.y == 0u || q.z == 0u || q.w == 0u) return -1;
+    g = (g + 4u) & t.mask;
+  }
+  return -1;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -191,19 +211,18 @@ struct SvTask { int32_t d; int32_t k; };
 
 // LDS of the slice / single-source workgroups:
 //   region (sketch in pass 1; XT in pass 2; dense (value, key) list in the select)
-//   PT (2 Lp slots) | pti i32[2 Lp] (prev-row position of a PT slot) | bitmap u64[bm_words] |
-//   walk flags u8[waves][HUB_WALK_FLAGS] | misc i32[64] | hist u32[256] (block select)
+//   PT (2 Lp slots) | pti i32[2 Lp] (prev-row position of a PT slot) | PT prefilter u32[128] |
+//   bitmap u64[bm_words] | misc i32[64] | hist u32[256] (block select)
 enum { SVM_FILL = 0, SVM_OVF = 1, SVM_U = 2, SVM_PT = 3, SVM_THETA = 8 /* u64: 8..9 */ };
 __host__ __device__ constexpr size_t sv_lds_bytes(int Lp, SvGeom G) {
-  return G.region() + x2_bytes(2 * Lp) + (size_t)8 * Lp + (size_t)G.bm_words() * 8 +
-         (size_t)G.waves * HUB_WALK_FLAGS + 256 + 1024;
+  return G.region() + x2_bytes(2 * Lp) + (size_t)8 * Lp + 4 * SV_BLOOM_WORDS + (size_t)G.bm_words() * 8 + 256 + 1024;
 }
 struct SvLds {
   unsigned char* region;
   X2Table pt;
   int* pti;
+  uint32_t* ptb;
   uint64_t* bm;
-  uint8_t* fl;
   int* misc;
   uint32_t* hist;
   int wlog;
@@ -215,8 +234,8 @@ __device__ __forceinline__ SvLds sv_carve(unsigned char* smem, int Lp, SvGeom G)
   x.region = p; p += G.region();
   x.pt = x2_carve(p, 2 * Lp); p += x2_bytes(2 * Lp);
   x.pti = reinterpret_cast<int*>(p); p += (size_t)8 * Lp;
+  x.ptb = reinterpret_cast<uint32_t*>(p); p += 4 * SV_BLOOM_WORDS;
   x.bm = reinterpret_cast<uint64_t*>(p); p += (size_t)G.bm_words() * 8;
-  x.fl = p; p += (size_t)G.waves * HUB_WALK_FLAGS;
   x.misc = reinterpret_cast<int*>(p); p += 256;
   x.hist = reinterpret_cast<uint32_t*>(p);
   x.wlog = G.wlog;
@@ -231,161 +250,151 @@ __device__ __forceinline__ void sv_lap(const IterArgs& a, int slot, long long& t
   t = now;
 }
 
-// the current row of v (L distinct keys) into PT, zeroed sums; misc cleared; pti = row position
+// the current row of v (L distinct keys) into PT with zeroed sums and its prefilter bits; misc
+// cleared; pti = row position
 __device__ __forceinline__ void sv_build_pt(const SvLds& x, const DevSlab& s, const IterArgs& a, int v, int Lp) {
   const int T = 2 * Lp;
   for (int i = threadIdx.x; i < T; i += blockDim.x) { x.pt.keys[i] = 0u; x.pt.a[i] = 0ull; x.pt.b[i] = 0ull; }
+  for (int i = threadIdx.x; i < SV_BLOOM_WORDS; i += blockDim.x) x.ptb[i] = 0u;
   if (threadIdx.x < 64) x.misc[threadIdx.x] = 0;
   __syncthreads();
   const int cur = (a.active == 1) ? a.sB : a.sA;
   const int64_t r = s.row(cur, v);
   const int len = s.len[s.lrow(cur, v)];
   for (int i = threadIdx.x; i < len; i += blockDim.x) {
+    const int key = s.key(s.ids[r + i]);
     bool ins;
-    const int h = x2_slot(x.pt, s.key(s.ids[r + i]), ins);
+    const int h = x2_slot(x.pt, key, ins);
     if (h >= 0) x.pti[h] = i;
+    const uint32_t bit = sv_bloom_bit(sv_hash(key));
+    atomicOr(&x.ptb[bit >> 5], 1u << (bit & 31u));
+  }
+}
+// the key's PT slot (-1: not a prev key)
+__device__ __forceinline__ int sv_pt_slot(const SvLds& x, int key, const SvHash& k) {
+  const uint32_t bit = sv_bloom_bit(k);
+  if (!((x.ptb[bit >> 5] >> (bit & 31u)) & 1u)) return -1;
+  return x2_find_h(x.pt, key, k.h);
+}
+
+// The wave's share of a slice: contiguous successors [c0, c1) taken row by row. Row metadata comes
+// per window of 64 successors, one successor per lane (colx two windows ahead, lengths one window
+// ahead, so neither load is waited on); a row's base and length are then read off its lane
+// (readlane: wave-uniform). A lane takes entries lane and 64 + lane of each row (rows of up to 128
+// entries; longer rows' further groups one at a time after the batch), so no lane looks up which
+// row it reads. NS rows a batch, the next batch's loads in flight while fb(valid[], key[], score[],
+// row base[]) uses the current one (slab index of group k = base[k / 2] + 64 (k & 1) + lane);
+// scores are loaded only with kScores.
+template <int NS>
+struct SvBatch {
+  bool valid[2 * NS];
+  int key[2 * NS];
+  double sv[2 * NS];
+  int64_t base[NS];
+};
+__device__ __forceinline__ int64_t sv_readlane64(int64_t x, int lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), lane);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <bool kScores, int NS, class FB>
+__device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, const IterArgs& a, int64_t c0, int64_t c1,
+                                        FB fb) {
+  const int lane = lane_id();
+  const int L = s.L;
+  // window metadata: cx of windows w + 1 (ncx) and w + 2 (nncx) in flight, length of w + 1 (nln)
+  auto colx_at = [&](int64_t w0) { return w0 + lane < c1 ? g.colx[w0 + lane] : (int32_t)-1; };
+  auto len_of = [&](int32_t cx) { return cx == -1 ? 0 : s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)]; };
+  auto base_of = [&](int32_t cx) { return cx == -1 ? (int64_t)0 : s.row(read_slot(a, cx), cx & 0x7fffffff); };
+  int32_t ncx = colx_at(c0);
+  int32_t nncx = c0 + WAVE < c1 ? colx_at(c0 + WAVE) : -1;
+  int nln = len_of(ncx);
+  for (int64_t w0 = c0; w0 < c1; w0 += WAVE) {
+    const int32_t cx = ncx;
+    const int ln = nln;
+    const int64_t base = base_of(cx);
+    ncx = nncx;
+    if (w0 + 2 * WAVE < c1) nncx = colx_at(w0 + 2 * WAVE);
+    nln = len_of(ncx);
+    const int nrows = (int)min((int64_t)WAVE, c1 - w0);
+    auto load = [&](int q0, SvBatch<NS>& bt) {
+#pragma unroll
+      for (int q = 0; q < NS; q++) {
+        const int qq = q0 + q < nrows ? q0 + q : nrows - 1;  // (past the window: row nrows - 1 again, masked)
+        const int rl = q0 + q < nrows ? __builtin_amdgcn_readlane(ln, qq) : 0;
+        bt.base[q] = sv_readlane64(base, qq);
+#pragma unroll
+        for (int hh = 0; hh < 2; hh++) {
+          const int k = 2 * q + hh;
+          const int idx = hh * WAVE + lane;
+          bt.valid[k] = idx < rl;
+          bt.key[k] = bt.valid[k] ? ld_nt(&s.ids[bt.base[q] + idx], a.nt & 1u) : 0;
+          bt.sv[k] = (kScores && bt.valid[k]) ? ld_nt(&s.sc[bt.base[q] + idx], a.nt & 1u) : 0.0;
+        }
+      }
+    };
+    SvBatch<NS> cur, nxt;
+    load(0, nxt);
+    for (int q0 = 0; q0 < nrows; q0 += NS) {
+      cur = nxt;
+      if (q0 + NS < nrows) load(q0 + NS, nxt);
+      fb(cur);
+      if (L > 2 * WAVE) {  // rows beyond two groups (L > 128 only)
+        for (int q = 0; q < NS && q0 + q < nrows; q++) {
+          const int rl = __builtin_amdgcn_readlane(ln, q0 + q);
+          for (int i0 = 2 * WAVE; i0 < rl; i0 += WAVE) {
+            SvBatch<NS> t;
+#pragma unroll
+            for (int k = 0; k < 2 * NS; k++) { t.valid[k] = false; t.key[k] = 0; t.sv[k] = 0.0; }
+#pragma unroll
+            for (int k = 0; k < NS; k++) t.base[k] = cur.base[q] + i0;
+            t.valid[0] = i0 + lane < rl;
+            t.key[0] = t.valid[0] ? s.ids[t.base[0] + lane] : 0;
+            t.sv[0] = (kScores && t.valid[0]) ? s.sc[t.base[0] + lane] : 0.0;
+            fb(t);
+          }
+        }
+      }
+    }
   }
 }
 
-// successors [b0, b1) of a slice, one contiguous chunk per wave, windows of 64 successors
-template <class F>
-__device__ __forceinline__ void sv_walk(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
-                                        int64_t b0, int64_t b1, F f) {
+// the wave's contiguous successor chunk of [b0, b1), as wave-uniform (scalar) bounds
+__device__ __forceinline__ int64_t sv_uniform(int64_t x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ void sv_chunk(int64_t b0, int64_t b1, int64_t& c0, int64_t& c1) {
   const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
   const int64_t chunk = (b1 - b0 + W - 1) / W;
-  const int64_t c0 = b0 + (int64_t)wv * chunk, c1 = min(b1, c0 + chunk);
-  uint8_t* fl = x.fl + (size_t)wv * HUB_WALK_FLAGS;
-  for (int64_t w0 = c0; w0 < c1; w0 += WAVE) hub_window_walk(g, s, a, w0, min(c1, w0 + WAVE), fl, f);
+  c0 = sv_uniform(b0 + (int64_t)wv * chunk);
+  c1 = sv_uniform(min(b1, c0 + chunk));
 }
 
 // pass 1 over successors [b0, b1): prev keys exactly into PT, every other key into the sketch
+constexpr int SV_NS1 = 4, SV_NS2 = 4;  // rows per batch in pass 1 (keys and scores) and pass 2 (keys)
 __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
                                          int64_t b0, int64_t b1, double factor, uint32_t* sk) {
-  sv_walk(g, s, a, x, b0, b1, [&](bool valid, int id, double sv, bool) {
-    if (!valid) return;
-    const double p = sv * factor;
-    const int h = x2_find(x.pt, id);
-    if (h >= 0) {
-      unsigned long long lo;
-      uint32_t hi;
-      xs_conv(p, lo, hi);
-      x2_add(x.pt, h, lo, hi);
-    } else {
-      sv_sketch_add(sk, id, sv_units(p), x.wlog);
+  int64_t c0, c1;
+  sv_chunk(b0, b1, c0, c1);
+  sv_rows<true, SV_NS1>(g, s, a, c0, c1, [&](const SvBatch<SV_NS1>& bt) {
+#pragma unroll
+    for (int k = 0; k < 2 * SV_NS1; k++) {
+      if (!bt.valid[k]) continue;
+      const SvHash hk = sv_hash(bt.key[k]);
+      const double p = bt.sv[k] * factor;
+      const int h = sv_pt_slot(x, bt.key[k], hk);
+      if (h >= 0) {
+        unsigned long long lo;
+        uint32_t hi;
+        xs_conv(p, lo, hi);
+        x2_add(x.pt, h, lo, hi);
+      } else {
+        sv_sketch_add(sk, hk, sv_units(p), x.wlog);
+      }
     }
   });
-}
-
-// The candidates of successors [i0, e) (<= 64) like hub_window_walk, a batch of HUB_TW_BATCH
-// groups at a time (the next batch's loads in flight): fb(valid[], key[], ridx[], score[]) with each
-// candidate's slab index; scores are loaded only with kScores (pass 2 loads a score only for a
-// candidate that passes).
-template <bool kScores, class FB>
-__device__ __forceinline__ void sv_window(const DevGraph& g, const DevSlab& s, const IterArgs& a, int64_t i0,
-                                          int64_t e, uint8_t* fl, FB fb) {
-  constexpr int NB = HUB_TW_BATCH;
-  const int64_t i = i0 + lane_id();
-  int u = 0, sl = 0, ln = 0;
-  if (i < e) {
-    const int32_t cx = g.colx[i];
-    u = cx & 0x7fffffff;
-    sl = read_slot(a, cx);
-    ln = s.len[s.lrow(sl, u)];
-  }
-  const int incl = wave_incl_scan(ln);
-  const int total = __builtin_amdgcn_readlane(incl, WAVE - 1);
-  const bool flags = !__ballot(i < e && ln == 0);
-  auto load = [&](int g0, int (&key)[NB], int64_t (&ri)[NB], double (&sv)[NB]) {
-    if (flags) {
-#pragma unroll
-      for (int q = 0; q < NB / 4; q++) reinterpret_cast<uint32_t*>(fl)[q * WAVE + lane_id()] = 0u;
-      wave_fence();
-      if (incl > g0 && incl < g0 + WAVE * NB) fl[incl - g0] = 1;
-      wave_fence();
-    }
-#pragma unroll
-    for (int k = 0; k < NB; k++) {
-      const int c = g0 + k * WAVE + lane_id();
-      int j = 0;
-      if (flags) {
-        const int G = g0 + k * WAVE;
-        const uint64_t ends = __ballot(fl[k * WAVE + lane_id()] != 0) & ~1ull;
-        j = __popcll(__ballot(incl <= G)) + __popcll(ends & (lanemask_lt() | (1ull << lane_id())));
-      } else {
-#pragma unroll
-        for (int step = 32; step; step >>= 1) {
-          const int pv = __shfl(incl, j + step - 1);
-          if (pv <= c) j += step;
-        }
-      }
-      const int jj = j < WAVE ? j : WAVE - 1;
-      const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
-      const int ex = jj > 0 ? exv : 0;
-      const int uj = __shfl(u, jj);
-      const int sj = __shfl(sl, jj);
-      key[k] = 0;
-      ri[k] = 0;
-      sv[k] = 0.0;
-      if (c < total) {
-        ri[k] = s.row(sj, uj) + (c - ex);
-        key[k] = ld_nt(&s.ids[ri[k]], a.nt & 1u);
-        if (kScores) sv[k] = ld_nt(&s.sc[ri[k]], a.nt & 1u);
-      }
-    }
-  };
-  int key[NB], nkey[NB];
-  int64_t ri[NB], nri[NB];
-  double sv[NB], nsv[NB];
-  if (total > 0) load(0, nkey, nri, nsv);
-  for (int g0 = 0; g0 < total; g0 += WAVE * NB) {
-    bool valid[NB];
-#pragma unroll
-    for (int k = 0; k < NB; k++) {
-      key[k] = nkey[k];
-      ri[k] = nri[k];
-      sv[k] = nsv[k];
-      valid[k] = g0 + k * WAVE + lane_id() < total;
-    }
-    if (g0 + WAVE * NB < total) load(g0 + WAVE * NB, nkey, nri, nsv);
-    fb(valid, key, ri, sv);
-  }
-}
-
-// pass 1, one batch at a time: the first PT group of every candidate read at once, the rare
-// longer probes after, then the exact PT adds or the sketch adds
-__device__ __forceinline__ void sv_pass1b(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
-                                          int64_t b0, int64_t b1, double factor, uint32_t* sk) {
-  constexpr int NB = HUB_TW_BATCH;
-  const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
-  const int64_t chunk = (b1 - b0 + W - 1) / W;
-  const int64_t c0 = b0 + (int64_t)wv * chunk, c1 = min(b1, c0 + chunk);
-  uint8_t* fl = x.fl + (size_t)wv * HUB_WALK_FLAGS;
-  for (int64_t w0 = c0; w0 < c1; w0 += WAVE)
-    sv_window<true>(g, s, a, w0, min(c1, w0 + WAVE), fl, [&](const bool (&valid)[NB], const int (&key)[NB],
-                                                            const int64_t (&)[NB], const double (&sv)[NB]) {
-      uint4 q[NB];
-      uint32_t g0[NB];
-#pragma unroll
-      for (int k = 0; k < NB; k++) {
-        g0[k] = hash32((uint32_t)key[k]) & x.pt.mask & ~3u;
-        q[k] = *reinterpret_cast<const uint4*>(x.pt.keys + g0[k]);
-      }
-#pragma unroll
-      for (int k = 0; k < NB; k++) {
-        if (!valid[k]) continue;
-        int h = xt_match(q[k], g0[k], (uint32_t)key[k] + 1u);
-        if (h < 0 && q[k].x && q[k].y && q[k].z && q[k].w) h = x2_find(x.pt, key[k]);  // (a full group: probe on)
-        const double p = sv[k] * factor;
-        if (h >= 0) {
-          unsigned long long lo;
-          uint32_t hi;
-          xs_conv(p, lo, hi);
-          x2_add(x.pt, h, lo, hi);
-        } else {
-          sv_sketch_add(sk, key[k], sv_units(p), x.wlog);
-        }
-      }
-    });
 }
 
 // pass 2 over successors [b0, b1): keys outside PT that pass the sieve, exactly into XT (budget
@@ -394,65 +403,69 @@ __device__ __forceinline__ void sv_pass1b(const DevGraph& g, const DevSlab& s, c
 // together), then the inserts.
 __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
                                          const X2Table& xt, int64_t b0, int64_t b1, double factor, int budget) {
-  constexpr int NB = HUB_TW_BATCH;
-  const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
-  const int64_t chunk = (b1 - b0 + W - 1) / W;
-  const int64_t c0 = b0 + (int64_t)wv * chunk, c1 = min(b1, c0 + chunk);
-  uint8_t* fl = x.fl + (size_t)wv * HUB_WALK_FLAGS;
-  for (int64_t w0 = c0; w0 < c1; w0 += WAVE)
-    sv_window<false>(g, s, a, w0, min(c1, w0 + WAVE), fl, [&](const bool (&valid)[NB], const int (&key)[NB],
-                                                             const int64_t (&ri)[NB], const double (&)[NB]) {
-      bool want[NB];
-      bool any = false;
+  int64_t c0, c1;
+  sv_chunk(b0, b1, c0, c1);
+  const uint32_t* bm32 = reinterpret_cast<const uint32_t*>(x.bm);
+  const int lane = lane_id();
+  sv_rows<false, SV_NS2>(g, s, a, c0, c1, [&](const SvBatch<SV_NS2>& bt) {
+    constexpr int NG = 2 * SV_NS2;
+    bool want[NG];
+    bool any = false;
 #pragma unroll
-      for (int k = 0; k < NB; k++) {
-        want[k] = valid[k] && sv_passes(x.bm, key[k], x.wlog);
-        if (want[k]) want[k] = x2_find(x.pt, key[k]) < 0;
-        any = any || want[k];
+    for (int k = 0; k < NG; k++) {
+      want[k] = false;
+      if (!bt.valid[k]) continue;
+      const SvHash hk = sv_hash(bt.key[k]);
+      want[k] = sv_passes(bm32, hk, x.wlog);
+      if (want[k]) want[k] = sv_pt_slot(x, bt.key[k], hk) < 0;
+      any = any || want[k];
+    }
+    if (!__ballot(any)) return;
+    double sv[NG];
+#pragma unroll
+    for (int k = 0; k < NG; k++)
+      sv[k] = want[k] ? ld_nt(&s.sc[bt.base[k >> 1] + (k & 1) * WAVE + lane], a.nt & 1u) : 0.0;
+#pragma unroll
+    for (int k = 0; k < NG; k++) {
+      if (!__ballot(want[k])) continue;
+      if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
+        if (lane_id() == 0) x.misc[SVM_OVF] = 1;
+        return;
       }
-      if (!__ballot(any)) return;
-      double sv[NB];
-#pragma unroll
-      for (int k = 0; k < NB; k++) sv[k] = want[k] ? ld_nt(&s.sc[ri[k]], a.nt & 1u) : 0.0;
-#pragma unroll
-      for (int k = 0; k < NB; k++) {
-        if (!__ballot(want[k])) continue;
-        if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
-          if (lane_id() == 0) x.misc[SVM_OVF] = 1;
-          return;
-        }
-        bool ins = false;
-        int h = -1;
-        if (want[k]) h = x2_slot(xt, key[k], ins);
-        const int nins = __popcll(__ballot(ins));
-        if (nins && lane_id() == 0) atomicAdd(&x.misc[SVM_FILL], nins);
-        if (__ballot(want[k] && h < 0) && lane_id() == 0) x.misc[SVM_OVF] = 1;
-        if (h >= 0) {
-          unsigned long long lo;
-          uint32_t hi;
-          xs_conv(sv[k] * factor, lo, hi);
-          x2_add(xt, h, lo, hi);
-        }
-        if (a.diag && lane_id() == 0) diag_add(a.diag, 138, (unsigned long long)__popcll(__ballot(want[k])));
+      bool ins = false;
+      int h = -1;
+      if (want[k]) h = x2_slot(xt, bt.key[k], ins);
+      const int nins = __popcll(__ballot(ins));
+      if (nins && lane_id() == 0) atomicAdd(&x.misc[SVM_FILL], nins);
+      if (__ballot(want[k] && h < 0) && lane_id() == 0) x.misc[SVM_OVF] = 1;
+      if (h >= 0) {
+        unsigned long long lo;
+        uint32_t hi;
+        xs_conv(sv[k] * factor, lo, hi);
+        x2_add(xt, h, lo, hi);
       }
-    });
+      if (a.diag && lane_id() == 0) diag_add(a.diag, 138, (unsigned long long)__popcll(__ballot(want[k])));
+    }
+  });
 }
 
 // the self seed (1 - d) of v: into PT when v is a prev key, else into the sketch (pass 1)
 __device__ __forceinline__ void sv_seed1(const SvLds& x, int v, double seed, uint32_t* sk) {
-  const int h = x2_find(x.pt, v);
+  const SvHash hk = sv_hash(v);
+  const int h = sv_pt_slot(x, v, hk);
   if (h >= 0) {
     unsigned long long lo;
     uint32_t hi;
     xs_conv(seed, lo, hi);
     x2_add(x.pt, h, lo, hi);
   } else {
-    sv_sketch_add(sk, v, sv_units(seed), x.wlog);
+    sv_sketch_add(sk, hk, sv_units(seed), x.wlog);
   }
 }
 // ... and into XT in pass 2 when v is not a prev key and passes
 __device__ __forceinline__ void sv_seed2(const SvLds& x, const X2Table& xt, int v, double seed) {
-  if (x2_find(x.pt, v) >= 0 || !sv_passes(x.bm, v, x.wlog)) return;
+  const SvHash hk = sv_hash(v);
+  if (sv_pt_slot(x, v, hk) >= 0 || !sv_passes(reinterpret_cast<const uint32_t*>(x.bm), hk, x.wlog)) return;
   bool ins;
   const int h = x2_slot(xt, v, ins);
   if (h < 0) { x.misc[SVM_OVF] = 1; return; }
@@ -509,6 +522,8 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
     return;
   }
   long long tph = a.diag ? (long long)clock64() : 0;
+  // PPR_DIAG per size class: 256 + 8 class + {setup, pass 1, bound, pass 2, select, sources, rows, handed back}
+  const int dg = 256 + 8 * (G.wlog == 13 ? 0 : G.wlog == 12 ? 1 : 2);
   uint32_t* sk = reinterpret_cast<uint32_t*>(x.region);
   sv_clear_region(x, G.sketch_bytes());
   sv_build_pt(x, s, a, v, Lp);
@@ -517,11 +532,11 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
     *reinterpret_cast<unsigned long long*>(&x.misc[SVM_THETA]) = ~0ull;
     sv_seed1(x, v, 1.0 - a.damping, sk);
   }
+  sv_lap(a, dg + 0, tph);
   const int64_t b = g.rp[v], e = g.rp[v + 1];
-  if (a.whatif & WI_SV_P1WALK) sv_pass1(g, s, a, x, b, e, sd.factor, sk);
-  else sv_pass1b(g, s, a, x, b, e, sd.factor, sk);
+  sv_pass1(g, s, a, x, b, e, sd.factor, sk);
   __syncthreads();
-  sv_lap(a, 145, tph);
+  sv_lap(a, dg + 1, tph);
   // bound: the smallest exact total of the L prev keys
   const int Tpt = 2 * Lp;
   const double theta = sv_theta(x, Tpt, [&](int i) {
@@ -533,14 +548,15 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
   const X2Table xt = x2_carve(x.region, G.xt);
   sv_clear_region(x, x2_bytes(G.xt));
   __syncthreads();
-  sv_lap(a, 146, tph);
+  sv_lap(a, dg + 2, tph);
   if (threadIdx.x == 0) sv_seed2(x, xt, v, 1.0 - a.damping);
   sv_pass2(g, s, a, x, xt, b, e, sd.factor, budget);
   __syncthreads();
-  sv_lap(a, 147, tph);
+  sv_lap(a, dg + 3, tph);
+  if (a.diag && threadIdx.x == 0) { diag_add(a.diag, dg + 5, 1ull); diag_add(a.diag, dg + 6, (unsigned long long)(e - b)); }
   if (x.misc[SVM_OVF] || x.misc[SVM_FILL] > budget + G.waves * WAVE) {
     if (threadIdx.x == 0) ovl[1 + atomicAdd(&ovl[0], 1)] = d;
-    if (a.diag && threadIdx.x == 0) diag_add(a.diag, 137, 1ull);
+    if (a.diag && threadIdx.x == 0) { diag_add(a.diag, 137, 1ull); diag_add(a.diag, dg + 7, 1ull); }
     return;
   }
   // dense (value, key) list of PT u {XT keys >= theta}: the table's slot values into registers
@@ -616,7 +632,7 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
   }
   __syncthreads();
   if (threadIdx.x == 0) out_n[d] = x.misc[SVM_PT];
-  if (threadIdx.x == 0) sv_lap(a, 148, tph);
+  if (threadIdx.x == 0) sv_lap(a, dg + 4, tph);
 }
 
 // the row of a one-slice source from its selected entries (k_sv1): one wave per source -- sort in
@@ -667,8 +683,7 @@ __global__ void __launch_bounds__(SV_THREADS) k_svA(DevGraph g, DevSlab s, IterA
   if (tk.k == 0 && threadIdx.x == 0) sv_seed1(x, v, 1.0 - a.damping, sk);
   int64_t b0, b1;
   sv_slice(g.rp[v], g.rp[v + 1], tk.k, sd.S, b0, b1);
-  if (a.whatif & WI_SV_P1WALK) sv_pass1(g, s, a, x, b0, b1, sd.factor, sk);
-  else sv_pass1b(g, s, a, x, b0, b1, sd.factor, sk);
+  sv_pass1(g, s, a, x, b0, b1, sd.factor, sk);
   __syncthreads();
   uint32_t* gs = gsk + sd.gsk;
   for (int c = threadIdx.x; c < SV_R * (1 << G.wlog); c += blockDim.x) {

@@ -160,6 +160,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   const int v = list[w];
   const int64_t b = g.rp[v], e = g.rp[v + 1];
   const double factor = merge_factor(a, e - b);
+  long long tl = a.diag ? (long long)clock64() : 0;  // PPR_DIAG: wave-tier phases, slots 280..287
   for (int i = lane_id(); i < T; i += WAVE) { t.keys[i] = 0u; t.lo[i] = 0ull; t.hi[i] = 0u; }
   wave_fence();
   if (lane_id() == 0) {
@@ -192,6 +193,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
                       WalkRowMin{&mb, (int)s.L});
   }
   wave_fence();
+  fs_lap(a, 280, 1, tl);  // (slot 281: setup + walk)
 #pragma unroll
   for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
   // keys below the pruning bound cannot reach the top-L (a full successor row puts L distinct keys
@@ -244,8 +246,10 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
     U = U2;
   }
   if (dlast && !a.unit && lane_id() == 0) dlast[v] = D;  // (init counts predict nothing)
+  fs_lap(a, 280, 2, tl);  // (slot 282: settle + compact)
+  if (a.diag && !a.unit && lane_id() == 0) { diag_add(a.diag, 280, 1ull); diag_add(a.diag, 287, (unsigned long long)U); }
   finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return vals[i]; }, s, a, hist, rv, rk, Lp, hk, hv,
-                mf, maxdiff, stats);
+                mf, maxdiff, stats, a.unit ? -1 : 283);  // (283 select, 284 row write, 285 norm1)
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -153,6 +153,7 @@ struct ppr_plan {
   // the partition stage of batch i+1 runs on the plan's stream (two scratch regions), and the wave
   // tiers run on stream3 beside the whole hub pipeline (disjoint sources)
   int hub_streams = 2;
+  hipStream_t stream_wave = nullptr;  // the wave tiers' stream (stream3; stream2 in the exact sum with the sieve)
   int wave_wpb = 1;                // PPR_WAVE_WPB: waves per block of k_merge_lds (1, 2 or 4)
   int tile_wpb_p = 4096;           // PPR_TILE_WPB_P: count / scatter run one wave per block from this maxP on
   int tile_split_logp = 10;        // PPR_TILE_SPLIT_LOGP: count / scatter tiles of sources with P <= 2^this
@@ -330,9 +331,22 @@ inline void plan_free(ppr_plan* p) {
                 (double)h[189], h[183] / 1e9, h[184] / 1e9, h[185] / 1e9, h[186] / 1e9, h[187] / 1e9);
       if (h[135] || h[149])
         fprintf(stderr, "ppr_diag sieve: %llu one-slice sources (%llu handed back), %llu multi-slice; passing keys %.3e "
-                "(candidates %.3e), entries beside the prev keys at the select %.3e; one-slice Gcycles (thread 0) "
-                "pass1 %.2f bound+bitmap %.2f pass2 %.2f select+row %.2f\n", h[135], h[137], h[149], (double)h[136],
-                (double)h[138], (double)h[139], h[145] / 1e9, h[146] / 1e9, h[147] / 1e9, h[148] / 1e9);
+                "(candidates %.3e), entries beside the prev keys at the select %.3e\n", h[135], h[137], h[149],
+                (double)h[136], (double)h[138], (double)h[139]);
+      if (h[280])
+        fprintf(stderr, "ppr_diag wave tier: %llu sources, %.1f kept entries each; kcycles per source (lane 0): "
+                "setup+walk %.2f settle %.2f select %.2f row write %.2f norm1 %.2f\n", h[280],
+                (double)h[287] / (double)h[280], h[281] / 1e3 / (double)h[280], h[282] / 1e3 / (double)h[280],
+                h[283] / 1e3 / (double)h[280], h[284] / 1e3 / (double)h[280], h[285] / 1e3 / (double)h[280]);
+      for (int c = 0; c < 3; c++) {
+        const unsigned long long* q = h + 256 + 8 * c;
+        if (q[5])
+          fprintf(stderr, "ppr_diag sieve class %s: %llu sources, %.1f successor rows each, %llu handed back; Mcycles "
+                  "per source (thread 0): setup %.3f pass1 %.3f bound %.3f pass2 %.3f select %.3f\n",
+                  c == 0 ? "large" : c == 1 ? "mid" : "small", q[5], (double)q[6] / (double)q[5], q[7],
+                  q[0] / 1e6 / (double)q[5], q[1] / 1e6 / (double)q[5], q[2] / 1e6 / (double)q[5],
+                  q[3] / 1e6 / (double)q[5], q[4] / 1e6 / (double)q[5]);
+      }
       if (h[154])
         fprintf(stderr, "ppr_diag k_xb: %llu workgroups, %.3e records (%.0f per bucket); Gcycles (thread 0) setup+accumulate "
                 "%.2f settle %.2f select %.2f emit %.2f\n", h[154], (double)h[159], (double)h[159] / (double)h[154],

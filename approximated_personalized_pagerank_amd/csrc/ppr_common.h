@@ -27,7 +27,7 @@ constexpr int PPR_NSTATS = 8;         // device counters: candidates, algorithmi
 // PPR_DIAG counters (u64, printed at plan destruction, plan.h): PPR_DIAG_BASE counters, plus as
 // many per shard -- per-wave counters go to a shard picked by block and wave, so hundreds of
 // millions of waves do not serialise on a few addresses (that contention distorted the timings)
-constexpr int PPR_DIAG_BASE = 256;
+constexpr int PPR_DIAG_BASE = 288;  // (256..279: the sieve's size classes, merge_sv.h)
 constexpr int PPR_DIAG_SHARDS = 256;
 constexpr int PPR_DIAG_SLOTS = PPR_DIAG_BASE * (1 + PPR_DIAG_SHARDS);
 __device__ __forceinline__ void diag_add(unsigned long long* d, int idx, unsigned long long v) {
@@ -221,13 +221,21 @@ __device__ __forceinline__ int write_slot(const IterArgs& a) {
 
 // Epilogue of one source, run by ONE wave: select the top-L of U candidates (keys/vals in LDS
 // or HBM), sort the row, write it to the next slot, norm1 against the old row, fold maxDiff.
+// (PPR_DIAG, dg >= 0: lane 0 adds its cycles of select / row write / norm1 to slots dg .. dg + 2)
+__device__ __forceinline__ void fs_lap(const IterArgs& a, int dg, int k, long long& t) {
+  if (dg < 0 || !a.diag || lane_id() != 0) return;
+  const long long now = (long long)clock64();
+  diag_add(a.diag, dg + k, (unsigned long long)(now - t));
+  t = now;
+}
 template <class KeyAt, class ValAt>
 __device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt valat,
                                               const DevSlab& s, const IterArgs& a, uint32_t* hist,
                                               uint64_t* rv, int* rk, int Lp, int* hk, int* hv,
                                               int* mf, unsigned long long* maxdiff,
-                                              unsigned long long* stats) {
+                                              unsigned long long* stats, int dg = -1) {
   const int L = s.L;
+  long long tl = (dg >= 0 && a.diag) ? (long long)clock64() : 0;
   int cnt;
   if (U <= L) {
     for (int i = lane_id(); i < U; i += WAVE) { rv[i] = dbits(valat(i)); rk[i] = keyat(i); }
@@ -264,12 +272,15 @@ __device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt v
   }
   const int cur = (a.active == 1) ? a.sB : a.sA;
   const int nxt = cur ^ 1;
+  fs_lap(a, dg, 0, tl);
   // rv/rk are left in the stored (hash) order: norm1 walks the new row in that order
   write_row(s, nxt, v, rv, rk, cnt, Lp, false, 1.0);
+  fs_lap(a, dg, 1, tl);
   const int64_t ro = s.row(cur, v);
   const int olen = s.len[s.lrow(cur, v)];
   const double d1 = row_norm1(rv, rk, cnt, s.ids + ro, s.sc + ro, olen, hk, hv, mf, 2 * Lp,
                               [&](int32_t id) { return s.key(id); });
+  fs_lap(a, dg, 2, tl);
   if (lane_id() == 0) {
     // maxDiff only grows: skip the contended atomic when a larger value is already published
     const unsigned long long b = (unsigned long long)dbits(d1);

@@ -4,6 +4,9 @@
 #   tests[:K]   pytest -m gpu tests (K: a -k filter)
 #   bench       bench.py default line (no cpu / e2e legs unless FULL=1)
 #   diag        bench.py one step with PPR_DIAG=1 PPR_TIMING=1
+#   prof        rocprofv3 --kernel-trace --stats over one job (+1 warmup): kernel_stats.csv, timeline
+#   sq          two SQ counter passes (one rocprofv3 run each) over one job: sq_summary.txt
+#   pmc         FETCH_SIZE and WRITE_SIZE passes over one job: pmc.json (tools/pmc_summary.py)
 #   env:VAR=X   export VAR=X for the following steps
 #   ab:VAR=X[,VAR2=Y]  one bench line (2 steps, 1 warmup) with those variables set, ms_per_step printed
 # Stops at the first failing step (a GPU fault, abort or time limit ends the session).
@@ -26,6 +29,33 @@ for step in "$@"; do
       PPR_DIAG=1 PPR_TIMING=1 timeout -k 10 300 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e \
         > "$out/diag.json" 2> "$out/diag.err" || { echo "diag failed rc=$?"; tail -20 "$out/diag.err"; exit 1; }
       grep -E "ppr_diag|ppr_timing" "$out/diag.err" | head -40 ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp) ; export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv rocpd -d "$out/prof" -o run -- python3 bench.py --steps 1 --warmup 1 \
+        --no-cpu-baseline --no-e2e > "$out/prof.json" 2> "$out/prof.err" || { echo "prof failed rc=$?"; tail -20 "$out/prof.err"; exit 1; }
+      ks=$(find "$out/prof" -name "*kernel_stats.csv" | head -1); cp "$ks" "$out/kernel_stats.csv"
+      db=$(find "$out/prof" -name "*results.db" | head -1)
+      python3 tools/timeline.py "$db" > "$out/timeline.txt" 2>/dev/null || true
+      find "$out/prof" -name "*.db" -size +60M -delete
+      head -25 "$out/kernel_stats.csv" | cut -d, -f1-8 ;;
+    sq)
+      export TMPDIR=/tmp
+      P1="--steps 1 --warmup 0 --no-cpu-baseline --no-e2e"
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM \
+        -d "$out/sqa" -o run -f csv -- python3 bench.py $P1 > "$out/sqa.log" 2>&1 || { echo "sq a failed"; exit 1; }
+      timeout -s KILL 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM \
+        -d "$out/sqb" -o run -f csv -- python3 bench.py $P1 > "$out/sqb.log" 2>&1 || { echo "sq b failed"; exit 1; }
+      python3 tools/sq_summary.py $(find "$out/sqa" "$out/sqb" -name "*counter_collection.csv") > "$out/sq_summary.txt"
+      find "$out/sqa" "$out/sqb" -name "*counter_collection.csv" -size +20M -delete
+      head -60 "$out/sq_summary.txt" ;;
+    pmc)
+      export TMPDIR=/tmp
+      P1="--steps 1 --warmup 0 --no-cpu-baseline --no-e2e"
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run -f csv -- python3 bench.py $P1 > "$out/fetch.json" 2> "$out/fetch.err" || { echo "fetch failed"; exit 1; }
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run -f csv -- python3 bench.py $P1 > "$out/write.json" 2> "$out/write.err" || { echo "write failed"; exit 1; }
+      python3 tools/pmc_summary.py $(find "$out/fetch" -name "*counter_collection.csv") $(find "$out/write" -name "*counter_collection.csv") 1 exact > "$out/pmc.json"
+      find "$out/fetch" "$out/write" -name "*counter_collection.csv" -size +20M -delete
+      head -c 1500 "$out/pmc.json" ;;
     env:*)
       export "${step#env:}" ;;
     ab:*)

@@ -13,7 +13,7 @@ for path in sys.argv[1:]:
         k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pprk::", "")
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
 for k, c in sorted(acc.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", kv[1].get("SQ_LDS_IDX_ACTIVE", 0))):
-    if not any(x in k for x in ("hub", "merge", "classify", "k_x")):
+    if not any(x in k for x in ("hub", "merge", "classify", "k_x", "k_sv")):
         continue
     print(k)
     wc = c.get("SQ_WAVE_CYCLES", 0)
