@@ -47,6 +47,7 @@
 #include "merge_hot.h"
 #include "merge_xs.h"
 #include "merge_sv.h"
+#include "merge_xg.h"
 
 using namespace pprk;
 
@@ -383,6 +384,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       if (e4) p->xr_fill = std::max(20, std::min(85, atoi(e4)));
       const char* e5 = getenv("PPR_XR_DSCALE");
       if (e5) p->xr_dscale = std::max(1, std::min(1000, atoi(e5)));
+      const char* e6 = getenv("PPR_HUB_MAX_LOGP");
+      if (e6) p->hub_max_logp = std::max(1, std::min(HUB_MAX_LOGP, atoi(e6)));
+      const char* e7 = getenv("PPR_XG_CAP");
+      p->xg_cap = std::max<int>((int)L, std::min(XG_CAP, e7 ? atoi(e7) : XG_CAP));
       while (xr_lds_bytes(p->xr_T, p->xr_T / (8 * WAVE), p->Lp) > 160 * 1024 && p->xr_T > 1024) p->xr_T /= 2;
       p->xr_W = p->xr_T / (8 * WAVE);
       if (xr_lds_bytes(p->xr_T, p->xr_W, p->Lp) > 160 * 1024 || xf_lds_bytes(p->Lp, 64) > 160 * 1024) {
@@ -464,6 +469,9 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         {(const void*)k_svA, "k_svA"},
         {(const void*)k_svB, "k_svB"},
         {(const void*)k_svF, "k_svF"},
+        {(const void*)k_svfin, "k_svfin"},
+        {(const void*)k_xfin1, "k_xfin1"},
+        {(const void*)k_xg_fin, "k_xg_fin"},
     };
     for (const auto& k : big_lds)
       if (hipFuncSetAttribute(k.first, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
@@ -727,7 +735,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     // exact sum: buckets sized by the expected distinct keys (dest), one workgroup table each
     const int64_t capb = (int64_t)p->xr_T * p->xr_fill / 100;
     for (size_t i = 0; i < nbig; i++)
-      lpv[i] = (uint8_t)std::max(1, std::min(HUB_MAX_LOGP, ceil_log2((dest[i] + capb - 1) / capb)));
+      lpv[i] = (uint8_t)std::max(1, std::min(p->hub_max_logp, ceil_log2((dest[i] + capb - 1) / capb)));
   } else {
     for (size_t i = 0; i < nbig; i++) lpv[i] = (uint8_t)logp_of(cand[i]);
   }
@@ -1190,6 +1198,68 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
   return PPR_OK;
 }
 
+// Exact-sum merge in one HBM table (merge_xg.h) of sources the bucket partition can not split
+// finely enough (more expected distinct keys than 2^hub_max_logp tables hold), one source at a time
+// on the plan stream: walk, digit-by-digit search of the L-th largest selection key, compaction,
+// finish. Its cost is a few passes over a table of 2 x candidates slots (20 B each).
+static int run_xg(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& src, const std::vector<int32_t>& cand,
+                  unsigned long long* maxdiff) {
+  hipStream_t st = p->stream;
+  DevGraph g{p->d_rp, p->d_colx, p->n};
+  const DevSlab s = dev_slab(p);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  for (size_t i = 0; i < src.size(); i++) {
+    const int v = src[i];
+    int64_t T = 1024;
+    while (T < 2 * (int64_t)cand[i] + 64) T <<= 1;
+    size_t off = 0;
+    const size_t o_k = off;  off = al(off + 4 * (size_t)T);
+    const size_t o_a = off;  off = al(off + 8 * (size_t)T);
+    const size_t o_b = off;  off = al(off + 8 * (size_t)T);
+    const size_t o_st = off; off = al(off + sizeof(XgState));
+    const size_t o_h = off;  off = al(off + 4 * (size_t)XG_BINS);
+    const size_t o_e = off;  off = al(off + 4);
+    const size_t zeroed = off;  // table, state, histogram, error flag
+    const size_t o_dk = off; off = al(off + 4 * (size_t)XG_CAP);
+    const size_t o_dv = off; off = al(off + 8 * (size_t)XG_CAP);
+    { int rc = ensure_dev(&p->d_xg, &p->xg_bytes, off); if (rc) return rc; }
+    unsigned char* b = p->d_xg;
+    uint32_t* keys = (uint32_t*)(b + o_k);
+    unsigned long long* A = (unsigned long long*)(b + o_a);
+    unsigned long long* B = (unsigned long long*)(b + o_b);
+    XgState* stp = (XgState*)(b + o_st);
+    uint32_t* hist = (uint32_t*)(b + o_h);
+    int32_t* err = (int32_t*)(b + o_e);
+    int32_t* dk = (int32_t*)(b + o_dk);
+    double* dv = (double*)(b + o_dv);
+    HIP_OK(hipMemsetAsync(b, 0, zeroed, st));
+    const int64_t deg = p->h_rp[v + 1] - p->h_rp[v];
+    const int64_t blocks = std::max<int64_t>(1, (deg + 4 * WAVE - 1) / (4 * WAVE));
+    hipLaunchKernelGGL(k_xg_walk, dim3((unsigned)blocks), dim3(256), 0, st, g, s, a, v, T, keys, A, B, stp);
+    HIP_OK(hipGetLastError());
+    const unsigned gb = (unsigned)std::min<int64_t>(2048, (T + 1023) / 1024);
+    for (int lvl = 0; lvl < XG_LEVELS; lvl++) {
+      hipLaunchKernelGGL(k_xg_hist, dim3(gb), dim3(1024), 0, st, v, T, keys, A, B, stp, lvl, hist);
+      HIP_OK(hipGetLastError());
+      hipLaunchKernelGGL(k_xg_pick, dim3(1), dim3(256), 0, st, stp, lvl, hist, (int)p->L, p->xg_cap);
+      HIP_OK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_xg_compact, dim3((unsigned)std::min<int64_t>(8192, (T + 255) / 256)), dim3(256), 0, st, v, T,
+                       keys, A, B, stp, dk, dv);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(k_xg_fin, dim3(1), dim3(64), xg_fin_lds_bytes(p->Lp), st, s, a, v, stp, dk, dv, p->Lp, maxdiff,
+                       p->d_stats, err);
+    HIP_OK(hipGetLastError());
+    p->merge_launches += 4 + 2 * XG_LEVELS;
+    int32_t herr = 0;
+    HIP_OK(hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (herr) return PPR_ERR_HIP;  // (a table of 2 x candidates slots can not fill)
+    p->xg_sources++;
+  }
+  return PPR_OK;
+}
+
 // Exact-sum merge of the hub sources src[0..n) (candidate counts cand, out-degrees deg, expected
 // distinct keys dest): a source whose keys fit xr_rmax workgroup tables is walked by that many
 // range workgroups (k_xr; one range finishes the source itself, several append to a list that
@@ -1201,7 +1271,6 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
                           const std::vector<int64_t>& dest, unsigned long long* maxdiff, int depth) {
   const size_t n = src.size();
   if (!n) return PPR_OK;
-  if (depth > 12) return PPR_ERR_RANGE;  // (cannot happen: estimates grow 4x per redo)
   hipStream_t st = p->stream;
   hipStream_t sw = p->stream3 ? p->stream3 : st;
   DevGraph g{p->d_rp, p->d_colx, p->n};
@@ -1214,16 +1283,25 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
                       {std::min(4096, p->xr_T), std::min(4096, p->xr_T) / 512},
                       {p->xr_T, p->xr_T / 512}};
   auto cap_of = [&](int T) { return (int64_t)T * p->xr_fill / 100; };
-  std::vector<int32_t> rng;            // ranges per walked source (0: partitioned)
+  std::vector<int32_t> rng;            // ranges per walked source (0: partitioned, -1: HBM table)
   std::vector<uint8_t> ci;             // table class of a walked source
   rng.resize(n);
   ci.resize(n);
   std::vector<int32_t> bsrc, bcand;    // partitioned: sources | candidate counts, then degrees
   std::vector<int32_t> bdest;
   const int64_t capA = cap_of(p->xr_T);
+  // the bucket partition's reach: 2^hub_max_logp tables; a source expected beyond it -- or still
+  // overflowing after XG_REDO redos -- goes to the HBM table (rng -1), which can not overflow
+  const int64_t reach = capA << p->hub_max_logp;
+  constexpr int XG_REDO = 8;
+  std::vector<int32_t> xgs, xgc;
   for (size_t i = 0; i < n; i++) {
     const int64_t R = std::max<int64_t>(1, (dest[i] + capA - 1) / capA);
-    if (R <= p->xr_rmax || !p->hub_enabled) {
+    if (depth > XG_REDO || (p->hub_enabled && R > p->xr_rmax && dest[i] > reach)) {
+      rng[i] = -1;
+      xgs.push_back(src[i]);
+      xgc.push_back(cand[i]);
+    } else if (R <= p->xr_rmax || !p->hub_enabled) {
       rng[i] = (int32_t)R;
       int c = 2;
       if (R == 1) c = dest[i] <= cap_of(cls[0].T) ? 0 : dest[i] <= cap_of(cls[1].T) ? 1 : 2;
@@ -1240,7 +1318,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
   int64_t pt = 0;
   for (int pass = 0; pass < 2; pass++)
     for (size_t i = 0; i < n; i++) {
-      if (!rng[i] || (rng[i] > 1) != (pass == 0)) continue;
+      if (rng[i] <= 0 || (rng[i] > 1) != (pass == 0)) continue;
       const int32_t d = (int32_t)xd.size();
       XDesc x;
       x.v = src[i];
@@ -1338,7 +1416,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
     {
       size_t k = 0;
       for (size_t i = 0; i < n; i++)
-        if (!rng[i]) { cd[k] = cand[i]; cd[nb + k] = deg[i]; k++; }
+        if (rng[i] == 0) { cd[k] = cand[i]; cd[nb + k] = deg[i]; k++; }
     }
     int rc = run_hubs(p, a, bsrc.data(), cd.data(), nb, maxdiff, fallback, bdest.data());
     if (rc) return rc;
@@ -1354,6 +1432,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       for (int32_t d : od) fallback.push_back(xd[d].v);
     }
   }
+  if (!xgs.empty()) { int rc = run_xg(p, a, xgs, xgc, maxdiff); if (rc) return rc; }
   if (fallback.empty()) return PPR_OK;
   // overflowed tables: those sources again, expecting 4x the distinct keys
   p->xr_redo += (int64_t)fallback.size();
@@ -1415,8 +1494,8 @@ static void kst_fold(ppr_plan* p, int g) {
 }
 
 struct SvRun {
-  std::vector<int32_t> v;   // source of each descriptor
-  size_t o_ovl = 0;         // offset of the overflow list in d_sv
+  std::vector<int32_t> pos;  // index into the caller's source list of each descriptor
+  size_t o_ovl = 0;          // offset of the overflow list in d_sv
   bool live = false;
 };
 
@@ -1429,34 +1508,36 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   DevGraph g{p->d_rp, p->d_colx, p->n};
   const DevSlab s = dev_slab(p);
   const int Lp = p->Lp;
-  // multi-slice sources first (descriptors [0, nm)), then the one-slice ones by size class (large,
-  // mid, small), each by candidates, descending
-  std::vector<size_t> multi, one;
-  for (size_t i = 0; i < n; i++) ((int64_t)cand[i] > p->sv_slice ? multi : one).push_back(i);
-  std::stable_sort(one.begin(), one.end(), [&](size_t x, size_t y) { return cand[x] > cand[y]; });
-  const size_t nm = multi.size(), nx = n;
+  // descriptor order: multi-slice sources first (descriptors [0, nm)), then the one-slice ones by
+  // size class (large, mid, small), each by candidates descending in eighth-octave steps (largest
+  // first keeps the tail short). A counting sort: the host plans hundreds of thousands of sources
+  // per iteration while the wave tier runs, and this planning is on the critical path.
+  auto klass = [&](int64_t c) { return c > p->sv_slice ? 0 : c >= p->sv_mid ? 1 : c >= p->sv_small ? 2 : 3; };
+  auto step = [](int64_t c) { return std::min(255, (int)(8.0 * std::log2((double)std::max<int64_t>(1, c)))); };
+  constexpr int NKEY = 4 * 256;
+  std::vector<uint32_t> cnt(NKEY + 1, 0u);
+  std::vector<uint16_t> key(n);
+  for (size_t i = 0; i < n; i++) {
+    key[i] = (uint16_t)(klass(cand[i]) * 256 + (255 - step(cand[i])));
+    cnt[key[i] + 1]++;
+  }
+  for (int k = 0; k < NKEY; k++) cnt[k + 1] += cnt[k];
+  const size_t nm = cnt[256], nx = n;
+  size_t cls_end[3] = {cnt[512], cnt[768], cnt[NKEY]};  // one-slice class ends (descriptor indices)
+  run.pos.resize(nx);
+  for (size_t i = 0; i < n; i++) run.pos[cnt[key[i]]++] = (int32_t)i;
   // SURVEY s8d bytes of a sieved source: row pointer, its successors' ids and lengths, their rows,
   // its own old row (full: L) and the new one, the length
   auto sv_algo_bytes = [&](size_t i) {
     return 8.0 + 8.0 * deg[i] + 12.0 * ((double)cand[i] - 1.0) + 24.0 * (double)p->L + 4.0;
   };
-  size_t cls_end[3] = {0, 0, 0};  // one-slice class boundaries (indices into `one`): large | mid | small
-  {
-    size_t k = 0;
-    while (k < one.size() && (int64_t)cand[one[k]] >= p->sv_mid) k++;
-    cls_end[0] = k;
-    while (k < one.size() && (int64_t)cand[one[k]] >= p->sv_small) k++;
-    cls_end[1] = k;
-    cls_end[2] = one.size();
-  }
-  std::vector<SvDesc> desc;
+  std::vector<SvDesc> desc(nm);
   std::vector<SvTask> tasks;
-  desc.reserve(nx);
-  run.v.clear();
   int64_t tg_total = 0;
   for (size_t k = 0; k < nm; k++) {
-    const size_t i = multi[k];
-    SvDesc d{};
+    const size_t i = (size_t)run.pos[k];
+    SvDesc& d = desc[k];
+    d = SvDesc{};
     d.v = src[i];
     d.S = (int32_t)std::min<int64_t>(((int64_t)cand[i] + p->sv_slice - 1) / p->sv_slice, std::max<int32_t>(1, deg[i]));
     d.factor = p->damping / (double)deg[i];
@@ -1468,24 +1549,16 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
     d.gxt = tg_total;
     tg_total += d.tg;
     for (int s2 = 0; s2 < d.S; s2++) tasks.push_back(SvTask{(int32_t)k, s2});
-    desc.push_back(d);
-    run.v.push_back(d.v);
-  }
-  for (size_t i : one) {
-    SvDesc d{};
-    d.v = src[i];
-    d.S = 1;
-    d.factor = p->damping / (double)deg[i];
-    desc.push_back(d);
-    run.v.push_back(d.v);
   }
   const size_t nt = tasks.size();
-  // d_sv: desc | tasks | one-slice selections (keys, values) | zeroed: ovl[1 + nx] | selected
-  // counts[nx] | oflag[nm] | gpt | gsk | gkeys | ga | gb
+  // d_sv: node ids [nx] | multi descriptors [nm] | tasks | one-slice selections (keys, values) |
+  // zeroed: ovl[1 + nx] | selected counts[nx] | oflag[nm] | gpt | gsk | gkeys | ga | gb
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   size_t off = 0;
-  const size_t o_d = off; off = al(off + sizeof(SvDesc) * nx);
+  const size_t o_v = off; off = al(off + 4 * nx);
+  const size_t o_d = off; off = al(off + sizeof(SvDesc) * (nm + 1));
   const size_t o_t = off; off = al(off + sizeof(SvTask) * (nt + 1));
+  const size_t up = off;
   const size_t o_sk = off; off = al(off + 4 * (size_t)Lp * nx);
   const size_t o_sv = off; off = al(off + 8 * (size_t)Lp * nx);
   const size_t o_z = off;
@@ -1499,10 +1572,11 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   const size_t o_gb = off; off = al(off + 8 * (size_t)tg_total);
   const size_t total = off;
   { int r = ensure_dev(&p->d_sv, &p->sv_bytes, total); if (r) return r; }
-  const size_t up = o_t + sizeof(SvTask) * nt;
   { int r = ensure_pinned(&p->h_sv_pin, &p->h_sv_bytes, up); if (r) return r; }
   unsigned char* hb = (unsigned char*)p->h_sv_pin;
-  std::memcpy(hb + o_d, desc.data(), sizeof(SvDesc) * nx);
+  int32_t* hv = (int32_t*)(hb + o_v);
+  for (size_t k = 0; k < nx; k++) hv[k] = src[(size_t)run.pos[k]];
+  if (nm) std::memcpy(hb + o_d, desc.data(), sizeof(SvDesc) * nm);
   if (nt) std::memcpy(hb + o_t, tasks.data(), sizeof(SvTask) * nt);
   unsigned char* b = p->d_sv;
   hipStream_t s1 = p->stream_sv, s2 = p->stream_sv2, s3 = p->stream_sv3;
@@ -1513,6 +1587,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   HIP_OK(hipEventRecord(p->ev_sv, s3));
   if (s1 != s3) HIP_OK(hipStreamWaitEvent(s1, p->ev_sv, 0));
   if (s2 != s3) HIP_OK(hipStreamWaitEvent(s2, p->ev_sv, 0));
+  const int32_t* d_v = (const int32_t*)(b + o_v);
   const SvDesc* d_d = (const SvDesc*)(b + o_d);
   const SvTask* d_t = (const SvTask*)(b + o_t);
   int32_t* d_ov = (int32_t*)(b + o_ov);
@@ -1531,21 +1606,21 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
     // mid on stream_sv3, so each class's tail overlaps another's work
     const SvGeom geo[3] = {SV_LARGE, SV_MID, SV_SMALL};
     hipStream_t cs[3] = {s2, s3, s2};
-    size_t c0 = 0;
+    size_t c0 = nm;
     for (int c = 0; c < 3; c++) {
-      const size_t cnt = cls_end[c] - c0;
-      const int d0 = (int)(nm + c0);
+      const size_t cnt_c = cls_end[c] - c0;
+      const int d0 = (int)c0;
       double bytes = 0.0;
-      for (size_t k = c0; k < cls_end[c]; k++) bytes += sv_algo_bytes(one[k]);
+      for (size_t k = c0; k < cls_end[c]; k++) bytes += sv_algo_bytes((size_t)run.pos[k]);
       c0 = cls_end[c];
-      if (!cnt) continue;
+      if (!cnt_c) continue;
       const SvGeom G = geo[c];
       kst_begin(p, 1 + c, cs[c]);
-      hipLaunchKernelGGL(k_sv1, dim3((unsigned)cnt), dim3(G.threads()), sv_lds_bytes(Lp, G), cs[c], g, s, a, d_d, d0, Lp,
-                         G, std::min(p->sv_budget, G.budget), d_ov, d_ok, d_ovv, d_on);
+      hipLaunchKernelGGL(k_sv1, dim3((unsigned)cnt_c), dim3(G.threads()), sv_lds_bytes(Lp, G), cs[c], g, s, a, d_v, d0,
+                         Lp, G, std::min(p->sv_budget, G.budget), d_ov, d_ok, d_ovv, d_on);
       HIP_OK(hipGetLastError());
-      hipLaunchKernelGGL(k_svfin, dim3((unsigned)cnt), dim3(64), svfin_lds_bytes(Lp), cs[c], s, a, d_d, d0, d_ok, d_ovv,
-                         d_on, Lp, maxdiff, p->d_stats);
+      hipLaunchKernelGGL(k_svfin, dim3((unsigned)cnt_c), dim3(64), svfin_lds_bytes(Lp), cs[c], s, a, d_v, d0, d_ok,
+                         d_ovv, d_on, Lp, maxdiff, p->d_stats);
       HIP_OK(hipGetLastError());
       kst_end(p, 1 + c, cs[c], bytes);
       p->merge_launches += 2;
@@ -1553,7 +1628,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   }
   if (nm) {
     double bytes = 0.0;
-    for (size_t i : multi) bytes += sv_algo_bytes(i);
+    for (size_t k = 0; k < nm; k++) bytes += sv_algo_bytes((size_t)run.pos[k]);
     kst_begin(p, 4, s1);
     hipLaunchKernelGGL(k_svA, dim3((unsigned)nt), dim3(SV_THREADS), lds, s1, g, s, a, d_d, d_t, Lp, d_sk, d_pt);
     HIP_OK(hipGetLastError());
@@ -1572,7 +1647,8 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   return PPR_OK;
 }
 
-// wait for the sieve, append the sources it handed back (table overflows) to `back`
+// wait for the sieve, append the sources it handed back (table overflows) to `back`, as indices
+// into the list sieve_launch was given
 static int sieve_collect(ppr_plan* p, SvRun& run, std::vector<int32_t>& back) {
   if (!run.live) return PPR_OK;
   run.live = false;
@@ -1592,7 +1668,7 @@ static int sieve_collect(ppr_plan* p, SvRun& run, std::vector<int32_t>& back) {
   std::vector<int32_t> od(novf);
   HIP_OK(hipMemcpyAsync(od.data(), p->d_sv + run.o_ovl + 4, 4 * (size_t)novf, hipMemcpyDeviceToHost, p->stream_sv));
   HIP_OK(hipStreamSynchronize(p->stream_sv));
-  for (int32_t d : od) back.push_back(run.v[(size_t)d]);
+  for (int32_t d : od) back.push_back(run.pos[(size_t)d]);
   p->sv_redo += novf;
   return PPR_OK;
 }
@@ -1604,6 +1680,13 @@ static int sieve_collect(ppr_plan* p, SvRun& run, std::vector<int32_t>& back) {
 // engines with the distinct-key estimate planned on the host
 static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int64_t count, unsigned long long* maxdiff) {
   if (count <= 0) return PPR_OK;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto lap = [&](int k, std::chrono::steady_clock::time_point& t) {
+    const auto t2 = now();
+    p->xh_s[k] += std::chrono::duration<double>(t2 - t).count();
+    t = t2;
+  };
+  auto tl = now();
   hipStream_t st = p->stream;
   const size_t nh = (size_t)count;
   {
@@ -1625,8 +1708,9 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
   HIP_OK(hipStreamSynchronize(st));
   std::vector<int32_t> hcopy(h, h + 5 * nh);  // (the pinned buffer is restaged by later calls)
   h = hcopy.data();
+  lap(0, tl);  // gather + copy back
   const bool sieve = p->sv_enabled && a.xs && !a.unit && !a.mc && p->hot_n == 0;
-  std::vector<int32_t> src, cand, deg, ssrc, scand, sdeg;
+  std::vector<int32_t> src, cand, deg, ssrc, scand, sdeg, sidx;
   std::vector<int64_t> dest;
   // distinct keys expected: the last merge's count (rows change little between updates) plus a
   // margin, else (first merge) 60 % of the candidates; never more than the candidates + 1
@@ -1643,6 +1727,7 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
       ssrc.push_back(h[i]);
       scand.push_back(c);
       sdeg.push_back(h[2 * nh + i]);
+      sidx.push_back((int32_t)i);
     } else {
       src.push_back(h[i]);
       cand.push_back(c);
@@ -1650,27 +1735,29 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
       dest.push_back(estimate(i));
     }
   }
+  lap(1, tl);  // classification
   SvRun run;
   if (!ssrc.empty()) { int r = sieve_launch(p, a, ssrc, scand, sdeg, maxdiff, run); if (r) return r; }
+  lap(2, tl);  // sieve planning + launches
   if (!src.empty()) { int r = run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0); if (r) return r; }
+  lap(3, tl);  // range / partition engines (their syncs included)
   std::vector<int32_t> back;
   { int r = sieve_collect(p, run, back); if (r) return r; }
+  lap(4, tl);  // waiting for the sieve
   if (back.empty()) return PPR_OK;
   // handed back: the range / partition engines, with the usual estimate
-  std::vector<std::pair<int32_t, size_t>> idx(nh);
-  for (size_t i = 0; i < nh; i++) idx[i] = {h[i], i};
-  std::sort(idx.begin(), idx.end());
   src.clear(); cand.clear(); deg.clear(); dest.clear();
-  for (int32_t v : back) {
-    auto it = std::lower_bound(idx.begin(), idx.end(), std::make_pair(v, (size_t)0));
-    if (it == idx.end() || it->first != v) return PPR_ERR_HIP;
-    const size_t i = it->second;
-    src.push_back(v);
+  for (int32_t k : back) {
+    const size_t i = (size_t)sidx[(size_t)k];
+    src.push_back(h[i]);
     cand.push_back(h[nh + i]);
     deg.push_back(h[2 * nh + i]);
     dest.push_back(estimate(i));
   }
-  return run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0);
+  lap(5, tl);  // hand-back planning
+  const int r = run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0);
+  lap(6, tl);  // hand-backs merged
+  return r;
 }
 
 // classify + launch all tiers for `count` sources of `list`; the span is timed with events on

@@ -507,14 +507,13 @@ __device__ __forceinline__ void sv_clear_region(const SvLds& x, size_t bytes) {
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterArgs a, const SvDesc* desc, int d0,
+__global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterArgs a, const int32_t* vid, int d0,
                                                     int Lp, SvGeom G, int budget, int32_t* ovl, int32_t* out_k,
                                                     double* out_v, int32_t* out_n) {
   extern __shared__ __align__(16) unsigned char smem[];
   const SvLds x = sv_carve(smem, Lp, G);
   const int d = d0 + (int)blockIdx.x;
-  const SvDesc sd = desc[d];
-  const int v = sd.v;
+  const int v = vid[d];
   const int L = s.L;
   // (the host sends only sources with a full current row: L keys to bound with)
   if (s.len[s.lrow((a.active == 1) ? a.sB : a.sA, v)] != L) {
@@ -534,7 +533,8 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
   }
   sv_lap(a, dg + 0, tph);
   const int64_t b = g.rp[v], e = g.rp[v + 1];
-  sv_pass1(g, s, a, x, b, e, sd.factor, sk);
+  const double factor = merge_factor(a, e - b);
+  sv_pass1(g, s, a, x, b, e, factor, sk);
   __syncthreads();
   sv_lap(a, dg + 1, tph);
   // bound: the smallest exact total of the L prev keys
@@ -550,7 +550,7 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
   __syncthreads();
   sv_lap(a, dg + 2, tph);
   if (threadIdx.x == 0) sv_seed2(x, xt, v, 1.0 - a.damping);
-  sv_pass2(g, s, a, x, xt, b, e, sd.factor, budget);
+  sv_pass2(g, s, a, x, xt, b, e, factor, budget);
   __syncthreads();
   sv_lap(a, dg + 3, tph);
   if (a.diag && threadIdx.x == 0) { diag_add(a.diag, dg + 5, 1ull); diag_add(a.diag, dg + 6, (unsigned long long)(e - b)); }
@@ -638,14 +638,14 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
 // the row of a one-slice source from its selected entries (k_sv1): one wave per source -- sort in
 // hash order, write, range index, norm1 against the old row, maxDiff (finish_source)
 __host__ __device__ constexpr size_t svfin_lds_bytes(int Lp) { return (size_t)Lp * 12 + 1024 + (size_t)Lp * 20; }
-__global__ void __launch_bounds__(64) k_svfin(DevSlab s, IterArgs a, const SvDesc* desc, int d0, const int32_t* in_k,
+__global__ void __launch_bounds__(64) k_svfin(DevSlab s, IterArgs a, const int32_t* vid, int d0, const int32_t* in_k,
                                               const double* in_v, const int32_t* in_n, int Lp,
                                               unsigned long long* maxdiff, unsigned long long* stats) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int d = d0 + (int)blockIdx.x;
   const int n = in_n[d];
   if (n <= 0) return;  // handed back (a written source has L >= 1 entries)
-  const int v = desc[d].v;
+  const int v = vid[d];
   uint64_t* rv = reinterpret_cast<uint64_t*>(smem);
   int* rk = reinterpret_cast<int*>(smem + (size_t)Lp * 8);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem + (size_t)Lp * 12);

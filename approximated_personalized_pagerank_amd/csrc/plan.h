@@ -203,6 +203,13 @@ struct ppr_plan {
   void* h_xs_pin = nullptr;           // pinned staging of its descriptors and tasks
   size_t h_xs_bytes = 0;
   int64_t xr_redo = 0;                // sources redone after a table overflow (PPR_TIMING at destroy)
+  // exact-sum HBM-table fallback (merge_xg.h): sources past the bucket partition's reach
+  int hub_max_logp = 12;              // PPR_HUB_MAX_LOGP (tests): most bucket bits of an exact-sum partition
+                                      // (<= merge_hub.h HUB_MAX_LOGP)
+  unsigned char* d_xg = nullptr;      // table | dense list | state | histogram
+  size_t xg_bytes = 0;
+  int64_t xg_sources = 0;             // sources merged there (PPR_TIMING at destroy)
+  int xg_cap = 1 << 16;               // dense list of the selection (PPR_XG_CAP, tests: L <= cap <= XG_CAP)
   // sieve merge of the wide exact-sum sources (merge_sv.h): PPR_SV=0 turns it off
   bool sv_enabled = false;
   int64_t sv_slice = 1LL << 18;       // PPR_SV_SLICE: candidates per slice workgroup
@@ -217,6 +224,7 @@ struct ppr_plan {
   void* h_sv_pin = nullptr;           // pinned staging of descriptors and tasks, overflow count
   size_t h_sv_bytes = 0;
   int64_t sv_sources = 0, sv_redo = 0;  // sieved sources, handed back after an overflow (PPR_TIMING)
+  double xh_s[8] = {};                // run_xhubs host sections, s (PPR_TIMING at destroy)
   // MCCompletePathV2 (mccp2.hip)
   bool mc = false;
   int32_t* d_mc_walk = nullptr;       // walk set W (nodes read before their final basket exists)
@@ -266,12 +274,19 @@ inline void plan_free(ppr_plan* p) {
   if (p->h_desc_pin) hipHostFree(p->h_desc_pin);
   if (p->h_xs_pin) hipHostFree(p->h_xs_pin);
   hipFree(p->d_sv);
+  hipFree(p->d_xg);
   if (p->h_sv_pin) hipHostFree(p->h_sv_pin);
   if (p->ev_sv) hipEventDestroy(p->ev_sv);
   if (getenv("PPR_TIMING") && p->sv_sources)
     fprintf(stderr, "ppr_timing sieve_sources %lld sieve_redo %lld\n", (long long)p->sv_sources, (long long)p->sv_redo);
+  if (getenv("PPR_TIMING") && p->sv_sources)
+    fprintf(stderr, "ppr_timing xhubs_host_s gather %.4f classify %.4f sieve_launch %.4f engines %.4f sieve_wait %.4f "
+            "handback_plan %.4f handback_run %.4f\n", p->xh_s[0], p->xh_s[1], p->xh_s[2], p->xh_s[3], p->xh_s[4],
+            p->xh_s[5], p->xh_s[6]);
   if (getenv("PPR_TIMING") && p->xr_redo)
     fprintf(stderr, "ppr_timing xr_redo_sources %lld\n", (long long)p->xr_redo);
+  if (getenv("PPR_TIMING") && p->xg_sources)
+    fprintf(stderr, "ppr_timing hbm_table_sources %lld\n", (long long)p->xg_sources);
   if (getenv("PPR_TIMING") && p->spec_redo)
     fprintf(stderr, "ppr_timing spec_redo_sources %lld\n", (long long)p->spec_redo);
   if (getenv("PPR_TIMING") && p->host_plan_calls)

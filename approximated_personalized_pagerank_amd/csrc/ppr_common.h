@@ -228,6 +228,111 @@ __device__ __forceinline__ void fs_lap(const IterArgs& a, int dg, int k, long lo
   diag_add(a.diag, dg + k, (unsigned long long)(now - t));
   t = now;
 }
+// Register epilogue of a GRank row of cnt <= 128 entries (Lp <= 128): lane l holds the new
+// entries l and l + 64 (k0/v0, k1/v1, candidate order) and the old row's entries l and l + 64
+// (o0/os0, o1/os1, stored order, loaded before the select). hash_b is a bijection, so an entry's
+// place in the stored order is its rank -- the number of entries with a smaller hash -- counted
+// against every other entry's hash read with v_readlane (no sort network, no LDS round trips); the
+// range index is a 64-bin count and a wave scan. The row is stored straight from the ranks. norm1 keeps
+// oracle/grank_oracle.c:norm1_rows' lane pattern exactly: lane l adds |new - old| of the stored
+// positions l then l + 64 (the d values are permuted into stored order through LDS), then the
+// unmatched old entries l then l + 64, then the xor butterfly. LDS: hk/hv (2 Lp), mf (Lp), rv
+// (old scores by position, Lp), hist (d by position: <= 128 doubles = its 1 KB).
+__device__ __forceinline__ double finish_row_reg(const DevSlab& s, int nxt, int v, int cnt, int k0, uint64_t v0,
+                                                 int k1, uint64_t v1, int o0, double os0, int o1, double os1,
+                                                 int olen, uint64_t* rv, uint32_t* hist, int* hk, int* hv, int* mf,
+                                                 int Lp, const IterArgs& a, int dg, long long& tl) {
+  const int l = lane_id();
+  const bool e0 = l < cnt, e1 = l + WAVE < cnt;
+  const uint32_t h0 = hash_b((uint32_t)k0), h1 = hash_b((uint32_t)k1);
+  // range index: entries per hash range (LDS counts), inclusive scan over the 64 lanes
+  hist[l] = 0u;
+  wave_fence();
+  if (e0) atomicAdd(&hist[h0 >> (32 - RANGE_BITS)], 1u);
+  if (e1) atomicAdd(&hist[h1 >> (32 - RANGE_BITS)], 1u);
+  wave_fence();
+  const int rx = wave_incl_scan((int)hist[l]);
+  int r0 = 0, r1 = 0;
+  // (cnt is wave-uniform: scalar loops; entries past cnt hash EMPTY's value and are counted out
+  // by the trip counts, 4 lanes per trip so the compares interleave)
+  const int n0 = cnt < WAVE ? cnt : WAVE;
+  auto cmp4 = [&](uint32_t hv, int i) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t sh = (uint32_t)__builtin_amdgcn_readlane((int)hv, i + u);
+      r0 += sh < h0;
+      r1 += sh < h1;
+    }
+  };
+  auto cmp1 = [&](uint32_t hv, int i) {
+    const uint32_t sh = (uint32_t)__builtin_amdgcn_readlane((int)hv, i);
+    r0 += sh < h0;
+    r1 += sh < h1;
+  };
+  int i = 0;
+  for (; i + 4 <= n0; i += 4) cmp4(h0, i);
+  for (; i < n0; i++) cmp1(h0, i);
+  const int n1 = cnt - WAVE;
+  for (i = 0; i + 4 <= n1; i += 4) cmp4(h1, i);
+  for (; i < n1; i++) cmp1(h1, i);
+  const int64_t r = s.row(nxt, v);
+  uint64_t mn = ~0ull;
+  if (e0) { s.ids[r + r0] = s.enc(k0); s.sc[r + r0] = bitsd(v0); mn = v0; }
+  if (e1) { s.ids[r + r1] = s.enc(k1); s.sc[r + r1] = bitsd(v1); mn = v1 < mn ? v1 : mn; }
+  mn = wave_min_u64(mn);
+  s.rix[s.xrow(nxt, v) + l] = (uint16_t)rx;
+  if (l == 0) {
+    s.len[s.lrow(nxt, v)] = cnt;
+    s.rmin[s.lrow(nxt, v)] = cnt ? bitsd(mn) : 0.0;
+  }
+  fs_lap(a, dg, 1, tl);
+  // norm1: LDS hash of the old keys (positions j, scores rv[j]), probed by the new keys
+  const int hsize = 2 * Lp;
+  const uint32_t hmask = (uint32_t)hsize - 1;
+  for (int i = l; i < hsize; i += WAVE) hk[i] = EMPTY;
+  const bool f0 = l < olen, f1 = l + WAVE < olen;
+  if (f0) { mf[l] = 0; rv[l] = dbits(os0); }
+  if (f1) { mf[l + WAVE] = 0; rv[l + WAVE] = dbits(os1); }
+  wave_fence();
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    if (!(q ? f1 : f0)) continue;
+    const int key = q ? o1 : o0;
+    uint32_t h = hash32((uint32_t)key) & hmask;
+    for (int c = 0; c < hsize; c++) {  // 2 Lp slots hold at most L keys: never full
+      const int prev = atomicCAS(&hk[h], EMPTY, key);
+      if (prev == EMPTY) { hv[h] = l + q * WAVE; break; }
+      h = (h + 1) & hmask;
+    }
+  }
+  wave_fence();
+  double* dd = reinterpret_cast<double*>(hist);
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    if (!(q ? e1 : e0)) continue;
+    const int key = q ? k1 : k0;
+    uint32_t h = hash32((uint32_t)key) & hmask;
+    double o = 0.0;
+    for (int c = 0; c < hsize; c++) {
+      const int cur = hk[h];
+      if (cur == key) { const int j = hv[h]; o = bitsd(rv[j]); mf[j] = 1; break; }
+      if (cur == EMPTY) break;
+      h = (h + 1) & hmask;
+    }
+    dd[q ? r1 : r0] = fabs(bitsd(q ? v1 : v0) - o);
+  }
+  wave_fence();
+  double p = 0.0;
+  if (e0) p += dd[l];
+  if (e1) p += dd[l + WAVE];
+  if (f0 && !mf[l]) p += os0;
+  if (f1 && !mf[l + WAVE]) p += os1;
+#pragma unroll
+  for (int o = 32; o; o >>= 1) p = p + __shfl_xor(p, o);
+  wave_fence();
+  return p;
+}
+
 template <class KeyAt, class ValAt>
 __device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt valat,
                                               const DevSlab& s, const IterArgs& a, uint32_t* hist,
@@ -235,7 +340,21 @@ __device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt v
                                               int* mf, unsigned long long* maxdiff,
                                               unsigned long long* stats, int dg = -1) {
   const int L = s.L;
+  U = __builtin_amdgcn_readfirstlane(U);  // (wave-uniform: scalar loop bounds below)
   long long tl = (dg >= 0 && a.diag) ? (long long)clock64() : 0;
+  // GRank rows of <= 128 entries take the register epilogue: the old row is loaded here, ahead of
+  // the select, whose work hides its latency (all L entries of the row, masked by its length later)
+  const bool reg = Lp <= 2 * WAVE && !a.unit && !a.mc;
+  const int cur = (a.active == 1) ? a.sB : a.sA;
+  int o0 = EMPTY, o1 = EMPTY, olen = 0;
+  double os0 = 0.0, os1 = 0.0;
+  if (reg) {
+    const int64_t ro = s.row(cur, v);
+    const int l = lane_id();
+    olen = __builtin_amdgcn_readfirstlane(s.len[s.lrow(cur, v)]);
+    if (l < L) { o0 = s.ids[ro + l]; os0 = s.sc[ro + l]; }
+    if (l + WAVE < L) { o1 = s.ids[ro + l + WAVE]; os1 = s.sc[ro + l + WAVE]; }
+  }
   int cnt;
   if (U <= L) {
     for (int i = lane_id(); i < U; i += WAVE) { rv[i] = dbits(valat(i)); rk[i] = keyat(i); }
@@ -270,16 +389,25 @@ __device__ __forceinline__ void finish_source(int v, int U, KeyAt keyat, ValAt v
     write_row(s, 0, v, rv, rk, cnt, Lp, true, f);
     return;
   }
-  const int cur = (a.active == 1) ? a.sB : a.sA;
   const int nxt = cur ^ 1;
   fs_lap(a, dg, 0, tl);
-  // rv/rk are left in the stored (hash) order: norm1 walks the new row in that order
-  write_row(s, nxt, v, rv, rk, cnt, Lp, false, 1.0);
-  fs_lap(a, dg, 1, tl);
-  const int64_t ro = s.row(cur, v);
-  const int olen = s.len[s.lrow(cur, v)];
-  const double d1 = row_norm1(rv, rk, cnt, s.ids + ro, s.sc + ro, olen, hk, hv, mf, 2 * Lp,
-                              [&](int32_t id) { return s.key(id); });
+  double d1;
+  if (reg) {
+    const int l = lane_id();
+    const int k0 = l < cnt ? rk[l] : EMPTY, k1 = l + WAVE < cnt ? rk[l + WAVE] : EMPTY;
+    const uint64_t v0 = l < cnt ? rv[l] : 0ull, v1 = l + WAVE < cnt ? rv[l + WAVE] : 0ull;
+    wave_fence();
+    d1 = finish_row_reg(s, nxt, v, cnt, k0, v0, k1, v1, l < olen ? s.key(o0) : EMPTY, os0,
+                        l + WAVE < olen ? s.key(o1) : EMPTY, os1, olen, rv, hist, hk, hv, mf, Lp, a, dg, tl);
+  } else {
+    // rv/rk are left in the stored (hash) order: norm1 walks the new row in that order
+    write_row(s, nxt, v, rv, rk, cnt, Lp, false, 1.0);
+    fs_lap(a, dg, 1, tl);
+    const int64_t ro = s.row(cur, v);
+    const int olen2 = s.len[s.lrow(cur, v)];
+    d1 = row_norm1(rv, rk, cnt, s.ids + ro, s.sc + ro, olen2, hk, hv, mf, 2 * Lp,
+                   [&](int32_t id) { return s.key(id); });
+  }
   fs_lap(a, dg, 2, tl);
   if (lane_id() == 0) {
     // maxDiff only grows: skip the contended atomic when a larger value is already published

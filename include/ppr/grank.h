@@ -52,7 +52,7 @@ namespace hipdetail {
 // duration of the calls that are materialising results; the last of several concurrent calls to
 // finish sets it back to MALLOC_TOP_PAD_ (else glibc's 128 KB) -- glibc has no getter for a value
 // the application may have set itself, so an application that sets M_TOP_PAD should leave
-// PPR_HEAP_PAD unset (INTEGRATION.md "Host threads and memory").
+// PPR_HEAP_PAD unset (INTEGRATION.md "Process-wide side effects").
 struct HeapGrowth {
 #if defined(__GLIBC__)
   static std::atomic<int>& active() {

@@ -344,3 +344,37 @@ def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):
         assert sieved == 0
     if want == "redo":
         assert redo > 0
+
+
+@pytest.mark.parametrize("henv", [
+    # the bucket partition limited to 2 buckets of 819 keys: every source expected beyond them
+    # goes to the HBM table (merge_xg.h); the selection list at its largest (all keys at once)
+    {"PPR_XR_T": "1024", "PPR_XR_RMAX": "1", "PPR_HUB_MAX_LOGP": "1"},
+    # ... with the list capped at L: the digit search runs through score and tie digits
+    {"PPR_XR_T": "1024", "PPR_XR_RMAX": "1", "PPR_HUB_MAX_LOGP": "1", "PPR_XG_CAP": "1"},
+    # estimates 20x too low: partitioned sources overflow at the saturated bucket count and are
+    # redone in the HBM table instead of identical partitions
+    {"PPR_XR_T": "1024", "PPR_XR_RMAX": "1", "PPR_HUB_MAX_LOGP": "1", "PPR_XR_DSCALE": "5"},
+    # no wave tiers: every source through the workgroup engines (init in unit mode too)
+    {"PPR_XR_T": "1024", "PPR_XR_RMAX": "1", "PPR_HUB_MAX_LOGP": "1", "PPR_TIER_MASK": "0x20", "PPR_XG_CAP": "300"},
+])
+def test_gpu_hbm_table_fallback_bit_exact(henv, monkeypatch, capfd):
+    """sources past the exact-sum bucket partition's reach (2^hub_max_logp tables) are merged in one
+    HBM table and still match the oracle's exact sum bit for bit (no PPR_ERR_RANGE after
+    12 identical redos)"""
+    for k, v in henv.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("PPR_SV", "0")
+    monkeypatch.setenv("PPR_TIMING", "1")
+    for scale, K, L, it in [(11, 16, 32, 6), (12, 32, 128, 5), (12, 16, 512, 3)]:
+        g = ppr.rmat(scale, seed=291 + scale)
+        part = g.partitions()
+        r = ppr.grank_csr(g, K, L, it, 0.85, -1.0, part=part, device=0)
+        o = oracle.grank(g.row_ptr, g.col, part, K, L, it, 0.85, -1.0)
+        assert np.array_equal(r.max_diff, o["max_diff"])
+        assert np.array_equal(r.lens, o["lens"])
+        assert np.array_equal(r.ids, o["ids"])
+        assert np.array_equal(r.scores, o["scores"])
+    err = capfd.readouterr().err
+    n = sum(int(x.split()[2]) for x in err.splitlines() if x.startswith("ppr_timing hbm_table_sources"))
+    assert n > 0
