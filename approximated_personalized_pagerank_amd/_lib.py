@@ -70,6 +70,7 @@ ERRORS = {
     10: "device out of memory",
     11: "parameter outside the supported range",
     12: "source node not part of the graph",
+    13: "a hash table ran out of slots (table sizing error)",
 }
 
 

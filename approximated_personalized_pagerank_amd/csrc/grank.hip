@@ -287,6 +287,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     if (ent) p->nt_loads = (int)strtol(ent, nullptr, 0) & 3;
     const char* ewi = getenv("PPR_WHATIF");
     if (ewi) p->whatif = (int)strtol(ewi, nullptr, 0);
+    const char* etd = getenv("PPR_WAVE_TDIV");  // tests: wave-tier tables T >> this (bounded probes run out)
+    if (etd) p->wave_tdiv = std::max(0, std::min(6, atoi(etd)));
     const char* exr = getenv("PPR_XROUTE");
     if (exr && atoi(exr) == 0) p->xroute = false;
     const char* e9e = getenv("PPR_WG_PASSES");  // tests: force workgroup-tier overflows
@@ -401,6 +403,9 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
           p->tierCap[t] = 0;
         }
       TRY(dalloc(&p->d_dlast, n));
+      TRY(dalloc(&p->d_wovl, n + 1));
+      const char* e9 = getenv("PPR_XR_BUDGET");
+      p->xr_budget_over = e9 && strcmp(e9, "over") == 0;
       if (hipMemset(p->d_dlast, 0, 4 * (size_t)(n > 0 ? n : 1)) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
       int32_t caps[NT + 1];
       for (int t = 0; t <= NT; t++) caps[t] = p->tierCap[t];
@@ -1052,7 +1057,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
     }
     if (a.xs) {
       // exact sum: one workgroup per bucket, then one per source over the buckets' lists
-      const int budget = std::min(p->xr_T * 85 / 100, p->xr_T - p->xr_W * WAVE - WAVE);
+      const int budget = p->xr_budget_over ? 2 * p->xr_T : std::min(p->xr_T * 85 / 100, p->xr_T - p->xr_W * WAVE - WAVE);
       if (nbuck) {
         hipLaunchKernelGGL(k_xb, dim3((unsigned)nbuck), dim3(64 * p->xr_W), xr_lds_bytes(p->xr_T, p->xr_W, p->Lp), sb, s,
                            a, d_desc, d_buck, d_cmx, d_sd, d_st, d_tau, p->xr_T, budget, p->Lp, d_xt, d_pk, d_ps, d_pc,
@@ -1389,7 +1394,9 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
     for (int c = 0; c < 3; c++) {
       if (tasks[c].empty()) continue;
       const int T = cls[c].T, W = cls[c].W;
-      const int budget = std::min(T * 85 / 100, T - W * WAVE - WAVE);
+      // (PPR_XR_BUDGET=over, tests: no budget stop -- the tables fill and the bounded probes run
+      // out, which must end in the overflow redo)
+      const int budget = p->xr_budget_over ? 2 * T : std::min(T * 85 / 100, T - W * WAVE - WAVE);
       hipLaunchKernelGGL(k_xr, dim3((unsigned)tasks[c].size()), dim3(64 * W), xr_lds_bytes(T, W, p->Lp), sw, g, s, a,
                          d_xd, d_tk + tofs[c], T, budget, p->Lp, d_xt, d_pk, d_ps, d_pc, d_ds, d_of, d_ov);
       HIP_OK(hipGetLastError());
@@ -1767,10 +1774,22 @@ int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count
   if (count <= 0) return PPR_OK;
   // MC combine levels are timed as a whole by the caller: no per-level event sync
   if (!a.mc) HIP_OK(hipEventRecord(p->ev_m0, p->stream));
+  p->wave_x_launched = false;
   int rc = run_merge_impl(p, a, list, count, maxdiff);
   if (p->stream_wave && p->stream_wave != p->stream) {  // the wave tiers ran on their own stream
     HIP_OK(hipEventRecord(p->ev_wave, p->stream_wave));
     HIP_OK(hipStreamWaitEvent(p->stream, p->ev_wave, 0));
+  }
+  if (!rc && p->wave_x_launched) {
+    // exact wave tier: sources whose table ran out (only with PPR_WAVE_TDIV: the tables hold 4/3 of
+    // the tier's candidate cap) wrote no row; the workgroup engines merge them again
+    int32_t nw = 0;
+    HIP_OK(hipMemcpyAsync(&nw, p->d_wovl, 4, hipMemcpyDeviceToHost, p->stream));
+    HIP_OK(hipStreamSynchronize(p->stream));
+    if (nw) {
+      p->wave_redo += nw;
+      rc = run_xhubs(p, a, p->d_wovl + 1, nw, maxdiff);
+    }
   }
   if (rc || a.mc) return rc;
   HIP_OK(hipEventRecord(p->ev_m1, p->stream));
@@ -1923,14 +1942,18 @@ reclassify:
     const int wpb = p->wave_wpb;
     const int64_t blocks = ((int64_t)cnt[t] + wpb - 1) / wpb;
     if (a.xs) {
-      hipLaunchKernelGGL(k_merge_lds_x, dim3((unsigned)blocks), dim3(64 * wpb), lds_wave_bytes_x(p->tierT[t], p->Lp) * wpb,
-                         sw, g, s, a, p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], p->tierT[t], p->Lp, maxdiff,
-                         p->d_stats, p->d_dlast);
+      if (!p->wave_x_launched) HIP_OK(hipMemsetAsync(p->d_wovl, 0, 4, sw));
+      p->wave_x_launched = true;
+      const int Tw = std::max(64, p->tierT[t] >> p->wave_tdiv);  // (PPR_WAVE_TDIV: tests of the overflow redo)
+      hipLaunchKernelGGL(k_merge_lds_x, dim3((unsigned)blocks), dim3(64 * wpb), lds_wave_bytes_x(Tw, p->Lp) * wpb,
+                         sw, g, s, a, p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], Tw, p->Lp, maxdiff,
+                         p->d_stats, p->d_dlast, p->d_wovl);
     } else {
-      const size_t bytes = lds_wave_bytes(p->tierT[t], p->Lp) * wpb;
+      const int Tw = std::max(64, p->tierT[t] >> p->wave_tdiv);  // (PPR_WAVE_TDIV: tests of the bounded probes)
+      const size_t bytes = lds_wave_bytes(Tw, p->Lp) * wpb;
       hipLaunchKernelGGL(p->hot_n > 0 ? k_merge_lds<true> : k_merge_lds<false>, dim3((unsigned)blocks), dim3(64 * wpb),
                          bytes, sw, g, s, a,
-                         p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], p->tierT[t], p->Lp,
+                         p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], Tw, p->Lp,
                          maxdiff, p->d_stats);
     }
     HIP_OK(hipGetLastError());
@@ -2080,11 +2103,24 @@ extern "C" int ppr_grank_plan_read_maxdiff(ppr_plan* p, int32_t it, double* maxd
   return PPR_OK;
 }
 
+// this module's bounded-probe error word (ppr_device.h probe_fail): PPR_ERR_PROBE once set (and
+// cleared), read once per run (a device-wide sync)
+int probe_take() {
+  unsigned int v = 0u;
+  HIP_OK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_probe_err), sizeof(v), 0, hipMemcpyDeviceToHost));
+  if (!v) return PPR_OK;
+  const unsigned int z = 0u;
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_probe_err), &z, sizeof(z), 0, hipMemcpyHostToDevice));
+  return PPR_ERR_PROBE;
+}
+
 extern "C" int ppr_grank_plan_finish(ppr_plan* p, int32_t iterations_run) {
   if (!p || iterations_run < 0) return PPR_ERR_ARG;
   if (p->n == 0) return PPR_OK;
   HIP_OK(hipSetDevice(p->device));
-  return launch_topk(p, ((iterations_run + 1) / 2) & 1, (iterations_run / 2) & 1);
+  const int rc = launch_topk(p, ((iterations_run + 1) / 2) & 1, (iterations_run / 2) & 1);
+  if (rc) return rc;
+  return probe_take();
 }
 
 int launch_topk(ppr_plan* p, int sA, int sB) {
@@ -2878,6 +2914,7 @@ extern "C" const char* ppr_strerror(int code) {
     case PPR_ERR_OOM: return "device out of memory";
     case PPR_ERR_RANGE: return "parameter outside the supported range";
     case PPR_ERR_SOURCE: return "source node not part of the graph";
+    case PPR_ERR_PROBE: return "a hash table ran out of slots (table sizing error)";
     default: return "unknown error";
   }
 }

@@ -209,7 +209,23 @@ extern "C" int ppr_mccp2_plan_combine(ppr_plan* p) {
     p->merge_ms += ms;
   }
   // final keepTop(K) (:252-256): prefix of every row in slot 0
-  return launch_topk(p, 0, 0);
+  {
+    const int rc = launch_topk(p, 0, 0);
+    if (rc) return rc;
+  }
+  // bounded probes: the combine's merge kernels (grank.hip's word) and the walks (this module's)
+  {
+    const int rc = probe_take();
+    if (rc) return rc;
+  }
+  unsigned int v = 0u;
+  HIP_OK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_probe_err), sizeof(v), 0, hipMemcpyDeviceToHost));
+  if (v) {
+    const unsigned int z = 0u;
+    HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_probe_err), &z, sizeof(z), 0, hipMemcpyHostToDevice));
+    return PPR_ERR_PROBE;
+  }
+  return PPR_OK;
 }
 
 extern "C" int ppr_mccp2_plan_run(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_stats* st) {

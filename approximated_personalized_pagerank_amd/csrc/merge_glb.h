@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArg
 
   auto slot_of = [&](int key) -> uint64_t {
     uint64_t h = hash32((uint32_t)key) & mask;
-    for (;;) {
+    for (uint64_t n = 0; n <= mask; n++) {
       const int prev = atomicCAS(&keys[h], EMPTY, key);
       if (prev == EMPTY) {
         __hip_atomic_store(&acc[h], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -89,6 +89,8 @@ __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArg
       if (prev == key) return h;
       h = (h + 1) & mask;
     }
+    probe_fail();  // (>= 2 x candidates slots: cannot happen)
+    return (uint64_t)0;
   };
   if (lane_id() == 0) {
     const uint64_t h = slot_of(v);

@@ -406,7 +406,7 @@ struct BucketWave {
       // really pass its budget -- not whenever it holds more than budget - 64 keys
       const int maybe_new = __popcll(__ballot(cv[k] && c0[k] != kk[k]));
       if (fill + maybe_new > budget) overflow = true;
-      bool ins = false;
+      bool ins = false, lost = false;
       uint32_t h = 0;
       if (cv[k] && !overflow) {
         h = h0[k];
@@ -419,9 +419,11 @@ struct BucketWave {
             if (prev == kk[k]) break;
           }
           h = (h + 1 == (uint32_t)T) ? 0u : h + 1;
-          c = t.keys[h];
+          if (h == h0[k]) { lost = true; break; }  // (bounded: back at the start, the table is full --
+          c = t.keys[h];                            // the bucket spills like one past its budget)
         }
       }
+      if (__ballot(lost)) overflow = true;
       sl[k] = h;
       fill += __popcll(__ballot(ins));
       wave_fence();
@@ -579,14 +581,16 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     if (nt + maybe_new > budget) return false;
     uint32_t h = sl[k], o = 0;
     bool fresh = false;
+    bool lost = false;
     if (v) {
       unsigned long long w = c0[k];
-      for (;;) {
+      lost = true;  // (bounded probe: a full table fails the pass, the caller takes more passes)
+      for (int n = 0; n < 2 * T; n++) {
         const uint32_t wk = (uint32_t)w;
-        if (wk == (uint32_t)kk[k]) { o = (uint32_t)(atomicAdd(&word[h], ONE) >> 32) & 0xffffu; break; }
+        if (wk == (uint32_t)kk[k]) { o = (uint32_t)(atomicAdd(&word[h], ONE) >> 32) & 0xffffu; lost = false; break; }
         if (wk == 0xffffffffu) {
           const unsigned long long prev = atomicCAS(&word[h], EMPTYW, ONE | (uint32_t)kk[k]);
-          if (prev == EMPTYW) { fresh = true; break; }  // occurrence 0
+          if (prev == EMPTYW) { fresh = true; lost = false; break; }  // occurrence 0
           w = prev;  // taken meanwhile (a lower lane or an earlier group): test the same slot again
           continue;
         }
@@ -594,6 +598,7 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
         w = word[h];
       }
     }
+    if (__ballot(lost)) return false;
     sl[k] = h;
     occ[k] = o;
     const uint64_t fm = __ballot(fresh);

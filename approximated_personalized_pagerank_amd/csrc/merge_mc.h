@@ -73,12 +73,15 @@ struct McTable {
 
 __device__ __forceinline__ uint32_t mc_find(const McTable& t, int key, bool& present) {
   uint32_t h = hash32((uint32_t)key) & t.mask;
-  for (;;) {
+  for (uint32_t n = 0; n <= t.mask; n++) {
     const int k = t.keys[h];
     if (k == key) { present = true; return h; }
     if (k == EMPTY) { present = false; return h; }
     h = (h + 1) & t.mask;
   }
+  probe_fail();  // (the walk table holds at most L + 64 keys of its 2^k >= 2 (L + 64) slots)
+  present = true;
+  return 0u;
 }
 
 // lanes of `valid` holding the same slot (ballots over the slot bits)
@@ -101,12 +104,14 @@ __device__ __forceinline__ uint32_t mc_apply(const McTable& t, bool valid, int k
   const bool absent = valid && !present;
   if (!frozen && __ballot(absent)) {
     if (absent) {
-      for (;;) {
+      bool done = false;
+      for (uint32_t n = 0; n <= t.mask && !done; n++) {
         const int prev = atomicCAS(&t.keys[h], EMPTY, key);
-        if (prev == EMPTY) { t.cnt[h] = 0ull; t.rr[h] = 0u; break; }
-        if (prev == key) break;
-        h = (h + 1) & t.mask;
+        if (prev == EMPTY) { t.cnt[h] = 0ull; t.rr[h] = 0u; done = true; }
+        else if (prev == key) done = true;
+        else h = (h + 1) & t.mask;
       }
+      if (!done) { probe_fail(); h = 0u; }
     }
     wave_fence();
     // lanes holding the same new key share a slot: the lowest lane is its first occurrence

@@ -72,13 +72,20 @@ struct XTable {
 };
 
 // find-or-insert `key`, then add X: the low word's returning add yields its carry, which goes
-// with the high word into hi. Returns true when this lane inserted the key.
-__device__ __forceinline__ bool xt_add(const XTable& t, int key, unsigned long long xlo, uint32_t xhi) {
+// with the high word into hi. Returns 1 when this lane inserted the key, 0 when it was there, -1
+// when the probe ran out (T/4 groups visited or T/4 insert races lost: the table is full) -- no
+// add then, and the caller takes its overflow path. Every caller sizes or budgets its table so
+// that this cannot happen; the bound turns a sizing bug into a redone source instead of a hang
+// (tests: PPR_WAVE_TDIV, PPR_XR_BUDGET=over force it).
+__device__ __forceinline__ int xt_add(const XTable& t, int key, unsigned long long xlo, uint32_t xhi) {
   const uint32_t tag = (uint32_t)key + 1u;
   uint32_t g = hash32((uint32_t)key) & t.mask & ~3u;
-  bool ins = false;
-  uint32_t h;
+  int ins = 0;
+  uint32_t h = 0;
+  const uint32_t groups = (t.mask + 1u) >> 2;
+  uint32_t moves = 0, races = 0;
   for (;;) {
+    if (moves >= groups || races > groups) return -1;
     const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g);
     if (q.x == tag) { h = g; break; }
     if (q.y == tag) { h = g + 1; break; }
@@ -87,11 +94,13 @@ __device__ __forceinline__ bool xt_add(const XTable& t, int key, unsigned long l
     const int e = q.x == 0u ? 0 : q.y == 0u ? 1 : q.z == 0u ? 2 : q.w == 0u ? 3 : -1;
     if (e >= 0) {
       const uint32_t prev = atomicCAS(&t.keys[g + e], 0u, tag);
-      if (prev == 0u) { h = g + e; ins = true; break; }
+      if (prev == 0u) { h = g + e; ins = 1; break; }
       if (prev == tag) { h = g + e; break; }
+      races++;
       continue;  // another key took it: read the group again
     }
     g = (g + 4u) & t.mask;
+    moves++;
   }
   const unsigned long long old = atomicAdd(&t.lo[h], xlo);
   const uint32_t up = xhi + ((old + xlo < old) ? 1u : 0u);
@@ -103,24 +112,30 @@ __device__ __forceinline__ bool xt_add(const XTable& t, int key, unsigned long l
 __device__ __forceinline__ int xt_match(const uint4& q, uint32_t g, uint32_t tag) {
   return q.x == tag ? (int)g : q.y == tag ? (int)g + 1 : q.z == tag ? (int)g + 2 : q.w == tag ? (int)g + 3 : -1;
 }
-// find-or-insert only (xt_add's probe loop); returns the slot, `ins` when this lane inserted
-__device__ __forceinline__ uint32_t xt_slot(const XTable& t, int key, bool& ins) {
+// find-or-insert only (xt_add's bounded probe); returns the slot, `ins` when this lane inserted,
+// -1 when the table is full
+__device__ __forceinline__ int xt_slot(const XTable& t, int key, bool& ins) {
   const uint32_t tag = (uint32_t)key + 1u;
   uint32_t g = hash32((uint32_t)key) & t.mask & ~3u;
   ins = false;
-  for (;;) {
+  const uint32_t groups = (t.mask + 1u) >> 2;
+  uint32_t moves = 0, races = 0;
+  while (moves < groups && races <= groups) {
     const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g);
     const int m = xt_match(q, g, tag);
-    if (m >= 0) return (uint32_t)m;
+    if (m >= 0) return m;
     const int e = q.x == 0u ? 0 : q.y == 0u ? 1 : q.z == 0u ? 2 : q.w == 0u ? 3 : -1;
     if (e >= 0) {
       const uint32_t prev = atomicCAS(&t.keys[g + e], 0u, tag);
-      if (prev == 0u) { ins = true; return g + e; }
-      if (prev == tag) return g + e;
+      if (prev == 0u) { ins = true; return (int)(g + e); }
+      if (prev == tag) return (int)(g + e);
+      races++;
       continue;
     }
     g = (g + 4u) & t.mask;
+    moves++;
   }
+  return -1;
 }
 
 __host__ __device__ constexpr size_t xt_bytes(int T) { return (size_t)T * 16; }
@@ -141,9 +156,12 @@ __host__ __device__ constexpr size_t lds_wave_bytes_x(int T, int Lp) {
   return (size_t)T * 16 + (size_t)Lp * 12 + 1024 + (size_t)Lp * 20;
 }
 
+// (a table that runs out -- never, at T >= 4/3 of the tier's candidate cap, unless PPR_WAVE_TDIV
+// shrinks it for the tests -- writes no row: the source goes to `wovl` ([0] count, then sources)
+// and the host merges it again with the workgroup engines)
 __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, IterArgs a, const int32_t* list,
                                                      int64_t count, int T, int Lp, unsigned long long* maxdiff,
-                                                     unsigned long long* stats, int32_t* dlast) {
+                                                     unsigned long long* stats, int32_t* dlast, int32_t* wovl) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
@@ -163,11 +181,12 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   long long tl = a.diag ? (long long)clock64() : 0;  // PPR_DIAG: wave-tier phases, slots 280..287
   for (int i = lane_id(); i < T; i += WAVE) { t.keys[i] = 0u; t.lo[i] = 0ull; t.hi[i] = 0u; }
   wave_fence();
+  bool bad = false;
   if (lane_id() == 0) {
     unsigned long long lo;
     uint32_t hi;
     xs_conv(self_seed(a, e - b), lo, hi);
-    xt_add(t, v, lo, hi);
+    bad = xt_add(t, v, lo, hi) < 0;
   }
   wave_fence();
   unsigned long long mb = 0;
@@ -177,7 +196,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
     xs_conv(factor, flo, fhi);  // init: every successor contributes 1.0 * d/deg
     for (int64_t e0 = b; e0 < e; e0 += WAVE) {
       const int64_t i = e0 + lane_id();
-      if (i < e) xt_add(t, g.colx[i] & 0x7fffffff, flo, fhi);
+      if (i < e && xt_add(t, g.colx[i] & 0x7fffffff, flo, fhi) < 0) bad = true;
     }
   } else {
     for (int64_t e0 = b; e0 < e; e0 += WAVE)
@@ -187,12 +206,16 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
                           unsigned long long lo;
                           uint32_t hi;
                           xs_conv(sv * factor, lo, hi);
-                          xt_add(t, id, lo, hi);
+                          if (xt_add(t, id, lo, hi) < 0) bad = true;
                         }
                       },
                       WalkRowMin{&mb, (int)s.L});
   }
   wave_fence();
+  if (__ballot(bad)) {  // table ran out: no row, the host redoes the source
+    if (lane_id() == 0) wovl[1 + atomicAdd(&wovl[0], 1)] = v;
+    return;
+  }
   fs_lap(a, 280, 1, tl);  // (slot 281: setup + walk)
 #pragma unroll
   for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
@@ -307,15 +330,18 @@ __device__ __forceinline__ void xr_clear(const XrLds& x, int T) {
 
 // one accumulated contribution of the calling lane (valid lanes only); a group's new keys are
 // counted by its wave's lowest lane (the workgroup's distinct-key budget, xr_stop)
+// a probe that ran out of slots: the fill count jumps past any budget, so the workgroup stops and
+// the source takes the overflow redo
+constexpr int XR_FULL = 1 << 24;
 __device__ __forceinline__ void xr_apply(const XrLds& x, bool valid, int key, double p, int budget) {
-  bool ins = false;
+  int r = 0;
   if (valid) {
     unsigned long long lo;
     uint32_t hi;
     xs_conv(p, lo, hi);
-    ins = xt_add(x.t, key, lo, hi);
+    r = xt_add(x.t, key, lo, hi);
   }
-  const int n = __popcll(__ballot(ins));
+  const int n = __popcll(__ballot(r > 0)) + (__ballot(r < 0) ? XR_FULL : 0);
   if (n && lane_id() == 0) atomicAdd(&x.w.misc[XM_FILL], n);  // (no return: xr_stop reads the count)
 }
 // every wave checks the shared count before each group: once it passes the budget no wave starts
@@ -650,8 +676,10 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
           if (h[k] < 0) v[k] = false;
         } else {
           bool ins = false;
-          if (v[k] && h[k] < 0) h[k] = (int)xt_slot(x.t, key[k], ins);
-          const int nins = __popcll(__ballot(ins));
+          if (v[k] && h[k] < 0) h[k] = xt_slot(x.t, key[k], ins);
+          const bool full = v[k] && h[k] < 0;  // (the probe ran out: overflow redo)
+          if (full) v[k] = false;
+          const int nins = __popcll(__ballot(ins)) + (__ballot(full) ? XR_FULL : 0);
           if (nins && lane_id() == 0) atomicAdd(&x.w.misc[XM_FILL], nins);
         }
       }
@@ -698,8 +726,8 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
   }
   // the hot key's register sums (a lane's sum stays below the key's total < 2^95): once per lane
   if (hk >= 0 && (hlo | hhi)) {
-    const bool ins = xt_add(x.t, hk, hlo, hhi);
-    if (ins) atomicAdd(&x.w.misc[XM_FILL], 1);
+    const int r = xt_add(x.t, hk, hlo, hhi);
+    if (r) atomicAdd(&x.w.misc[XM_FILL], r > 0 ? 1 : XR_FULL);
   }
   __syncthreads();
   xr_lap(a, 155, tph);

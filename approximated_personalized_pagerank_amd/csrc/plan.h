@@ -209,6 +209,12 @@ struct ppr_plan {
   unsigned char* d_xg = nullptr;      // table | dense list | state | histogram
   size_t xg_bytes = 0;
   int64_t xg_sources = 0;             // sources merged there (PPR_TIMING at destroy)
+  // bounded probes (tests force them to run out): exact wave-tier overflow list and knobs
+  int32_t* d_wovl = nullptr;          // [1 + n]: count, sources whose wave-tier table ran out
+  bool wave_x_launched = false;
+  int wave_tdiv = 0;                  // PPR_WAVE_TDIV (tests): wave-tier tables T >> this
+  bool xr_budget_over = false;        // PPR_XR_BUDGET=over (tests): range / bucket tables fill up
+  int64_t wave_redo = 0;              // wave-tier sources redone (PPR_TIMING at destroy)
   int xg_cap = 1 << 16;               // dense list of the selection (PPR_XG_CAP, tests: L <= cap <= XG_CAP)
   // sieve merge of the wide exact-sum sources (merge_sv.h): PPR_SV=0 turns it off
   bool sv_enabled = false;
@@ -275,6 +281,7 @@ inline void plan_free(ppr_plan* p) {
   if (p->h_xs_pin) hipHostFree(p->h_xs_pin);
   hipFree(p->d_sv);
   hipFree(p->d_xg);
+  hipFree(p->d_wovl);
   if (p->h_sv_pin) hipHostFree(p->h_sv_pin);
   if (p->ev_sv) hipEventDestroy(p->ev_sv);
   if (getenv("PPR_TIMING") && p->sv_sources)
@@ -285,6 +292,8 @@ inline void plan_free(ppr_plan* p) {
             p->xh_s[5], p->xh_s[6]);
   if (getenv("PPR_TIMING") && p->xr_redo)
     fprintf(stderr, "ppr_timing xr_redo_sources %lld\n", (long long)p->xr_redo);
+  if (getenv("PPR_TIMING") && p->wave_redo)
+    fprintf(stderr, "ppr_timing wave_redo_sources %lld\n", (long long)p->wave_redo);
   if (getenv("PPR_TIMING") && p->xg_sources)
     fprintf(stderr, "ppr_timing hbm_table_sources %lld\n", (long long)p->xg_sources);
   if (getenv("PPR_TIMING") && p->spec_redo)
@@ -430,5 +439,6 @@ int launch_topk(ppr_plan* p, int sA, int sB);
 // classify + every merge tier for `count` sources of the device list `list`
 // MC combine: read and redo the last level's deferred hub overflow list (host sync)
 int run_merge_flush(ppr_plan* p, const IterArgs& a, unsigned long long* maxdiff);
+int probe_take();  // grank.hip: PPR_ERR_PROBE when one of its kernels' bounded probes ran out
 int run_merge(ppr_plan* p, const IterArgs& a, const int32_t* list, int64_t count,
               unsigned long long* maxdiff);

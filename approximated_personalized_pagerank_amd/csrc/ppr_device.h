@@ -33,6 +33,13 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 __device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
 __device__ __forceinline__ double bitsd(uint64_t x) { return __longlong_as_double((long long)x); }
 
+// A hash probe that ran out of slots (every table is sized or budgeted so that this cannot happen;
+// a bounded probe turns a sizing bug into an error instead of a hang): each module's kernels set
+// its word, the host reads it once per run and fails the run with PPR_ERR_PROBE. Engines with an
+// overflow path (the exact-sum tables, the workgroup / bucket tables) take that path instead.
+static __device__ unsigned int g_probe_err = 0u;
+__device__ __forceinline__ void probe_fail() { atomicOr(&g_probe_err, 1u); }
+
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
@@ -98,7 +105,7 @@ __device__ __forceinline__ void table_clear(const LdsTable& t) {
 // find-or-insert; an inserting lane zeroes the accumulator (reference: operator[] value-inits)
 __device__ __forceinline__ uint32_t table_slot(const LdsTable& t, int key) {
   uint32_t h = hash32((uint32_t)key) & t.mask;
-  for (;;) {
+  for (uint32_t n = 0; n <= t.mask; n++) {
     const int cur = t.keys[h];
     if (cur == key) return h;
     if (cur == EMPTY) {
@@ -108,6 +115,8 @@ __device__ __forceinline__ uint32_t table_slot(const LdsTable& t, int key) {
     }
     h = (h + 1) & t.mask;
   }
+  probe_fail();  // (T >= 4/3 of the tier's candidate cap: cannot happen; PPR_WAVE_TDIV forces it)
+  return 0u;
 }
 
 __device__ __forceinline__ double readlane_d(double x, int lane) {
@@ -514,11 +523,13 @@ __device__ __forceinline__ double row_norm1(const uint64_t* rv, const int* rk, i
   for (int j = lane_id(); j < olen; j += WAVE) {
     const int key = dec(oid[j]);  // the old row's stored id -> key
     uint32_t h = hash32((uint32_t)key) & hmask;
-    for (;;) {
+    bool done = false;
+    for (uint32_t n = 0; n <= hmask && !done; n++) {  // (2 Lp slots for <= L keys: never full)
       const int prev = atomicCAS(&hk[h], EMPTY, key);
-      if (prev == EMPTY) { hv[h] = j; break; }
+      if (prev == EMPTY) { hv[h] = j; done = true; }
       h = (h + 1) & hmask;
     }
+    if (!done) probe_fail();
   }
   wave_fence();
   double p = 0.0;
@@ -526,7 +537,7 @@ __device__ __forceinline__ double row_norm1(const uint64_t* rv, const int* rk, i
     const int key = rk[i];
     uint32_t h = hash32((uint32_t)key) & hmask;
     double o = 0.0;
-    for (;;) {
+    for (uint32_t n = 0; n <= hmask; n++) {
       const int cur = hk[h];
       if (cur == key) { const int j = hv[h]; o = osc[j]; mf[j] = 1; break; }
       if (cur == EMPTY) break;

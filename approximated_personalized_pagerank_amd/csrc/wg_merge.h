@@ -27,7 +27,7 @@ constexpr int WG_WIN = WG_THREADS;               // successors per window
 __device__ __forceinline__ uint32_t wg_slot(int* keys, double* acc, uint32_t T, uint32_t h0,
                                             int key, uint32_t* fill, uint32_t budget) {
   uint32_t h = h0;
-  for (;;) {
+  for (uint32_t n = 0; n < T; n++) {
     const int cur = keys[h];
     if (cur == key) return h;
     if (cur == EMPTY) {
@@ -38,6 +38,7 @@ __device__ __forceinline__ uint32_t wg_slot(int* keys, double* acc, uint32_t T, 
     }
     h = (h + 1 == T) ? 0 : h + 1;
   }
+  return 0xffffffffu;  // (full: the caller's overflow pass)
 }
 
 struct WgLds {

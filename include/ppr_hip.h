@@ -38,7 +38,9 @@ enum {
   PPR_ERR_HIP = 9,       /* HIP runtime failure (no device, launch failure, ...) */
   PPR_ERR_OOM = 10,      /* device allocation failed */
   PPR_ERR_RANGE = 11,    /* L / K / node count beyond what the kernels support */
-  PPR_ERR_SOURCE = 12    /* "source node not part of the graph" include/internal/pprSingleSource.h:39 */
+  PPR_ERR_SOURCE = 12,   /* "source node not part of the graph" include/internal/pprSingleSource.h:39 */
+  PPR_ERR_PROBE = 13     /* a bounded hash probe ran out of slots: a table sizing error (never on a
+                            correct build; the exact-sum engines redo such a source instead) */
 };
 
 /* graph in dense CSR form (borrowed; host memory unless a *_dev entry point says otherwise) */

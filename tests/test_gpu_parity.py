@@ -378,3 +378,44 @@ def test_gpu_hbm_table_fallback_bit_exact(henv, monkeypatch, capfd):
     err = capfd.readouterr().err
     n = sum(int(x.split()[2]) for x in err.splitlines() if x.startswith("ppr_timing hbm_table_sources"))
     assert n > 0
+
+
+@pytest.mark.parametrize("benv,what", [
+    ({"PPR_WAVE_TDIV": "3"}, "wave_redo_sources"),   # wave-tier tables at 1/8 size: their bounded
+                                                     # probes run out, the sources are redone
+    ({"PPR_XR_BUDGET": "over"}, "xr_redo_sources"),  # range / bucket tables without a budget stop:
+                                                     # they fill, the probes run out, overflow redo
+    ({"PPR_XR_BUDGET": "over", "PPR_SV": "0", "PPR_TIER_MASK": "0x20"}, "xr_redo_sources"),
+])
+def test_gpu_bounded_probes_exhausted_exact(benv, what, monkeypatch, capfd):
+    """every LDS hash probe is bounded (ADVICE/VERDICT r3): forced to run out, the exact-sum engines
+    redo the source and the result stays bit-exact (no hang, no lost contribution)"""
+    for k, v in benv.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("PPR_TIMING", "1")
+    for scale, K, L, it in [(11, 16, 32, 5), (12, 32, 128, 4)]:
+        g = ppr.rmat(scale, seed=391 + scale)
+        part = g.partitions()
+        r = ppr.grank_csr(g, K, L, it, 0.85, -1.0, part=part, device=0)
+        o = oracle.grank(g.row_ptr, g.col, part, K, L, it, 0.85, -1.0)
+        assert np.array_equal(r.max_diff, o["max_diff"])
+        assert np.array_equal(r.lens, o["lens"])
+        assert np.array_equal(r.ids, o["ids"])
+        assert np.array_equal(r.scores, o["scores"])
+    err = capfd.readouterr().err
+    n = sum(int(x.split()[2]) for x in err.splitlines() if x.startswith("ppr_timing " + what))
+    assert n > 0
+
+
+def test_gpu_bounded_probes_exhausted_chain_fails_loudly(monkeypatch, chain_sum):
+    """the chain-order wave tier has no redo path: a table forced too small (PPR_WAVE_TDIV) must end
+    the run with PPR_ERR_PROBE -- not hang, not return rows -- and leave the library usable"""
+    monkeypatch.setenv("PPR_WAVE_TDIV", "4")
+    g = ppr.rmat(11, seed=5)
+    part = g.partitions()
+    with pytest.raises(ppr.PprError, match="ran out of slots"):
+        ppr.grank_csr(g, 16, 64, 3, 0.85, -1.0, part=part, device=0)
+    monkeypatch.delenv("PPR_WAVE_TDIV")
+    r = ppr.grank_csr(g, 16, 64, 3, 0.85, -1.0, part=part, device=0)
+    o = oracle.grank(g.row_ptr, g.col, part, 16, 64, 3, 0.85, -1.0)
+    assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])
