@@ -287,6 +287,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     if (ent) p->nt_loads = (int)strtol(ent, nullptr, 0) & 3;
     const char* ewi = getenv("PPR_WHATIF");
     if (ewi) p->whatif = (int)strtol(ewi, nullptr, 0);
+    const char* ebd = getenv("PPR_WAVE_BY_D");  // exact sum: wave tiers sized by the last distinct-key count
+    if (ebd) p->wave_by_d = atoi(ebd) != 0;
     const char* etd = getenv("PPR_WAVE_TDIV");  // tests: wave-tier tables T >> this (bounded probes run out)
     if (etd) p->wave_tdiv = std::max(0, std::min(6, atoi(etd)));
     const char* exr = getenv("PPR_XROUTE");
@@ -1899,13 +1901,15 @@ reclassify:
   const int64_t cls_pb = (int64_t)cls_pw * WAVES_PER_BLOCK;
   const int64_t nb = (count + cls_pb - 1) / cls_pb;
   hipLaunchKernelGGL(k_classify, dim3((unsigned)nb), dim3(256), 0, st, g, s, a, list, count,
-                     p->d_tier_cap, p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big, cls_pw);
+                     p->d_tier_cap, p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big, cls_pw,
+                     (p->wave_by_d && a.xs && !a.unit && !a.mc) ? (const int32_t*)p->d_dlast : nullptr);
   HIP_OK(hipGetLastError());
   if (!a.unit && p->max_deg > CLS_BIG_DEG) {
     // grid-stride over the long-list sources, at most one block per listed source
     hipLaunchKernelGGL(k_classify_big, dim3((unsigned)std::min<int64_t>(256, count)), dim3(CLS_BIG_THREADS), 0, st, g,
                        s, a, p->d_tier_cap,
-                       p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big);
+                       p->d_tier_lists, p->d_tier_cnt, p->n, p->d_cand, p->d_stats, p->d_big,
+                       (p->wave_by_d && a.xs && !a.unit && !a.mc) ? (const int32_t*)p->d_dlast : nullptr);
   }
   HIP_OK(hipGetLastError());
   uint32_t cnt[NLISTS + 1];

@@ -10,9 +10,11 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <chrono>
 #include <vector>
 
 #include "../../include/ppr_hip.h"
@@ -67,48 +69,22 @@ int ppr_find_partitions_csr(const ppr_csr* g, uint8_t* part) {
   const int64_t m = rp[n];
   const int nth = host_threads();
   std::atomic<bool> bad(false);
-  // predecessor lists: per-thread destination counts over contiguous source ranges, then each
-  // thread fills its own offsets (no atomics; lists end up in source order)
-  const int tt = (int64_t)n * nth * 4 <= (int64_t)512 << 20 ? nth : 1;
-  std::vector<std::vector<int32_t>> cnt(tt);
-  std::vector<int64_t> prp(n + 1, 0);
-  parallel_for(n, tt, [&](int64_t b, int64_t e, int t) {
-    std::vector<int32_t>& c = cnt[t];
-    c.assign(n, 0);
-    for (int64_t v = b; v < e; v++)
-      for (int64_t k = rp[v]; k < rp[v + 1]; k++) {
-        const int32_t s = col[k];
-        if (s < 0 || s >= n) { bad = true; return; }
-        c[s]++;
-      }
+  const bool tm = getenv("PPR_TIMING") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!tm) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    fprintf(stderr, "ppr_timing partitions %s %.4f\n", what, std::chrono::duration<double>(t1 - t0).count());
+    t0 = t1;
+  };
+  // (successor ids checked here; no predecessor lists are built: the union-find needs none, and the
+  // BFS below finds a node's predecessors in the frontier from its own successor list)
+  parallel_for(n, nth, [&](int64_t b, int64_t e, int) {
+    for (int64_t k = rp[b]; k < rp[e]; k++)
+      if (col[k] < 0 || col[k] >= n) { bad = true; return; }
   });
   if (bad) return PPR_ERR_GRAPH;
-  parallel_for(n, nth, [&](int64_t b, int64_t e, int) {
-    for (int64_t s = b; s < e; s++) {
-      int64_t x = 0;
-      for (int t = 0; t < tt; t++) x += cnt[t].empty() ? 0 : cnt[t][s];
-      prp[s + 1] = x;
-    }
-  });
-  for (int64_t i = 0; i < n; i++) prp[i + 1] += prp[i];
-  parallel_for(n, nth, [&](int64_t b, int64_t e, int) {  // counts -> each thread's write offsets
-    for (int64_t s = b; s < e; s++) {
-      int64_t o = prp[s];
-      for (int t = 0; t < tt; t++) {
-        if (cnt[t].empty()) continue;
-        const int32_t c = cnt[t][s];
-        cnt[t][s] = (int32_t)(o - prp[s]);
-        o += c;
-      }
-    }
-  });
-  std::vector<int32_t> pcol(m > 0 ? m : 1);
-  parallel_for(n, tt, [&](int64_t b, int64_t e, int t) {
-    std::vector<int32_t>& c = cnt[t];
-    for (int64_t v = b; v < e; v++)
-      for (int64_t k = rp[v]; k < rp[v + 1]; k++) pcol[prp[col[k]] + c[col[k]]++] = (int32_t)v;
-  });
-  cnt.clear();
+  lap("check");
   // weakly connected components, representative = smallest id (lock-free union by index)
   std::vector<int32_t> parent(n);
   for (int64_t v = 0; v < n; v++) parent[v] = (int32_t)v;
@@ -136,34 +112,68 @@ int ppr_find_partitions_csr(const ppr_csr* g, uint8_t* part) {
         }
       }
   });
-  // multi-source BFS from every component's smallest node
+  lap("union_find");
+  // multi-source BFS from every component's smallest node over the undirected graph, with out-edges
+  // only: a level joins (a) the unvisited successors of the frontier (top-down, CAS) and then (b)
+  // every unvisited node with a successor in the frontier (a predecessor of it: bottom-up over the
+  // shrinking list of unvisited nodes, stopping at the first hit). Depths are the shortest
+  // undirected distances either way; no predecessor lists (a transpose cost more than this).
   std::vector<int32_t> depth(n, -1);
-  std::vector<int32_t> front;
+  std::vector<int32_t> front, rest;
   for (int64_t v = 0; v < n; v++)
     if (find((int32_t)v) == (int32_t)v) { depth[v] = 0; front.push_back((int32_t)v); }
-  std::vector<std::vector<int32_t>> next(nth);
+  {
+    std::vector<std::vector<int32_t>> part_rest(nth);
+    parallel_for(n, nth, [&](int64_t b, int64_t e, int t) {
+      for (int64_t v = b; v < e; v++)
+        if (depth[v] == -1) part_rest[t].push_back((int32_t)v);
+    });
+    for (auto& x : part_rest) rest.insert(rest.end(), x.begin(), x.end());
+  }
+  std::vector<std::vector<int32_t>> next(nth), keep(nth);
   for (int32_t d = 0; !front.empty(); d++) {
     for (auto& x : next) x.clear();
     parallel_for((int64_t)front.size(), nth, [&](int64_t b, int64_t e, int t) {
       std::vector<int32_t>& out = next[t];
-      auto visit = [&](int32_t s) {
-        int32_t expect = -1;
-        if (__atomic_load_n(&depth[s], __ATOMIC_RELAXED) == -1 &&
-            __atomic_compare_exchange_n(&depth[s], &expect, d + 1, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED))
-          out.push_back(s);
-      };
       for (int64_t i = b; i < e; i++) {
         const int32_t x = front[i];
-        for (int64_t k = rp[x]; k < rp[x + 1]; k++) visit(col[k]);
-        for (int64_t k = prp[x]; k < prp[x + 1]; k++) visit(pcol[k]);
+        for (int64_t k = rp[x]; k < rp[x + 1]; k++) {
+          const int32_t s = col[k];
+          int32_t expect = -1;
+          if (__atomic_load_n(&depth[s], __ATOMIC_RELAXED) == -1 &&
+              __atomic_compare_exchange_n(&depth[s], &expect, d + 1, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED))
+            out.push_back(s);
+        }
       }
     });
+    // bottom-up: the still unvisited nodes with a successor at depth d (their writes go to their
+    // own entry only, after which they are at d + 1, never d)
+    for (auto& x : keep) x.clear();
+    parallel_for((int64_t)rest.size(), nth, [&](int64_t b, int64_t e, int t) {
+      std::vector<int32_t>& out = next[t];
+      std::vector<int32_t>& kp = keep[t];
+      for (int64_t i = b; i < e; i++) {
+        const int32_t v = rest[i];
+        if (__atomic_load_n(&depth[v], __ATOMIC_RELAXED) != -1) continue;  // (joined top-down)
+        bool hit = false;
+        for (int64_t k = rp[v]; k < rp[v + 1] && !hit; k++) hit = __atomic_load_n(&depth[col[k]], __ATOMIC_RELAXED) == d;
+        if (hit) {
+          __atomic_store_n(&depth[v], d + 1, __ATOMIC_RELAXED);
+          out.push_back(v);
+        } else {
+          kp.push_back(v);
+        }
+      }
+    });
+    rest.clear();
+    for (auto& x : keep) rest.insert(rest.end(), x.begin(), x.end());
     front.clear();
     for (auto& x : next) front.insert(front.end(), x.begin(), x.end());
   }
   parallel_for(n, nth, [&](int64_t b, int64_t e, int) {
     for (int64_t v = b; v < e; v++) part[v] = (uint8_t)(depth[v] & 1);
   });
+  lap("bfs");
   return PPR_OK;
 }
 

@@ -22,6 +22,15 @@ inline void parallel_for(int64_t n, int nthreads, F f) {
   for (auto& t : th) t.join();
 }
 
+// one thread per task index 0..k-1 (for a few coarse tasks, which parallel_for would run serially)
+template <class F>
+inline void parallel_tasks(int k, F f) {
+  std::vector<std::thread> th;
+  for (int t = 1; t < k; t++) th.emplace_back(f, t);
+  if (k > 0) f(0);
+  for (auto& t : th) t.join();
+}
+
 inline int hw_threads() {
   unsigned h = std::thread::hardware_concurrency();
   if (h == 0) h = 1;

@@ -43,12 +43,24 @@ __device__ __forceinline__ long long succ_len_sum(const DevGraph& g, const DevSl
   return c;
 }
 
+// Tier rule: the candidates + 1 bound a source's distinct keys, so a table of 4/3 of them never
+// fills. With `dlast` (exact sum, PPR_WAVE_BY_D) a source is sized by its last merge's distinct keys
+// + 1/8 + 64 instead, when that is smaller: a table that still runs out sends the source to the
+// overflow redo (k_merge_lds_x's bounded probes).
+__device__ __forceinline__ int64_t tier_need(int64_t need, const int32_t* dlast, int v) {
+  if (!dlast) return need;
+  const int64_t d = dlast[v];
+  if (d <= 0) return need;
+  const int64_t e = d + d / 8 + 64;
+  return e < need ? e : need;
+}
+
 __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArgs a,
                                                   const int32_t* list, int64_t count,
                                                   const int32_t* tier_cap, int32_t* tier_lists,
                                                   uint32_t* tier_cnt, int64_t list_cap,
                                                   int32_t* cand, unsigned long long* stats,
-                                                  int32_t* big_list, int per_wave) {
+                                                  int32_t* big_list, int per_wave, const int32_t* dlast) {
   // per_wave sources per wave (CLS_PER_WAVE, or 1 for a short list), per_block per block
   const int per_block = per_wave * WAVES_PER_BLOCK;
   __shared__ int s_tier[CLS_PER_BLOCK];
@@ -83,7 +95,8 @@ __global__ void __launch_bounds__(256) k_classify(DevGraph g, DevSlab s, IterArg
       const int64_t need = c + 1;
       cand[v] = (int32_t)(need > 0x7fffffff ? 0x7fffffff : need);
       int t = 0;
-      while (t < NT + 1 && need > tier_cap[t]) t++;
+      const int64_t tneed = tier_need(need, dlast, v);
+      while (t < NT + 1 && tneed > tier_cap[t]) t++;
       s_tier[slot] = t;
       s_src[slot] = v;
       const int ownlen = (a.unit || a.mc) ? 0 : s.len[s.lrow(a.active == 0 ? a.sA : a.sB, v)];
@@ -123,7 +136,7 @@ __global__ void __launch_bounds__(CLS_BIG_THREADS) k_classify_big(DevGraph g, De
                                                                   const int32_t* tier_cap, int32_t* tier_lists,
                                                                   uint32_t* tier_cnt, int64_t list_cap,
                                                                   int32_t* cand, unsigned long long* stats,
-                                                                  const int32_t* big_list) {
+                                                                  const int32_t* big_list, const int32_t* dlast) {
   __shared__ long long red[CLS_BIG_THREADS / WAVE];
   const uint32_t nbig = __hip_atomic_load(&tier_cnt[NLISTS + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (uint32_t i = blockIdx.x; i < nbig; i += gridDim.x) {
@@ -140,7 +153,8 @@ __global__ void __launch_bounds__(CLS_BIG_THREADS) k_classify_big(DevGraph g, De
       const int64_t need = c + 1;
       cand[v] = (int32_t)(need > 0x7fffffff ? 0x7fffffff : need);
       int t = 0;
-      while (t < NT + 1 && need > tier_cap[t]) t++;
+      const int64_t tneed = tier_need(need, dlast, v);
+      while (t < NT + 1 && tneed > tier_cap[t]) t++;
       tier_lists[(int64_t)t * list_cap + atomicAdd(&tier_cnt[t], 1u)] = v;
       if (a.stats) {
         const int ownlen = a.mc ? 0 : s.len[s.lrow(a.active == 0 ? a.sA : a.sB, v)];

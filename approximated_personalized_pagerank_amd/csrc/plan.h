@@ -213,6 +213,7 @@ struct ppr_plan {
   int32_t* d_wovl = nullptr;          // [1 + n]: count, sources whose wave-tier table ran out
   bool wave_x_launched = false;
   int wave_tdiv = 0;                  // PPR_WAVE_TDIV (tests): wave-tier tables T >> this
+  bool wave_by_d = false;             // PPR_WAVE_BY_D: exact-sum wave tiers by last distinct keys
   bool xr_budget_over = false;        // PPR_XR_BUDGET=over (tests): range / bucket tables fill up
   int64_t wave_redo = 0;              // wave-tier sources redone (PPR_TIMING at destroy)
   int xg_cap = 1 << 16;               // dense list of the selection (PPR_XG_CAP, tests: L <= cap <= XG_CAP)

@@ -261,6 +261,8 @@ def test_gpu_speculative_bound_bit_exact(env, want_redo, monkeypatch, capfd, cha
     {"PPR_TIER_MASK": "0x0"},                                     # no wave tier: every source in workgroups
     {"PPR_TIER_MASK": "0xf"},                                     # no partition: ranges only
     {"PPR_WAVE_WPB": "4"},                                        # 4-wave blocks in the wave tier
+    {"PPR_WAVE_BY_D": "1"},                                       # wave tiers sized by last distinct keys
+    {"PPR_WAVE_BY_D": "1", "PPR_XR_DSCALE": "5"},                 # ... with every overflow path busy
 ])
 def test_gpu_exact_sum_paths_bit_exact(xenv, monkeypatch):
     """the exact-sum engines (merge_xs.h: wave tier, range workgroups, bucket workgroups, list
