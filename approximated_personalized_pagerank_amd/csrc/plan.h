@@ -220,7 +220,9 @@ struct ppr_plan {
   // sieve merge of the wide exact-sum sources (merge_sv.h): PPR_SV=0 turns it off
   bool sv_enabled = false;
   int64_t sv_slice = 1LL << 18;       // PPR_SV_SLICE: candidates per slice workgroup
-  int64_t sv_min = 0;                 // PPR_SV_MIN: sources with fewer candidates keep the range engines
+  int64_t sv_min = 4096;              // PPR_SV_MIN: sources with fewer candidates keep the range engines
+                                      // (measured: 4096 beats 0 by 2-3 % -- the smallest sources overflow the
+                                      // 4-wave class's sketch and were handed back -- and 16384 by 5 %)
   int sv_budget = 2457;               // PPR_SV_BUDGET (tests): passing keys a table takes (<= SV_XT_BUDGET)
   int64_t sv_small = 16384, sv_mid = 65536;  // PPR_SV_SMALL / PPR_SV_MID: one-slice size classes by candidates
   hipStream_t stream_sv = nullptr, stream_sv2 = nullptr, stream_sv3 = nullptr;  // large + multi-slice | mid | small

@@ -324,6 +324,7 @@ def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):
     """the sieve merge of the wide sources (merge_sv.h: exact prev-key sums + count-min sketch,
     exact second pass for the keys the sketch cannot rule out) equals the oracle's exact sum bit for
     bit -- one-slice and multi-slice sources, table overflows handed back, mixed with every tier"""
+    monkeypatch.setenv("PPR_SV_MIN", "0")  # (every size class at these scales; variants may raise it)
     for k, v in senv.items():
         monkeypatch.setenv(k, v)
     monkeypatch.setenv("PPR_TIMING", "1")
@@ -385,9 +386,13 @@ def test_gpu_hbm_table_fallback_bit_exact(henv, monkeypatch, capfd):
 @pytest.mark.parametrize("benv,what", [
     ({"PPR_WAVE_TDIV": "3"}, "wave_redo_sources"),   # wave-tier tables at 1/8 size: their bounded
                                                      # probes run out, the sources are redone
-    ({"PPR_XR_BUDGET": "over"}, "xr_redo_sources"),  # range / bucket tables without a budget stop:
-                                                     # they fill, the probes run out, overflow redo
-    ({"PPR_XR_BUDGET": "over", "PPR_SV": "0", "PPR_TIER_MASK": "0x20"}, "xr_redo_sources"),
+    # range / bucket tables of 1024 slots without a budget stop, planned for 1/20 of their keys, every
+    # source through them (no sieve, no wave tier): they fill up, the probes run out, overflow redo --
+    # in the range workgroups, and in the bucket workgroups of the partition
+    ({"PPR_XR_BUDGET": "over", "PPR_XR_T": "1024", "PPR_SV": "0", "PPR_TIER_MASK": "0x20", "PPR_XR_DSCALE": "5"},
+     "xr_redo_sources"),
+    ({"PPR_XR_BUDGET": "over", "PPR_XR_T": "1024", "PPR_SV": "0", "PPR_TIER_MASK": "0x20", "PPR_XR_RMAX": "1",
+      "PPR_XR_DSCALE": "5"}, "xr_redo_sources"),
 ])
 def test_gpu_bounded_probes_exhausted_exact(benv, what, monkeypatch, capfd):
     """every LDS hash probe is bounded (ADVICE/VERDICT r3): forced to run out, the exact-sum engines

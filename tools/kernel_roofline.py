@@ -1,12 +1,15 @@
 """Per-kernel roofline table of one GRank job from a round's profile set (tools/profile_round.sh):
 
-    python tools/kernel_roofline.py STATS.csv FETCH.csv WRITE.csv TRACE_STEPS PMC_STEPS [SQ_SUMMARY.txt]
+    python tools/kernel_roofline.py STATS.csv FETCH.csv WRITE.csv TRACE_STEPS PMC_STEPS [SQ_SUMMARY.txt] [BENCH.json]
 
 STATS.csv  rocprofv3 --kernel-trace --stats summary (TotalDurationNs per kernel)
 FETCH.csv  rocprofv3 --pmc FETCH_SIZE counter collection (KiB; x2 on gfx950, MI355X_MICROARCH.md "HBM")
 WRITE.csv  rocprofv3 --pmc WRITE_SIZE counter collection (KiB)
 TRACE_STEPS / PMC_STEPS  jobs in the traced run and in each PMC run
-SQ_SUMMARY tools/sq_summary.py output: the wave-cycle fractions waiting / issuing (optional)
+SQ_SUMMARY tools/sq_summary.py output: the wave-cycle fractions waiting / issuing (optional; "-": none)
+BENCH.json the bench line of the traced build (optional): its roofline.kernels give each kernel
+           group's algorithmic bytes per job (counted on the device per tier), which
+           are joined with the group's kernels' traced time and PMC traffic ("groups" below)
 
 Per kernel, per job: summed launch durations, HBM bytes (2 x FETCH + WRITE), their rate and the
 fraction of the 8 TB/s peak, and a bound label: "hbm" when the rate is >= 60 % of the measured
@@ -65,7 +68,8 @@ def main():
     steps, psteps = int(sys.argv[4]), int(sys.argv[5])
     d, calls = durations(stats)
     f, w = pmc(fetch), pmc(write)
-    q = sq(sys.argv[6]) if len(sys.argv) > 6 else {}
+    q = sq(sys.argv[6]) if len(sys.argv) > 6 and sys.argv[6] != "-" else {}
+    bench = json.load(open(sys.argv[7])) if len(sys.argv) > 7 else None
     rows = []
     for k in sorted(d, key=lambda k: -d[k]):
         t = d[k] / steps
@@ -80,9 +84,35 @@ def main():
                      "hbm_bytes_per_job": b, "read_bytes": 2 * f.get(k, 0.0) / psteps, "write_bytes": w.get(k, 0.0) / psteps,
                      "gbps": round(rate / 1e9, 1), "frac_of_peak": round(rate / PEAK, 4),
                      "sq_wait_frac": wait, "sq_active_frac": act, "bound": bound})
-    json.dump({"note": __doc__.split("\n\n")[2].replace("\n", " "), "trace_steps": steps, "pmc_steps": psteps,
-               "kernels": rows}, sys.stdout,
-              indent=1)
+    out = {"note": __doc__.split("\n\n")[2].replace("\n", " "), "trace_steps": steps, "pmc_steps": psteps,
+           "kernels": rows}
+    if bench:
+        # kernel groups of the bench line (bench.py KERNEL_GROUPS): their kernels by name
+        members = {"wave tier": ["k_merge_lds_x"], "sieve one-slice": ["k_sv1", "k_svfin"],
+                   "sieve multi-slice": ["k_svA", "k_svB", "k_svF"]}
+        kb = bench["roofline"].get("kernels", {})
+        algo = {"wave tier": sum(v["algo_bytes_per_step"] for k, v in kb.items() if k.startswith("wave tier")),
+                "sieve one-slice": sum(v["algo_bytes_per_step"] for k, v in kb.items() if k.startswith("sieve")
+                                       and "multi" not in k),
+                "sieve multi-slice": sum(v["algo_bytes_per_step"] for k, v in kb.items() if "multi" in k)}
+        groups = {}
+        for gname, ks in members.items():
+            t = sum(d.get(k, 0.0) for k in ks) / steps
+            hb = sum(2 * f.get(k, 0.0) + w.get(k, 0.0) for k in ks) / psteps
+            a = algo[gname]
+            groups[gname] = {"kernels": ks, "algo_bytes_per_job": a, "kernel_time_s_per_job": round(t, 4),
+                             "hbm_bytes_per_job": hb, "traffic_over_algo": round(hb / a, 3) if a else None,
+                             "algo_gbps": round(a / t / 1e9, 1) if t else None,
+                             "algo_frac_of_peak": round(a / t / PEAK, 4) if t else None}
+        rest = [r for r in rows if not any(r["kernel"] in ks for ks in members.values())]
+        groups["range / partition engines and the rest"] = {
+            "kernels": [r["kernel"] for r in rest], "algo_bytes_per_job": bench["roofline"]["algo_bytes_per_step"] - sum(algo.values()),
+            "hbm_bytes_per_job": sum(r["hbm_bytes_per_job"] for r in rest)}
+        out["groups"] = groups
+        out["merge_phase"] = {"algo_bytes_per_job": bench["roofline"]["algo_bytes_per_step"],
+                              "merge_s_per_job": bench["roofline"]["merge_ms_per_step"] / 1e3,
+                              "frac": bench["roofline"]["frac"]}
+    json.dump(out, sys.stdout, indent=1)
     print()
 
 
