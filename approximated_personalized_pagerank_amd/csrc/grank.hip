@@ -371,6 +371,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     const char* es = getenv("PPR_SUM");
     if (es && !strcmp(es, "chain")) p->xsum = false;
     if (es && !strcmp(es, "exact") && !mc) p->xsum = true;
+    // MCCompletePathV2's combine: PPR_MC_SUM=exact sums with the same order-free engines (72 fraction
+    // bits, merge_xs.h XS_F_MC; restated by oracle/mc_oracle.c's exact mode)
+    const char* em = getenv("PPR_MC_SUM");
+    if (mc) p->xsum = em && !strcmp(em, "exact");
     if (p->xsum) {
       // the order-bound alternatives of the chain path do not apply: no hot pass, no speculative
       // bound, no workgroup tier (its overflow would fall to the chain-order HBM table)
@@ -674,6 +678,7 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   a.iter = unit ? -1 : it;
   a.spec = (unit || p->hot_cap > 0 || it < p->spec_from) ? 0.0 : p->spec_ratio;
   a.xs = p->xsum ? 1u : 0u;
+  a.xsf = XS_F;
   if (unit) { a.sA = 0; a.sB = 0; a.active = -1; return a; }
   a.sA = ((it + 1) / 2) & 1;
   a.sB = (it / 2) & 1;
@@ -1246,13 +1251,13 @@ static int run_xg(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& sr
     HIP_OK(hipGetLastError());
     const unsigned gb = (unsigned)std::min<int64_t>(2048, (T + 1023) / 1024);
     for (int lvl = 0; lvl < XG_LEVELS; lvl++) {
-      hipLaunchKernelGGL(k_xg_hist, dim3(gb), dim3(1024), 0, st, v, T, keys, A, B, stp, lvl, hist);
+      hipLaunchKernelGGL(k_xg_hist, dim3(gb), dim3(1024), 0, st, v, T, keys, A, B, stp, lvl, hist, a.xsf);
       HIP_OK(hipGetLastError());
       hipLaunchKernelGGL(k_xg_pick, dim3(1), dim3(256), 0, st, stp, lvl, hist, (int)p->L, p->xg_cap);
       HIP_OK(hipGetLastError());
     }
     hipLaunchKernelGGL(k_xg_compact, dim3((unsigned)std::min<int64_t>(8192, (T + 255) / 256)), dim3(256), 0, st, v, T,
-                       keys, A, B, stp, dk, dv);
+                       keys, A, B, stp, dk, dv, a.xsf);
     HIP_OK(hipGetLastError());
     hipLaunchKernelGGL(k_xg_fin, dim3(1), dim3(64), xg_fin_lds_bytes(p->Lp), st, s, a, v, stp, dk, dv, p->Lp, maxdiff,
                        p->d_stats, err);
@@ -1331,8 +1336,9 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       x.v = src[i];
       x.R = rng[i];
       x.pt_off = pt;
-      x.factor = p->damping / (double)deg[i];
-      x.selfval = 1.0 - p->damping;
+      // (merge_factor / self_seed of ppr_common.h: GRank d/deg and 1 - d, the MC combine 1 and 1/f)
+      x.factor = a.mc ? 1.0 : p->damping / (double)deg[i];
+      x.selfval = a.mc ? 1.0 / (p->damping / (double)deg[i]) : 1.0 - p->damping;
       pt += (int64_t)rng[i] * L;  // every range appends at most L entries (one range: the whole top-L)
       xd.push_back(x);
       for (int r = 0; r < rng[i]; r++) tasks[ci[i]].push_back(XTask{d, r});

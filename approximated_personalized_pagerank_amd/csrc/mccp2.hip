@@ -171,7 +171,10 @@ extern "C" int ppr_mccp2_plan_combine(ppr_plan* p) {
   a.unit = 0u;
   a.stats = (p->flags & PPR_FLAG_STATS) ? 1u : 0u;
   a.mc = 1u;
-  a.xs = 0u;  // the combine keeps the reference's order (include/mccompletepathv2.h:228-240)
+  // the reference's order (include/mccompletepathv2.h:228-240) by default; PPR_MC_SUM=exact: the
+  // order-free exact sum with 72 fraction bits (merge_xs.h XS_F_MC)
+  a.xs = p->xsum ? 1u : 0u;
+  a.xsf = XS_F_MC;
   a.rp = p->d_rp;
   a.diag = p->d_diag;
   a.lds_rank = p->lds_rank;

@@ -86,10 +86,10 @@ __device__ __forceinline__ void x2_add(const X2Table& t, int h, unsigned long lo
   atomicAdd(&t.b[h], (lo >> 32) | ((unsigned long long)hi << 32));
 }
 // X = B * 2^32 + A (< 2^95) rounded to a double like xs_to_double
-__device__ __forceinline__ double x2_value(unsigned long long A, unsigned long long B) {
+__device__ __forceinline__ double x2_value(unsigned long long A, unsigned long long B, int F = XS_F) {
   const unsigned long long lo = ((B & 0xffffffffull) << 32) + A;
   const uint32_t hi = (uint32_t)(B >> 32) + (lo < A ? 1u : 0u);
-  return xs_to_double(hi, lo);
+  return xs_to_double(hi, lo, F);
 }
 // membership probe of a table that no longer changes: the slot of `key` or -1. (Insert-only
 // group probing: a key sits in the first group of its sequence that had an empty slot when it was

@@ -62,10 +62,10 @@ __device__ __forceinline__ int64_t xg_slot(uint32_t* keys, int64_t T, int key) {
   return -1;
 }
 __device__ __forceinline__ void xg_add(uint32_t* keys, unsigned long long* A, unsigned long long* B, int64_t T,
-                                       int key, double p, XgState* st) {
+                                       int key, double p, XgState* st, int F) {
   unsigned long long lo;
   uint32_t hi;
-  xs_conv(p, lo, hi);
+  xs_conv(p, lo, hi, F);
   const int64_t h = xg_slot(keys, T, key);
   if (h < 0) { st->err = 1; return; }
   atomicAdd(&A[h], lo & 0xffffffffull);
@@ -80,16 +80,16 @@ __global__ void __launch_bounds__(256) k_xg_walk(DevGraph g, DevSlab s, IterArgs
   const int64_t b = g.rp[v], e = g.rp[v + 1];
   const double factor = merge_factor(a, e - b);
   const int64_t w0 = b + ((int64_t)blockIdx.x * 4 + wv) * WAVE;
-  if (blockIdx.x == 0 && threadIdx.x == 0) xg_add(keys, A, B, T, v, self_seed(a, e - b), st);
+  if (blockIdx.x == 0 && threadIdx.x == 0) xg_add(keys, A, B, T, v, self_seed(a, e - b), st, a.xsf);
   if (w0 >= e) return;
   hub_window_walk(g, s, a, w0, min(e, w0 + WAVE), fl + wv * HUB_WALK_FLAGS, [&](bool valid, int id, double sv, bool) {
-    if (valid) xg_add(keys, A, B, T, a.unit ? id : s.key(id), sv * factor, st);
+    if (valid) xg_add(keys, A, B, T, a.unit ? id : s.key(id), sv * factor, st, a.xsf);
   });
 }
 
 __global__ void __launch_bounds__(1024) k_xg_hist(int v, int64_t T, const uint32_t* keys, const unsigned long long* A,
                                                   const unsigned long long* B, const XgState* st, int level,
-                                                  uint32_t* ghist) {
+                                                  uint32_t* ghist, int F) {
   __shared__ uint32_t h[XG_BINS];
   if (st->done) return;
   for (int i = threadIdx.x; i < XG_BINS; i += blockDim.x) h[i] = 0u;
@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(1024) k_xg_hist(int v, int64_t T, const uint32
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t kt = keys[i];
     if (!kt) continue;
-    const unsigned __int128 k = xg_key(x2_value(A[i], B[i]), (int)kt - 1, ts);
+    const unsigned __int128 k = xg_key(x2_value(A[i], B[i], F), (int)kt - 1, ts);
     if (level > 0 && (k >> top) != (P >> top)) continue;
     atomicAdd(&h[(uint32_t)(k >> sh) & (XG_BINS - 1)], 1u);
   }
@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(256) k_xg_pick(XgState* st, int level, uint32_
 
 __global__ void __launch_bounds__(256) k_xg_compact(int v, int64_t T, const uint32_t* keys, const unsigned long long* A,
                                                     const unsigned long long* B, XgState* st, int32_t* dk,
-                                                    double* dv) {
+                                                    double* dv, int F) {
   const uint32_t ts = tie_salt(v);
   const unsigned __int128 P = xg_prefix(*st);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T; i += (int64_t)gridDim.x * blockDim.x) {
@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(256) k_xg_compact(int v, int64_t T, const uint
     bool keep = false;
     double val = 0.0;
     if (kt) {
-      val = x2_value(A[i], B[i]);
+      val = x2_value(A[i], B[i], F);
       keep = xg_key(val, (int)kt - 1, ts) >= P;
     }
     if (keep) {

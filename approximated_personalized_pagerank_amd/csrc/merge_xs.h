@@ -22,16 +22,16 @@
 
 namespace pprk {
 
-constexpr int XS_F = 93;   // fraction bits of the fixed-point sums (oracle/grank_oracle.c XS_F)
+// (XS_F / XS_F_MC, the fixed-point fraction bits: ppr_common.h)
 constexpr double XR_SPEC = 0.9;  // speculative bound of a whole-source table: this x its previous L-th score
 
-// floor(p * 2^93) of p in [0, 4): lo = low 64 bits, hi = bits 64..94
-__device__ __forceinline__ void xs_conv(double p, unsigned long long& lo, uint32_t& hi) {
+// floor(p * 2^F) of p in [0, 2^(95 - F)): lo = low 64 bits, hi = bits 64..94 (F = 93: p < 4)
+__device__ __forceinline__ void xs_conv(double p, unsigned long long& lo, uint32_t& hi, int F = XS_F) {
   const unsigned long long b = dbits(p);
   int e = (int)((b >> 52) & 0x7ffu);
   unsigned long long m = b & ((1ull << 52) - 1ull);
   if (e) m |= 1ull << 52; else e = 1;
-  const int sh = e - 1075 + XS_F;
+  const int sh = e - 1075 + F;
   if (sh >= 0) {
     lo = m << sh;
     hi = sh > 11 ? (uint32_t)(m >> (64 - sh)) : 0u;
@@ -43,21 +43,21 @@ __device__ __forceinline__ void xs_conv(double p, unsigned long long& lo, uint32
 
 // X * 2^-93 rounded to nearest even: the top 64 bits of X with a sticky bit, one correctly rounded
 // u64 -> f64 conversion, an exact power-of-two scale (oracle_xs_to_double)
-__device__ __forceinline__ double xs_to_double(uint32_t hi, unsigned long long lo) {
-  if (hi == 0u) return ldexp((double)lo, -XS_F);
+__device__ __forceinline__ double xs_to_double(uint32_t hi, unsigned long long lo, int F = XS_F) {
+  if (hi == 0u) return ldexp((double)lo, -F);
   const int n = 32 - __clz(hi);
   const unsigned long long top = ((unsigned long long)hi << (64 - n)) | (lo >> n);
   const unsigned long long sticky = (lo & ((1ull << n) - 1ull)) != 0ull ? 1ull : 0ull;
-  return ldexp((double)(top | sticky), n - XS_F);
+  return ldexp((double)(top | sticky), n - F);
 }
 
 // value of a single contribution p as the exact path stores it: a lower bound of the total of any
 // key that receives p (totals of nonnegative terms only grow, rounding is monotone)
-__device__ __forceinline__ double xs_single(double p) {
+__device__ __forceinline__ double xs_single(double p, int F = XS_F) {
   unsigned long long lo;
   uint32_t hi;
-  xs_conv(p, lo, hi);
-  return xs_to_double(hi, lo);
+  xs_conv(p, lo, hi, F);
+  return xs_to_double(hi, lo, F);
 }
 
 // LDS table of 16-B slots in three arrays: keys u32 (key + 1, 0 = empty), lo u64 (low word of the
@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   if (lane_id() == 0) {
     unsigned long long lo;
     uint32_t hi;
-    xs_conv(self_seed(a, e - b), lo, hi);
+    xs_conv(self_seed(a, e - b), lo, hi, a.xsf);
     bad = xt_add(t, v, lo, hi) < 0;
   }
   wave_fence();
@@ -193,7 +193,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   if (a.unit) {
     unsigned long long flo;
     uint32_t fhi;
-    xs_conv(factor, flo, fhi);  // init: every successor contributes 1.0 * d/deg
+    xs_conv(factor, flo, fhi, a.xsf);  // init: every successor contributes 1.0 * d/deg
     for (int64_t e0 = b; e0 < e; e0 += WAVE) {
       const int64_t i = e0 + lane_id();
       if (i < e && xt_add(t, g.colx[i] & 0x7fffffff, flo, fhi) < 0) bad = true;
@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
                         if (valid) {
                           unsigned long long lo;
                           uint32_t hi;
-                          xs_conv(sv * factor, lo, hi);
+                          xs_conv(sv * factor, lo, hi, a.xsf);
                           if (xt_add(t, id, lo, hi) < 0) bad = true;
                         }
                       },
@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   for (int o = 32; o; o >>= 1) { const unsigned long long y = __shfl_xor(mb, o); mb = y > mb ? y : mb; }
   // keys below the pruning bound cannot reach the top-L (a full successor row puts L distinct keys
   // at >= the single-contribution value of its minimum)
-  const double tau = (!a.unit && mb) ? xs_single(bitsd(mb) * factor) : 0.0;
+  const double tau = (!a.unit && mb) ? xs_single(bitsd(mb) * factor, a.xsf) : 0.0;
   // settle + compact in place: (double value, key) pairs over the front of the table
   double* vals = reinterpret_cast<double*>(t.lo);
   int* keys = reinterpret_cast<int*>(t.keys);
@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
     const uint32_t kt = t.keys[i];
     const unsigned long long lo = t.lo[i];
     const bool occ = kt != 0u;
-    const double x = occ ? xs_to_double(t.hi[i], lo) : 0.0;
+    const double x = occ ? xs_to_double(t.hi[i], lo, a.xsf) : 0.0;
     const bool keep = occ && x >= tau;
     const uint64_t m = __ballot(keep);
     D += __popcll(__ballot(occ));
@@ -333,12 +333,12 @@ __device__ __forceinline__ void xr_clear(const XrLds& x, int T) {
 // a probe that ran out of slots: the fill count jumps past any budget, so the workgroup stops and
 // the source takes the overflow redo
 constexpr int XR_FULL = 1 << 24;
-__device__ __forceinline__ void xr_apply(const XrLds& x, bool valid, int key, double p, int budget) {
+__device__ __forceinline__ void xr_apply(const XrLds& x, bool valid, int key, double p, int budget, int F) {
   int r = 0;
   if (valid) {
     unsigned long long lo;
     uint32_t hi;
-    xs_conv(p, lo, hi);
+    xs_conv(p, lo, hi, F);
     r = xt_add(x.t, key, lo, hi);
   }
   const int n = __popcll(__ballot(r > 0)) + (__ballot(r < 0) ? XR_FULL : 0);
@@ -390,7 +390,7 @@ __device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& 
 #pragma unroll
   for (int j = 0; j < XR_SLOTS; j++) {
     const bool in = (int)threadIdx.x + j * (int)blockDim.x < T;
-    kv[j] = xs_to_double(kh[j], kl[j]);
+    kv[j] = xs_to_double(kh[j], kl[j], a.xsf);
     kk[j] = (in && kt[j] && kv[j] >= tau0) ? (int)kt[j] - 1 : -1;
     c += kk[j] >= 0 ? 1 : 0;
     c_hi += (kk[j] >= 0 && kv[j] >= ts_hi) ? 1 : 0;
@@ -525,7 +525,7 @@ __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, 
   if (threadIdx.x == 0 && xr_in(v, r, R)) {
     unsigned long long lo;
     uint32_t hi;
-    xs_conv(xd.selfval, lo, hi);
+    xs_conv(xd.selfval, lo, hi, a.xsf);
     xt_add(x.t, v, lo, hi);
     x.w.misc[XM_FILL] = 1;
   }
@@ -537,14 +537,14 @@ __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, 
   uint8_t* fl = x.fl + (size_t)wv * HUB_WALK_FLAGS;
   auto fn = [&](bool valid, int id, double sv, bool) {
     if (xr_stop(x, budget)) return;  // (uniform per wave: one LDS read per group)
-    xr_apply(x, valid && xr_in(id, r, R), id, sv * factor, budget);
+    xr_apply(x, valid && xr_in(id, r, R), id, sv * factor, budget, a.xsf);
   };
   if (a.unit) {
     for (int64_t e0 = b + (int64_t)wv * WAVE; e0 < e; e0 += (int64_t)W * WAVE) {
       const int64_t i = e0 + lane_id();
       const int key = i < e ? (g.colx[i] & 0x7fffffff) : 0;
       if (xr_stop(x, budget)) break;
-      xr_apply(x, i < e && xr_in(key, r, R), key, factor, budget);
+      xr_apply(x, i < e && xr_in(key, r, R), key, factor, budget, a.xsf);
     }
   } else {
     // each wave walks its own contiguous share of the successor list (one window setup per 64
@@ -572,7 +572,7 @@ __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, 
   if (lane_id() == 0 && mb) atomicMax(reinterpret_cast<unsigned long long*>(&x.w.misc[8]), mb);
   __syncthreads();
   const unsigned long long mbb = *reinterpret_cast<unsigned long long*>(&x.w.misc[8]);
-  const double tau_rows = (!a.unit && mbb) ? xs_single(bitsd(mbb) * factor) : 0.0;
+  const double tau_rows = (!a.unit && mbb) ? xs_single(bitsd(mbb) * factor, a.xsf) : 0.0;
   // one-range source: its previous L-th score (row minimum of a full current row) x XR_SPEC as a
   // speculative bound (scores move little between updates; the check in xr_finish keeps it exact)
   double tau_spec = 0.0;
@@ -607,7 +607,7 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
   if (threadIdx.x == 0 && (int)hub_digit(v, d.logP) == tk.x) {
     unsigned long long lo;
     uint32_t hi;
-    xs_conv(self_seed(a, deg), lo, hi);
+    xs_conv(self_seed(a, deg), lo, hi, a.xsf);
     xt_add(x.t, v, lo, hi);
     x.w.misc[XM_FILL] = 1;
   }
@@ -656,7 +656,7 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
       const int64_t gk = g0 + (int64_t)k * W;
       key[k] = rec_key(hr.r[k]);
       v[k] = gk < ng && gk * WAVE + lane_id() < nb;
-      xs_conv(rec_sc(hr.r[k]) * factor, lo[k], hi[k]);
+      xs_conv(rec_sc(hr.r[k]) * factor, lo[k], hi[k], a.xsf);
       if (v[k] && key[k] == hk) {
         const unsigned long long nl = hlo + lo[k];
         hhi += hi[k] + (nl < hlo ? 1u : 0u);
@@ -739,7 +739,7 @@ __global__ void __launch_bounds__(1024) k_xb(DevSlab s, IterArgs a, const HubDes
     if (threadIdx.x == 0 && atomicExch(&oflag[tk.d], 1) == 0) ovl[1 + atomicAdd(&ovl[0], 1)] = v;
     return;
   }
-  const double tau_rows = (!a.unit && tau_b[tk.d]) ? xs_single(bitsd(tau_b[tk.d]) * factor) : 0.0;
+  const double tau_rows = (!a.unit && tau_b[tk.d]) ? xs_single(bitsd(tau_b[tk.d]) * factor, a.xsf) : 0.0;
   XDesc xd;
   xd.v = v; xd.R = 0; xd.pt_off = d.pt_off; xd.factor = factor; xd.selfval = 0.0;
   xr_finish(x, T, s, a, xd, tk.d, true, tau_rows, 0.0, xtau, pk, ps, pc, dsum, a.diag ? &tph : nullptr, 156);

@@ -146,6 +146,11 @@ __device__ __forceinline__ void write_row(const DevSlab& s, int slot, int v, uin
   wave_fence();
 }
 
+constexpr int XS_F = 93;     // fraction bits of the exact sums (merge_xs.h; oracle/grank_oracle.c XS_F)
+constexpr int XS_F_MC = 72;  // ... in the MC combine (IterArgs::xsf): its totals reach deg / d (the seed
+                             // 1/f and up to deg successor baskets of scores <= 1), < 2^22 at RMAT-22,
+                             // so 72 fraction bits keep every total below 2^94 (oracle/mc_oracle.c)
+
 struct IterArgs {
   int sA, sB;        // read slot of successors whose colx bit 31 is 0 / 1
   int active;        // partition updated in this iteration (-1 = init)
@@ -161,7 +166,8 @@ struct IterArgs {
                              // should not evict the scatter's partially written staging lines from L2)
   uint32_t whatif;           // PPR_WHATIF bits that act inside kernels (timing experiments, plan.h;
                              // bits 0-15 as set by the user, WI_* below set per launch by the host)
-  uint32_t xs;               // exact-sum GRank merge (merge_xs.h), never in the MC combine
+  uint32_t xs;               // exact-sum merge (merge_xs.h): GRank by default, the MC combine with PPR_MC_SUM=exact
+  int xsf;                   // its fixed-point fraction bits (merge_xs.h XS_F, XS_F_MC)
   int iter;                  // GRank iteration (diagnostics)
   double spec;               // speculative pruning ratio (PPR_SPEC; 0 = off): spec_tau below
 };

@@ -83,28 +83,31 @@ int oracle_get_sum(void) { return g_sum_exact; }
 #define XS_F 93 /* fixed-point fraction bits (approximated_personalized_pagerank_amd/csrc/merge_xs.h) */
 typedef unsigned __int128 xs_t;
 
-/* floor(p * 2^93) of a double p >= 0 (p < 4 in GRank: every basket sums to <= 1) */
-static xs_t xs_conv(double p) {
+/* floor(p * 2^F) of a double p >= 0 (GRank: F = 93, p < 4, every basket sums to <= 1; the MC
+ * combine's exact mode: F = 72, mc_oracle.c) */
+xs_t oracle_xs_conv_f(double p, int F) {
   uint64_t b;
   memcpy(&b, &p, 8);
   int e = (int)((b >> 52) & 0x7ff);
   uint64_t m = b & ((1ull << 52) - 1);
   if (e) m |= 1ull << 52; else e = 1;
-  const int sh = e - 1075 + XS_F;
+  const int sh = e - 1075 + F;
   if (sh >= 0) return (xs_t)m << sh;
   if (-sh >= 64) return 0;
   return (xs_t)(m >> -sh);
 }
+static xs_t xs_conv(double p) { return oracle_xs_conv_f(p, XS_F); }
 
-/* X * 2^-93 rounded to nearest even (X < 2^95): the top 64 bits with a sticky bit, one correctly
+/* X * 2^-F rounded to nearest even (X < 2^95): the top 64 bits with a sticky bit, one correctly
  * rounded u64 -> double conversion, an exact power-of-two scale */
-double oracle_xs_to_double(uint64_t hi, uint64_t lo) {
-  if (hi == 0) return ldexp((double)lo, -XS_F);
+double oracle_xs_to_double_f(uint64_t hi, uint64_t lo, int F) {
+  if (hi == 0) return ldexp((double)lo, -F);
   const int n = 64 - __builtin_clzll(hi);
   const uint64_t top = (hi << (64 - n)) | (lo >> n);
   const uint64_t sticky = (lo & ((1ull << n) - 1)) != 0;
-  return ldexp((double)(top | sticky), n - XS_F);
+  return ldexp((double)(top | sticky), n - F);
 }
+double oracle_xs_to_double(uint64_t hi, uint64_t lo) { return oracle_xs_to_double_f(hi, lo, XS_F); }
 static double xs_to_double(xs_t x) { return oracle_xs_to_double((uint64_t)(x >> 64), (uint64_t)x); }
 void oracle_xs_conv(double p, uint64_t* hi, uint64_t* lo) {
   const xs_t x = xs_conv(p);

@@ -291,6 +291,19 @@ static int walk_node(int64_t n, const int64_t* rp, const int32_t* col, int32_t s
   return size;
 }
 
+/* ---- summation mode of the combine (oracle_set_mc_sum; the HIP plan's PPR_MC_SUM): chain = the
+ * reference's in-order `map[k] += x` (include/mccompletepathv2.h:240-241); exact = every term (and
+ * the seed 1/f) converted exactly to floor(x * 2^72) and summed in 128-bit integers, the total
+ * rounded once (grank_oracle.c's exact sum with 72 fraction bits: MC totals reach deg / d) */
+typedef unsigned __int128 xs_t;
+xs_t oracle_xs_conv_f(double p, int F);
+double oracle_xs_to_double_f(uint64_t hi, uint64_t lo, int F);
+#define XS_F_MC 72 /* approximated_personalized_pagerank_amd/csrc/merge_xs.h XS_F_MC */
+static int g_mc_exact = 0;
+void oracle_set_mc_sum(int exact) { g_mc_exact = exact ? 1 : 0; }
+int oracle_get_mc_sum(void) { return g_mc_exact; }
+static double mc_value(xs_t x) { return oracle_xs_to_double_f((uint64_t)(x >> 64), (uint64_t)x, XS_F_MC); }
+
 typedef struct { int32_t key; double sc; uint32_t tie; } ment_t;
 /* output order: (score desc, key asc) */
 static int cmp_ment(const void* a, const void* b) {
@@ -339,6 +352,7 @@ int oracle_mccp2(int64_t n, const int64_t* rp, const int32_t* col, int32_t K, in
   uint8_t* adm = (uint8_t*)calloc((size_t)n, 1);
   uint32_t* rrc = (uint32_t*)calloc((size_t)n, sizeof(uint32_t));
   double* acc = (double*)calloc((size_t)n, sizeof(double));
+  xs_t* xacc = g_mc_exact ? (xs_t*)calloc((size_t)n, sizeof(xs_t)) : NULL;
   uint8_t* touched = (uint8_t*)calloc((size_t)n, 1);
   ment_t* ent = (ment_t*)malloc(sizeof(ment_t) * (size_t)n);
   for (int64_t i = 0; i < n; i++) {
@@ -350,6 +364,7 @@ int oracle_mccp2(int64_t n, const int64_t* rp, const int32_t* col, int32_t K, in
     ent[U++].key = v;
     touched[v] = 1;
     acc[v] = 1.0 / f;                                  /* (:226) */
+    if (xacc) xacc[v] = oracle_xs_conv_f(1.0 / f, XS_F_MC);
     for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
       const int32_t s = col[e];
       const int32_t* rk;
@@ -367,11 +382,15 @@ int oracle_mccp2(int64_t n, const int64_t* rp, const int32_t* col, int32_t K, in
       }
       for (int32_t t = 0; t < rl; t++) {              /* map[k] += x (:240-241) */
         const int32_t k = rk[t];
-        if (!touched[k]) { touched[k] = 1; acc[k] = 0.0; ent[U++].key = k; }
-        acc[k] = acc[k] + rs[t];
+        if (!touched[k]) { touched[k] = 1; acc[k] = 0.0; if (xacc) xacc[k] = 0; ent[U++].key = k; }
+        if (xacc) xacc[k] += oracle_xs_conv_f(rs[t], XS_F_MC);
+        else acc[k] = acc[k] + rs[t];
       }
     }
-    for (int64_t t = 0; t < U; t++) { ent[t].sc = acc[ent[t].key]; touched[ent[t].key] = 0; }
+    for (int64_t t = 0; t < U; t++) {
+      ent[t].sc = xacc ? mc_value(xacc[ent[t].key]) : acc[ent[t].key];
+      touched[ent[t].key] = 0;
+    }
     const int64_t keep = U < L ? U : L;
     mkeep(ent, U, keep, v);                            /* keepTop(L) (:243) */
     for (int64_t t = 0; t < keep; t++) {              /* *= factor (:246-247) */
@@ -402,6 +421,7 @@ int oracle_mccp2(int64_t n, const int64_t* rp, const int32_t* col, int32_t K, in
   }
   free(order); free(pos); free(fid); free(fsc); free(flen); free(wid); free(wsc); free(wlen);
   free(haswalk); free(cnt); free(adm); free(rrc); free(acc); free(touched); free(ent);
+  free(xacc);
   return 0;
 }
 
@@ -415,6 +435,7 @@ int oracle_mc_combine(int64_t n, const int64_t* rp, const int32_t* col, const in
                       const int32_t* w_ids, const double* w_sc, const int32_t* w_len,
                       const int32_t* list, int64_t count, int32_t* out_ids, double* out_sc, int32_t* out_len) {
   double* acc = (double*)calloc((size_t)n, sizeof(double));
+  xs_t* xacc = g_mc_exact ? (xs_t*)calloc((size_t)n, sizeof(xs_t)) : NULL;
   uint8_t* touched = (uint8_t*)calloc((size_t)n, 1);
   int64_t cap = 16;
   ment_t* ent = (ment_t*)malloc(sizeof(ment_t) * (size_t)cap);
@@ -431,6 +452,7 @@ int oracle_mc_combine(int64_t n, const int64_t* rp, const int32_t* col, const in
     ent[U++].key = v;
     touched[v] = 1;
     acc[v] = 1.0 / f;
+    if (xacc) xacc[v] = oracle_xs_conv_f(1.0 / f, XS_F_MC);
     for (int64_t e = rp[v]; e < rp[v + 1]; e++) {
       const int32_t s = col[e];
       const int fin = pos[s] < pos[v];
@@ -439,11 +461,15 @@ int oracle_mc_combine(int64_t n, const int64_t* rp, const int32_t* col, const in
       const int32_t rl = fin ? f_len[s] : w_len[s];
       for (int32_t t = 0; t < rl; t++) {
         const int32_t k = rk[t];
-        if (!touched[k]) { touched[k] = 1; acc[k] = 0.0; ent[U++].key = k; }
-        acc[k] = acc[k] + rs[t];
+        if (!touched[k]) { touched[k] = 1; acc[k] = 0.0; if (xacc) xacc[k] = 0; ent[U++].key = k; }
+        if (xacc) xacc[k] += oracle_xs_conv_f(rs[t], XS_F_MC);
+        else acc[k] = acc[k] + rs[t];
       }
     }
-    for (int64_t t = 0; t < U; t++) { ent[t].sc = acc[ent[t].key]; touched[ent[t].key] = 0; }
+    for (int64_t t = 0; t < U; t++) {
+      ent[t].sc = xacc ? mc_value(xacc[ent[t].key]) : acc[ent[t].key];
+      touched[ent[t].key] = 0;
+    }
     const int64_t keep = U < L ? U : L;
     mkeep(ent, U, keep, v);
     for (int64_t t = 0; t < keep; t++) { ent[t].sc = ent[t].sc * f; }
@@ -454,6 +480,6 @@ int oracle_mc_combine(int64_t n, const int64_t* rp, const int32_t* col, const in
     }
     out_len[q] = (int32_t)keep;
   }
-  free(acc); free(touched); free(ent);
+  free(acc); free(touched); free(ent); free(xacc);
   return 0;
 }

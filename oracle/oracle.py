@@ -69,6 +69,10 @@ def lib():
         L.oracle_xs_to_double.restype = ctypes.c_double
         L.oracle_xs_conv.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_xs_conv.restype = None
+        L.oracle_set_mc_sum.argtypes = [ctypes.c_int]
+        L.oracle_set_mc_sum.restype = None
+        L.oracle_get_mc_sum.argtypes = []
+        L.oracle_get_mc_sum.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -104,6 +108,32 @@ class sum_mode:
 
     def __exit__(self, *exc):
         set_sum(self.prev)
+
+
+def set_mc_sum(mode: str) -> None:
+    """MCCompletePathV2 combine summation of every later oracle call (mc_oracle.c): "chain" (default,
+    the reference's in-order map[k] += x) or "exact" (72-bit fixed point, the HIP plan's PPR_MC_SUM=exact)."""
+    assert mode in SUM_MODES, mode
+    lib().oracle_set_mc_sum(1 if mode == "exact" else 0)
+
+
+def get_mc_sum() -> str:
+    return "exact" if lib().oracle_get_mc_sum() else "chain"
+
+
+class mc_sum_mode:
+    """with oracle.mc_sum_mode("exact"): ... -- the MC combine's mode for the block, restored after"""
+
+    def __init__(self, mode: str):
+        self.mode, self.prev = mode, None
+
+    def __enter__(self):
+        self.prev = get_mc_sum()
+        set_mc_sum(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        set_mc_sum(self.prev)
 
 
 def xs_conv(p: float):

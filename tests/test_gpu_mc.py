@@ -69,6 +69,41 @@ def test_gpu_mc_merge_paths_bit_exact(mask, monkeypatch):
     check_vs_oracle(ppr.rmat(10, seed=91), 16, 48, 100, 0.85, walks=False)
 
 
+@pytest.mark.parametrize("scale,K,L,R,env", [
+    (9, 8, 16, 200, {}),
+    (11, 16, 64, 300, {}),
+    (12, 32, 200, 100, {}),
+    (8, 4, 1000, 50, {}),
+    (10, 16, 48, 100, {"PPR_TIER_MASK": "0x20"}),   # no wave tier: every source through the workgroups
+    (11, 16, 64, 100, {"PPR_XR_DSCALE": "5"}),      # estimates 20x too low: overflow redos
+    (11, 16, 64, 100, {"PPR_XR_RMAX": "1"}),        # multi-table sources partitioned (k_xb)
+])
+def test_gpu_mc_exact_sum_bit_exact(scale, K, L, R, env, monkeypatch):
+    """PPR_MC_SUM=exact: the combine on the order-free exact-sum engines (72 fraction bits) equals the
+    oracle's exact MC mode bit for bit, walks included"""
+    monkeypatch.setenv("PPR_MC_SUM", "exact")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    with oracle.mc_sum_mode("exact"):
+        check_vs_oracle(ppr.rmat(scale, seed=scale * 7 + L), K, L, R, 0.85)
+
+
+def test_gpu_mc_exact_sum_eat_vs_reference():
+    """the exact MC combine on the reference's own dataset: bit-exact vs the oracle's exact mode and
+    the same top-K as the reference's run within the chain mode's band"""
+    import os
+    os.environ["PPR_MC_SUM"] = "exact"
+    try:
+        f = load("m4_eat_k50_l200")
+        with oracle.mc_sum_mode("exact"):
+            r = check_vs_oracle(ppr.Csr(f["rp"], f["col"]), f["K"], f["L"], f["iters"], f["damping"], walks=False)
+    finally:
+        del os.environ["PPR_MC_SUM"]
+    z = f["z"]
+    s = z["sample"]
+    assert jaccard_rows(r.ids[s], r.lens[s], z["ids"], np.minimum(z["cnt"], f["K"])).mean() >= 0.98
+
+
 @pytest.mark.parametrize("env", [
     {"PPR_TIER_MASK": "0x20", "PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "2048", "PPR_SEG_T": "256"},  # overflows
     {"PPR_TIER_MASK": "0x20", "PPR_HUB_SEG": "1", "PPR_SEG_BUCKET": "2048", "PPR_SEG_T": "256",

@@ -167,3 +167,21 @@ def test_quality_eat_vs_reference():
     j = jaccard_rows(o["ids"][s], o["lens"][s], z["ids"], np.minimum(z["cnt"], f["K"])).mean()
     # measured 0.987 (two reference runs: 0.987)
     assert j >= 0.98
+
+
+@pytest.mark.parametrize("name", ["m3_rmat10_k16_l64", "m1_ring100_k10_l20", "m2_random100_full"])
+def test_exact_combine_mode_matches_chain(name):
+    """the combine's exact mode (72-bit fixed point, order-free; the HIP plan's PPR_MC_SUM=exact)
+    keeps the chain mode's rows: the same keys and scores within 1e-12 relative for > 99.9 % of the
+    entries (a near-tie cut at an earlier node can keep another key there, and the baskets of later
+    nodes that read it differ downstream -- as between any two summation orders)"""
+    f = load(name)
+    a = oracle.mccp2(f["rp"], f["col"], f["K"], f["L"], min(f["iters"], 2000), f["damping"], 3)
+    with oracle.mc_sum_mode("exact"):
+        b = oracle.mccp2(f["rp"], f["col"], f["K"], f["L"], min(f["iters"], 2000), f["damping"], 3)
+    assert oracle.get_mc_sum() == "chain"
+    assert np.array_equal(a["lens"], b["lens"])
+    assert (a["ids"] == b["ids"]).mean() > 0.999
+    ok = a["ids"] == b["ids"]
+    rel = np.abs(a["scores"] - b["scores"]) / np.maximum(np.abs(a["scores"]), 1e-300)
+    assert (rel[ok] <= 1e-12).mean() > 0.999
