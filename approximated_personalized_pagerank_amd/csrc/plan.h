@@ -224,7 +224,9 @@ struct ppr_plan {
                                       // (measured: 4096 beats 0 by 2-3 % -- the smallest sources overflow the
                                       // 4-wave class's sketch and were handed back -- and 16384 by 5 %)
   int sv_budget = 2457;               // PPR_SV_BUDGET (tests): passing keys a table takes (<= SV_XT_BUDGET)
-  int64_t sv_small = 16384, sv_mid = 65536;  // PPR_SV_SMALL / PPR_SV_MID: one-slice size classes by candidates
+  int64_t sv_small = 32768, sv_mid = 65536;  // PPR_SV_SMALL / PPR_SV_MID: one-slice size classes by candidates
+                                      // (same-box sweep of SV_SMALL 16 K / 32 K / 48 K / 64 K: 1632 / 1589-1594 /
+                                      // 1593 / 1664 ms per job; SV_MID 32 K / 131 K: +-0)
   hipStream_t stream_sv = nullptr, stream_sv2 = nullptr, stream_sv3 = nullptr;  // large + multi-slice | mid | small
                                       // (borrowed: stream2 / stream4 / stream5, not owned)
   hipEvent_t ev_sv = nullptr;
