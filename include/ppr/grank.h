@@ -133,11 +133,51 @@ struct KeyIndex {
   std::unique_ptr<std::atomic<int32_t>[]> slot;
   uint64_t mask = 0;
   KeyStore<Key> ks;
+  // integer keys of <= 32 bits in a dense range (span <= 4 n + 1024: ids, as in the reference's
+  // examples and RMAT graphs): a direct key -> id array instead of the hash, one memory access per
+  // lookup (the flatten's successor lookups were two cache misses each: slot, then the key copy)
+  std::vector<int32_t> direct;
+  int64_t lo = 0;
+  template <typename K = Key>
+  typename std::enable_if<std::is_integral<K>::value && sizeof(K) <= 4, bool>::type build_direct(
+      const std::vector<const Key*>& k, size_t nt) {
+    if (k.empty()) return false;
+    std::vector<int64_t> mn(nt, INT64_MAX), mx(nt, INT64_MIN);
+    std::vector<size_t> part(nt + 1);
+    for (size_t t = 0; t <= nt; t++) part[t] = k.size() * t / nt;
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nt; t++)
+      th.emplace_back([&, t] {
+        for (size_t i = part[t]; i < part[t + 1]; i++) {
+          const int64_t x = (int64_t)*k[i];
+          mn[t] = std::min(mn[t], x);
+          mx[t] = std::max(mx[t], x);
+        }
+      });
+    for (auto& x : th) x.join();
+    const int64_t a = *std::min_element(mn.begin(), mn.end()), b = *std::max_element(mx.begin(), mx.end());
+    if (b - a > 4 * (int64_t)k.size() + 1024) return false;
+    lo = a;
+    direct.resize((size_t)(b - a + 1));
+    parallel_ranges(direct.size(), nt, [&](size_t x0, size_t x1) {
+      for (size_t i = x0; i < x1; i++) direct[i] = -1;
+    });
+    parallel_ranges(k.size(), nt, [&](size_t x0, size_t x1) {
+      for (size_t v = x0; v < x1; v++) direct[(size_t)((int64_t)*k[v] - lo)] = (int32_t)v;
+    });
+    return true;
+  }
+  template <typename K = Key>
+  typename std::enable_if<!(std::is_integral<K>::value && sizeof(K) <= 4), bool>::type build_direct(
+      const std::vector<const Key*>&, size_t) {
+    return false;
+  }
   static uint64_t mix(uint64_t x) {  // splitmix64 finaliser: std::hash of integers is the identity
     x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL; x ^= x >> 27; x *= 0x94d049bb133111ebULL; x ^= x >> 31;
     return x;
   }
   void build(const std::vector<const Key*>& k, size_t nt) {
+    if (build_direct(k, nt)) return;
     ks.build(k, nt);
     uint64_t cap = 16;
     while (cap < 2 * (uint64_t)k.size()) cap <<= 1;
@@ -158,12 +198,22 @@ struct KeyIndex {
     });
   }
   int32_t find(const Key& key) const {  // -1: not a key of the graph
+    if (!direct.empty()) return find_direct(key);
     uint64_t h = mix((uint64_t)std::hash<Key>()(key)) & mask;
     for (;;) {
       const int32_t s = slot[h].load(std::memory_order_relaxed);
       if (s < 0 || ks.at((size_t)s) == key) return s;
       h = (h + 1) & mask;
     }
+  }
+  template <typename K = Key>
+  typename std::enable_if<std::is_integral<K>::value && sizeof(K) <= 4, int32_t>::type find_direct(const K& key) const {
+    const int64_t i = (int64_t)key - lo;
+    return (i < 0 || i >= (int64_t)direct.size()) ? -1 : direct[(size_t)i];
+  }
+  template <typename K = Key>
+  typename std::enable_if<!(std::is_integral<K>::value && sizeof(K) <= 4), int32_t>::type find_direct(const K&) const {
+    return -1;
   }
 };
 

@@ -4,7 +4,8 @@
 // materialisation -- compiled with g++ -fsanitize=address,undefined (build.build_host_asan) and run
 // on RMAT graphs, printing digests the test compares with the production library's results.
 //   host_asan_test graph <scale> <seed>   digests of partitions / executionOrder / CSR
-//   host_asan_test flatten <scale>        map graph -> CSR -> fake rows -> result maps
+//   host_asan_test flatten <scale>        map graph -> CSR -> fake rows -> result maps (dense ids)
+//   host_asan_test flatten_sparse <scale> the same with keys spread over the int range
 //   host_asan_test csv <path>             ppr_import_edge_csv digests
 #include <cstdint>
 #include <cstdio>
@@ -49,13 +50,19 @@ int main(int argc, char** argv) {
            (unsigned long long)fnv(part.data(), part.size()), (unsigned long long)fnv(order.data(), 4 * order.size()));
     return 0;
   }
-  if (mode == "flatten") {
+  if (mode == "flatten" || mode == "flatten_sparse") {
     std::vector<int64_t> rp;
     std::vector<int32_t> col;
     rmat(atoi(argv[2]), 42, rp, col);
     const int64_t n = (int64_t)rp.size() - 1;
+    // flatten_sparse: keys spread over the int range (the KeyIndex hash, not its dense-id array)
+    const bool sparse = mode == "flatten_sparse";
+    auto key = [&](int64_t v) { return sparse ? (int)((uint32_t)v * 2654435761u >> 1) : (int)v; };
     std::unordered_map<int, std::vector<int>> graph;
-    for (int64_t v = n - 1; v >= 0; v--) graph[(int)v].assign(col.begin() + rp[v], col.begin() + rp[v + 1]);
+    for (int64_t v = n - 1; v >= 0; v--) {
+      std::vector<int>& s = graph[key(v)];
+      for (int64_t e = rp[v]; e < rp[v + 1]; e++) s.push_back(key(col[e]));
+    }
     const size_t nt = 8;
     ppr::hipdetail::Flat<int> f = ppr::hipdetail::flatten(graph, nt);
     // CSR of the dense ids must describe the same graph

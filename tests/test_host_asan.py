@@ -53,6 +53,11 @@ def test_flatten_and_materialise_sanitized(asan):
     assert run(asan, "flatten", 16)["bad"] == 0
 
 
+def test_flatten_sparse_keys_sanitized(asan):
+    """keys far apart take the KeyIndex hash (dense ids take its direct array)"""
+    assert run(asan, "flatten_sparse", 14)["bad"] == 0
+
+
 def test_csv_import_sanitized(asan, tmp_path):
     path = tmp_path / "g.csv"
     rng = np.random.default_rng(3)
