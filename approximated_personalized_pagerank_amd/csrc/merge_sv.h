@@ -271,11 +271,31 @@ __device__ __forceinline__ void sv_build_pt(const SvLds& x, const DevSlab& s, co
     atomicOr(&x.ptb[bit >> 5], 1u << (bit & 31u));
   }
 }
-// the key's PT slot (-1: not a prev key)
+// the key's PT slot (-1: not a prev key): the prefilter bit, then the key's group of four matched
+// with selects (no branches); an empty slot in the group ends the search, a full group (PT is half
+// full: a few per cent of the keys) probes on
+__device__ __forceinline__ int x2_find_from(const X2Table& t, uint32_t tag, uint32_t g) {
+  for (uint32_t n = 0; n <= t.mask; n += 4) {
+    const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g);
+    const int m = xt_match(q, g, tag);
+    if (m >= 0) return m;
+    if (q.x == 0u || q.y == 0u || q.z == 0u || q.w == 0u) return -1;
+    g = (g + 4u) & t.mask;
+  }
+  return -1;
+}
 __device__ __forceinline__ int sv_pt_slot(const SvLds& x, int key, const SvHash& k) {
   const uint32_t bit = sv_bloom_bit(k);
   if (!((x.ptb[bit >> 5] >> (bit & 31u)) & 1u)) return -1;
-  return x2_find_h(x.pt, key, k.h);
+  const uint32_t tag = (uint32_t)key + 1u;
+  const uint32_t g = k.h & x.pt.mask & ~3u;
+  const uint4 q = *reinterpret_cast<const uint4*>(x.pt.keys + g);
+  int m = q.w == tag ? (int)g + 3 : -1;
+  m = q.z == tag ? (int)g + 2 : m;
+  m = q.y == tag ? (int)g + 1 : m;
+  m = q.x == tag ? (int)g : m;
+  if (m < 0 && min(min(q.x, q.y), min(q.z, q.w)) != 0u) m = x2_find_from(x.pt, tag, (g + 4u) & x.pt.mask);
+  return m;
 }
 
 // The wave's share of a slice: contiguous successors [c0, c1) taken row by row. Row metadata comes
@@ -334,12 +354,9 @@ __device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, con
         }
       }
     };
-    SvBatch<NS> cur, nxt;
-    load(0, nxt);
-    for (int q0 = 0; q0 < nrows; q0 += NS) {
-      cur = nxt;
-      if (q0 + NS < nrows) load(q0 + NS, nxt);
-      fb(cur);
+    // two batch buffers in turn (no per-batch copy of one into the other); sched_barrier keeps the
+    // next batch's loads ahead of this batch's work without pulling its first uses up
+    auto tail = [&](const SvBatch<NS>& cur, int q0) {
       if (L > 2 * WAVE) {  // rows beyond two groups (L > 128 only)
         for (int q = 0; q < NS && q0 + q < nrows; q++) {
           const int rl = __builtin_amdgcn_readlane(ln, q0 + q);
@@ -356,6 +373,21 @@ __device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, con
           }
         }
       }
+    };
+    SvBatch<NS> ba, bb;
+    load(0, ba);
+    for (int q0 = 0; q0 < nrows; q0 += 2 * NS) {
+      if (q0 + NS < nrows) load(q0 + NS, bb);
+      __builtin_amdgcn_sched_barrier(0);
+      fb(ba);
+      tail(ba, q0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q0 + NS >= nrows) break;
+      if (q0 + 2 * NS < nrows) load(q0 + 2 * NS, ba);
+      __builtin_amdgcn_sched_barrier(0);
+      fb(bb);
+      tail(bb, q0 + NS);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
@@ -373,48 +405,6 @@ __device__ __forceinline__ void sv_chunk(int64_t b0, int64_t b1, int64_t& c0, in
   c1 = sv_uniform(min(b1, c0 + chunk));
 }
 
-// PT membership of SV_PH groups at once (phased): the prefilter words of all groups are read back
-// to back, then the first probe group of every prefilter hit, then the (rare) longer probes -- two
-// LDS round trips for the groups together instead of one or two per group in turn (the per-group
-// form waited on LDS latency: ~2 K cycles per 8-group batch of a mid-class wave). ok[j] gates the
-// lanes that look; slot[j] = the PT slot or -1.
-constexpr int SV_PH = 4;
-__device__ __forceinline__ int x2_find_from(const X2Table& t, uint32_t tag, uint32_t g) {
-  for (uint32_t n = 0; n <= t.mask; n += 4) {
-    const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g);
-    const int m = xt_match(q, g, tag);
-    if (m >= 0) return m;
-    if (q.x == 0u || q.y == 0u || q.z == 0u || q.w == 0u) return -1;
-    g = (g + 4u) & t.mask;
-  }
-  return -1;
-}
-__device__ __forceinline__ void sv_pt_slots(const SvLds& x, const bool (&ok)[SV_PH], const int (&key)[SV_PH],
-                                            const SvHash (&hk)[SV_PH], int (&slot)[SV_PH]) {
-  uint32_t bw[SV_PH];
-#pragma unroll
-  for (int j = 0; j < SV_PH; j++) bw[j] = ok[j] ? x.ptb[sv_bloom_bit(hk[j]) >> 5] : 0u;
-  bool hit[SV_PH];
-  uint4 q[SV_PH];
-  uint32_t g[SV_PH];
-#pragma unroll
-  for (int j = 0; j < SV_PH; j++) {
-    hit[j] = ok[j] && ((bw[j] >> (sv_bloom_bit(hk[j]) & 31u)) & 1u);
-    g[j] = hk[j].h & x.pt.mask & ~3u;
-    q[j] = hit[j] ? *reinterpret_cast<const uint4*>(x.pt.keys + g[j]) : make_uint4(1u, 1u, 1u, 1u);
-  }
-#pragma unroll
-  for (int j = 0; j < SV_PH; j++) {
-    slot[j] = -1;
-    if (!hit[j]) continue;
-    const uint32_t tag = (uint32_t)key[j] + 1u;
-    const int m = xt_match(q[j], g[j], tag);
-    if (m >= 0) { slot[j] = m; continue; }
-    if (q[j].x == 0u || q[j].y == 0u || q[j].z == 0u || q[j].w == 0u) continue;
-    slot[j] = x2_find_from(x.pt, tag, (g[j] + 4u) & x.pt.mask);  // (the group was full: probe on)
-  }
-}
-
 // pass 1 over successors [b0, b1): prev keys exactly into PT, every other key into the sketch
 constexpr int SV_NS1 = 4, SV_NS2 = 4;  // rows per batch in pass 1 (keys and scores) and pass 2 (keys)
 __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
@@ -423,29 +413,18 @@ __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, co
   sv_chunk(b0, b1, c0, c1);
   sv_rows<true, SV_NS1>(g, s, a, c0, c1, [&](const SvBatch<SV_NS1>& bt) {
 #pragma unroll
-    for (int k0 = 0; k0 < 2 * SV_NS1; k0 += SV_PH) {
-      bool ok[SV_PH];
-      int key[SV_PH], slot[SV_PH];
-      SvHash hk[SV_PH];
-#pragma unroll
-      for (int j = 0; j < SV_PH; j++) {
-        ok[j] = bt.valid[k0 + j];
-        key[j] = bt.key[k0 + j];
-        hk[j] = sv_hash(key[j]);
-      }
-      sv_pt_slots(x, ok, key, hk, slot);
-#pragma unroll
-      for (int j = 0; j < SV_PH; j++) {
-        if (!ok[j]) continue;
-        const double p = bt.sv[k0 + j] * factor;
-        if (slot[j] >= 0) {
-          unsigned long long lo;
-          uint32_t hi;
-          xs_conv(p, lo, hi);
-          x2_add(x.pt, slot[j], lo, hi);
-        } else {
-          sv_sketch_add(sk, hk[j], sv_units(p), x.wlog);
-        }
+    for (int k = 0; k < 2 * SV_NS1; k++) {
+      if (!__ballot(bt.valid[k])) continue;
+      const SvHash hk = sv_hash(bt.key[k]);
+      const int h = bt.valid[k] ? sv_pt_slot(x, bt.key[k], hk) : -2;
+      const double p = bt.sv[k] * factor;
+      if (h >= 0) {
+        unsigned long long lo;
+        uint32_t hi;
+        xs_conv(p, lo, hi);
+        x2_add(x.pt, h, lo, hi);
+      } else if (h == -1) {
+        sv_sketch_add(sk, hk, sv_units(p), x.wlog);
       }
     }
   });
@@ -453,9 +432,8 @@ __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, co
 
 // pass 2 over successors [b0, b1): keys outside PT that pass the sieve, exactly into XT (budget
 // checked before every group that inserts; past it the workgroup only flags the overflow). Per
-// batch: the sieve tests of all its groups (bitmap words read together, then the PT check of the
-// passing lanes, phased), then the passing candidates' scores (loads in flight together), then
-// the inserts.
+// batch: the sieve tests of all its groups (the PT check only for passing lanes), then the passing
+// candidates' scores (loads in flight together), then the inserts.
 __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
                                          const X2Table& xt, int64_t b0, int64_t b1, double factor, int budget) {
   int64_t c0, c1;
@@ -467,22 +445,11 @@ __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, co
     bool want[NG];
     bool any = false;
 #pragma unroll
-    for (int k0 = 0; k0 < NG; k0 += SV_PH) {
-      bool ok[SV_PH];
-      int key[SV_PH], slot[SV_PH];
-      SvHash hk[SV_PH];
-#pragma unroll
-      for (int j = 0; j < SV_PH; j++) {
-        key[j] = bt.key[k0 + j];
-        hk[j] = sv_hash(key[j]);
-        ok[j] = bt.valid[k0 + j] && sv_passes(bm32, hk[j], x.wlog);
-      }
-      sv_pt_slots(x, ok, key, hk, slot);
-#pragma unroll
-      for (int j = 0; j < SV_PH; j++) {
-        want[k0 + j] = ok[j] && slot[j] < 0;
-        any = any || want[k0 + j];
-      }
+    for (int k = 0; k < NG; k++) {
+      const SvHash hk = sv_hash(bt.key[k]);
+      want[k] = bt.valid[k] && sv_passes(bm32, hk, x.wlog);
+      if (__ballot(want[k]) && want[k]) want[k] = sv_pt_slot(x, bt.key[k], hk) < 0;
+      any = any || want[k];
     }
     if (!__ballot(any)) return;
     double sv[NG];
