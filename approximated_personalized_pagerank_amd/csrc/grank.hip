@@ -428,6 +428,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       const char* s6 = getenv("PPR_SV_MID");
       if (s5) p->sv_small = std::max<int64_t>(0, atoll(s5));
       if (s6) p->sv_mid = std::max<int64_t>(0, atoll(s6));
+      const char* s7 = getenv("PPR_SV_REDO");
+      p->sv_redo_mid = !(s7 && atoi(s7) == 0);
       const char* s3 = getenv("PPR_SV_BUDGET");
       if (s3) p->sv_budget = std::max(0, std::min(SV_XT_BUDGET, atoi(s3)));
       // Streams of the exact sum: a process has 4 hardware queues (HIP's default), and streams
@@ -477,6 +479,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         {(const void*)k_xfinal<XDesc>, "k_xfinal<XDesc>"},
         {(const void*)k_xfinal<HubDesc>, "k_xfinal<HubDesc>"},
         {(const void*)k_sv1, "k_sv1"},
+        {(const void*)k_sv1_redo, "k_sv1_redo"},
         {(const void*)k_svA, "k_svA"},
         {(const void*)k_svB, "k_svB"},
         {(const void*)k_svF, "k_svF"},
@@ -1511,6 +1514,7 @@ static void kst_fold(ppr_plan* p, int g) {
 struct SvRun {
   std::vector<int32_t> pos;  // index into the caller's source list of each descriptor
   size_t o_ovl = 0;          // offset of the overflow list in d_sv
+  size_t o_os = 0;           // ... and of the small class's first overflows (redone on the device)
   bool live = false;
 };
 
@@ -1578,6 +1582,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   const size_t o_sv = off; off = al(off + 8 * (size_t)Lp * nx);
   const size_t o_z = off;
   const size_t o_ov = off; off = al(off + 4 * (1 + nx));
+  const size_t o_os = off; off = al(off + 4 * (1 + nx));  // small class's first overflows (device redo)
   const size_t o_sn = off; off = al(off + 4 * nx);
   const size_t o_of = off; off = al(off + 4 * (nm + 1));
   const size_t o_pt = off; off = al(off + 8 * 2 * (size_t)Lp * nm);
@@ -1606,6 +1611,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   const SvDesc* d_d = (const SvDesc*)(b + o_d);
   const SvTask* d_t = (const SvTask*)(b + o_t);
   int32_t* d_ov = (int32_t*)(b + o_ov);
+  int32_t* d_os = (int32_t*)(b + o_os);
   int32_t* d_of = (int32_t*)(b + o_of);
   unsigned long long* d_pt = (unsigned long long*)(b + o_pt);
   uint32_t* d_sk = (uint32_t*)(b + o_gs);
@@ -1631,9 +1637,19 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
       if (!cnt_c) continue;
       const SvGeom G = geo[c];
       kst_begin(p, 1 + c, cs[c]);
+      // the small class's overflows are redone at once with the mid geometry (it hands back ~7 % of
+      // its sources, the mid class < 0.5 %); only a second overflow reaches the host
+      const bool redo = c == 2 && p->sv_redo_mid;
       hipLaunchKernelGGL(k_sv1, dim3((unsigned)cnt_c), dim3(G.threads()), sv_lds_bytes(Lp, G), cs[c], g, s, a, d_v, d0,
-                         Lp, G, std::min(p->sv_budget, G.budget), d_ov, d_ok, d_ovv, d_on);
+                         Lp, G, std::min(p->sv_budget, G.budget), redo ? d_os : d_ov, d_ok, d_ovv, d_on);
       HIP_OK(hipGetLastError());
+      if (redo) {
+        hipLaunchKernelGGL(k_sv1_redo, dim3((unsigned)std::min<size_t>(cnt_c, 512)), dim3(SV_MID.threads()),
+                           sv_lds_bytes(Lp, SV_MID), cs[c], g, s, a, d_v, d_os, Lp, SV_MID,
+                           std::min(p->sv_budget, SV_MID.budget), d_ov, d_ok, d_ovv, d_on);
+        HIP_OK(hipGetLastError());
+        p->merge_launches++;
+      }
       hipLaunchKernelGGL(k_svfin, dim3((unsigned)cnt_c), dim3(64), svfin_lds_bytes(Lp), cs[c], s, a, d_v, d0, d_ok,
                          d_ovv, d_on, Lp, maxdiff, p->d_stats);
       HIP_OK(hipGetLastError());
@@ -1658,6 +1674,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   }
   p->sv_sources += (int64_t)nx;
   run.o_ovl = o_ov;
+  run.o_os = o_os;
   run.live = true;
   return PPR_OK;
 }
@@ -1675,9 +1692,11 @@ static int sieve_collect(ppr_plan* p, SvRun& run, std::vector<int32_t>& back) {
     HIP_OK(hipEventRecord(p->ev_sv, p->stream_sv3));
     HIP_OK(hipStreamWaitEvent(p->stream_sv, p->ev_sv, 0));
   }
-  int32_t novf = 0;
+  int32_t novf = 0, nsm = 0;
   HIP_OK(hipMemcpyAsync(&novf, p->d_sv + run.o_ovl, 4, hipMemcpyDeviceToHost, p->stream_sv));
+  HIP_OK(hipMemcpyAsync(&nsm, p->d_sv + run.o_os, 4, hipMemcpyDeviceToHost, p->stream_sv));
   HIP_OK(hipStreamSynchronize(p->stream_sv));
+  p->sv_redo_dev += nsm;
   for (int g = 1; g < ppr_plan::NKST; g++) kst_fold(p, g);
   if (!novf) return PPR_OK;
   std::vector<int32_t> od(novf);

@@ -538,12 +538,12 @@ __device__ __forceinline__ void sv_clear_region(const SvLds& x, size_t bytes) {
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterArgs a, const int32_t* vid, int d0,
-                                                    int Lp, SvGeom G, int budget, int32_t* ovl, int32_t* out_k,
-                                                    double* out_v, int32_t* out_n) {
-  extern __shared__ __align__(16) unsigned char smem[];
+// one source (descriptor d) of a one-slice class, the whole workgroup; a source that overflows
+// (or has no full row) goes to `ovl` and writes nothing
+__device__ __forceinline__ void sv1_source(unsigned char* smem, DevGraph g, DevSlab s, IterArgs a, const int32_t* vid,
+                                           int d, int Lp, SvGeom G, int budget, int32_t* ovl, int32_t* out_k,
+                                           double* out_v, int32_t* out_n) {
   const SvLds x = sv_carve(smem, Lp, G);
-  const int d = d0 + (int)blockIdx.x;
   const int v = vid[d];
   const int L = s.L;
   // (the host sends only sources with a full current row: L keys to bound with)
@@ -664,6 +664,30 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterA
   __syncthreads();
   if (threadIdx.x == 0) out_n[d] = x.misc[SVM_PT];
   if (threadIdx.x == 0) sv_lap(a, dg + 4, tph);
+}
+
+__global__ void __launch_bounds__(SV_THREADS) k_sv1(DevGraph g, DevSlab s, IterArgs a, const int32_t* vid, int d0,
+                                                    int Lp, SvGeom G, int budget, int32_t* ovl, int32_t* out_k,
+                                                    double* out_v, int32_t* out_n) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  sv1_source(smem, g, s, a, vid, d0 + (int)blockIdx.x, Lp, G, budget, ovl, out_k, out_v, out_n);
+}
+
+// the sources a smaller class handed back (`list`: [0] count, [1..] descriptors), again with a
+// larger geometry G, grid-stride; a second overflow goes to `ovl` (the host's hand-back list). It
+// runs on the handing class's stream right after it: no host round trip for the first overflow.
+// (8 waves: the mid geometry; the grid-stride loop needs more than the 128 VGPRs of 16 waves)
+static_assert(SV_MID.waves == 8, "k_sv1_redo launch bounds: the mid geometry");
+__global__ void __launch_bounds__(8 * WAVE) k_sv1_redo(DevGraph g, DevSlab s, IterArgs a, const int32_t* vid,
+                                                         const int32_t* list, int Lp, SvGeom G, int budget,
+                                                         int32_t* ovl, int32_t* out_k, double* out_v,
+                                                         int32_t* out_n) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int n = list[0];
+  for (int k = (int)blockIdx.x; k < n; k += (int)gridDim.x) {
+    __syncthreads();  // the previous source's LDS reads are done
+    sv1_source(smem, g, s, a, vid, list[1 + k], Lp, G, budget, ovl, out_k, out_v, out_n);
+  }
 }
 
 // the row of a one-slice source from its selected entries (k_sv1): one wave per source -- sort in

@@ -223,6 +223,7 @@ struct ppr_plan {
   int64_t sv_min = 4096;              // PPR_SV_MIN: sources with fewer candidates keep the range engines
                                       // (measured: 4096 beats 0 by 2-3 % -- the smallest sources overflow the
                                       // 4-wave class's sketch and were handed back -- and 16384 by 5 %)
+  bool sv_redo_mid = true;            // PPR_SV_REDO=0: small-class overflows go straight to the host hand-back
   int sv_budget = 2457;               // PPR_SV_BUDGET (tests): passing keys a table takes (<= SV_XT_BUDGET)
   int64_t sv_small = 32768, sv_mid = 65536;  // PPR_SV_SMALL / PPR_SV_MID: one-slice size classes by candidates
                                       // (same-box sweep of SV_SMALL 16 K / 32 K / 48 K / 64 K: 1632 / 1589-1594 /
@@ -235,6 +236,7 @@ struct ppr_plan {
   void* h_sv_pin = nullptr;           // pinned staging of descriptors and tasks, overflow count
   size_t h_sv_bytes = 0;
   int64_t sv_sources = 0, sv_redo = 0;  // sieved sources, handed back after an overflow (PPR_TIMING)
+  int64_t sv_redo_dev = 0;            // small-class overflows redone on the device (mid geometry)
   double xh_s[8] = {};                // run_xhubs host sections, s (PPR_TIMING at destroy)
   // MCCompletePathV2 (mccp2.hip)
   bool mc = false;
@@ -290,7 +292,8 @@ inline void plan_free(ppr_plan* p) {
   if (p->h_sv_pin) hipHostFree(p->h_sv_pin);
   if (p->ev_sv) hipEventDestroy(p->ev_sv);
   if (getenv("PPR_TIMING") && p->sv_sources)
-    fprintf(stderr, "ppr_timing sieve_sources %lld sieve_redo %lld\n", (long long)p->sv_sources, (long long)p->sv_redo);
+    fprintf(stderr, "ppr_timing sieve_sources %lld sieve_redo %lld sieve_redo_dev %lld\n", (long long)p->sv_sources,
+            (long long)p->sv_redo, (long long)p->sv_redo_dev);
   if (getenv("PPR_TIMING") && p->sv_sources)
     fprintf(stderr, "ppr_timing xhubs_host_s gather %.4f classify %.4f sieve_launch %.4f engines %.4f sieve_wait %.4f "
             "handback_plan %.4f handback_run %.4f\n", p->xh_s[0], p->xh_s[1], p->xh_s[2], p->xh_s[3], p->xh_s[4],

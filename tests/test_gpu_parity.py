@@ -318,6 +318,12 @@ def test_gpu_exact_sum_init_hubs_and_damping():
     ({"PPR_SV_SMALL": "0", "PPR_SV_MID": "0", "PPR_TIER_MASK": "0x0"}, "sieve"),  # every one-slice source 16 waves
     ({"PPR_SV_SMALL": "1000000000", "PPR_SV_MID": "1000000000"}, "sieve"),        # ... 4 waves
     ({"PPR_SV_SMALL": "0", "PPR_SV_MID": "1000000000", "PPR_SV_BUDGET": "40"}, "redo"),  # ... 8 waves
+    # every one-slice source in the 4-wave class (614 passing keys): the wide ones overflow and are
+    # redone on the device with the 8-wave geometry (1228); with it off they go to the host
+    ({"PPR_SV_SMALL": "1000000000", "PPR_SV_MID": "1000000000", "PPR_TIER_MASK": "0x0"}, "devredo"),
+    ({"PPR_SV_SMALL": "1000000000", "PPR_SV_MID": "1000000000", "PPR_TIER_MASK": "0x0", "PPR_SV_REDO": "0"}, "redo"),
+    # both geometries overflow: device redo, then the host hand-back
+    ({"PPR_SV_SMALL": "1000000000", "PPR_SV_MID": "1000000000", "PPR_SV_BUDGET": "8"}, "devredo+redo"),
     ({"PPR_SV": "0"}, None),                                  # off: range / partition engines only
 ])
 def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):
@@ -341,12 +347,17 @@ def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):
     lines = [x.split() for x in err.splitlines() if x.startswith("ppr_timing sieve_sources")]
     sieved = sum(int(x[2]) for x in lines)
     redo = sum(int(x[4]) for x in lines)
+    redo_dev = sum(int(x[6]) for x in lines)
     if want:
         assert sieved > 0
     else:
         assert sieved == 0
-    if want == "redo":
+    if "redo" in (want or "").split("+"):
         assert redo > 0
+    if "devredo" in (want or "").split("+"):
+        assert redo_dev > 0
+    if senv.get("PPR_SV_REDO") == "0":
+        assert redo_dev == 0
 
 
 @pytest.mark.parametrize("henv", [

@@ -7,6 +7,8 @@
 #   prof        rocprofv3 --kernel-trace --stats over one job (+1 warmup): kernel_stats.csv, timeline
 #   sq          two SQ counter passes (one rocprofv3 run each) over one job: sq_summary.txt
 #   pmc         FETCH_SIZE and WRITE_SIZE passes over one job: pmc.json (tools/pmc_summary.py)
+#   mctrace     kernel trace of one MC job, per-level breakdown (tools/mc_trace.py): mc_trace.txt
+#   mclog       PPR_MC_LEVEL_LOG per-level times of one MC job (tools/mc_levels.py): mc_levels.txt
 #   env:VAR=X   export VAR=X for the following steps
 #   ab:VAR=X[,VAR2=Y]  one bench line (2 steps, 1 warmup) with those variables set, ms_per_step printed
 # Stops at the first failing step (a GPU fault, abort or time limit ends the session).
@@ -56,6 +58,17 @@ for step in "$@"; do
       python3 tools/pmc_summary.py $(find "$out/fetch" -name "*counter_collection.csv") $(find "$out/write" -name "*counter_collection.csv") 1 exact > "$out/pmc.json"
       find "$out/fetch" "$out/write" -name "*counter_collection.csv" -size +20M -delete
       head -c 1500 "$out/pmc.json" ;;
+    mctrace)
+      export TMPDIR=/tmp
+      timeout -k 10 400 rocprofv3 --kernel-trace -f csv -d "$out/mct" -o run -- python3 bench.py --workload mc --steps 1 --warmup 0 \
+        --no-cpu-baseline --no-e2e > "$out/mct.json" 2> "$out/mct.err" || { echo "mctrace failed rc=$?"; tail -20 "$out/mct.err"; exit 1; }
+      python3 tools/mc_trace.py $(find "$out/mct" -name "*kernel_trace.csv" | head -1) > "$out/mc_trace.txt"
+      find "$out/mct" -name "*kernel_trace.csv" -size +40M -delete
+      head -30 "$out/mc_trace.txt" ;;
+    mclog)
+      PPR_MC_LEVEL_LOG=1 timeout -k 10 300 python -u bench.py --workload mc --steps 1 --warmup 0 --no-cpu-baseline --no-e2e \
+        > "$out/mclog.json" 2> "$out/mclog.err" || { echo "mclog failed rc=$?"; tail -20 "$out/mclog.err"; exit 1; }
+      python3 tools/mc_levels.py "$out/mclog.err" > "$out/mc_levels.txt"; cat "$out/mc_levels.txt" ;;
     env:*)
       export "${step#env:}" ;;
     ab:*)
