@@ -49,14 +49,22 @@ def sum_mode():
 def pmc_traffic(tag, mode):
     """HBM bytes per step of the merge phase from the newest committed rocprofv3 PMC summary of this
     workload in this summation mode (tools/pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, separate
-    passes; a summary without a "sum" field predates the exact sum: chain), or None."""
+    passes; a summary without a "sum" field predates the exact sum: chain), its path and the source
+    digest of the library it profiled (tools/gpu_run.sh pmc stamps it), or None."""
     import glob
     for path in sorted(glob.glob(os.path.join(PROFILES, f"*_{tag}_pmc.json")), reverse=True):
         with open(path) as f:
             d = json.load(f)
         if d.get("sum", "chain") == mode:
-            return d.get("merge_phase_traffic_bytes"), os.path.relpath(path, ROOT)
-    return None, None
+            return d.get("merge_phase_traffic_bytes"), os.path.relpath(path, ROOT), d.get("build")
+    return None, None, None
+
+
+def lib_build():
+    """source digest of the loaded HIP library (ppr_build_info: ppr_src_sha256=...)"""
+    from approximated_personalized_pagerank_amd import _lib
+    info = _lib.lib().ppr_build_info().decode()
+    return info.split("ppr_src_sha256=")[1].split()[0] if "ppr_src_sha256=" in info else None
 
 
 def mc_cpu_baseline(scale, K, L, walks, damping, seed):
@@ -419,9 +427,10 @@ def main():
         kernels[k] = {"algo_bytes_per_step": v["algo_bytes"] / steps, "ms_per_step": v["ms"] / steps,
                       "launches_per_step": v["launches"] / steps, "achieved": gbs, "frac": gbs / HBM_PEAK_GBS}
     dominant = max(kernels, key=lambda k: kernels[k]["ms_per_step"]) if kernels else None
-    traffic, traffic_src = (None, None)
+    traffic, traffic_src, traffic_build = (None, None, None)
     if (args.scale, args.K, args.L, args.iters) == (22, 64, 128, 30):
-        traffic, traffic_src = pmc_traffic("grank_rmat22_k64_l128", sum_mode())
+        traffic, traffic_src, traffic_build = pmc_traffic("grank_rmat22_k64_l128", sum_mode())
+    build = lib_build()
     line = {
         "metric": f"source-nodes/sec grank K={args.K} L={args.L} on RMAT-{args.scale}; 1/2/4/8 MI355X + HBM GB/s",
         "value": value,
@@ -453,10 +462,13 @@ def main():
                      "merge_ms_per_step": stats["merge_ms"] / steps,
                      "merge_launches_per_step": stats["launches"] / steps,
                      "traffic": traffic, "traffic_source": traffic_src,
+                     # the PMC summary's library against this run's: equal = the same kernels profiled
+                     "traffic_build": traffic_build, "traffic_same_build": traffic_build == build if traffic_build else None,
                      "dominant_kernel": dominant,
                      "kernels": kernels},
         "cpu_baseline": cpu,
         "end_to_end": e2e,
+        "build": build,
     }
     print(json.dumps(line), flush=True)
 

@@ -153,3 +153,16 @@ def test_bench_parses_timing_lines():
     assert d["partitions_s"] == 0.786 and d["work_s"] == 0.051
     assert d["flatten_s"] == 1.17 and d["csr_call_s"] == 4.82 and d["materialize_s"] == 2.81
     assert bench.parse_ppr_timing("") == {}
+
+
+def test_bench_traffic_summary_names_its_build():
+    """roofline.traffic comes from a committed PMC summary stamped with the source digest of the
+    library it profiled (tools/stamp_build.py), which the bench line sets beside its own build"""
+    import importlib
+    import sys
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    bench = importlib.import_module("bench")
+    traffic, src, build = bench.pmc_traffic("grank_rmat22_k64_l128", "exact")
+    assert traffic and traffic > 0 and src.startswith("profiles/")
+    assert build and len(build) == 64 and all(c in "0123456789abcdef" for c in build)

@@ -56,6 +56,7 @@ for step in "$@"; do
       timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run -f csv -- python3 bench.py $P1 > "$out/fetch.json" 2> "$out/fetch.err" || { echo "fetch failed"; exit 1; }
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run -f csv -- python3 bench.py $P1 > "$out/write.json" 2> "$out/write.err" || { echo "write failed"; exit 1; }
       python3 tools/pmc_summary.py $(find "$out/fetch" -name "*counter_collection.csv") $(find "$out/write" -name "*counter_collection.csv") 1 exact > "$out/pmc.json"
+      python3 tools/stamp_build.py "$out/pmc.json"
       find "$out/fetch" "$out/write" -name "*counter_collection.csv" -size +20M -delete
       head -c 1500 "$out/pmc.json" ;;
     mctrace)
