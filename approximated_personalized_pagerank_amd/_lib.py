@@ -48,7 +48,7 @@ def embedded_digest(path: str = LIB_PATH):
     return m.group(1).decode() if m else None
 # A/B experiments only (tools/build_variant.py): load a variant build of the same ABI instead
 if os.environ.get("PPR_LIB_VARIANT"):
-    LIB_PATH = os.path.join(PKG_DIR, "libppr_hip_" + os.environ["PPR_LIB_VARIANT"] + ".so")
+    LIB_PATH = os.path.join(PKG_DIR, "libpprab_" + os.environ["PPR_LIB_VARIANT"] + ".so")
     if not os.path.exists(LIB_PATH):  # never let build() compile the product sources under its name
         raise FileNotFoundError(f"PPR_LIB_VARIANT: {LIB_PATH} missing (tools/build_variant.py builds it)")
 

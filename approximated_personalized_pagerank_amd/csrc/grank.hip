@@ -293,6 +293,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     if (etd) p->wave_tdiv = std::max(0, std::min(6, atoi(etd)));
     const char* exr = getenv("PPR_XROUTE");
     if (exr && atoi(exr) == 0) p->xroute = false;
+    const char* exb = getenv("PPR_XTEST_BADSIZE");
+    if (exb) p->xtest_badsize = atoi(exb);
     const char* e9e = getenv("PPR_WG_PASSES");  // tests: force workgroup-tier overflows
     if (e9e) p->wg_max_passes = std::max(1, std::min(WG_MAX_PASSES, atoi(e9e)));
     const char* e9d = getenv("PPR_FUSED_MAX");
@@ -375,6 +377,18 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     // bits, merge_xs.h XS_F_MC; restated by oracle/mc_oracle.c's exact mode)
     const char* em = getenv("PPR_MC_SUM");
     if (mc) p->xsum = em && !strcmp(em, "exact");
+    if (mc && p->xsum) {
+      // the 96-bit accumulators hold totals below 2^(95 - 72) = 2^23: a combine total is at most
+      // the seed 1/f = deg/d plus deg baskets' entries (MC entries stay near 1), so refuse a graph
+      // whose widest node could pass it instead of wrapping silently
+      // (PPR_MC_XS_LOG2 lowers the limit: tests)
+      const char* el = getenv("PPR_MC_XS_LOG2");
+      const double lim = std::ldexp(1.0, el ? std::max(1, std::min(23, atoi(el))) : 95 - XS_F_MC);
+      int64_t maxdeg = 0;
+      for (int64_t v = 0; v < n; v++) maxdeg = std::max<int64_t>(maxdeg, row_ptr[v + 1] - row_ptr[v]);
+      const double seed = damping > 0.0 ? (double)std::max<int64_t>(1, maxdeg) / damping : 1.0;
+      if ((double)maxdeg + seed >= lim) { plan_free(p); return PPR_ERR_RANGE; }
+    }
     if (p->xsum) {
       // the order-bound alternatives of the chain path do not apply: no hot pass, no speculative
       // bound, no workgroup tier (its overflow would fall to the chain-order HBM table)
@@ -2499,18 +2513,22 @@ struct LocalGroup {
   bool failed = false;
   std::vector<unsigned char*> bufs;
   std::vector<unsigned long long> md;
+  std::vector<int> ok;                             // routed exchange: every rank's size check
   std::vector<std::vector<unsigned char*>> pbufs;  // routed blocks: [sender][receiver]
   std::vector<std::vector<int64_t>> psz;
   explicit LocalGroup(int n_)
-      : n(n_), bufs(n_), md(n_), pbufs(n_, std::vector<unsigned char*>(n_)), psz(n_, std::vector<int64_t>(n_)) {}
+      : n(n_), bufs(n_), md(n_), ok(n_, 1), pbufs(n_, std::vector<unsigned char*>(n_)),
+        psz(n_, std::vector<int64_t>(n_)) {}
   bool barrier() {
     std::unique_lock<std::mutex> lk(mu);
     if (failed) return false;
     const int64_t g = gen;
     if (++arrived == n) { arrived = 0; gen++; cv.notify_all(); return true; }
-    const bool ok = cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || failed; });
-    if (!ok || failed) { failed = true; cv.notify_all(); return false; }
-    return true;
+    cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || failed; });
+    if (gen != g) return true;  // (everyone arrived: a failure flagged since is the next barrier's)
+    failed = true;
+    cv.notify_all();
+    return false;
   }
   void fail() { std::lock_guard<std::mutex> lk(mu); failed = true; cv.notify_all(); }
 };
@@ -2529,14 +2547,14 @@ static int x_blocks(ppr_plan* p, const std::vector<int64_t>& b, const std::vecto
     HIP_OK(hipStreamSynchronize(s));
     return G.barrier() ? PPR_OK : PPR_ERR_HIP;  // no rank reuses its send buffer before all copied
   }
-  NCCL_OK(ncclGroupStart());
-  for (int r = 0; r < p->nranks; r++) {
+  ncclResult_t nr = ncclGroupStart();
+  for (int r = 0; r < p->nranks && nr == ncclSuccess; r++) {
     if (b[r + 1] == b[r]) continue;
     unsigned char* dst = r == p->rank ? p->d_xsend : p->d_xrecv + xo[r];
-    NCCL_OK(ncclBroadcast(p->d_xsend, dst, (size_t)sz[r], ncclUint8, r, p->comm, s));
+    nr = ncclBroadcast(p->d_xsend, dst, (size_t)sz[r], ncclUint8, r, p->comm, s);
   }
-  NCCL_OK(ncclGroupEnd());
-  return PPR_OK;
+  const ncclResult_t ne = ncclGroupEnd();  // (always closed, whatever failed inside)
+  return nr == ncclSuccess && ne == ncclSuccess ? PPR_OK : PPR_ERR_HIP;
 }
 
 // maxDiff >= 0: the IEEE bit patterns order like the values, so an integer MAX is exact
@@ -2687,7 +2705,7 @@ static int x_exchange_routed(ppr_plan* p, uint32_t it, const XRoute& xr) {
   if (rc) return rc;
   rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, std::max<size_t>(8, ro[W]));
   if (rc) return rc;
-  rc = ensure_dev(&p->d_xsz, &p->xsz_bytes, 16 * (size_t)W);
+  rc = ensure_dev(&p->d_xsz, &p->xsz_bytes, 16 * (size_t)W + 8);
   if (rc) return rc;
   int64_t* tx = reinterpret_cast<int64_t*>(p->d_xsz);
   int64_t* rx = tx + W;
@@ -2698,41 +2716,68 @@ static int x_exchange_routed(ppr_plan* p, uint32_t it, const XRoute& xr) {
     p->x_rows_sent += xr.scnt[q][d];
   }
   std::vector<int64_t> hsz(2 * (size_t)W, 0);
+  // Every rank checks the block sizes it is about to receive and the ranks agree on the outcome
+  // BEFORE any block moves: a rank that bailed out alone would leave its peers blocked in their
+  // sends / receives (a grouped RCCL call cannot be abandoned half-posted).
+  auto size_ok = [&](int r, int64_t z) { return z >= 8 && (size_t)z <= ro[r + 1] - ro[r]; };
   if (p->lgroup) {
     LocalGroup& G = *p->lgroup;
     HIP_OK(hipMemcpyAsync(hsz.data(), tx, 8 * (size_t)W, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));  // this rank's blocks are complete
-    for (int d = 0; d < W; d++) { G.pbufs[me][d] = p->d_xsend + so[d]; G.psz[me][d] = xr.scnt[q][d] ? hsz[d] : 0; }
+    for (int d = 0; d < W; d++) {
+      G.pbufs[me][d] = p->d_xsend + so[d];
+      G.psz[me][d] = xr.scnt[q][d] ? hsz[d] + (me == p->xtest_badsize ? ((int64_t)1 << 40) : 0) : 0;
+    }
     if (!G.barrier()) return PPR_ERR_HIP;
+    int mine_ok = 1;
+    for (int r = 0; r < W; r++)
+      if (r != me && xr.rcnt[q][r] && !size_ok(r, G.psz[r][me])) mine_ok = 0;
+    G.ok[me] = mine_ok;
+    if (!G.barrier()) return PPR_ERR_HIP;
+    for (int r = 0; r < W; r++)
+      if (!G.ok[r]) return PPR_ERR_RANGE;  // (every rank returns here, none is left waiting)
     for (int r = 0; r < W; r++) {
       if (r == me || !xr.rcnt[q][r]) continue;
       const int64_t z = G.psz[r][me];
-      if (z < 8 || (size_t)z > ro[r + 1] - ro[r]) return PPR_ERR_HIP;  // (lists disagree)
       hsz[W + r] = z;
       HIP_OK(hipMemcpyAsync(p->d_xrecv + ro[r], G.pbufs[r][me], (size_t)z, hipMemcpyDeviceToDevice, s));
     }
     HIP_OK(hipStreamSynchronize(s));
     if (!G.barrier()) return PPR_ERR_HIP;  // no rank reuses its send buffer before all copied
   } else {
-    NCCL_OK(ncclGroupStart());
-    for (int d = 0; d < W; d++) {
-      if (d == me) continue;
-      if (xr.scnt[q][d]) NCCL_OK(ncclSend(tx + d, 1, ncclInt64, d, p->comm, s));
-      if (xr.rcnt[q][d]) NCCL_OK(ncclRecv(rx + d, 1, ncclInt64, d, p->comm, s));
+    if (me == p->xtest_badsize) {
+      HIP_OK(hipMemcpyAsync(hsz.data(), tx, 8 * (size_t)W, hipMemcpyDeviceToHost, s));
+      HIP_OK(hipStreamSynchronize(s));
+      for (int d = 0; d < W; d++) hsz[d] += (int64_t)1 << 40;
+      HIP_OK(hipMemcpyAsync(tx, hsz.data(), 8 * (size_t)W, hipMemcpyHostToDevice, s));
     }
-    NCCL_OK(ncclGroupEnd());
+    ncclResult_t nr = ncclGroupStart();
+    for (int d = 0; d < W && nr == ncclSuccess; d++) {
+      if (d == me) continue;
+      if (xr.scnt[q][d]) nr = ncclSend(tx + d, 1, ncclInt64, d, p->comm, s);
+      if (nr == ncclSuccess && xr.rcnt[q][d]) nr = ncclRecv(rx + d, 1, ncclInt64, d, p->comm, s);
+    }
+    const ncclResult_t ne = ncclGroupEnd();  // (always closed, whatever failed inside)
+    if (nr != ncclSuccess || ne != ncclSuccess) return PPR_ERR_HIP;
     HIP_OK(hipMemcpyAsync(hsz.data(), tx, 16 * (size_t)W, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    NCCL_OK(ncclGroupStart());
-    for (int d = 0; d < W; d++) {
+    int32_t* okd = reinterpret_cast<int32_t*>(rx + W);  // (d_xsz holds 2 W + 1 words)
+    int32_t mine_ok = 1;
+    for (int d = 0; d < W; d++)
+      if (d != me && xr.rcnt[q][d] && !size_ok(d, hsz[W + d])) mine_ok = 0;
+    HIP_OK(hipMemcpyAsync(okd, &mine_ok, 4, hipMemcpyHostToDevice, s));
+    NCCL_OK(ncclAllReduce(okd, okd, 1, ncclInt32, ncclMin, p->comm, s));
+    HIP_OK(hipMemcpyAsync(&mine_ok, okd, 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (!mine_ok) return PPR_ERR_RANGE;  // every rank saw the same minimum: none posts a block
+    nr = ncclGroupStart();
+    for (int d = 0; d < W && nr == ncclSuccess; d++) {
       if (d == me) continue;
-      if (xr.scnt[q][d]) NCCL_OK(ncclSend(p->d_xsend + so[d], (size_t)hsz[d], ncclUint8, d, p->comm, s));
-      if (xr.rcnt[q][d]) {
-        if (hsz[W + d] < 8 || (size_t)hsz[W + d] > ro[d + 1] - ro[d]) return PPR_ERR_HIP;
-        NCCL_OK(ncclRecv(p->d_xrecv + ro[d], (size_t)hsz[W + d], ncclUint8, d, p->comm, s));
-      }
+      if (xr.scnt[q][d]) nr = ncclSend(p->d_xsend + so[d], (size_t)hsz[d], ncclUint8, d, p->comm, s);
+      if (nr == ncclSuccess && xr.rcnt[q][d]) nr = ncclRecv(p->d_xrecv + ro[d], (size_t)hsz[W + d], ncclUint8, d, p->comm, s);
     }
-    NCCL_OK(ncclGroupEnd());
+    const ncclResult_t ne2 = ncclGroupEnd();
+    if (nr != ncclSuccess || ne2 != ncclSuccess) return PPR_ERR_HIP;
   }
   for (int r = 0; r < W; r++) {
     if (r == me || !xr.rcnt[q][r]) continue;

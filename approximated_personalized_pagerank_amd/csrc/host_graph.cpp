@@ -131,7 +131,18 @@ int ppr_find_partitions_csr(const ppr_csr* g, uint8_t* part) {
     for (auto& x : part_rest) rest.insert(rest.end(), x.begin(), x.end());
   }
   std::vector<std::vector<int32_t>> next(nth), keep(nth);
-  for (int32_t d = 0; !front.empty(); d++) {
+  // The bottom-up scan costs O(|rest|) per level, O(depth x n) in all: fine on small-diameter graphs
+  // (RMAT-22: ~20 levels), minutes on a long path or a road network. Once the scans have cost
+  // more than the graph itself, the predecessor lists are built once and the remaining levels go
+  // top-down over both edge directions (O(n + m) from there on).
+  double scanned = 0.0;
+  const double scan_cap = 2.0 * (double)(n + m) + 1e6;
+  std::vector<int64_t> prp;
+  std::vector<int32_t> pcol;
+  int32_t d = 0;
+  for (; !front.empty(); d++) {
+    if (scanned > scan_cap || getenv("PPR_BFS_TRANSPOSE")) break;
+    scanned += (double)rest.size();
     for (auto& x : next) x.clear();
     parallel_for((int64_t)front.size(), nth, [&](int64_t b, int64_t e, int t) {
       std::vector<int32_t>& out = next[t];
@@ -169,6 +180,39 @@ int ppr_find_partitions_csr(const ppr_csr* g, uint8_t* part) {
     for (auto& x : keep) rest.insert(rest.end(), x.begin(), x.end());
     front.clear();
     for (auto& x : next) front.insert(front.end(), x.begin(), x.end());
+  }
+  if (!front.empty()) {
+    // transposed mode: predecessor lists (counting sort by target), then plain top-down levels
+    // over successors and predecessors
+    prp.assign(n + 1, 0);
+    for (int64_t k = 0; k < m; k++) prp[col[k] + 1]++;
+    for (int64_t i = 0; i < n; i++) prp[i + 1] += prp[i];
+    pcol.resize(m > 0 ? m : 1);
+    {
+      std::vector<int64_t> fill(prp.begin(), prp.end() - 1);
+      for (int64_t v = 0; v < n; v++)
+        for (int64_t k = rp[v]; k < rp[v + 1]; k++) pcol[fill[col[k]]++] = (int32_t)v;
+    }
+    if (tm) fprintf(stderr, "ppr_timing partitions transposed_at_level %d\n", (int)d);
+    for (; !front.empty(); d++) {
+      for (auto& x : next) x.clear();
+      parallel_for((int64_t)front.size(), nth, [&](int64_t b, int64_t e, int t) {
+        std::vector<int32_t>& out = next[t];
+        auto visit = [&](int32_t s) {
+          int32_t expect = -1;
+          if (__atomic_load_n(&depth[s], __ATOMIC_RELAXED) == -1 &&
+              __atomic_compare_exchange_n(&depth[s], &expect, d + 1, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED))
+            out.push_back(s);
+        };
+        for (int64_t i = b; i < e; i++) {
+          const int32_t x = front[i];
+          for (int64_t k = rp[x]; k < rp[x + 1]; k++) visit(col[k]);
+          for (int64_t k = prp[x]; k < prp[x + 1]; k++) visit(pcol[k]);
+        }
+      });
+      front.clear();
+      for (auto& x : next) front.insert(front.end(), x.begin(), x.end());
+    }
   }
   parallel_for(n, nth, [&](int64_t b, int64_t e, int) {
     for (int64_t v = b; v < e; v++) part[v] = (uint8_t)(depth[v] & 1);

@@ -134,28 +134,25 @@ __device__ __forceinline__ int x2_slot(const X2Table& t, int key, bool& ins) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// One hash per key: hash32 (a bijection, so distinct keys never share it), which also places the
-// key in PT; a cheap derived word for the third sketch row and the PT prefilter. (Independent of
-// hash_b, which orders the stored rows.)
-struct SvHash {
-  uint32_t h, h2;
-};
-__device__ __forceinline__ SvHash sv_hash(int key) {
-  SvHash r;
-  r.h = hash32((uint32_t)key);
-  r.h2 = r.h * 0x85EBCA77u + 0x27D4EB2Fu;
-  r.h2 ^= r.h2 >> 15;
-  return r;
+// One cheap hash per key (full-rate 24-bit multiplies: v_mul_lo_u32 is a quarter-rate VALU op,
+// and the walk hashes every candidate twice). Its low bits place the key in PT, three bit fields
+// give its sketch cells. (Independent of hash_b, which orders the stored rows; the quality only
+// moves the false-positive rate, never the result.)
+__device__ __forceinline__ uint32_t sv_mix(uint32_t x) {
+  x ^= x >> 16;                    // (bits 24-31 reach the 24-bit multiply through bits 8-15)
+  x = __umul24(x, 0x9E3779u);
+  x ^= x >> 13;
+  x = __umul24(x, 0x5BD1E9u) ^ (x >> 24);
+  x ^= x >> 15;
+  return x;
 }
-// sketch cell of row j (rows of 2^wlog counters, wlog <= 13)
-__device__ __forceinline__ uint32_t sv_cell(const SvHash& k, int j, int wlog) {
+// sketch cell of row j (rows of 2^wlog counters, wlog <= 13): bits 0.., bits 13.., and a 24-bit
+// product of the rest
+__device__ __forceinline__ uint32_t sv_cell(uint32_t h, int j, int wlog) {
   const uint32_t m = (1u << wlog) - 1u;
-  const uint32_t c = j == 0 ? (k.h & m) : j == 1 ? ((k.h >> 13) & m) : (k.h2 >> (32 - wlog));
+  const uint32_t c = j == 0 ? (h & m) : j == 1 ? ((h >> 13) & m) : ((uint32_t)__umul24(h ^ (h >> 19), 0x2C1B3Du) >> (32 - wlog));
   return ((uint32_t)j << wlog) + c;
 }
-// PT prefilter: one of 4096 bits per key; a clear bit proves the key is not a prev key
-constexpr int SV_BLOOM_WORDS = 128;
-__device__ __forceinline__ uint32_t sv_bloom_bit(const SvHash& k) { return (k.h2 >> 4) & 4095u; }
 // an upper bound of p * 2^31 in counter units: fl(p) is within 2^-24 relative of p, the factor
 // 2^31 (1 + 2^-20) -- exact in single precision -- and the +1 after the truncation cover that and
 // the product's rounding (f >= p 2^31 (1 + 2^-20)(1 - 2^-24)^2 > p 2^31)
@@ -170,30 +167,105 @@ __device__ __forceinline__ uint32_t sv_thr(double theta) {
   const double x = floor(ldexp(theta, SV_UNIT_LOG) * (1.0 - 0x1p-40));
   return x <= 0.0 ? 0u : x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
 }
-__device__ __forceinline__ void sv_sketch_add(uint32_t* sk, const SvHash& k, uint32_t u, int wlog) {
+__device__ __forceinline__ void sv_sketch_add(uint32_t* sk, uint32_t h, uint32_t u, int wlog) {
 #pragma unroll
-  for (int j = 0; j < SV_R; j++) atomicAdd(&sk[sv_cell(k, j, wlog)], u);
+  for (int j = 0; j < SV_R; j++) atomicAdd(&sk[sv_cell(h, j, wlog)], u);
 }
 // every counter of the key at or above the threshold (bitmap of the counters that are; the three
 // words are read together)
-__device__ __forceinline__ bool sv_passes(const uint32_t* bm, const SvHash& k, int wlog) {
+__device__ __forceinline__ bool sv_passes(const uint32_t* bm, uint32_t h, int wlog) {
   uint32_t w[SV_R], c[SV_R];
 #pragma unroll
-  for (int j = 0; j < SV_R; j++) { c[j] = sv_cell(k, j, wlog); w[j] = bm[c[j] >> 5]; }
+  for (int j = 0; j < SV_R; j++) { c[j] = sv_cell(h, j, wlog); w[j] = bm[c[j] >> 5]; }
   return ((w[0] >> (c[0] & 31u)) & (w[1] >> (c[1] & 31u)) & (w[2] >> (c[2] & 31u)) & 1u) != 0u;
 }
-// PT membership: the prefilter bit, then the probe from the key's hash
-__device__ __forceinline__ int x2_find_h(const X2Table& t, int key, uint32_t h) {
-  const uint32_t tag = (uint32_t)key + 1u;
-  uint32_t g = h & t.mask & ~3u;
-  for (uint32_t n = 0; n <= t.mask; n += 4) {
-    const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g);
-    const int m = xt_match(q, g, tag);
-    if (m >= 0) return m;
-    if (q.x == 0u || q.y == 0u || q.z == 0u || q.w == 0u) return -1;
-    g = (g + 4u) & t.mask;
+// The split accumulator's two addends of one contribution p = fl(s * f), from t = p * 2^61:
+// X = floor(p * 2^93) (merge_xs.h xs_conv), A = X mod 2^32, B = X >> 32 = floor(t). t is exact
+// (a power-of-two scale), and so is t = fl(s * (f * 2^61)) -- rounding commutes with the scale
+// (for p below 2^-93, where the two could differ in the subnormal range, X = 0 either way). No
+// integer shifts and no branches: B's words are two truncating conversions, and t - B < 2^32 and
+// its fraction are exact (they are multiples of ulp(t)), so A = trunc(frac(t) * 2^32).
+__device__ __forceinline__ void sv_split_t(double t, unsigned long long& A, unsigned long long& B) {
+  const uint32_t bh = (uint32_t)(t * 0x1p-32);             // t < 2^63 (p < 4)
+  const double r = t - (double)bh * 0x1p32;                // [0, 2^32), exact
+  const uint32_t bl = (uint32_t)r;
+  A = (unsigned long long)(uint32_t)((r - (double)bl) * 0x1p32);
+  B = ((unsigned long long)bh << 32) | bl;
+}
+__device__ __forceinline__ void sv_split_add_t(unsigned long long* a, unsigned long long* b, int i, double t) {
+  unsigned long long A, B;
+  sv_split_t(t, A, B);
+  atomicAdd(&a[i], A);
+  atomicAdd(&b[i], B);
+}
+__device__ __forceinline__ void sv_split_add(unsigned long long* a, unsigned long long* b, int i, double p) {
+  sv_split_add_t(a, b, i, p * 0x1p61);
+}
+// counter units of t = p * 2^61: an upper bound of p * 2^31 (sv_units). GRank contributions are
+// <= 1, so f < 2^31 + 2^12 and the conversion never saturates.
+__device__ __forceinline__ uint32_t sv_units_t(double t) {
+  const float f = (float)t * 0x1.00001p-30f;
+  return (uint32_t)f + 1u;
+}
+
+// ---------------------------------------------------------------------------------------------
+// PT: the L keys of the source's current row, in T = 4 Lp slots probed as aligned groups of four
+// (one ds_read_b128 from the key's home group: load 1/4, so a home group rarely fills). A key that
+// found its home group full sits in the next group with room, and bit 31 of the home group's first
+// tag word says so -- a lookup continues past its home group only then (< 1 % of the groups; keys
+// and their tags (key + 1) stay below 2^31). Accumulators are indexed by slot; slots T .. T + 63 are
+// per-lane dummies, so a lane whose key is not in PT adds there instead of branching around the add.
+struct SvPt {
+  uint32_t* keys;            // [T] key + 1 (0 = empty); bit 31 of word 4 g: home group g overflowed
+  unsigned long long* a;     // [T + 64] split accumulators (A: low 32 bits of each X_i; B: X_i >> 32)
+  unsigned long long* b;     // [T + 64]
+  int* pos;                  // [T] row position of the slot's key
+  int T;
+  uint32_t gmask;            // T / 4 - 1
+};
+__host__ __device__ constexpr size_t svpt_bytes(int Lp) { return (size_t)4 * Lp * 24 + 64 * 16; }
+__device__ __forceinline__ SvPt svpt_carve(unsigned char* p, int Lp) {
+  SvPt t;
+  t.T = 4 * Lp;
+  t.a = reinterpret_cast<unsigned long long*>(p); p += (size_t)(t.T + 64) * 8;
+  t.b = reinterpret_cast<unsigned long long*>(p); p += (size_t)(t.T + 64) * 8;
+  t.keys = reinterpret_cast<uint32_t*>(p); p += (size_t)t.T * 4;
+  t.pos = reinterpret_cast<int*>(p);
+  t.gmask = (uint32_t)(t.T / 4) - 1u;
+  return t;
+}
+constexpr uint32_t SV_OVF_BIT = 0x80000000u;
+// the slot of tag past its home group g4 (the group overflowed): groups in order until the tag or
+// an empty slot (the key would have taken it)
+__device__ __forceinline__ int svpt_find_from(const SvPt& t, uint32_t tag, uint32_t g4) {
+  for (int n = 0; n < (int)t.gmask + 1; n++) {
+    g4 = (g4 + 4u) & (uint32_t)(t.T - 1);
+    const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g4);
+    const uint32_t x = q.x & ~SV_OVF_BIT;
+    if (x == tag) return (int)g4;
+    if (q.y == tag) return (int)g4 + 1;
+    if (q.z == tag) return (int)g4 + 2;
+    if (q.w == tag) return (int)g4 + 3;
+    if (x == 0u || q.y == 0u || q.z == 0u || q.w == 0u) return -1;
   }
   return -1;
+}
+// the PT slot of `key` (hash h) or -1; `active` lanes only take the rare continuation. Wave-wide:
+// every lane of the wave must call it (one ballot).
+__device__ __forceinline__ int svpt_slot(const SvPt& t, int key, uint32_t h, bool active) {
+  const uint32_t tag = (uint32_t)key + 1u;
+  const uint32_t g4 = (h & t.gmask) << 2;
+  const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g4);
+  int m = q.w == tag ? 3 : -1;
+  m = q.z == tag ? 2 : m;
+  m = q.y == tag ? 1 : m;
+  m = (q.x & ~SV_OVF_BIT) == tag ? 0 : m;
+  int slot = m >= 0 ? (int)g4 + m : -1;
+  const bool more = active && m < 0 && (q.x & SV_OVF_BIT);
+  if (__builtin_expect(__ballot(more) != 0ull, 0)) {
+    if (more) slot = svpt_find_from(t, tag, g4);
+  }
+  return slot;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -211,18 +283,15 @@ struct SvDesc {
 struct SvTask { int32_t d; int32_t k; };
 
 // LDS of the slice / single-source workgroups:
-//   region (sketch in pass 1; XT in pass 2; dense (value, key) list in the select)
-//   PT (2 Lp slots) | pti i32[2 Lp] (prev-row position of a PT slot) | PT prefilter u32[128] |
-//   bitmap u64[bm_words] | misc i32[64] | hist u32[256] (block select)
-enum { SVM_FILL = 0, SVM_OVF = 1, SVM_U = 2, SVM_PT = 3, SVM_THETA = 8 /* u64: 8..9 */ };
+//   region (sketch in pass 1; XT in pass 2; dense (value, key) list in the select) | PT (svpt_bytes)
+//   | bitmap u64[bm_words] | misc i32[64] | hist u32[256] (block select)
+enum { SVM_FILL = 0, SVM_OVF = 1, SVM_U = 2, SVM_PT = 3, SVM_ROWS = 4, SVM_THETA = 8 /* u64: 8..9 */ };
 __host__ __device__ constexpr size_t sv_lds_bytes(int Lp, SvGeom G) {
-  return G.region() + x2_bytes(2 * Lp) + (size_t)8 * Lp + 4 * SV_BLOOM_WORDS + (size_t)G.bm_words() * 8 + 256 + 1024;
+  return G.region() + svpt_bytes(Lp) + (size_t)G.bm_words() * 8 + 256 + 1024;
 }
 struct SvLds {
   unsigned char* region;
-  X2Table pt;
-  int* pti;
-  uint32_t* ptb;
+  SvPt pt;
   uint64_t* bm;
   int* misc;
   uint32_t* hist;
@@ -233,9 +302,7 @@ __device__ __forceinline__ SvLds sv_carve(unsigned char* smem, int Lp, SvGeom G)
   SvLds x;
   unsigned char* p = smem;
   x.region = p; p += G.region();
-  x.pt = x2_carve(p, 2 * Lp); p += x2_bytes(2 * Lp);
-  x.pti = reinterpret_cast<int*>(p); p += (size_t)8 * Lp;
-  x.ptb = reinterpret_cast<uint32_t*>(p); p += 4 * SV_BLOOM_WORDS;
+  x.pt = svpt_carve(p, Lp); p += svpt_bytes(Lp);
   x.bm = reinterpret_cast<uint64_t*>(p); p += (size_t)G.bm_words() * 8;
   x.misc = reinterpret_cast<int*>(p); p += 256;
   x.hist = reinterpret_cast<uint32_t*>(p);
@@ -251,12 +318,11 @@ __device__ __forceinline__ void sv_lap(const IterArgs& a, int slot, long long& t
   t = now;
 }
 
-// the current row of v (L distinct keys) into PT with zeroed sums and its prefilter bits; misc
-// cleared; pti = row position
+// the current row of v (L distinct keys) into PT with zeroed sums (dummies included); misc cleared
 __device__ __forceinline__ void sv_build_pt(const SvLds& x, const DevSlab& s, const IterArgs& a, int v, int Lp) {
-  const int T = 2 * Lp;
-  for (int i = threadIdx.x; i < T; i += blockDim.x) { x.pt.keys[i] = 0u; x.pt.a[i] = 0ull; x.pt.b[i] = 0ull; }
-  for (int i = threadIdx.x; i < SV_BLOOM_WORDS; i += blockDim.x) x.ptb[i] = 0u;
+  const SvPt& t = x.pt;
+  for (int i = threadIdx.x; i < t.T; i += blockDim.x) t.keys[i] = 0u;
+  for (int i = threadIdx.x; i < t.T + 64; i += blockDim.x) { t.a[i] = 0ull; t.b[i] = 0ull; }
   if (threadIdx.x < 64) x.misc[threadIdx.x] = 0;
   __syncthreads();
   const int cur = (a.active == 1) ? a.sB : a.sA;
@@ -264,53 +330,34 @@ __device__ __forceinline__ void sv_build_pt(const SvLds& x, const DevSlab& s, co
   const int len = s.len[s.lrow(cur, v)];
   for (int i = threadIdx.x; i < len; i += blockDim.x) {
     const int key = s.key(s.ids[r + i]);
-    bool ins;
-    const int h = x2_slot(x.pt, key, ins);
-    if (h >= 0) x.pti[h] = i;
-    const uint32_t bit = sv_bloom_bit(sv_hash(key));
-    atomicOr(&x.ptb[bit >> 5], 1u << (bit & 31u));
+    const uint32_t tag = (uint32_t)key + 1u;
+    const uint32_t home = (sv_mix((uint32_t)key) & t.gmask) << 2;
+    uint32_t g4 = home;
+    for (int n = 0; n <= (int)t.gmask; n++) {  // (T = 4 L slots: a free slot always exists)
+      int got = -1;
+#pragma unroll
+      for (int j = 0; j < 4 && got < 0; j++)
+        if (atomicCAS(&t.keys[g4 + j], 0u, tag) == 0u) got = (int)g4 + j;
+      if (got >= 0) { t.pos[got] = i; break; }
+      if (g4 == home) atomicOr(&t.keys[home], SV_OVF_BIT);  // (its first word is taken: never reads 0)
+      g4 = (g4 + 4u) & (uint32_t)(t.T - 1);
+    }
   }
-}
-// the key's PT slot (-1: not a prev key): the prefilter bit, then the key's group of four matched
-// with selects (no branches); an empty slot in the group ends the search, a full group (PT is half
-// full: a few per cent of the keys) probes on
-__device__ __forceinline__ int x2_find_from(const X2Table& t, uint32_t tag, uint32_t g) {
-  for (uint32_t n = 0; n <= t.mask; n += 4) {
-    const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g);
-    const int m = xt_match(q, g, tag);
-    if (m >= 0) return m;
-    if (q.x == 0u || q.y == 0u || q.z == 0u || q.w == 0u) return -1;
-    g = (g + 4u) & t.mask;
-  }
-  return -1;
-}
-__device__ __forceinline__ int sv_pt_slot(const SvLds& x, int key, const SvHash& k) {
-  const uint32_t bit = sv_bloom_bit(k);
-  if (!((x.ptb[bit >> 5] >> (bit & 31u)) & 1u)) return -1;
-  const uint32_t tag = (uint32_t)key + 1u;
-  const uint32_t g = k.h & x.pt.mask & ~3u;
-  const uint4 q = *reinterpret_cast<const uint4*>(x.pt.keys + g);
-  int m = q.w == tag ? (int)g + 3 : -1;
-  m = q.z == tag ? (int)g + 2 : m;
-  m = q.y == tag ? (int)g + 1 : m;
-  m = q.x == tag ? (int)g : m;
-  if (m < 0 && min(min(q.x, q.y), min(q.z, q.w)) != 0u) m = x2_find_from(x.pt, tag, (g + 4u) & x.pt.mask);
-  return m;
 }
 
 // The wave's share of a slice: contiguous successors [c0, c1) taken row by row. Row metadata comes
 // per window of 64 successors, one successor per lane (colx two windows ahead, lengths one window
-// ahead, so neither load is waited on); a row's base and length are then read off its lane
-// (readlane: wave-uniform). A lane takes entries lane and 64 + lane of each row (rows of up to 128
-// entries; longer rows' further groups one at a time after the batch), so no lane looks up which
-// row it reads. NS rows a batch, the next batch's loads in flight while fb(valid[], key[], score[],
-// row base[]) uses the current one (slab index of group k = base[k / 2] + 64 (k & 1) + lane);
-// scores are loaded only with kScores.
+// ahead); a row's base and length are read off its lane into scalar registers. A lane takes
+// entries lane and 64 + lane of each row (rows of up to 128 entries; longer rows' further groups
+// one at a time after the batch), loads issued unconditionally inside the row (a row slot always
+// holds L entries: lanes past the row's length read stale entries and are masked, no exec branch).
+// NS rows a batch, the next batch's loads in flight while fb(key, score, valid) takes the current
+// batch's groups; scores are loaded only with kScores. Every branch here is wave-uniform.
 template <int NS>
 struct SvBatch {
-  bool valid[2 * NS];
   int key[2 * NS];
   double sv[2 * NS];
+  int rl[NS];        // row length (0: no row)
   int64_t base[NS];
 };
 __device__ __forceinline__ int64_t sv_readlane64(int64_t x, int lane) {
@@ -323,7 +370,7 @@ __device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, con
                                         FB fb) {
   const int lane = lane_id();
   const int L = s.L;
-  // window metadata: cx of windows w + 1 (ncx) and w + 2 (nncx) in flight, length of w + 1 (nln)
+  const int lcl = lane < L ? lane : 0;  // (rows narrower than a wave: stay inside the row slot)
   auto colx_at = [&](int64_t w0) { return w0 + lane < c1 ? g.colx[w0 + lane] : (int32_t)-1; };
   auto len_of = [&](int32_t cx) { return cx == -1 ? 0 : s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)]; };
   auto base_of = [&](int32_t cx) { return cx == -1 ? (int64_t)0 : s.row(read_slot(a, cx), cx & 0x7fffffff); };
@@ -341,52 +388,53 @@ __device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, con
     auto load = [&](int q0, SvBatch<NS>& bt) {
 #pragma unroll
       for (int q = 0; q < NS; q++) {
-        const int qq = q0 + q < nrows ? q0 + q : nrows - 1;  // (past the window: row nrows - 1 again, masked)
-        const int rl = q0 + q < nrows ? __builtin_amdgcn_readlane(ln, qq) : 0;
-        bt.base[q] = sv_readlane64(base, qq);
+        const bool has = q0 + q < nrows;
+        const int qq = has ? q0 + q : 0;
+        bt.rl[q] = has ? __builtin_amdgcn_readlane(ln, qq) : 0;
+        bt.base[q] = has ? sv_readlane64(base, qq) : (int64_t)0;  // (row 0: a valid address)
+        bt.key[2 * q] = s.ids[bt.base[q] + lcl];
+        if (kScores) bt.sv[2 * q] = s.sc[bt.base[q] + lcl];
+        if (bt.rl[q] > WAVE) {
+          bt.key[2 * q + 1] = s.ids[bt.base[q] + WAVE + lane];
+          if (kScores) bt.sv[2 * q + 1] = s.sc[bt.base[q] + WAVE + lane];
+        } else {
+          bt.key[2 * q + 1] = 0;
+          if (kScores) bt.sv[2 * q + 1] = 0.0;
+        }
+      }
+    };
+    auto run = [&](const SvBatch<NS>& bt) {
 #pragma unroll
-        for (int hh = 0; hh < 2; hh++) {
-          const int k = 2 * q + hh;
-          const int idx = hh * WAVE + lane;
-          bt.valid[k] = idx < rl;
-          bt.key[k] = bt.valid[k] ? ld_nt(&s.ids[bt.base[q] + idx], a.nt & 1u) : 0;
-          bt.sv[k] = (kScores && bt.valid[k]) ? ld_nt(&s.sc[bt.base[q] + idx], a.nt & 1u) : 0.0;
+      for (int k = 0; k < 2 * NS; k++) {
+        const int rl = bt.rl[k >> 1];
+        if (rl <= (k & 1) * WAVE) continue;
+        fb(bt.key[k], kScores ? bt.sv[k] : 0.0, (k & 1) * WAVE + lane < rl, bt.base[k >> 1] + (k & 1) * WAVE + lane);
+      }
+      if (L > 2 * WAVE) {  // rows beyond two groups (L > 128 only)
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+          const int rl = bt.rl[q];
+          for (int i0 = 2 * WAVE; i0 < rl; i0 += WAVE) {
+            const int64_t idx = bt.base[q] + i0 + lane;
+            const bool ok = i0 + lane < rl;
+            fb(ok ? s.ids[idx] : 0, (kScores && ok) ? s.sc[idx] : 0.0, ok, idx);
+          }
         }
       }
     };
     // two batch buffers in turn (no per-batch copy of one into the other); sched_barrier keeps the
     // next batch's loads ahead of this batch's work without pulling its first uses up
-    auto tail = [&](const SvBatch<NS>& cur, int q0) {
-      if (L > 2 * WAVE) {  // rows beyond two groups (L > 128 only)
-        for (int q = 0; q < NS && q0 + q < nrows; q++) {
-          const int rl = __builtin_amdgcn_readlane(ln, q0 + q);
-          for (int i0 = 2 * WAVE; i0 < rl; i0 += WAVE) {
-            SvBatch<NS> t;
-#pragma unroll
-            for (int k = 0; k < 2 * NS; k++) { t.valid[k] = false; t.key[k] = 0; t.sv[k] = 0.0; }
-#pragma unroll
-            for (int k = 0; k < NS; k++) t.base[k] = cur.base[q] + i0;
-            t.valid[0] = i0 + lane < rl;
-            t.key[0] = t.valid[0] ? s.ids[t.base[0] + lane] : 0;
-            t.sv[0] = (kScores && t.valid[0]) ? s.sc[t.base[0] + lane] : 0.0;
-            fb(t);
-          }
-        }
-      }
-    };
     SvBatch<NS> ba, bb;
     load(0, ba);
     for (int q0 = 0; q0 < nrows; q0 += 2 * NS) {
       if (q0 + NS < nrows) load(q0 + NS, bb);
       __builtin_amdgcn_sched_barrier(0);
-      fb(ba);
-      tail(ba, q0);
+      run(ba);
       __builtin_amdgcn_sched_barrier(0);
       if (q0 + NS >= nrows) break;
       if (q0 + 2 * NS < nrows) load(q0 + 2 * NS, ba);
       __builtin_amdgcn_sched_barrier(0);
-      fb(bb);
-      tail(bb, q0 + NS);
+      run(bb);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
@@ -405,117 +453,107 @@ __device__ __forceinline__ void sv_chunk(int64_t b0, int64_t b1, int64_t& c0, in
   c1 = sv_uniform(min(b1, c0 + chunk));
 }
 
-// pass 1 over successors [b0, b1): prev keys exactly into PT, every other key into the sketch
-constexpr int SV_NS1 = 4, SV_NS2 = 4;  // rows per batch in pass 1 (keys and scores) and pass 2 (keys)
+// pass 1 over successors [b0, b1): prev keys exactly into PT, every other key into the sketch.
+// Branch-free per group: the PT probe for every lane, the split add to the key's PT slot or the
+// lane's dummy slot, the sketch adds with 0 units for PT keys and masked lanes.
+#ifndef PPR_SV_NS1
+#define PPR_SV_NS1 4
+#endif
+#ifndef PPR_SV_NS2
+#define PPR_SV_NS2 8
+#endif
+// rows per batch in pass 1 (keys and scores) and pass 2 (keys only: a lighter group, so more rows
+// in flight to cover the gather latency); build-time knobs for A/B variants (tools/build_variant.py)
+constexpr int SV_NS1 = PPR_SV_NS1, SV_NS2 = PPR_SV_NS2;
 __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
                                          int64_t b0, int64_t b1, double factor, uint32_t* sk) {
   int64_t c0, c1;
   sv_chunk(b0, b1, c0, c1);
-  sv_rows<true, SV_NS1>(g, s, a, c0, c1, [&](const SvBatch<SV_NS1>& bt) {
-#pragma unroll
-    for (int k = 0; k < 2 * SV_NS1; k++) {
-      if (!__ballot(bt.valid[k])) continue;
-      const SvHash hk = sv_hash(bt.key[k]);
-      const int h = bt.valid[k] ? sv_pt_slot(x, bt.key[k], hk) : -2;
-      const double p = bt.sv[k] * factor;
-      if (h >= 0) {
-        unsigned long long lo;
-        uint32_t hi;
-        xs_conv(p, lo, hi);
-        x2_add(x.pt, h, lo, hi);
-      } else if (h == -1) {
-        sv_sketch_add(sk, hk, sv_units(p), x.wlog);
-      }
-    }
+  const int dummy = x.pt.T + lane_id();
+  const double f61 = factor * 0x1p61;
+  sv_rows<true, SV_NS1>(g, s, a, c0, c1, [&](int key, double sc, bool valid, int64_t) {
+    const uint32_t h = sv_mix((uint32_t)key);
+    const int slot = svpt_slot(x.pt, key, h, valid);
+    const bool inpt = valid && slot >= 0;
+    const double t = sc * f61;  // p * 2^61, exact (sv_split_t)
+    sv_split_add_t(x.pt.a, x.pt.b, inpt ? slot : dummy, t);
+    sv_sketch_add(sk, h, (valid && !inpt) ? sv_units_t(t) : 0u, x.wlog);
   });
 }
 
 // pass 2 over successors [b0, b1): keys outside PT that pass the sieve, exactly into XT (budget
 // checked before every group that inserts; past it the workgroup only flags the overflow). Per
-// batch: the sieve tests of all its groups (the PT check only for passing lanes), then the passing
-// candidates' scores (loads in flight together), then the inserts.
+// group the sieve test (three bitmap words) for every lane without a branch; a group with a
+// passing lane (a small minority) then checks PT, loads the passing scores and inserts.
 __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
                                          const X2Table& xt, int64_t b0, int64_t b1, double factor, int budget) {
   int64_t c0, c1;
   sv_chunk(b0, b1, c0, c1);
   const uint32_t* bm32 = reinterpret_cast<const uint32_t*>(x.bm);
-  const int lane = lane_id();
-  sv_rows<false, SV_NS2>(g, s, a, c0, c1, [&](const SvBatch<SV_NS2>& bt) {
-    constexpr int NG = 2 * SV_NS2;
-    bool want[NG];
-    bool any = false;
-#pragma unroll
-    for (int k = 0; k < NG; k++) {
-      const SvHash hk = sv_hash(bt.key[k]);
-      want[k] = bt.valid[k] && sv_passes(bm32, hk, x.wlog);
-      if (__ballot(want[k]) && want[k]) want[k] = sv_pt_slot(x, bt.key[k], hk) < 0;
-      any = any || want[k];
+  const double f61 = factor * 0x1p61;
+  sv_rows<false, SV_NS2>(g, s, a, c0, c1, [&](int key, double, bool valid, int64_t idx) {
+    const uint32_t h = sv_mix((uint32_t)key);
+    bool want = valid && sv_passes(bm32, h, x.wlog);
+    if (__builtin_expect(__ballot(want) == 0ull, 1)) return;
+    want = want && svpt_slot(x.pt, key, h, want) < 0;
+    if (!__ballot(want)) return;
+    const double sc = want ? s.sc[idx] : 0.0;
+    if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
+      if (lane_id() == 0) x.misc[SVM_OVF] = 1;
+      return;
     }
-    if (!__ballot(any)) return;
-    double sv[NG];
-#pragma unroll
-    for (int k = 0; k < NG; k++)
-      sv[k] = want[k] ? ld_nt(&s.sc[bt.base[k >> 1] + (k & 1) * WAVE + lane], a.nt & 1u) : 0.0;
-#pragma unroll
-    for (int k = 0; k < NG; k++) {
-      if (!__ballot(want[k])) continue;
-      if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
-        if (lane_id() == 0) x.misc[SVM_OVF] = 1;
-        return;
-      }
-      bool ins = false;
-      int h = -1;
-      if (want[k]) h = x2_slot(xt, bt.key[k], ins);
-      const int nins = __popcll(__ballot(ins));
-      if (nins && lane_id() == 0) atomicAdd(&x.misc[SVM_FILL], nins);
-      if (__ballot(want[k] && h < 0) && lane_id() == 0) x.misc[SVM_OVF] = 1;
-      if (h >= 0) {
-        unsigned long long lo;
-        uint32_t hi;
-        xs_conv(sv[k] * factor, lo, hi);
-        x2_add(xt, h, lo, hi);
-      }
-      if (a.diag && lane_id() == 0) diag_add(a.diag, 138, (unsigned long long)__popcll(__ballot(want[k])));
-    }
+    bool ins = false;
+    int hs = -1;
+    if (want) hs = x2_slot(xt, key, ins);
+    const int nins = __popcll(__ballot(ins));
+    if (nins && lane_id() == 0) atomicAdd(&x.misc[SVM_FILL], nins);
+    if (__ballot(want && hs < 0) && lane_id() == 0) x.misc[SVM_OVF] = 1;
+    if (hs >= 0) sv_split_add_t(xt.a, xt.b, hs, sc * f61);
+    if (a.diag && lane_id() == 0) diag_add(a.diag, 138, (unsigned long long)__popcll(__ballot(want)));
   });
 }
 
-// the self seed (1 - d) of v: into PT when v is a prev key, else into the sketch (pass 1)
+// the self seed (1 - d) of v: into PT when v is a prev key, else into the sketch (pass 1; one thread)
+__device__ __forceinline__ int svpt_slot1(const SvPt& t, int key) {
+  const uint32_t tag = (uint32_t)key + 1u;
+  const uint32_t g4 = (sv_mix((uint32_t)key) & t.gmask) << 2;
+  const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g4);
+  if ((q.x & ~SV_OVF_BIT) == tag) return (int)g4;
+  if (q.y == tag) return (int)g4 + 1;
+  if (q.z == tag) return (int)g4 + 2;
+  if (q.w == tag) return (int)g4 + 3;
+  return (q.x & SV_OVF_BIT) ? svpt_find_from(t, tag, g4) : -1;
+}
 __device__ __forceinline__ void sv_seed1(const SvLds& x, int v, double seed, uint32_t* sk) {
-  const SvHash hk = sv_hash(v);
-  const int h = sv_pt_slot(x, v, hk);
-  if (h >= 0) {
-    unsigned long long lo;
-    uint32_t hi;
-    xs_conv(seed, lo, hi);
-    x2_add(x.pt, h, lo, hi);
-  } else {
-    sv_sketch_add(sk, hk, sv_units(seed), x.wlog);
-  }
+  const int h = svpt_slot1(x.pt, v);
+  if (h >= 0) sv_split_add(x.pt.a, x.pt.b, h, seed);
+  else sv_sketch_add(sk, sv_mix((uint32_t)v), sv_units(seed), x.wlog);
 }
 // ... and into XT in pass 2 when v is not a prev key and passes
 __device__ __forceinline__ void sv_seed2(const SvLds& x, const X2Table& xt, int v, double seed) {
-  const SvHash hk = sv_hash(v);
-  if (sv_pt_slot(x, v, hk) >= 0 || !sv_passes(reinterpret_cast<const uint32_t*>(x.bm), hk, x.wlog)) return;
+  if (svpt_slot1(x.pt, v) >= 0 || !sv_passes(reinterpret_cast<const uint32_t*>(x.bm), sv_mix((uint32_t)v), x.wlog)) return;
   bool ins;
   const int h = x2_slot(xt, v, ins);
   if (h < 0) { x.misc[SVM_OVF] = 1; return; }
   if (ins) atomicAdd(&x.misc[SVM_FILL], 1);
-  unsigned long long lo;
-  uint32_t hi;
-  xs_conv(seed, lo, hi);
-  x2_add(xt, h, lo, hi);
+  sv_split_add(xt.a, xt.b, h, seed);
 }
 
-// sieve bitmap: bit c = counter c >= thr (one ballot per 64 counters)
+// sieve bitmap: bit c = counter c >= thr (one ballot per 64 counters); misc[SVM_ROWS] bit j = row j
+// has a set bit (a row without one proves that no key outside PT passes: pass 2 is skipped)
 template <class Get>
 __device__ __forceinline__ void sv_bitmap(const SvLds& x, uint32_t thr, Get get) {
   const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
+  const int per_row = x.bm_words / SV_R;
+  int rows = 0;
   for (int w = wv; w < x.bm_words; w += W) {
     const uint64_t m = __ballot(get(w * 64 + lane_id()) >= thr);
     if (lane_id() == 0) x.bm[w] = m;
+    if (m) rows |= 1 << (w / per_row);
   }
+  if (lane_id() == 0 && rows) atomicOr(&x.misc[SVM_ROWS], rows);
 }
+__device__ __forceinline__ bool sv_rows_all(const SvLds& x) { return x.misc[SVM_ROWS] == (1 << SV_R) - 1; }
 
 // theta = the smallest of the L prev totals (value bits; every value >= 0), published in misc
 template <class Val>
@@ -569,9 +607,9 @@ __device__ __forceinline__ void sv1_source(unsigned char* smem, DevGraph g, DevS
   __syncthreads();
   sv_lap(a, dg + 1, tph);
   // bound: the smallest exact total of the L prev keys
-  const int Tpt = 2 * Lp;
+  const int Tpt = x.pt.T;
   const double theta = sv_theta(x, Tpt, [&](int i) {
-    return x.pt.keys[i] ? x2_value(x.pt.a[i], x.pt.b[i]) : bitsd(~0ull >> 1);  // (empty: above every value)
+    return (x.pt.keys[i] & ~SV_OVF_BIT) ? x2_value(x.pt.a[i], x.pt.b[i]) : bitsd(~0ull >> 1);  // (empty: above every value)
   });
   const uint32_t thr = sv_thr(theta);
   sv_bitmap(x, thr, [&](int c) { return sk[c]; });
@@ -580,9 +618,15 @@ __device__ __forceinline__ void sv1_source(unsigned char* smem, DevGraph g, DevS
   sv_clear_region(x, x2_bytes(G.xt));
   __syncthreads();
   sv_lap(a, dg + 2, tph);
-  if (threadIdx.x == 0) sv_seed2(x, xt, v, 1.0 - a.damping);
-  sv_pass2(g, s, a, x, xt, b, e, factor, budget);
-  __syncthreads();
+  // a sketch row with no counter at or above thr: no key outside PT can pass, pass 2 would insert
+  // nothing (exact skip)
+  if (sv_rows_all(x)) {
+    if (threadIdx.x == 0) sv_seed2(x, xt, v, 1.0 - a.damping);
+    sv_pass2(g, s, a, x, xt, b, e, factor, budget);
+    __syncthreads();
+  } else if (a.diag && threadIdx.x == 0) {
+    diag_add(a.diag, 145, 1ull);
+  }
   sv_lap(a, dg + 3, tph);
   if (a.diag && threadIdx.x == 0) { diag_add(a.diag, dg + 5, 1ull); diag_add(a.diag, dg + 6, (unsigned long long)(e - b)); }
   if (x.misc[SVM_OVF] || x.misc[SVM_FILL] > budget + G.waves * WAVE) {
@@ -618,12 +662,13 @@ __device__ __forceinline__ void sv1_source(unsigned char* smem, DevGraph g, DevS
     if (xk[j] >= 0) { dv[base] = xv[j]; dk[base] = xk[j]; base++; }
   for (int i0 = 0; i0 < Tpt; i0 += blockDim.x) {
     const int i = i0 + (int)threadIdx.x;
-    const bool has = i < Tpt && x.pt.keys[i] != 0u;
+    const uint32_t kt = i < Tpt ? (x.pt.keys[i] & ~SV_OVF_BIT) : 0u;
+    const bool has = kt != 0u;
     const uint64_t m = __ballot(has);
     int b0 = 0;
     if (m && lane_id() == 0) b0 = atomicAdd(&x.misc[SVM_U], __popcll(m));
     b0 = __shfl(b0, 0) + __popcll(m & lanemask_lt());
-    if (has) { dv[b0] = x2_value(x.pt.a[i], x.pt.b[i]); dk[b0] = (int)x.pt.keys[i] - 1; }
+    if (has) { dv[b0] = x2_value(x.pt.a[i], x.pt.b[i]); dk[b0] = (int)kt - 1; }
   }
   __syncthreads();
   const int U = x.misc[SVM_U];
@@ -631,6 +676,7 @@ __device__ __forceinline__ void sv1_source(unsigned char* smem, DevGraph g, DevS
     diag_add(a.diag, 135, 1ull);
     diag_add(a.diag, 136, (unsigned long long)x.misc[SVM_FILL]);
     diag_add(a.diag, 139, (unsigned long long)(U - L));
+    if (U == L) diag_add(a.diag, 146, 1ull);
   }
   // top-L of the dense list (every thread: a block radix select when U > L), emitted for k_svfin,
   // which writes the row at full occupancy once this LDS-heavy workgroup is gone
@@ -746,10 +792,10 @@ __global__ void __launch_bounds__(SV_THREADS) k_svA(DevGraph g, DevSlab s, IterA
     if (u) atomicAdd(&gs[c], u);
   }
   unsigned long long* gp = gpt + sd.gpt;
-  for (int i = threadIdx.x; i < 2 * Lp; i += blockDim.x) {
-    if (!x.pt.keys[i]) continue;
+  for (int i = threadIdx.x; i < x.pt.T; i += blockDim.x) {
+    if (!(x.pt.keys[i] & ~SV_OVF_BIT)) continue;
     const unsigned long long A = x.pt.a[i], B = x.pt.b[i];
-    const int r = x.pti[i];
+    const int r = x.pt.pos[i];
     if (A) atomicAdd(&gp[2 * r], A);
     if (B) atomicAdd(&gp[2 * r + 1], B);
   }

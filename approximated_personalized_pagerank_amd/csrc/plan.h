@@ -141,6 +141,7 @@ struct ppr_plan {
   // consumer routing (grank.hip xroute_build): a row goes only to the ranks whose sources read it;
   // PPR_XROUTE=0 sends every row to every rank (the broadcast exchange)
   bool xroute = true;
+  int xtest_badsize = -1;             // tests (PPR_XTEST_BADSIZE=r): rank r advertises wrong block sizes
   int8_t* d_xowner = nullptr;         // [n] rank merging each active node (-1: dangling)
   uint32_t* d_xcmask = nullptr;       // [n] ranks reading each node's row
   int32_t* d_xlists = nullptr;        // per partition: send lists to each peer, receive lists from each peer
@@ -363,8 +364,9 @@ inline void plan_free(ppr_plan* p) {
                 (double)h[189], h[183] / 1e9, h[184] / 1e9, h[185] / 1e9, h[186] / 1e9, h[187] / 1e9);
       if (h[135] || h[149])
         fprintf(stderr, "ppr_diag sieve: %llu one-slice sources (%llu handed back), %llu multi-slice; passing keys %.3e "
-                "(candidates %.3e), entries beside the prev keys at the select %.3e\n", h[135], h[137], h[149],
-                (double)h[136], (double)h[138], (double)h[139]);
+                "(candidates %.3e), entries beside the prev keys at the select %.3e; pass 2 skipped (a sketch "
+                "row below the bound) %llu, sources with no new key (U = L) %llu\n", h[135], h[137], h[149],
+                (double)h[136], (double)h[138], (double)h[139], h[145], h[146]);
       if (h[280])
         fprintf(stderr, "ppr_diag wave tier: %llu sources, %.1f kept entries each; kcycles per source (lane 0): "
                 "setup+walk %.2f settle %.2f select %.2f row write %.2f norm1 %.2f\n", h[280],

@@ -142,6 +142,7 @@ struct KeyIndex {
   typename std::enable_if<std::is_integral<K>::value && sizeof(K) <= 4, bool>::type build_direct(
       const std::vector<const Key*>& k, size_t nt) {
     if (k.empty()) return false;
+    nt = std::max<size_t>(1, std::min(nt, k.size() / 4096));  // (no thread per 10 keys on tiny graphs)
     std::vector<int64_t> mn(nt, INT64_MAX), mx(nt, INT64_MIN);
     std::vector<size_t> part(nt + 1);
     for (size_t t = 0; t <= nt; t++) part[t] = k.size() * t / nt;

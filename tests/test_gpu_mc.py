@@ -181,3 +181,18 @@ def test_gpu_mc_walk_shards_compose():
     plan.combine()
     r = plan.fetch()
     assert np.array_equal(r.ids, full.ids) and np.array_equal(r.scores, full.scores)
+
+
+def test_gpu_mc_exact_sum_range_guard(monkeypatch):
+    """the exact MC combine's 96-bit totals (72 fraction bits) hold values below 2^23; a
+    graph whose widest node's seed deg/d plus deg entries could pass the limit is refused with
+    PPR_ERR_RANGE instead of wrapping. The limit lowered to 2^4 trips it on RMAT-10; the default
+    limit (2^23) does not."""
+    g = ppr.rmat(10, seed=3)
+    monkeypatch.setenv("PPR_MC_SUM", "exact")
+    monkeypatch.setenv("PPR_MC_XS_LOG2", "4")
+    with pytest.raises(ppr.PprError) as e:
+        ppr.mccp2_csr(g, 8, 16, 50, 0.85, seed=1, device=0)
+    assert e.value.code == 11
+    monkeypatch.delenv("PPR_MC_XS_LOG2")
+    ppr.mccp2_csr(g, 8, 16, 50, 0.85, seed=1, device=0)

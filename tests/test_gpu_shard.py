@@ -199,3 +199,27 @@ def test_gpu_routed_exchange_bit_exact_and_smaller(world, monkeypatch):
             assert np.array_equal(r.scores.view(np.uint64), ref.scores.view(np.uint64))
             pl.close()
     assert got["1"] < got["0"], got
+
+
+@pytest.mark.parametrize("bad", [0, 3])
+def test_gpu_routed_exchange_size_mismatch_fails_every_rank(bad, monkeypatch):
+    """a block size that does not fit its receive slot must fail the run on EVERY rank
+    (PPR_ERR_RANGE), not leave peers blocked in a half-posted exchange. Every rank checks the sizes
+    it is about to receive and the ranks agree on the outcome before any block moves (an
+    all-reduce MIN over RCCL; the host rendezvous here). PPR_XTEST_BADSIZE=r makes rank r advertise
+    sizes 2^40 too large."""
+    import time
+    import approximated_personalized_pagerank_amd as ppr
+    from approximated_personalized_pagerank_amd.shard import run_local_group
+    g = ppr.rmat(12, seed=5)
+    part = g.partitions()
+    monkeypatch.setenv("PPR_XROUTE", "1")
+    monkeypatch.setenv("PPR_XTEST_BADSIZE", str(bad))
+    plans = [ppr.GrankPlan(g, 16, 32, 0.85, part=part, device=0) for _ in range(4)]
+    t0 = time.time()
+    with pytest.raises(ppr.PprError) as e:
+        run_local_group(plans, 4, -1.0)
+    assert e.value.code == 11  # PPR_ERR_RANGE, not a barrier time-out
+    assert time.time() - t0 < 60.0
+    for pl in plans:
+        pl.close()

@@ -166,3 +166,42 @@ def test_bench_traffic_summary_names_its_build():
     traffic, src, build = bench.pmc_traffic("grank_rmat22_k64_l128", "exact")
     assert traffic and traffic > 0 and src.startswith("profiles/")
     assert build and len(build) == 64 and all(c in "0123456789abcdef" for c in build)
+
+
+def _path_csr(n, reverse=False):
+    """a directed path 0 -> 1 -> ... -> n-1 (or n-1 -> ... -> 0), one successor per node"""
+    rp = np.zeros(n + 1, dtype=np.int64)
+    if reverse:
+        rp[2:] = np.arange(1, n)
+        col = np.arange(0, n - 1, dtype=np.int32)
+    else:
+        rp[1:n] = np.arange(1, n)
+        rp[n] = n - 1
+        col = np.arange(1, n, dtype=np.int32)
+    return ppr.Csr(rp, col)
+
+
+@pytest.mark.parametrize("reverse", [False, True])
+def test_partitions_long_path_linear_time(reverse):
+    """the out-edge BFS scanned every unvisited node at every level, O(depth x n)
+    -- a 200 K-node path took minutes. Past 2 (n + m) of scanning it now switches to predecessor
+    lists. Partitions = the reference BFS's (oracle restatement of pprInternal.h:29-99): alternate
+    along the path from node 0, whichever way the edges point."""
+    import time
+    import oracle
+    n = 200_000
+    g = _path_csr(n, reverse)
+    t0 = time.time()
+    part = g.partitions()
+    assert time.time() - t0 < 10.0
+    assert np.array_equal(part, (np.arange(n) & 1).astype(np.uint8))
+    small = _path_csr(5000, reverse)
+    assert np.array_equal(small.partitions(), oracle.find_partitions(small.row_ptr, small.col))
+
+
+@pytest.mark.parametrize("name", ["g3_rmat12_k16_l32", "g3_rmat14_k32_l64", "g4_eat_k50_l100"])
+def test_partitions_transposed_mode_match_reference(name, monkeypatch):
+    """the predecessor-list levels (forced from level 0) give the reference's partitions too"""
+    monkeypatch.setenv("PPR_BFS_TRANSPOSE", "1")
+    f = load(name)
+    assert np.array_equal(ppr.Csr(f["rp"], f["col"]).partitions(), f["part"])

@@ -1,6 +1,6 @@
 """Build an experiment variant of the library beside the product one, for same-box A/B runs:
 
-    python tools/build_variant.py NAME [--rev GITREV] [DEFINE ...]   # -> libppr_hip_NAME.so
+    python tools/build_variant.py NAME [--rev GITREV] [DEFINE ...]   # -> libpprab_NAME.so (delete it after the A/B session)
     PPR_LIB_VARIANT=NAME python bench.py ...                          # loads the variant
 
 --rev builds the sources of a git revision (exported to /tmp) instead of the working tree.
@@ -27,4 +27,4 @@ if args and args[0] == "--rev":
                            "approximated_personalized_pagerank_amd/csrc"], check=True, capture_output=True).stdout
     subprocess.run(["tar", "-x", "-C", tmp], input=arch, check=True)
     csrc = os.path.join(tmp, "approximated_personalized_pagerank_amd", "csrc")
-print(b.build(out=os.path.join(PKG_DIR, f"libppr_hip_{name}.so"), defines=args, csrc=csrc, verbose=False))
+print(b.build(out=os.path.join(PKG_DIR, f"libpprab_{name}.so"), defines=args, csrc=csrc, verbose=False))
