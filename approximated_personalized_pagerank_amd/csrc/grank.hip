@@ -323,8 +323,14 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
   p->hub_wave_stride = (int)std::max(hub_wave_lds(p->hub_wave_t, p->hub_bw_ng), p->hub_bw2 ? bw2_lds(p->hub_wave_t) : 0);
   p->hub_lds_wave = (size_t)p->hub_wave_stride * p->hub_bw_waves;
   if (p->hub_streams == 2) {
+    // PPR_SV_PRIO=1: stream4 (the sieve's large and small classes) at the highest stream priority
+    // (experiment: the large class needs whole CUs and starves beside the wave tier)
+    const char* epr = getenv("PPR_SV_PRIO");
+    int prio_lo = 0, prio_hi = 0;
+    hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    const int prio4 = (epr && atoi(epr) == 1) ? prio_hi : (epr && atoi(epr) == 2) ? prio_lo : 0;
     if (hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&p->stream4, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&p->stream4, hipStreamNonBlocking, prio4) != hipSuccess ||
         hipStreamCreateWithFlags(&p->stream3, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&p->ev_wave, hipEventDisableTiming) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
     if (hipStreamCreateWithFlags(&p->stream5, hipStreamNonBlocking) != hipSuccess ||
@@ -432,7 +438,9 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       if (hipMemcpy(p->d_tier_cap, caps, sizeof(caps), hipMemcpyHostToDevice) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
       // the sieve (merge_sv.h) for the wide sources: its prev table takes 2 Lp <= one slot per thread
       const char* s0 = getenv("PPR_SV");
-      p->sv_enabled = !(s0 && atoi(s0) == 0) && 2 * p->Lp <= SV_THREADS &&
+      // (rows of at most two 64-entry groups: L <= 128; wider baskets take the range / partition
+      // engines, exact either way)
+      p->sv_enabled = !(s0 && atoi(s0) == 0) && p->Lp <= 2 * WAVE &&
                       sv_lds_bytes(p->Lp, SV_LARGE) <= 160 * 1024 && svf_lds_bytes(p->Lp) <= 160 * 1024;
       const char* s1 = getenv("PPR_SV_SLICE");
       const char* s2 = getenv("PPR_SV_MIN");
@@ -1295,6 +1303,36 @@ static int run_xg(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& sr
 // k_xfinal selects from) on the wave-tier stream, the others are partitioned into buckets of one
 // table each (run_hubs: count, scan, scatter, k_xb, k_xfinal) beside them. A table that overflows
 // sends its source back here with a larger estimate.
+// per-kernel roofline bookkeeping (plan.h NKST groups): events around a group's launches on its
+// stream; kst_fold reads the pair once the stream has been synchronised
+static void kst_reset(ppr_plan* p) {
+  for (int g = 0; g < ppr_plan::NKST; g++) {
+    p->kst_ms[g] = 0.0; p->kst_bytes[g] = 0.0; p->kst_pend_bytes[g] = 0.0;
+    p->kst_launches[g] = 0; p->kst_live[g] = false;
+  }
+}
+static void kst_begin(ppr_plan* p, int g, hipStream_t s) {
+  if (!p->ev_k[2 * g] && hipEventCreate(&p->ev_k[2 * g]) != hipSuccess) return;
+  if (!p->ev_k[2 * g + 1] && hipEventCreate(&p->ev_k[2 * g + 1]) != hipSuccess) return;
+  hipEventRecord(p->ev_k[2 * g], s);
+}
+static void kst_end(ppr_plan* p, int g, hipStream_t s, double bytes) {
+  if (!p->ev_k[2 * g + 1]) return;
+  hipEventRecord(p->ev_k[2 * g + 1], s);
+  p->kst_live[g] = true;
+  p->kst_pend_bytes[g] = bytes;
+}
+static void kst_fold(ppr_plan* p, int g) {
+  if (!p->kst_live[g]) return;
+  p->kst_live[g] = false;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, p->ev_k[2 * g], p->ev_k[2 * g + 1]) == hipSuccess) {
+    p->kst_ms[g] += ms;
+    p->kst_bytes[g] += p->kst_pend_bytes[g];
+    p->kst_launches[g]++;
+  }
+}
+
 static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& src,
                           const std::vector<int32_t>& cand, const std::vector<int32_t>& deg,
                           const std::vector<int64_t>& dest, unsigned long long* maxdiff, int depth) {
@@ -1416,7 +1454,20 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
     }
     HIP_OK(hipMemcpyAsync(b, hb, up, hipMemcpyHostToDevice, sw));
     HIP_OK(hipMemsetAsync(b + o_z, 0, total - o_z, sw));
-    for (int c = 0; c < 3; c++) {
+    // kernel-stat group 5: the range engines (k_xr, k_xfinal, k_xfin1) of this call on sw; SURVEY
+    // s8d bytes with the rows at min(L, candidates + 1) entries (the host knows no row lengths)
+    if (!a.unit && !a.mc) {
+      double bytes = 0.0;
+      for (size_t i = 0; i < n; i++)
+        if (rng[i] > 0)
+          bytes += 8.0 + 8.0 * deg[i] + 12.0 * ((double)cand[i] - 1.0) +
+                   24.0 * (double)std::min<int64_t>(L, (int64_t)cand[i] + 1) + 4.0;
+      kst_begin(p, 5, sw);
+      p->kst_pend_bytes[5] = bytes;
+    }
+    static const bool big_first = getenv("PPR_XR_ORDER") && atoi(getenv("PPR_XR_ORDER")) == 1;  // (experiment)
+    for (int c0 = 0; c0 < 3; c0++) {
+      const int c = big_first ? 2 - c0 : c0;
       if (tasks[c].empty()) continue;
       const int T = cls[c].T, W = cls[c].W;
       // (PPR_XR_BUDGET=over, tests: no budget stop -- the tables fill and the bounded probes run
@@ -1439,6 +1490,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       HIP_OK(hipGetLastError());
       p->merge_launches++;
     }
+    if (!a.unit && !a.mc) kst_end(p, 5, sw, p->kst_pend_bytes[5]);
   }
   // partitioned sources beside them
   std::vector<int32_t> fallback;
@@ -1457,6 +1509,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
     int32_t novf = 0;
     HIP_OK(hipMemcpyAsync(&novf, p->d_xs + o_ov, 4, hipMemcpyDeviceToHost, sw));
     HIP_OK(hipStreamSynchronize(sw));
+    kst_fold(p, 5);
     if (novf) {
       std::vector<int32_t> od(novf);
       HIP_OK(hipMemcpyAsync(od.data(), p->d_xs + o_ov + 4, 4 * (size_t)novf, hipMemcpyDeviceToHost, sw));
@@ -1495,36 +1548,6 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
 // The sieve (merge_sv.h) for sources `src` (candidate counts `cand`): one-slice sources by k_sv1 on
 // stream_sv2 (largest first), multi-slice sources by k_svA -> k_svB -> k_svF on stream_sv. The
 // launches are asynchronous; sieve_collect waits and returns the sources handed back.
-// per-kernel roofline bookkeeping (plan.h NKST groups): events around a group's launches on its
-// stream; kst_fold reads the pair once the stream has been synchronised
-static void kst_reset(ppr_plan* p) {
-  for (int g = 0; g < ppr_plan::NKST; g++) {
-    p->kst_ms[g] = 0.0; p->kst_bytes[g] = 0.0; p->kst_pend_bytes[g] = 0.0;
-    p->kst_launches[g] = 0; p->kst_live[g] = false;
-  }
-}
-static void kst_begin(ppr_plan* p, int g, hipStream_t s) {
-  if (!p->ev_k[2 * g] && hipEventCreate(&p->ev_k[2 * g]) != hipSuccess) return;
-  if (!p->ev_k[2 * g + 1] && hipEventCreate(&p->ev_k[2 * g + 1]) != hipSuccess) return;
-  hipEventRecord(p->ev_k[2 * g], s);
-}
-static void kst_end(ppr_plan* p, int g, hipStream_t s, double bytes) {
-  if (!p->ev_k[2 * g + 1]) return;
-  hipEventRecord(p->ev_k[2 * g + 1], s);
-  p->kst_live[g] = true;
-  p->kst_pend_bytes[g] = bytes;
-}
-static void kst_fold(ppr_plan* p, int g) {
-  if (!p->kst_live[g]) return;
-  p->kst_live[g] = false;
-  float ms = 0.f;
-  if (hipEventElapsedTime(&ms, p->ev_k[2 * g], p->ev_k[2 * g + 1]) == hipSuccess) {
-    p->kst_ms[g] += ms;
-    p->kst_bytes[g] += p->kst_pend_bytes[g];
-    p->kst_launches[g]++;
-  }
-}
-
 struct SvRun {
   std::vector<int32_t> pos;  // index into the caller's source list of each descriptor
   size_t o_ovl = 0;          // offset of the overflow list in d_sv
@@ -1790,8 +1813,12 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
   if (!src.empty()) { int r = run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0); if (r) return r; }
   lap(3, tl);  // range / partition engines (their syncs included)
   std::vector<int32_t> back;
+  const int64_t dev0 = p->sv_redo_dev;
   { int r = sieve_collect(p, run, back); if (r) return r; }
   lap(4, tl);  // waiting for the sieve
+  if (getenv("PPR_SV_LOG"))
+    fprintf(stderr, "ppr_sv_log it %d sieved %zu range %zu dev_redo %lld handed_back %zu\n", a.iter, ssrc.size(),
+            src.size(), (long long)(p->sv_redo_dev - dev0), back.size());
   if (back.empty()) return PPR_OK;
   // handed back: the range / partition engines, with the usual estimate
   src.clear(); cand.clear(); deg.clear(); dest.clear();
@@ -2090,6 +2117,9 @@ extern "C" int ppr_grank_plan_init(ppr_plan* p) {
   p->md_shared_it = -1;  // a new run: iteration numbers start over
   p->hot_n = 0;          // the hot set is rebuilt from this run's rows at iteration hot_at
   p->hot_built_it = -1;
+  // every job plans from its own merges only: the range engines' distinct-key estimates (d_dlast,
+  // the last merge's count) start over, so a repeated run is a cold call
+  if (p->d_dlast) HIP_OK(hipMemsetAsync(p->d_dlast, 0, 4 * (size_t)std::max<int64_t>(1, p->n), p->stream));
   IterArgs a = iter_args(p, 0, true);
   return run_merge(p, a, p->d_all, p->n, p->d_maxdiff + PPR_MAX_ITER_STATS);
 }

@@ -348,8 +348,8 @@ __device__ __forceinline__ void sv_build_pt(const SvLds& x, const DevSlab& s, co
 // The wave's share of a slice: contiguous successors [c0, c1) taken row by row. Row metadata comes
 // per window of 64 successors, one successor per lane (colx two windows ahead, lengths one window
 // ahead); a row's base and length are read off its lane into scalar registers. A lane takes
-// entries lane and 64 + lane of each row (rows of up to 128 entries; longer rows' further groups
-// one at a time after the batch), loads issued unconditionally inside the row (a row slot always
+// entries lane and 64 + lane of each row (rows of up to 128 entries: the sieve takes L <= 128,
+// grank.hip sv_enabled), loads issued unconditionally inside the row (a row slot always
 // holds L entries: lanes past the row's length read stale entries and are masked, no exec branch).
 // NS rows a batch, the next batch's loads in flight while fb(key, score, valid) takes the current
 // batch's groups; scores are loaded only with kScores. Every branch here is wave-uniform.
@@ -360,6 +360,17 @@ struct SvBatch {
   int rl[NS];        // row length (0: no row)
   int64_t base[NS];
 };
+// every group of a batch that holds entries: g(k, key, score, valid, slab index)
+template <int NS, class G>
+__device__ __forceinline__ void sv_groups(const SvBatch<NS>& bt, G g) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int k = 0; k < 2 * NS; k++) {
+    const int rl = bt.rl[k >> 1];
+    if ((k & 1) && rl <= WAVE) continue;  // (wave-uniform; a missing row, rl = 0, has no valid lane)
+    g(k, bt.key[k], bt.sv[k], (k & 1) * WAVE + lane < rl, bt.base[k >> 1] + (k & 1) * WAVE + lane);
+  }
+}
 __device__ __forceinline__ int64_t sv_readlane64(int64_t x, int lane) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, lane);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), lane);
@@ -369,8 +380,7 @@ template <bool kScores, int NS, class FB>
 __device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, const IterArgs& a, int64_t c0, int64_t c1,
                                         FB fb) {
   const int lane = lane_id();
-  const int L = s.L;
-  const int lcl = lane < L ? lane : 0;  // (rows narrower than a wave: stay inside the row slot)
+  const int lcl = lane < s.L ? lane : 0;  // (rows narrower than a wave: stay inside the row slot)
   auto colx_at = [&](int64_t w0) { return w0 + lane < c1 ? g.colx[w0 + lane] : (int32_t)-1; };
   auto len_of = [&](int32_t cx) { return cx == -1 ? 0 : s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)]; };
   auto base_of = [&](int32_t cx) { return cx == -1 ? (int64_t)0 : s.row(read_slot(a, cx), cx & 0x7fffffff); };
@@ -403,25 +413,7 @@ __device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, con
         }
       }
     };
-    auto run = [&](const SvBatch<NS>& bt) {
-#pragma unroll
-      for (int k = 0; k < 2 * NS; k++) {
-        const int rl = bt.rl[k >> 1];
-        if (rl <= (k & 1) * WAVE) continue;
-        fb(bt.key[k], kScores ? bt.sv[k] : 0.0, (k & 1) * WAVE + lane < rl, bt.base[k >> 1] + (k & 1) * WAVE + lane);
-      }
-      if (L > 2 * WAVE) {  // rows beyond two groups (L > 128 only)
-#pragma unroll
-        for (int q = 0; q < NS; q++) {
-          const int rl = bt.rl[q];
-          for (int i0 = 2 * WAVE; i0 < rl; i0 += WAVE) {
-            const int64_t idx = bt.base[q] + i0 + lane;
-            const bool ok = i0 + lane < rl;
-            fb(ok ? s.ids[idx] : 0, (kScores && ok) ? s.sc[idx] : 0.0, ok, idx);
-          }
-        }
-      }
-    };
+    auto run = [&](const SvBatch<NS>& bt) { fb(bt); };
     // two batch buffers in turn (no per-batch copy of one into the other); sched_barrier keeps the
     // next batch's loads ahead of this batch's work without pulling its first uses up
     SvBatch<NS> ba, bb;
@@ -460,8 +452,15 @@ __device__ __forceinline__ void sv_chunk(int64_t b0, int64_t b1, int64_t& c0, in
 #define PPR_SV_NS1 4
 #endif
 #ifndef PPR_SV_NS2
-#define PPR_SV_NS2 8
+#define PPR_SV_NS2 4
 #endif
+#ifndef PPR_SV_P2_SCORES
+#define PPR_SV_P2_SCORES 1
+#endif
+// pass 2 loads every candidate's score with its key (8 B more per candidate): the few groups with
+// a passing lane then insert without a dependent HBM round trip (PPR_WHATIF 512 / 1024 timings:
+// that round trip per group was 2/3 of pass 2)
+constexpr bool SV_P2_SCORES = PPR_SV_P2_SCORES != 0;
 // rows per batch in pass 1 (keys and scores) and pass 2 (keys only: a lighter group, so more rows
 // in flight to cover the gather latency); build-time knobs for A/B variants (tools/build_variant.py)
 constexpr int SV_NS1 = PPR_SV_NS1, SV_NS2 = PPR_SV_NS2;
@@ -471,13 +470,15 @@ __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, co
   sv_chunk(b0, b1, c0, c1);
   const int dummy = x.pt.T + lane_id();
   const double f61 = factor * 0x1p61;
-  sv_rows<true, SV_NS1>(g, s, a, c0, c1, [&](int key, double sc, bool valid, int64_t) {
-    const uint32_t h = sv_mix((uint32_t)key);
-    const int slot = svpt_slot(x.pt, key, h, valid);
-    const bool inpt = valid && slot >= 0;
-    const double t = sc * f61;  // p * 2^61, exact (sv_split_t)
-    sv_split_add_t(x.pt.a, x.pt.b, inpt ? slot : dummy, t);
-    sv_sketch_add(sk, h, (valid && !inpt) ? sv_units_t(t) : 0u, x.wlog);
+  sv_rows<true, SV_NS1>(g, s, a, c0, c1, [&](const SvBatch<SV_NS1>& bt) {
+    sv_groups(bt, [&](int, int key, double sc, bool valid, int64_t) {
+      const uint32_t h = sv_mix((uint32_t)key);
+      const int slot = svpt_slot(x.pt, key, h, valid);
+      const bool inpt = valid && slot >= 0;
+      const double t = sc * f61;  // p * 2^61, exact (sv_split_t)
+      sv_split_add_t(x.pt.a, x.pt.b, inpt ? slot : dummy, t);
+      sv_sketch_add(sk, h, (valid && !inpt) ? sv_units_t(t) : 0u, x.wlog);
+    });
   });
 }
 
@@ -491,25 +492,50 @@ __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, co
   sv_chunk(b0, b1, c0, c1);
   const uint32_t* bm32 = reinterpret_cast<const uint32_t*>(x.bm);
   const double f61 = factor * 0x1p61;
-  sv_rows<false, SV_NS2>(g, s, a, c0, c1, [&](int key, double, bool valid, int64_t idx) {
-    const uint32_t h = sv_mix((uint32_t)key);
-    bool want = valid && sv_passes(bm32, h, x.wlog);
-    if (__builtin_expect(__ballot(want) == 0ull, 1)) return;
-    want = want && svpt_slot(x.pt, key, h, want) < 0;
-    if (!__ballot(want)) return;
-    const double sc = want ? s.sc[idx] : 0.0;
-    if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
-      if (lane_id() == 0) x.misc[SVM_OVF] = 1;
-      return;
+  const int lane = lane_id();
+  sv_rows<SV_P2_SCORES, SV_NS2>(g, s, a, c0, c1, [&](const SvBatch<SV_NS2>& bt) {
+    constexpr int NG = 2 * SV_NS2;
+    bool want[NG];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < NG; k++) want[k] = false;
+    sv_groups(bt, [&](int k, int key, double, bool valid, int64_t) {
+      // (PPR_WHATIF 1024, timing only: the walk alone, every key fails the test)
+      want[k] = valid && ((a.whatif & 1024u) ? key == -7 : sv_passes(bm32, sv_mix((uint32_t)key), x.wlog));
+      any = any || want[k];
+    });
+    if (a.diag && lane == 0) {  // (PPR_DIAG: groups walked, groups with a lane past the bitmap test)
+      int ng = 0, np = 0;
+#pragma unroll
+      for (int k = 0; k < NG; k++) { ng += ((k & 1) ? bt.rl[k >> 1] > WAVE : bt.rl[k >> 1] > 0) ? 1 : 0; }
+      diag_add(a.diag, 190, (unsigned long long)ng);
+      (void)np;
     }
-    bool ins = false;
-    int hs = -1;
-    if (want) hs = x2_slot(xt, key, ins);
-    const int nins = __popcll(__ballot(ins));
-    if (nins && lane_id() == 0) atomicAdd(&x.misc[SVM_FILL], nins);
-    if (__ballot(want && hs < 0) && lane_id() == 0) x.misc[SVM_OVF] = 1;
-    if (hs >= 0) sv_split_add_t(xt.a, xt.b, hs, sc * f61);
-    if (a.diag && lane_id() == 0) diag_add(a.diag, 138, (unsigned long long)__popcll(__ballot(want)));
+    if (__builtin_expect(__ballot(any) == 0ull, 1)) return;
+    if (a.whatif & 512u) return;  // (timing only: no insert path)
+    // the few groups with a passing lane: PT check, score, insert
+#pragma unroll
+    for (int k = 0; k < NG; k++) {
+      if (!__ballot(want[k])) continue;
+      const int key = bt.key[k];
+      const bool w = want[k] && svpt_slot(x.pt, key, sv_mix((uint32_t)key), want[k]) < 0;
+      if (a.diag && lane == 0) diag_add(a.diag, 147, 1ull);
+      if (!__ballot(w)) continue;
+      if (a.diag && lane == 0) diag_add(a.diag, 148, 1ull);
+      const double sc = SV_P2_SCORES ? bt.sv[k] : (w ? s.sc[bt.base[k >> 1] + (k & 1) * WAVE + lane] : 0.0);
+      if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
+        if (lane == 0) x.misc[SVM_OVF] = 1;
+        return;
+      }
+      bool ins = false;
+      int hs = -1;
+      if (w) hs = x2_slot(xt, key, ins);
+      const int nins = __popcll(__ballot(ins));
+      if (nins && lane == 0) atomicAdd(&x.misc[SVM_FILL], nins);
+      if (__ballot(w && hs < 0) && lane == 0) x.misc[SVM_OVF] = 1;
+      if (hs >= 0) sv_split_add_t(xt.a, xt.b, hs, sc * f61);
+      if (a.diag && lane == 0) diag_add(a.diag, 138, (unsigned long long)__popcll(__ballot(w)));
+    }
   });
 }
 

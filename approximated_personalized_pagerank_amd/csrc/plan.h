@@ -82,7 +82,7 @@ struct ppr_plan {
   unsigned long long* d_stats = nullptr;    // PPR_NSTATS: candidates, algorithmic bytes, wave-tier bytes
   // per-kernel roofline (ppr_grank_plan_kernel_stats): HIP events around each kernel group on the
   // stream it runs on, algorithmic bytes of the sources it merged (SURVEY s8d per source)
-  static constexpr int NKST = 5;      // wave tier | sieve large | sieve mid | sieve small | sieve multi-slice
+  static constexpr int NKST = 6;      // wave tier | sieve large | sieve mid | sieve small | sieve multi-slice | range
   hipEvent_t ev_k[2 * NKST] = {};
   bool kst_live[NKST] = {};
   double kst_ms[NKST] = {}, kst_bytes[NKST] = {}, kst_pend_bytes[NKST] = {};
@@ -367,6 +367,9 @@ inline void plan_free(ppr_plan* p) {
                 "(candidates %.3e), entries beside the prev keys at the select %.3e; pass 2 skipped (a sketch "
                 "row below the bound) %llu, sources with no new key (U = L) %llu\n", h[135], h[137], h[149],
                 (double)h[136], (double)h[138], (double)h[139], h[145], h[146]);
+      if (h[190])
+        fprintf(stderr, "ppr_diag sieve pass 2: %.3e groups walked, %.3e with a lane past the bitmap test, %.3e with a "
+                "non-prev key past it (inserts)\n", (double)h[190], (double)h[147], (double)h[148]);
       if (h[280])
         fprintf(stderr, "ppr_diag wave tier: %llu sources, %.1f kept entries each; kcycles per source (lane 0): "
                 "setup+walk %.2f settle %.2f select %.2f row write %.2f norm1 %.2f\n", h[280],

@@ -155,7 +155,7 @@ class GrankPlan:
 
     KERNEL_GROUPS = ("wave tier k_merge_lds_x", "sieve large k_sv1+k_svfin (16 waves)",
                      "sieve mid k_sv1+k_svfin (8 waves)", "sieve small k_sv1+k_svfin (4 waves)",
-                     "sieve multi-slice k_svA+k_svB+k_svF")
+                     "sieve multi-slice k_svA+k_svB+k_svF", "range k_xr+k_xfinal+k_xfin1")
 
     def kernel_stats(self):
         """per kernel group of the last run(): SURVEY s8d algorithmic bytes of the sources it merged,

@@ -180,8 +180,10 @@ int ppr_grank_plan_exchange_bytes(ppr_plan* p, int64_t* recv_bytes, int64_t* row
 /* Per-kernel roofline of the last ppr_grank_plan_run (no reference counterpart: measurement).
  * Kernel groups, in this order: 0 wave tier (k_merge_lds_x), 1 sieve large (k_sv1 + k_svfin, 16
  * waves), 2 sieve mid (8 waves), 3 sieve small (4 waves), 4 sieve multi-slice (k_svA + k_svB +
- * k_svF). bytes: SURVEY s8d algorithmic bytes of the sources the group merged (the wave tier's
- * without the written rows); ms: HIP event time of the group's launches on its stream; launches:
+ * k_svF), 5 range engines (k_xr + k_xfinal + k_xfin1: sources the sieve does not take or hands
+ * back). bytes: SURVEY s8d algorithmic bytes of the sources the group merged (the wave tier's
+ * without the written rows; the range group's with rows of min(L, candidates + 1) entries); ms:
+ * HIP event time of the group's launches on its stream; launches:
  * event pairs summed. Up to n groups are written. */
 int ppr_grank_plan_kernel_stats(ppr_plan* p, int32_t n, double* bytes, double* ms, int64_t* launches);
 /* Tests: the same native loop with n plans of this process as the ranks (one thread each, block
