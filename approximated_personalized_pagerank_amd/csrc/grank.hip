@@ -1333,9 +1333,22 @@ static void kst_fold(ppr_plan* p, int g) {
   }
 }
 
+// A range-engine call whose completion is collected later (xhubs_finish): the launches are queued
+// on stream3 and the host goes on planning the sieve, so both run from the iteration's start.
+struct XhDefer {
+  bool want = false;   // the caller accepts a deferred completion
+  bool live = false;   // launches queued, not yet collected
+  int depth = 0;
+  size_t o_ov = 0;
+  std::vector<int32_t> src, cand, deg, xv;
+  std::vector<int64_t> dest;
+};
+static int xhubs_finish(ppr_plan* p, const IterArgs& a, XhDefer& df, unsigned long long* maxdiff);
+
 static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& src,
                           const std::vector<int32_t>& cand, const std::vector<int32_t>& deg,
-                          const std::vector<int64_t>& dest, unsigned long long* maxdiff, int depth) {
+                          const std::vector<int64_t>& dest, unsigned long long* maxdiff, int depth,
+                          XhDefer* defer = nullptr) {
   const size_t n = src.size();
   if (!n) return PPR_OK;
   hipStream_t st = p->stream;
@@ -1492,6 +1505,17 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
     }
     if (!a.unit && !a.mc) kst_end(p, 5, sw, p->kst_pend_bytes[5]);
   }
+  // deferred completion (no partitioned or HBM-table source in this call: those plan on the host
+  // from device counts and would serialise behind the range engines here anyway)
+  if (defer && defer->want && nx && bsrc.empty() && xgs.empty()) {
+    defer->live = true;
+    defer->depth = depth;
+    defer->o_ov = o_ov;
+    defer->src = src; defer->cand = cand; defer->deg = deg; defer->dest = dest;
+    defer->xv.resize(nx);
+    for (size_t i = 0; i < nx; i++) defer->xv[i] = xd[i].v;
+    return PPR_OK;
+  }
   // partitioned sources beside them
   std::vector<int32_t> fallback;
   if (!bsrc.empty()) {
@@ -1542,6 +1566,40 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
     }
   }
   return run_xhubs_list(p, a, rsrc, rcand, rdeg, rdest, maxdiff, depth + 1);
+}
+
+// the completion of a deferred run_xhubs_list: wait for the range engines, redo the overflowed
+// sources (synchronously, with 4x the estimate), exactly as the undeferred call does
+static int xhubs_finish(ppr_plan* p, const IterArgs& a, XhDefer& df, unsigned long long* maxdiff) {
+  if (!df.live) return PPR_OK;
+  df.live = false;
+  hipStream_t sw = p->stream3 ? p->stream3 : p->stream;
+  int32_t novf = 0;
+  HIP_OK(hipMemcpyAsync(&novf, p->d_xs + df.o_ov, 4, hipMemcpyDeviceToHost, sw));
+  HIP_OK(hipStreamSynchronize(sw));
+  kst_fold(p, 5);
+  if (!novf) return PPR_OK;
+  std::vector<int32_t> od(novf);
+  HIP_OK(hipMemcpyAsync(od.data(), p->d_xs + df.o_ov + 4, 4 * (size_t)novf, hipMemcpyDeviceToHost, sw));
+  HIP_OK(hipStreamSynchronize(sw));
+  p->xr_redo += novf;
+  std::vector<std::pair<int32_t, int32_t>> idx(df.src.size());
+  for (size_t i = 0; i < df.src.size(); i++) idx[i] = {df.src[i], (int32_t)i};
+  std::sort(idx.begin(), idx.end());
+  std::vector<int32_t> rsrc, rcand, rdeg;
+  std::vector<int64_t> rdest;
+  for (int32_t d : od) {
+    const int32_t v = df.xv[(size_t)d];
+    auto it = std::lower_bound(idx.begin(), idx.end(), std::make_pair(v, (int32_t)-1));
+    if (it == idx.end() || it->first != v) return PPR_ERR_HIP;
+    const size_t i = (size_t)it->second;
+    rsrc.push_back(df.src[i]);
+    rcand.push_back(df.cand[i]);
+    rdeg.push_back(df.deg[i]);
+    const int64_t grown = 4 * df.dest[i] + 64;
+    rdest.push_back(df.dest[i] >= (int64_t)df.cand[i] ? grown : std::min<int64_t>((int64_t)df.cand[i], grown));
+  }
+  return run_xhubs_list(p, a, rsrc, rcand, rdeg, rdest, maxdiff, df.depth + 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1752,12 +1810,26 @@ static int sieve_collect(ppr_plan* p, SvRun& run, std::vector<int32_t>& back) {
 static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int64_t count, unsigned long long* maxdiff) {
   if (count <= 0) return PPR_OK;
   auto now = [] { return std::chrono::steady_clock::now(); };
+  double lapv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto lap = [&](int k, std::chrono::steady_clock::time_point& t) {
     const auto t2 = now();
-    p->xh_s[k] += std::chrono::duration<double>(t2 - t).count();
+    const double d = std::chrono::duration<double>(t2 - t).count();
+    p->xh_s[k] += d;
+    lapv[k] += d;
     t = t2;
   };
   auto tl = now();
+  const auto t_in = tl;
+  struct LapLog {  // PPR_SV_LOG: this call's host phases (ms), printed when it returns
+    const IterArgs& a; double* v; std::chrono::steady_clock::time_point t0;
+    ~LapLog() {
+      if (!getenv("PPR_SV_LOG")) return;
+      const double tot = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      fprintf(stderr, "ppr_xh_laps it %d total %.2f gather %.2f classify %.2f sieve_launch %.2f engines %.2f "
+              "sieve_wait %.2f handback %.2f\n", a.iter, 1e3 * tot, 1e3 * v[0], 1e3 * v[1], 1e3 * v[2], 1e3 * v[3],
+              1e3 * v[4], 1e3 * (v[5] + v[6]));
+    }
+  } laplog{a, lapv, t_in};
   hipStream_t st = p->stream;
   const size_t nh = (size_t)count;
   {
@@ -1808,9 +1880,22 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
   }
   lap(1, tl);  // classification
   SvRun run;
+  // the larger of the two host plannings goes second: when the range engines take more sources
+  // than the sieve (the big partition's iterations: ~258 K mid-sized sources at RMAT-22), they are
+  // planned and queued first and collected after the sieve's launches (PPR_XH_FIRST=0: sieve first)
+  static const int xh_first = getenv("PPR_XH_FIRST") ? atoi(getenv("PPR_XH_FIRST")) : 1;
+  XhDefer df;
+  df.want = xh_first != 0 && src.size() > ssrc.size();
+  if (df.want) { int r = run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0, &df); if (r) return r; }
   if (!ssrc.empty()) { int r = sieve_launch(p, a, ssrc, scand, sdeg, maxdiff, run); if (r) return r; }
   lap(2, tl);  // sieve planning + launches
-  if (!src.empty()) { int r = run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0); if (r) return r; }
+  if (df.want) {
+    int r = xhubs_finish(p, a, df, maxdiff);
+    if (r) return r;
+  } else if (!src.empty()) {
+    int r = run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0);
+    if (r) return r;
+  }
   lap(3, tl);  // range / partition engines (their syncs included)
   std::vector<int32_t> back;
   const int64_t dev0 = p->sv_redo_dev;

@@ -18,6 +18,8 @@
 //                        reference never cuts a basket at a tie
 // Which keys survive among those tied at a top-L/top-K cut: a per-source hash of the key (the
 // reference leaves it to its hash-map history).
+// Limits (INTEGRATION.md "Limits"): L <= 4096 and deg(v) * L + 1 < 2^31 for every node; beyond
+// them the call prints "parameter outside the supported range" and exits (PPR_ERR_RANGE).
 #ifndef PPR_HIP_DROPIN_GRANK_H
 #define PPR_HIP_DROPIN_GRANK_H
 

@@ -437,3 +437,22 @@ def test_gpu_bounded_probes_exhausted_chain_fails_loudly(monkeypatch, chain_sum)
     r = ppr.grank_csr(g, 16, 64, 3, 0.85, -1.0, part=part, device=0)
     o = oracle.grank(g.row_ptr, g.col, part, 16, 64, 3, 0.85, -1.0)
     assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])
+
+
+def test_gpu_widest_basket_limit():
+    """the widest basket the kernels take, L = MAX_L = 4096 (L = 4097 is refused: tests/test_host.py
+    ::test_basket_width_limit_refused_without_device), bit-exact vs the oracle on a graph whose
+    baskets reach it (a node with 5000 successors)"""
+    n = 5001
+    d = {0: list(range(1, n))}
+    d.update({i: [0, (i % 4999) + 1] for i in range(1, n)})
+    csr = ppr.Csr.from_dict(d)
+    part = csr.partitions()
+    r = ppr.grank_csr(csr, 64, 4096, 3, 0.85, -1.0, part=part, device=0)
+    o = oracle.grank(csr.row_ptr, csr.col, part, 64, 4096, 3, 0.85, -1.0)
+    assert int(r.lens.max()) == 64
+    assert np.array_equal(r.lens, o["lens"]) and np.array_equal(r.ids, o["ids"])
+    assert np.array_equal(r.scores, o["scores"])
+    with pytest.raises(ppr.PprError) as e:
+        ppr.grank_csr(csr, 64, 4097, 3, 0.85, -1.0, part=part, device=0)
+    assert e.value.code == 11

@@ -205,3 +205,19 @@ def test_partitions_transposed_mode_match_reference(name, monkeypatch):
     monkeypatch.setenv("PPR_BFS_TRANSPOSE", "1")
     f = load(name)
     assert np.array_equal(ppr.Csr(f["rp"], f["col"]).partitions(), f["part"])
+
+
+def test_basket_width_limit_refused_without_device():
+    """L above MAX_L = 4096 (csrc/ppr_common.h) is refused with PPR_ERR_RANGE
+    (11) before any device work, by GRank and by MCCompletePathV2 (the reference merges any L,
+    include/grank.h:42-48; INTEGRATION.md "Limits"); L = 4096 passes the checks (run on the GPU:
+    tests/test_gpu_parity.py::test_gpu_widest_basket_limit)"""
+    L = _lib.lib()
+    rp = np.array([0, 1], dtype=np.int64)
+    col = np.array([0], dtype=np.int32)
+    c = _lib.csr_struct(rp, col)
+    out = ctypes.c_void_p()
+    assert L.ppr_grank_plan_create(ctypes.byref(c), None, 1, 4097, 0.85, None, ctypes.byref(out)) == 11
+    assert L.ppr_mccp2_plan_create(ctypes.byref(c), 1, 4097, 0.85, None, ctypes.byref(out)) == 11
+    assert L.ppr_grank_csr(ctypes.byref(c), None, 1, 4097, 2, 0.85, -1.0, None, None, None, None, None) == 11
+    assert "outside the supported range" in _lib.lib().ppr_strerror(11).decode()
