@@ -21,7 +21,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "libppr_hip.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 # every file the library is compiled from (csrc/ plus the public header), in digest order
-CSRC_SOURCES = ["grank.hip", "mccp2.hip", "exact_ppr.hip", "host_graph.cpp"]
+CSRC_SOURCES = ["grank.hip", "mccp2.hip", "exact_ppr.hip", "partition.hip", "host_graph.cpp"]
 # every header of csrc/ (a new one can not be left out of the provenance digest) and the C ABI
 CSRC_HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".h")) + [os.path.join("..", "..", "include", "ppr_hip.h")]
 
@@ -168,6 +168,8 @@ def lib() -> ctypes.CDLL:
         "ppr_grank_plan_exchange_bytes": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
         "ppr_grank_plan_kernel_stats": (ctypes.c_int, [vp, ctypes.c_int32, vp, vp, vp]),
         "ppr_grank_plan_run_local_group": (ctypes.c_int, [vp, i32, u32, f64, vp]),
+        "ppr_grank_plan_ends_time": (ctypes.c_int, [vp, i32, i32, i32, i32, vp]),
+        "ppr_find_partitions_csr_device": (ctypes.c_int, [vp, vp, i32]),
         "ppr_grank_plan_pack_host": (ctypes.c_int, [vp, i32, i64, i64, vp, i64, ctypes.POINTER(i64)]),
         "ppr_grank_plan_unpack_host": (ctypes.c_int, [vp, i32, i64, i64, vp, i64]),
         "ppr_plan_fetch_slot": (ctypes.c_int, [vp, i32, vp, vp, vp]),

@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -164,8 +165,16 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       else run = p->tierCap[t];
     }
   }
+  // init list: nodes with successors (merged), then the dangling ones (k_init_dangling)
   std::vector<int32_t> all(n > 0 ? n : 1);
-  for (int64_t v = 0; v < n; v++) all[v] = (int32_t)v;
+  {
+    int64_t k = 0;
+    for (int64_t v = 0; v < n; v++)
+      if (row_ptr[v + 1] > row_ptr[v]) all[k++] = (int32_t)v;
+    p->n_nd = k;
+    for (int64_t v = 0; v < n; v++)
+      if (row_ptr[v + 1] == row_ptr[v]) all[k++] = (int32_t)v;
+  }
   p->h_rp.assign(row_ptr, row_ptr + n + 1);
   for (int64_t v = 0; v < n; v++) p->max_deg = std::max<int64_t>(p->max_deg, row_ptr[v + 1] - row_ptr[v]);
 
@@ -616,8 +625,17 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
     });
     if (bad) return PPR_ERR_GRAPH;
   }
-  if (part_in) std::memcpy(part.data(), part_in, n);
-  else if (n) { rc = ppr_find_partitions_csr(g, part.data()); if (rc) return rc; }
+  if (part_in) {
+    std::memcpy(part.data(), part_in, n);
+  } else if (n) {
+    // on the device first (tens of ms at RMAT-22 instead of the host BFS's 0.3-0.5 s); the host BFS
+    // for graphs it declines (long paths) or when PPR_HOST_BFS=1
+    rc = getenv("PPR_HOST_BFS") && atoi(getenv("PPR_HOST_BFS")) == 1
+             ? PPR_ERR_RANGE
+             : ppr_find_partitions_csr_device(g, part.data(), (o && o->device >= 0) ? o->device : -1);
+    if (rc == PPR_ERR_RANGE) rc = ppr_find_partitions_csr(g, part.data());
+    if (rc) return rc;
+  }
   const auto t1 = now();
 
   // host-side CSR with partition bit of the successor
@@ -2196,6 +2214,31 @@ reclassify:
   return run_glb(p, a, big, maxdiff);
 }
 
+// a single contribution p as the exact sum stores it (merge_xs.h xs_single): floor(p * 2^F) rounded
+// back to the nearest double (the 128-bit integer's conversion is correctly rounded)
+static double xs_single_host(double p, int F) {
+  uint64_t b;
+  std::memcpy(&b, &p, 8);
+  int e = (int)((b >> 52) & 0x7ffu);
+  uint64_t m = b & ((1ull << 52) - 1ull);
+  if (e) m |= 1ull << 52; else e = 1;
+  const int sh = e - 1075 + F;
+  const unsigned __int128 X = sh >= 0 ? ((unsigned __int128)m << sh) : (sh > -64 ? (unsigned __int128)(m >> -sh) : 0);
+  return std::ldexp((double)X, -F);
+}
+
+// the dangling nodes' init rows (merge_glb.h k_init_dangling), on the plan stream; the seed as the
+// plan's summation stores it (the exact sum's fixed point, or the chain's 1 - d as is)
+static int init_dangling(ppr_plan* p, const int32_t* list, int64_t cnt) {
+  if (cnt <= 0) return PPR_OK;
+  const int64_t th = cnt * NRANGE;
+  const double seed = p->xsum ? xs_single_host(1.0 - p->damping, XS_F) : 1.0 - p->damping;
+  hipLaunchKernelGGL(k_init_dangling, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, p->stream, dev_slab(p), list, cnt,
+                     seed);
+  HIP_OK(hipGetLastError());
+  return PPR_OK;
+}
+
 extern "C" int ppr_grank_plan_init(ppr_plan* p) {
   if (!p) return PPR_ERR_ARG;
   HIP_OK(hipSetDevice(p->device));
@@ -2206,7 +2249,9 @@ extern "C" int ppr_grank_plan_init(ppr_plan* p) {
   // the last merge's count) start over, so a repeated run is a cold call
   if (p->d_dlast) HIP_OK(hipMemsetAsync(p->d_dlast, 0, 4 * (size_t)std::max<int64_t>(1, p->n), p->stream));
   IterArgs a = iter_args(p, 0, true);
-  return run_merge(p, a, p->d_all, p->n, p->d_maxdiff + PPR_MAX_ITER_STATS);
+  int rc = init_dangling(p, p->d_all + p->n_nd, p->n - p->n_nd);
+  if (rc) return rc;
+  return run_merge(p, a, p->d_all, p->n_nd, p->d_maxdiff + PPR_MAX_ITER_STATS);
 }
 
 extern "C" int ppr_grank_plan_active_count(ppr_plan* p, int32_t it, int64_t* count) {
@@ -2276,18 +2321,18 @@ extern "C" int ppr_grank_plan_finish(ppr_plan* p, int32_t iterations_run) {
   if (!p || iterations_run < 0) return PPR_ERR_ARG;
   if (p->n == 0) return PPR_OK;
   HIP_OK(hipSetDevice(p->device));
-  const int rc = launch_topk(p, ((iterations_run + 1) / 2) & 1, (iterations_run / 2) & 1);
+  const int rc = launch_topk(p, ((iterations_run + 1) / 2) & 1, (iterations_run / 2) & 1, nullptr, 0);
   if (rc) return rc;
   return probe_take();
 }
 
-int launch_topk(ppr_plan* p, int sA, int sB) {
+int launch_topk(ppr_plan* p, int sA, int sB, const int8_t* owner, int rank) {  // (defaults: plan.h)
   if (p->n == 0) return PPR_OK;
   const DevSlab s = dev_slab(p);
   const int wpb = p->Lp <= 1024 ? 4 : 1;  // one wave per row, Lp * 12 B of LDS each
   const int64_t blocks = (p->n + wpb - 1) / wpb;
   hipLaunchKernelGGL(k_topk, dim3((unsigned)blocks), dim3(64 * wpb), (size_t)wpb * p->Lp * 12, p->stream, s,
-                     p->d_part, sA, sB, (int)p->K, p->Lp, p->d_out_ids, p->d_out_sc, p->d_out_len);
+                     p->d_part, sA, sB, (int)p->K, p->Lp, p->d_out_ids, p->d_out_sc, p->d_out_len, owner, rank);
   HIP_OK(hipGetLastError());
   return PPR_OK;
 }
@@ -2804,13 +2849,15 @@ static int xroute_build(ppr_plan* p, const std::vector<int64_t> (&bd)[2], XRoute
 
 // the routed exchange of iteration it: per peer, the rows it reads; exact block sizes (one 8-byte
 // send / receive per peer first), then the blocks, then the unpacks
-static int x_exchange_routed(ppr_plan* p, uint32_t it, const XRoute& xr) {
+static int x_exchange_routed(ppr_plan* p, uint32_t it, const XRoute& xr, int slot = -1) {
   const int W = p->nranks, me = p->rank, q = (int)(it & 1);
   hipStream_t s = p->stream;
   int64_t rb = 0;
   ppr_grank_plan_row_bytes(p, &rb);
-  const int nxt = ((iter_args(p, (int)it, false).active == 1) ? iter_args(p, (int)it, false).sB
-                                                               : iter_args(p, (int)it, false).sA) ^ 1;
+  // (slot >= 0: the rows of partition it & 1 in that slot -- the sharded init's, slot 0)
+  const int nxt = slot >= 0 ? slot
+                            : ((iter_args(p, (int)it, false).active == 1) ? iter_args(p, (int)it, false).sB
+                                                                           : iter_args(p, (int)it, false).sA) ^ 1;
   std::vector<size_t> so(W + 1, 0), ro(W + 1, 0);
   for (int d = 0; d < W; d++) {
     so[d + 1] = so[d] + (xr.scnt[q][d] ? (size_t)(8 + xr.scnt[q][d] * rb) : 0);
@@ -2903,6 +2950,135 @@ static int x_exchange_routed(ppr_plan* p, uint32_t it, const XRoute& xr) {
   return PPR_OK;
 }
 
+// Sharded init (routed runs): every rank merges the init baskets of its own sources of both
+// partitions and of the dangling nodes (their {v: 1-d} rows are the same on every rank), then sends
+// each peer the init rows it reads -- the same consumer lists as an iteration's exchange, slot 0.
+static int init_sharded(ppr_plan* p, const std::vector<int64_t> (&bd)[2], const XRoute& xr) {
+  hipStream_t s = p->stream;
+  if (p->own_world != p->nranks || p->own_rank != p->rank || !p->d_own) {
+    const int64_t m0 = bd[0][p->rank + 1] - bd[0][p->rank], m1 = bd[1][p->rank + 1] - bd[1][p->rank];
+    if (!p->d_own) { int rc = dalloc(&p->d_own, std::max<int64_t>(1, p->n)); if (rc) return rc; }
+    if (m0) HIP_OK(hipMemcpyAsync(p->d_own, p->d_act[0] + bd[0][p->rank], 4 * (size_t)m0, hipMemcpyDeviceToDevice, s));
+    if (m1) HIP_OK(hipMemcpyAsync(p->d_own + m0, p->d_act[1] + bd[1][p->rank], 4 * (size_t)m1, hipMemcpyDeviceToDevice, s));
+    p->own_cnt = m0 + m1;
+    p->own_world = p->nranks;
+    p->own_rank = p->rank;
+  }
+  p->md_shared_it = -1;
+  p->hot_n = 0;
+  p->hot_built_it = -1;
+  if (p->d_dlast) HIP_OK(hipMemsetAsync(p->d_dlast, 0, 4 * (size_t)std::max<int64_t>(1, p->n), s));
+  IterArgs a = iter_args(p, 0, true);
+  int rc = init_dangling(p, p->d_all + p->n_nd, p->n - p->n_nd);
+  if (rc) return rc;
+  rc = run_merge(p, a, p->d_own, p->own_cnt, p->d_maxdiff + PPR_MAX_ITER_STATS);
+  if (rc) return rc;
+  for (uint32_t q = 0; q < 2; q++) {
+    rc = x_exchange_routed(p, q, xr, 0);
+    if (rc) return rc;
+  }
+  return PPR_OK;
+}
+
+// Sharded final top-K (routed runs): every rank selects the top-K of its own rows (and of the
+// dangling nodes') and the K-wide rows are all-gathered, one block per rank and partition -- instead
+// of an L-wide broadcast of every row and a top-K of all n rows on every rank
+static int x_gather_topk(ppr_plan* p, int q, const std::vector<int64_t>& b) {
+  const int W = p->nranks, me = p->rank;
+  hipStream_t s = p->stream;
+  const int64_t K = p->K;
+  const int64_t ob = 12 * K + 4;  // bytes of a K-entry row at most
+  std::vector<int64_t> sz(W);
+  std::vector<size_t> xo(W + 1, 0);
+  for (int r = 0; r < W; r++) {
+    const int64_t c = b[r + 1] - b[r];
+    sz[r] = 8 * (c + 1) + c * ob;
+    xo[r + 1] = xo[r] + (r == me ? 0 : (size_t)sz[r]);
+  }
+  int rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, (size_t)sz[me]);
+  if (rc) return rc;
+  rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, std::max<size_t>(8, xo[W]));
+  if (rc) return rc;
+  const int64_t mine = b[me + 1] - b[me];
+  const int32_t* ml = p->d_act[q] + b[me];
+  unsigned char* buf = p->d_xsend;
+  int64_t* off = reinterpret_cast<int64_t*>(buf);
+  if (mine == 0) {
+    HIP_OK(hipMemsetAsync(buf, 0, 8, s));
+  } else {
+    int64_t* rsz = reinterpret_cast<int64_t*>(buf + 8 * (mine + 1));  // (the payload area, free until the pack)
+    hipLaunchKernelGGL(k_osize, dim3((unsigned)((mine + 256) / 256)), dim3(256), 0, s, p->d_out_len, ml, mine, rsz);
+    size_t tmp = 0;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, rsz, off, (int)(mine + 1), s));
+    rc = ensure_dev(&p->d_xtmp, &p->xtmp_bytes, tmp);
+    if (rc) return rc;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(p->d_xtmp, tmp, rsz, off, (int)(mine + 1), s));
+    hipLaunchKernelGGL(k_opack, dim3((unsigned)((mine + 3) / 4)), dim3(256), 0, s, p->d_out_ids, p->d_out_sc,
+                       p->d_out_len, (int)K, ml, mine, buf);
+    HIP_OK(hipGetLastError());
+  }
+  p->x_bytes += (int64_t)xo[W];
+  rc = x_blocks(p, b, sz, xo, s);
+  if (rc) return rc;
+  for (int r = 0; r < W; r++) {
+    const int64_t c = b[r + 1] - b[r];
+    if (r == me || !c) continue;
+    hipLaunchKernelGGL(k_ounpack, dim3((unsigned)((c + 3) / 4)), dim3(256), 0, s, p->d_out_ids, p->d_out_sc,
+                       p->d_out_len, (int)K, p->d_act[q] + b[r], c, p->d_xrecv + xo[r]);
+    HIP_OK(hipGetLastError());
+  }
+  return PPR_OK;
+}
+
+// Measurement (tools/shard_floor.py): on this one plan, the device time rank `rank` of a `world`-rank
+// routed run spends in one of its sharded ends (the exchanges around them are not included):
+// what 0 = the top-K of its own rows and the dangling ones (of the plan's current rows: time it
+// after a job), what 1 = the init of its own sources and the dangling nodes (rewrites those rows).
+extern "C" int ppr_grank_plan_ends_time(ppr_plan* p, int32_t world, int32_t rank, int32_t iterations_run,
+                                        int32_t what, double* ms_out) {
+  if (!p || world < 1 || rank < 0 || rank >= world || world > 127 || iterations_run < 0 || what < 0 || what > 1)
+    return PPR_ERR_ARG;
+  HIP_OK(hipSetDevice(p->device));
+  hipStream_t s = p->stream;
+  std::vector<int64_t> bd[2];
+  shard_bounds(p->work[0], world, bd[0]);
+  shard_bounds(p->work[1], world, bd[1]);
+  float ms = 0.f;
+  if (what == 0) {
+    if (!p->d_xowner) { int rc = dalloc(&p->d_xowner, p->n); if (rc) return rc; }
+    HIP_OK(hipMemsetAsync(p->d_xowner, 0xff, (size_t)p->n, s));
+    for (int q = 0; q < 2; q++) {
+      if (!p->nact[q]) continue;
+      XBounds xb{};
+      xb.world = world;
+      for (int r = 0; r <= world; r++) xb.b[r] = bd[q][r];
+      hipLaunchKernelGGL(k_xowner, dim3((unsigned)((p->nact[q] + 255) / 256)), dim3(256), 0, s, p->d_act[q],
+                         p->nact[q], xb, p->d_xowner);
+    }
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(p->ev_a, s));
+    int rc = launch_topk(p, ((iterations_run + 1) / 2) & 1, (iterations_run / 2) & 1, p->d_xowner, rank);
+    if (rc) return rc;
+  } else {
+    const int64_t m0 = bd[0][rank + 1] - bd[0][rank], m1 = bd[1][rank + 1] - bd[1][rank];
+    if (!p->d_own) { int rc = dalloc(&p->d_own, std::max<int64_t>(1, p->n)); if (rc) return rc; }
+    p->own_world = 0;  // (init_sharded rebuilds its own list)
+    if (m0) HIP_OK(hipMemcpyAsync(p->d_own, p->d_act[0] + bd[0][rank], 4 * (size_t)m0, hipMemcpyDeviceToDevice, s));
+    if (m1) HIP_OK(hipMemcpyAsync(p->d_own + m0, p->d_act[1] + bd[1][rank], 4 * (size_t)m1, hipMemcpyDeviceToDevice, s));
+    HIP_OK(hipEventRecord(p->ev_a, s));
+    IterArgs a = iter_args(p, 0, true);
+    int rc = init_dangling(p, p->d_all + p->n_nd, p->n - p->n_nd);
+    if (rc) return rc;
+    rc = run_merge(p, a, p->d_own, m0 + m1, p->d_maxdiff + PPR_MAX_ITER_STATS);
+    if (rc) return rc;
+  }
+  HIP_OK(hipEventRecord(p->ev_b, s));
+  HIP_OK(hipEventSynchronize(p->ev_b));
+  hipEventElapsedTime(&ms, p->ev_a, p->ev_b);
+  if (ms_out) *ms_out = ms;
+  return probe_take();
+}
+
 extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance,
                                           ppr_stats* st) {
   if (!p) return PPR_ERR_ARG;
@@ -2917,17 +3093,22 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
   p->x_bytes = 0;
   p->x_rows_sent = 0;
   HIP_OK(hipEventRecord(p->ev_a, s));
-  int rc = ppr_grank_plan_init(p);
-  if (rc) return rc;
   std::vector<int64_t> bd[2];
   shard_bounds(p->work[0], p->nranks, bd[0]);
   shard_bounds(p->work[1], p->nranks, bd[1]);
-  // consumer routing: during the run a row goes only to the ranks that read it; the result rows of
-  // both partitions are broadcast once after the last iteration, so every rank ends with the
-  // whole slab (ppr_grank_plan_finish's top-K reads every row)
+  // consumer routing: during the run a row goes only to the ranks that read it. The ends are
+  // sharded too (PPR_XSHARD_ENDS=0: not): each rank inits its own sources and the dangling nodes
+  // and sends the init rows its peers read; at the end each rank selects the top-K of its own rows
+  // and the K-wide rows are all-gathered. Without them every rank inits every source, and the
+  // result rows of both partitions are broadcast L-wide so that every rank's top-K reads every row.
   const bool route = p->nranks > 1 && p->nranks <= 32 && p->xroute;
+  static const bool ends_env = !(getenv("PPR_XSHARD_ENDS") && atoi(getenv("PPR_XSHARD_ENDS")) == 0);
+  const bool shard_ends = route && ends_env;
   XRoute xr;
+  int rc = PPR_OK;
   if (route) { rc = xroute_build(p, bd, xr); if (rc) return rc; }
+  rc = shard_ends ? init_sharded(p, bd, xr) : ppr_grank_plan_init(p);
+  if (rc) return rc;
   double md[2] = {tolerance, tolerance};
   uint32_t it = 0;
   for (; it < iterations && std::max(md[0], md[1]) >= tolerance; it++) {
@@ -2949,15 +3130,26 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
       std::swap(md[0], md[1]);
     }
   }
-  if (route)
-    for (int q = 0; q < 2; q++) {  // each partition's rows as its last iteration wrote them
-      const int64_t last = (int64_t)it - 1 - (((int64_t)it - 1 - q) & 1);
-      if (last < 0 || (last & 1) != q) continue;
-      rc = x_exchange_bulk(p, (uint32_t)last, bd[q]);
+  if (shard_ends) {
+    rc = launch_topk(p, ((it + 1) / 2) & 1, (it / 2) & 1, p->d_xowner, p->rank);
+    if (rc) return rc;
+    for (int q = 0; q < 2; q++) {
+      rc = x_gather_topk(p, q, bd[q]);
       if (rc) return rc;
     }
-  rc = ppr_grank_plan_finish(p, (int32_t)it);
-  if (rc) return rc;
+    rc = probe_take();
+    if (rc) return rc;
+  } else {
+    if (route)
+      for (int q = 0; q < 2; q++) {  // each partition's rows as its last iteration wrote them
+        const int64_t last = (int64_t)it - 1 - (((int64_t)it - 1 - q) & 1);
+        if (last < 0 || (last & 1) != q) continue;
+        rc = x_exchange_bulk(p, (uint32_t)last, bd[q]);
+        if (rc) return rc;
+      }
+    rc = ppr_grank_plan_finish(p, (int32_t)it);
+    if (rc) return rc;
+  }
   HIP_OK(hipEventRecord(p->ev_b, s));
   HIP_OK(hipEventSynchronize(p->ev_b));
   if (st) {

@@ -140,11 +140,15 @@ __global__ void __launch_bounds__(64) k_merge_glb(DevGraph g, DevSlab s, IterArg
 // into LDS, keeps its top-K by the top-L rule (score desc, tie_w desc) and writes them by (score
 // desc, id asc)
 __global__ void __launch_bounds__(256) k_topk(DevSlab s, const uint8_t* part, int sA, int sB, int K, int Lp,
-                                              int32_t* oid, double* osc, int32_t* olen) {
+                                              int32_t* oid, double* osc, int32_t* olen, const int8_t* owner,
+                                              int rank) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   const int64_t v = (int64_t)blockIdx.x * (blockDim.x / WAVE) + wv;
   if (v >= s.n) return;
+  // sharded run: this rank's own rows and the dangling nodes' (identical everywhere) only -- the
+  // others' rows are stale here, their top-K arrive from their owners (grank.hip x_gather_topk)
+  if (owner && owner[v] >= 0 && owner[v] != rank) return;
   uint64_t* rv = reinterpret_cast<uint64_t*>(smem) + (size_t)wv * Lp;
   int* rk = reinterpret_cast<int*>(smem + (size_t)(blockDim.x / WAVE) * Lp * 8) + (size_t)wv * Lp;
   const int sl = part[v] ? sB : sA;
@@ -167,6 +171,30 @@ __global__ void __launch_bounds__(256) k_topk(DevSlab s, const uint8_t* part, in
   if (lane_id() == 0) olen[v] = k;
 }
 
+// Init of the dangling nodes (no successors): their basket is {v: 1-d} for good (include/grank.h
+// :64-83 -- the reference never merges them again), in both slots like every init row
+// (finish_source, unit mode), with its row minimum and 64-range index. One thread per (node,
+// range): no table, no select -- the merge engines spent as long on these 52 % of RMAT-22's nodes
+// as on all the others' init.
+__global__ void k_init_dangling(DevSlab s, const int32_t* list, int64_t cnt, double seed) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= cnt * NRANGE) return;
+  const int64_t v = list[t / NRANGE];
+  const int q = (int)(t % NRANGE);
+  const uint16_t x = row_range((int)v) <= (uint32_t)q ? 1 : 0;
+#pragma unroll
+  for (int sl = 0; sl < 2; sl++) {
+    s.rix[s.xrow(sl, v) + q] = x;
+    if (q == 0) {
+      const int64_t r = s.row(sl, v);
+      s.ids[r] = (int32_t)v;  // (init precedes any hot set: ids are stored as themselves)
+      s.sc[r] = seed;
+      s.len[s.lrow(sl, v)] = 1;
+      s.rmin[s.lrow(sl, v)] = seed;
+    }
+  }
+}
+
 // Row exchange for source sharding: one compact block per active-list range of `count` rows (the
 // next-slot rows the iteration wrote, in stored order):
 //   int64 off[count + 1]                payload offset of row r (off[0] = 0, off[count] = payload bytes)
@@ -186,6 +214,42 @@ __global__ void k_xsize(DevSlab s, int nxt, const int32_t* list, int64_t count, 
 // block bytes of a packed range -> *total (the size the ranks exchange before the payload)
 __global__ void k_xtotal(const int64_t* off, int64_t count, int64_t* total) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *total = 8 * (count + 1) + off[count];
+}
+
+// The final top-K rows of a sharded run travel in the same block layout (int64 off[count + 1], then
+// per row int32 ids[Le] and f64 scores[len]) from the output arrays: K entries at most a row.
+__global__ void k_osize(const int32_t* olen, const int32_t* list, int64_t count, int64_t* sz) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < count) sz[r] = xrow_bytes(olen[list[r]]);
+  else if (r == count) sz[r] = 0;
+}
+__global__ void k_opack(const int32_t* oid, const double* osc, const int32_t* olen, int K, const int32_t* list,
+                        int64_t count, unsigned char* buf) {
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
+  if (r >= count) return;
+  const int64_t* off = reinterpret_cast<const int64_t*>(buf);
+  const int64_t v = list[r];
+  const int len = olen[v];
+  unsigned char* row = buf + 8 * (count + 1) + off[r];
+  int32_t* rid = reinterpret_cast<int32_t*>(row);
+  double* rsc = reinterpret_cast<double*>(row + 4 * (int64_t)((len + 1) & ~1));
+  for (int i = lane_id(); i < len; i += WAVE) { rid[i] = oid[v * K + i]; rsc[i] = osc[v * K + i]; }
+}
+__global__ void k_ounpack(int32_t* oid, double* osc, int32_t* olen, int K, const int32_t* list, int64_t count,
+                          const unsigned char* buf) {
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x / WAVE) + (threadIdx.x >> 6);
+  if (r >= count) return;
+  const int64_t* off = reinterpret_cast<const int64_t*>(buf);
+  const int64_t v = list[r];
+  const int len = (int)((off[r + 1] - off[r]) / 12);
+  const unsigned char* row = buf + 8 * (count + 1) + off[r];
+  const int32_t* rid = reinterpret_cast<const int32_t*>(row);
+  const double* rsc = reinterpret_cast<const double*>(row + 4 * (int64_t)((len + 1) & ~1));
+  for (int i = lane_id(); i < K; i += WAVE) {
+    oid[v * K + i] = i < len ? rid[i] : -1;
+    osc[v * K + i] = i < len ? rsc[i] : 0.0;
+  }
+  if (lane_id() == 0) olen[v] = len;
 }
 
 __global__ void k_xpack(DevSlab s, int nxt, const int32_t* list, int64_t count, unsigned char* buf) {

@@ -49,7 +49,8 @@ struct ppr_plan {
   int32_t* d_len = nullptr;
   uint16_t* d_rix = nullptr;      // [2][n][NRANGE] row range index
   double* d_rmin = nullptr;       // [2][n] row minimum
-  int32_t* d_all = nullptr;       // 0..n-1 (init list)
+  int32_t* d_all = nullptr;       // init list: the n_nd nodes with successors, then the dangling ones
+  int64_t n_nd = 0;
   int32_t* d_act[2] = {nullptr, nullptr};
   int64_t nact[2] = {0, 0};
   int32_t* d_cand = nullptr;
@@ -143,6 +144,9 @@ struct ppr_plan {
   bool xroute = true;
   int xtest_badsize = -1;             // tests (PPR_XTEST_BADSIZE=r): rank r advertises wrong block sizes
   int8_t* d_xowner = nullptr;         // [n] rank merging each active node (-1: dangling)
+  int32_t* d_own = nullptr;           // sharded init: this rank's active nodes (both partitions), then
+  int64_t own_cnt = 0;                // every dangling node (identical on every rank)
+  int own_world = 0, own_rank = -1;   // the shard the list was built for
   uint32_t* d_xcmask = nullptr;       // [n] ranks reading each node's row
   int32_t* d_xlists = nullptr;        // per partition: send lists to each peer, receive lists from each peer
   size_t xlists_cap = 0;
@@ -283,7 +287,7 @@ inline void plan_free(ppr_plan* p) {
   if (p->stream4) hipStreamDestroy(p->stream4);
   if (p->comm) ncclCommDestroy(p->comm);
   hipFree(p->d_xsend); hipFree(p->d_xrecv); hipFree(p->d_xsz); hipFree(p->d_xtmp);
-  hipFree(p->d_xowner); hipFree(p->d_xcmask); hipFree(p->d_xlists);
+  hipFree(p->d_xowner); hipFree(p->d_xcmask); hipFree(p->d_xlists); hipFree(p->d_own);
   if (p->h_hub_pin) hipHostFree(p->h_hub_pin);
   if (p->h_desc_pin) hipHostFree(p->h_desc_pin);
   if (p->h_xs_pin) hipHostFree(p->h_xs_pin);
@@ -448,7 +452,7 @@ inline int dalloc(T** p, size_t count) {
 int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t K, uint32_t L,
                double damping, const ppr_opts* o, ppr_plan** out, bool mc = false);
 // final top-K: prefix K of the row in slot sA (partition 0 nodes) / sB (partition 1 nodes)
-int launch_topk(ppr_plan* p, int sA, int sB);
+int launch_topk(ppr_plan* p, int sA, int sB, const int8_t* owner = nullptr, int rank = 0);
 // classify + every merge tier for `count` sources of the device list `list`
 // MC combine: read and redo the last level's deferred hub overflow list (host sync)
 int run_merge_flush(ppr_plan* p, const IterArgs& a, unsigned long long* maxdiff);

@@ -85,7 +85,12 @@ def grank_csr(csr: Csr, K: int, L: int, iterations: int, damping: float, toleran
     res = GrankResult(ids, sc, lens)
     if n == 0:
         return res
-    p = csr.partitions() if part is None else np.ascontiguousarray(part, dtype=np.uint8)
+    # part="plan": none given -- plan creation computes them (on the device, the host BFS as fallback),
+    # as for the C++ drop-in templates
+    if isinstance(part, str) and part == "plan":
+        p = None
+    else:
+        p = csr.partitions() if part is None else np.ascontiguousarray(part, dtype=np.uint8)
     c = _lib.csr_struct(csr.row_ptr, csr.col)
     o = _lib.PprOpts(device, _flags(stats, sum_mode), None)
     st = _lib.PprStats()

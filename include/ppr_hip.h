@@ -90,6 +90,12 @@ const char* ppr_build_info(void);
 
 /* BFS 2-colouring of include/internal/pprInternal.h:29-99; part[i] = 0 for partitions.first */
 int ppr_find_partitions_csr(const ppr_csr* g, uint8_t* part);
+/* The same partitions computed on the device (`device` < 0: the current one): min-label components
+ * and a level-synchronous BFS from each component's first node (csrc/partition.hip). Returns
+ * PPR_ERR_RANGE for graphs that need more rounds than it allows (long paths): use the host BFS.
+ * ppr_grank_plan_create / ppr_grank_csr take it when the caller passes no partitions, falling back
+ * to the host BFS (PPR_HOST_BFS=1: the host BFS only). */
+int ppr_find_partitions_csr_device(const ppr_csr* g, uint8_t* part, int32_t device);
 
 /* MCCompletePathV2 node order, include/mccompletepathv2.h:36-113 (the same library sort on the
  * same records, so ties come out in the reference's order) */
@@ -177,6 +183,12 @@ int ppr_grank_plan_comm_init(ppr_plan* p, const void* id128, int32_t nranks, int
 int ppr_grank_plan_shard_bounds(ppr_plan* p, int32_t it, int32_t nranks, int64_t* bounds);
 int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance, ppr_stats* st);
 int ppr_grank_plan_exchange_bytes(ppr_plan* p, int64_t* recv_bytes, int64_t* rows_sent);
+/* Measurement (no reference counterpart; tools/shard_floor.py): device milliseconds that rank
+ * `rank` of a `world`-rank routed run spends in one of its sharded ends, timed on this one plan:
+ * what 0 = its final top-K (own rows and the dangling ones; time it after a job), what 1 = its init
+ * (own sources and the dangling nodes; rewrites those rows). */
+int ppr_grank_plan_ends_time(ppr_plan* p, int32_t world, int32_t rank, int32_t iterations_run, int32_t what,
+                             double* ms);
 /* Per-kernel roofline of the last ppr_grank_plan_run (no reference counterpart: measurement).
  * Kernel groups, in this order: 0 wave tier (k_merge_lds_x), 1 sieve large (k_sv1 + k_svfin, 16
  * waves), 2 sieve mid (8 waves), 3 sieve small (4 waves), 4 sieve multi-slice (k_svA + k_svB +

@@ -456,3 +456,43 @@ def test_gpu_widest_basket_limit():
     with pytest.raises(ppr.PprError) as e:
         ppr.grank_csr(csr, 64, 4097, 3, 0.85, -1.0, part=part, device=0)
     assert e.value.code == 11
+
+
+def _device_partitions(g):
+    import ctypes
+    from approximated_personalized_pagerank_amd import _lib
+    part = np.zeros(max(1, g.n), dtype=np.uint8)
+    c = _lib.csr_struct(g.row_ptr, g.col)
+    rc = _lib.lib().ppr_find_partitions_csr_device(ctypes.byref(c), part.ctypes.data, 0)
+    return rc, part[:g.n]
+
+
+def test_gpu_partitions_match_host():
+    """the device BFS 2-colouring (csrc/partition.hip, taken by plan creation when the caller passes
+    no partitions) equals the host BFS -- and so the reference's findPartitions -- on the reference
+    fixtures and on RMAT graphs; a long path exceeds its rounds (PPR_ERR_RANGE) and plan creation
+    takes the host BFS instead"""
+    from helpers import all_names, load
+    for name in all_names():
+        f = load(name)
+        g = ppr.Csr(f["rp"], f["col"])
+        rc, part = _device_partitions(g)
+        assert rc == 0 and np.array_equal(part, f["part"]), name
+    for scale, seed in [(12, 3), (16, 9), (20, 42)]:
+        g = ppr.rmat(scale, seed=seed)
+        rc, part = _device_partitions(g)
+        assert rc == 0 and np.array_equal(part, g.partitions()), scale
+    g = ppr.rmat(13, seed=8)
+    r = ppr.grank_csr(g, 16, 32, 4, 0.85, -1.0, part="plan", device=0)
+    o = oracle.grank(g.row_ptr, g.col, g.partitions(), 16, 32, 4, 0.85, -1.0)
+    assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])
+    n = 5000
+    rp = np.zeros(n + 1, dtype=np.int64)
+    rp[1:n] = np.arange(1, n)
+    rp[n] = n - 1
+    path = ppr.Csr(rp, np.arange(1, n, dtype=np.int32))
+    rc, _ = _device_partitions(path)
+    assert rc == 11
+    r = ppr.grank_csr(path, 4, 8, 3, 0.85, -1.0, part="plan", device=0)  # (device declines, host BFS)
+    o = oracle.grank(path.row_ptr, path.col, path.partitions(), 4, 8, 3, 0.85, -1.0)
+    assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])

@@ -70,9 +70,21 @@ def main():
         floor = sum(max(x["range_s"]) for x in per_it)
         total = sum(sum(x["range_s"]) for x in per_it)
         recv = sum(x["max_recv_bytes"] for x in per_it)
+        # the sharded ends of a routed run (grank.hip init_sharded / x_gather_topk): each rank's
+        # top-K of its own rows (after this job), then each rank's init of its own sources
+        ms = ctypes.c_double()
+        topk_ms, init_ms = [], []
+        for r in range(w):
+            _lib.check(_lib.lib().ppr_grank_plan_ends_time(plan._p, w, r, a.iters, 0, ctypes.byref(ms)), "ends_time")
+            topk_ms.append(ms.value)
+        for r in range(w):
+            _lib.check(_lib.lib().ppr_grank_plan_ends_time(plan._p, w, r, a.iters, 1, ctypes.byref(ms)), "ends_time")
+            init_ms.append(ms.value)
         res["worlds"][str(w)] = {"init_s": t_init, "merge_floor_s": floor, "merge_sum_s": total,
-                                 "max_rank_recv_bytes_per_job": recv, "iterations": per_it}
-        print(f"world {w}: init {t_init:.3f} s, slowest-rank merge {floor:.3f} s / job (all ranges {total:.3f} s), "
+                                 "max_rank_recv_bytes_per_job": recv, "sharded_topk_ms": topk_ms,
+                                 "sharded_init_ms": init_ms, "iterations": per_it}
+        print(f"world {w}: init {t_init:.3f} s (sharded: slowest rank {max(init_ms):.1f} ms), slowest-rank merge "
+              f"{floor:.3f} s / job (all ranges {total:.3f} s), sharded top-K slowest rank {max(topk_ms):.1f} ms, "
               f"largest per-rank receive {recv / 1e9:.1f} GB / job", flush=True)
     plan.close()
     if a.out:
