@@ -157,6 +157,9 @@ def lib() -> ctypes.CDLL:
         "ppr_grank_plan_unpack": (ctypes.c_int, [vp, i32, i64, i64, vp]),
         "ppr_grank_plan_fetch": (ctypes.c_int, [vp, vp, vp, vp]),
         "ppr_grank_plan_fetch_slab": (ctypes.c_int, [vp, i32, vp, vp, vp]),
+        "ppr_grank_plan_fetch_rows": (ctypes.c_int, [vp, i64, i64, vp, vp, vp]),
+        "ppr_host_alloc": (ctypes.c_int, [i64, ctypes.POINTER(vp)]),
+        "ppr_host_free": (None, [vp]),
         "ppr_grank_plan_stream": (vp, [vp]),
         "ppr_grank_plan_active_list": (ctypes.c_int, [vp, i32, vp]),
         "ppr_grank_plan_fold_maxdiff": (ctypes.c_int, [vp, i32, f64]),

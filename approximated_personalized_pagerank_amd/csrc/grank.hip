@@ -625,29 +625,50 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
     });
     if (bad) return PPR_ERR_GRAPH;
   }
-  if (part_in) {
-    std::memcpy(part.data(), part_in, n);
-  } else if (n) {
-    // on the device first (tens of ms at RMAT-22 instead of the host BFS's 0.3-0.5 s); the host BFS
-    // for graphs it declines (long paths) or when PPR_HOST_BFS=1
-    rc = getenv("PPR_HOST_BFS") && atoi(getenv("PPR_HOST_BFS")) == 1
-             ? PPR_ERR_RANGE
-             : ppr_find_partitions_csr_device(g, part.data(), (o && o->device >= 0) ? o->device : -1);
-    if (rc == PPR_ERR_RANGE) rc = ppr_find_partitions_csr(g, part.data());
-    if (rc) return rc;
-  }
+  // no partitions given: the BFS 2-colouring on the device, on the plan's own copy of the graph
+  // (raw successor ids uploaded once; the pass ORs the partition bits in) with the not yet used
+  // basket slab as its scratch -- tens of ms at RMAT-22 instead of the host BFS's 0.3-0.5 s. The
+  // host BFS for graphs the device pass declines (long paths: PPR_ERR_RANGE) or when PPR_HOST_BFS=1.
+  const bool dev_part = !part_in && n && !(getenv("PPR_HOST_BFS") && atoi(getenv("PPR_HOST_BFS")) == 1);
+  if (part_in) std::memcpy(part.data(), part_in, n);
+  else if (n && !dev_part && (rc = ppr_find_partitions_csr(g, part.data()))) return rc;
   const auto t1 = now();
-
-  // host-side CSR with partition bit of the successor
-  std::vector<int32_t> colx(m > 0 ? m : 1);
-  pprh::parallel_for(m, nth, [&](int64_t b, int64_t e, int) {
-    for (int64_t i = b; i < e; i++) colx[i] = g->col[i] | (part[g->col[i]] ? (int32_t)0x80000000 : 0);
-  });
+  // host-side CSR with partition bit of the successor (the device pass sets it itself)
+  std::vector<int32_t> colx;
+  auto build_colx = [&] {
+    colx.resize(m > 0 ? m : 1);
+    pprh::parallel_for(m, nth, [&](int64_t b, int64_t e, int) {
+      for (int64_t i = b; i < e; i++) colx[i] = g->col[i] | (part[g->col[i]] ? (int32_t)0x80000000 : 0);
+    });
+  };
+  if (!dev_part) build_colx();
   const auto t2 = now();
   ppr_plan* p = nullptr;
-  rc = plan_alloc(n, g->row_ptr, colx.data(), K, L, damping, o, &p);
+  rc = plan_alloc(n, g->row_ptr, dev_part ? g->col : colx.data(), K, L, damping, o, &p);
   if (rc) return rc;
   const auto t3 = now();
+  double part_dev_s = 0.0;
+  if (dev_part) {
+    const size_t slab = (size_t)2 * n * L;  // int32 entries of d_ids
+    int32_t* scr = nullptr;
+    bool own = false;
+    if ((size_t)m + 2 * (size_t)n + 2 <= slab) scr = p->d_ids;
+    else if (hipMalloc(&scr, 4 * ((size_t)m + 2 * (size_t)n + 2)) == hipSuccess) own = true;
+    else { plan_free(p); return PPR_ERR_OOM; }
+    rc = pprpart::partitions_core(p->d_rp, p->d_colx, n, m, p->d_part, part.data(), true, scr, scr + m,
+                                  scr + m + n, scr + m + 2 * n, p->stream);
+    if (own) hipFree(scr);
+    if (rc == PPR_ERR_RANGE) {  // (d_colx still raw)
+      rc = ppr_find_partitions_csr(g, part.data());
+      if (!rc) {
+        build_colx();
+        if (m && hipMemcpy(p->d_colx, colx.data(), 4 * (size_t)m, hipMemcpyHostToDevice) != hipSuccess) rc = PPR_ERR_HIP;
+      }
+    }
+    if (rc) { plan_free(p); return rc; }
+    part_dev_s = sec(t3, now());
+  }
+  const auto t4 = now();
   std::vector<int32_t> act[2];
   for (int64_t v = 0; v < n; v++)
     if (g->row_ptr[v + 1] > g->row_ptr[v]) act[part[v]].push_back((int32_t)v);
@@ -669,7 +690,7 @@ extern "C" int ppr_grank_plan_create(const ppr_csr* g, const uint8_t* part_in, u
   }
   if (timing)
     fprintf(stderr, "ppr_timing plan_create partitions_s %.3f colx_s %.3f alloc_upload_s %.3f work_s %.3f\n",
-            sec(t0, t1), sec(t1, t2), sec(t2, t3), sec(t3, now()));
+            sec(t0, t1) + part_dev_s, sec(t1, t2), sec(t2, t3), sec(t4, now()));
   p->nact[0] = (int64_t)act[0].size();
   p->nact[1] = (int64_t)act[1].size();
   if (p->hot_cap > 0 && n > 0) {
@@ -2422,6 +2443,31 @@ extern "C" int ppr_grank_plan_fetch(ppr_plan* p, int32_t* out_ids, double* out_s
   if (out_len) HIP_OK(hipMemcpyAsync(out_len, p->d_out_len, 4 * (size_t)p->n, hipMemcpyDeviceToHost, p->stream));
   HIP_OK(hipStreamSynchronize(p->stream));
   return PPR_OK;
+}
+
+extern "C" int ppr_grank_plan_fetch_rows(ppr_plan* p, int64_t begin, int64_t end, int32_t* out_ids,
+                                         double* out_scores, int32_t* out_len) {
+  if (!p || begin < 0 || end < begin || end > p->n) return PPR_ERR_ARG;
+  if (end == begin) return PPR_OK;
+  HIP_OK(hipSetDevice(p->device));
+  const size_t K = p->K, r0 = (size_t)begin, c = (size_t)(end - begin);
+  if (out_ids) HIP_OK(hipMemcpyAsync(out_ids, p->d_out_ids + r0 * K, 4 * c * K, hipMemcpyDeviceToHost, p->stream));
+  if (out_scores)
+    HIP_OK(hipMemcpyAsync(out_scores, p->d_out_sc + r0 * K, 8 * c * K, hipMemcpyDeviceToHost, p->stream));
+  if (out_len) HIP_OK(hipMemcpyAsync(out_len, p->d_out_len + r0, 4 * c, hipMemcpyDeviceToHost, p->stream));
+  HIP_OK(hipStreamSynchronize(p->stream));
+  return PPR_OK;
+}
+
+extern "C" int ppr_host_alloc(int64_t bytes, void** out) {
+  if (!out || bytes < 0) return PPR_ERR_ARG;
+  *out = nullptr;
+  if (bytes == 0) return PPR_OK;
+  return hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault) == hipSuccess ? PPR_OK : PPR_ERR_OOM;
+}
+
+extern "C" void ppr_host_free(void* ptr) {
+  if (ptr) (void)hipHostFree(ptr);
 }
 
 extern "C" int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, int32_t* ids,

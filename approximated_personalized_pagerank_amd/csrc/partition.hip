@@ -101,41 +101,25 @@ __global__ void k_bfs_parity(const int32_t* depth, int64_t n, uint8_t* part, int
   part[v] = (uint8_t)(d & 1);
 }
 
-}  // namespace pprpart
+// successors' partition bits into the CSR column words (the plan's colx: bit 31 = part of col)
+__global__ void k_col_mark(int32_t* col, int64_t m, const uint8_t* part) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < m) col[e] |= part[col[e]] ? (int32_t)0x80000000 : 0;
+}
 
-#define PP_OK(x)                                       \
-  do {                                                 \
-    if ((x) != hipSuccess) { rc = PPR_ERR_HIP; goto out; } \
+#define PP_OK(x)                                 \
+  do {                                           \
+    if ((x) != hipSuccess) return PPR_ERR_HIP;   \
   } while (0)
 
-// part[n] of the CSR graph on device `device` (the current one when < 0). PPR_ERR_RANGE: the graph
-// needs more rounds than the caps below (the caller takes the host BFS).
-extern "C" int ppr_find_partitions_csr_device(const ppr_csr* g, uint8_t* part, int32_t device) {
-  using namespace pprpart;
-  if (!g || !part || g->n < 0) return PPR_ERR_ARG;
-  const int64_t n = g->n;
-  if (n == 0) return PPR_OK;
-  if (n >= (1LL << 31) - 1) return PPR_ERR_RANGE;
-  const int64_t m = g->row_ptr[n];
+// The two passes on graph arrays already in HBM (d_col raw ids), on stream st: d_part[n] and the
+// host copy h_part[n]; mark: then OR the partition bits into d_col. Scratch: d_src[m], d_lab[n],
+// d_depth[n], d_flag[2]. PPR_ERR_RANGE leaves d_col untouched.
+int partitions_core(const int64_t* d_rp, int32_t* d_col, int64_t n, int64_t m, uint8_t* d_part, uint8_t* h_part,
+                    bool mark, int32_t* d_src, int32_t* d_lab, int32_t* d_depth, int32_t* d_flag, hipStream_t st) {
   constexpr int CC_ROUNDS = 64, BFS_LEVELS = 512;
-  int rc = PPR_OK;
-  int64_t* d_rp = nullptr;
-  int32_t *d_col = nullptr, *d_src = nullptr, *d_lab = nullptr, *d_depth = nullptr, *d_flag = nullptr;
-  uint8_t* d_part = nullptr;
-  hipStream_t st = nullptr;
   const unsigned bn = (unsigned)((n + 255) / 256), bm = (unsigned)((m + 255) / 256);
   int32_t h[2] = {0, 0};
-  if (device >= 0 && hipSetDevice(device) != hipSuccess) return PPR_ERR_HIP;
-  PP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  PP_OK(hipMalloc(&d_rp, 8 * (size_t)(n + 1)));
-  PP_OK(hipMalloc(&d_col, 4 * (size_t)(m > 0 ? m : 1)));
-  PP_OK(hipMalloc(&d_src, 4 * (size_t)(m > 0 ? m : 1)));
-  PP_OK(hipMalloc(&d_lab, 4 * (size_t)n));
-  PP_OK(hipMalloc(&d_depth, 4 * (size_t)n));
-  PP_OK(hipMalloc(&d_flag, 8));
-  PP_OK(hipMalloc(&d_part, (size_t)n));
-  PP_OK(hipMemcpyAsync(d_rp, g->row_ptr, 8 * (size_t)(n + 1), hipMemcpyHostToDevice, st));
-  if (m) PP_OK(hipMemcpyAsync(d_col, g->col, 4 * (size_t)m, hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_edge_src, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, d_rp, n, d_src);
   hipLaunchKernelGGL(k_cc_init, dim3(bn), dim3(256), 0, st, d_lab, n);
   PP_OK(hipGetLastError());
@@ -150,7 +134,7 @@ extern "C" int ppr_find_partitions_csr_device(const ppr_csr* g, uint8_t* part, i
       PP_OK(hipStreamSynchronize(st));
       if (!h[0]) break;
     }
-    if (r == CC_ROUNDS) { rc = PPR_ERR_RANGE; goto out; }
+    if (r == CC_ROUNDS) return PPR_ERR_RANGE;
   }
   hipLaunchKernelGGL(k_bfs_roots, dim3(bn), dim3(256), 0, st, d_lab, n, d_depth);
   PP_OK(hipGetLastError());
@@ -165,16 +149,49 @@ extern "C" int ppr_find_partitions_csr_device(const ppr_csr* g, uint8_t* part, i
       PP_OK(hipStreamSynchronize(st));
       if (!h[0]) break;
     }
-    if (d == BFS_LEVELS) { rc = PPR_ERR_RANGE; goto out; }
+    if (d == BFS_LEVELS) return PPR_ERR_RANGE;
   }
   PP_OK(hipMemsetAsync(d_flag, 0, 4, st));
   hipLaunchKernelGGL(k_bfs_parity, dim3(bn), dim3(256), 0, st, d_depth, n, d_part, d_flag);
   PP_OK(hipGetLastError());
-  PP_OK(hipMemcpyAsync(part, d_part, (size_t)n, hipMemcpyDeviceToHost, st));
+  PP_OK(hipMemcpyAsync(h_part, d_part, (size_t)n, hipMemcpyDeviceToHost, st));
   PP_OK(hipMemcpyAsync(h, d_flag, 4, hipMemcpyDeviceToHost, st));
   PP_OK(hipStreamSynchronize(st));
-  if (h[0]) rc = PPR_ERR_HIP;  // (a node no root reached: cannot happen)
-out:
+  if (h[0]) return PPR_ERR_HIP;  // (a node no root reached: cannot happen)
+  if (mark && m) {
+    hipLaunchKernelGGL(k_col_mark, dim3(bm), dim3(256), 0, st, d_col, m, d_part);
+    PP_OK(hipGetLastError());
+    PP_OK(hipStreamSynchronize(st));
+  }
+  return PPR_OK;
+}
+
+}  // namespace pprpart
+
+// part[n] of the CSR graph on device `device` (the current one when < 0). PPR_ERR_RANGE: the graph
+// needs more rounds than partitions_core's caps (the caller takes the host BFS).
+extern "C" int ppr_find_partitions_csr_device(const ppr_csr* g, uint8_t* part, int32_t device) {
+  using namespace pprpart;
+  if (!g || !part || g->n < 0) return PPR_ERR_ARG;
+  const int64_t n = g->n;
+  if (n == 0) return PPR_OK;
+  if (n >= (1LL << 31) - 1) return PPR_ERR_RANGE;
+  const int64_t m = g->row_ptr[n];
+  int rc = PPR_ERR_HIP;
+  int64_t* d_rp = nullptr;
+  int32_t *d_col = nullptr, *d_src = nullptr, *d_lab = nullptr, *d_depth = nullptr, *d_flag = nullptr;
+  uint8_t* d_part = nullptr;
+  hipStream_t st = nullptr;
+  if (device >= 0 && hipSetDevice(device) != hipSuccess) return PPR_ERR_HIP;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess && hipMalloc(&d_rp, 8 * (size_t)(n + 1)) == hipSuccess &&
+      hipMalloc(&d_col, 4 * (size_t)(m > 0 ? m : 1)) == hipSuccess &&
+      hipMalloc(&d_src, 4 * (size_t)(m > 0 ? m : 1)) == hipSuccess && hipMalloc(&d_lab, 4 * (size_t)n) == hipSuccess &&
+      hipMalloc(&d_depth, 4 * (size_t)n) == hipSuccess && hipMalloc(&d_flag, 8) == hipSuccess &&
+      hipMalloc(&d_part, (size_t)n) == hipSuccess &&
+      hipMemcpyAsync(d_rp, g->row_ptr, 8 * (size_t)(n + 1), hipMemcpyHostToDevice, st) == hipSuccess &&
+      (!m || hipMemcpyAsync(d_col, g->col, 4 * (size_t)m, hipMemcpyHostToDevice, st) == hipSuccess))
+    rc = partitions_core(d_rp, d_col, n, m, d_part, part, false, d_src, d_lab, d_depth, d_flag, st);
+  if (st) hipStreamSynchronize(st);
   hipFree(d_rp); hipFree(d_col); hipFree(d_src); hipFree(d_lab); hipFree(d_depth); hipFree(d_flag); hipFree(d_part);
   if (st) hipStreamDestroy(st);
   return rc;

@@ -451,6 +451,10 @@ inline int dalloc(T** p, size_t count) {
 // (mc: the MCCompletePathV2 combine's bucket defaults, HUB_BUCKET_MC / HUB_WAVE_T_MC)
 int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t K, uint32_t L,
                double damping, const ppr_opts* o, ppr_plan** out, bool mc = false);
+namespace pprpart {  // partition.hip: the BFS 2-colouring on graph arrays already in HBM
+int partitions_core(const int64_t* d_rp, int32_t* d_col, int64_t n, int64_t m, uint8_t* d_part, uint8_t* h_part,
+                    bool mark, int32_t* d_src, int32_t* d_lab, int32_t* d_depth, int32_t* d_flag, hipStream_t st);
+}
 // final top-K: prefix K of the row in slot sA (partition 0 nodes) / sB (partition 1 nodes)
 int launch_topk(ppr_plan* p, int sA, int sB, const int8_t* owner = nullptr, int rank = 0);
 // classify + every merge tier for `count` sources of the device list `list`

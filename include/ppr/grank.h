@@ -7,9 +7,10 @@
 // What happens per call (DESIGN.md "boundary"):
 //   1. dense ids = the graph's iteration order, CSR keeps every successor vector's order
 //      (the reference's partitions and summation order depend on both);
-//   2. ppr_grank_csr(): BFS partitions (include/internal/pprInternal.h:29-99), upload, init,
-//      iterations, final top-K on the device, download;
-//   3. the top-K rows are materialised back into unordered_map<Key, unordered_map<Key,double>>.
+//   2. ppr_grank_plan_create/run (ppr_grank_csr's steps): BFS partitions
+//      (include/internal/pprInternal.h:29-99), upload, init, iterations, final top-K on the device;
+//   3. the top-K rows come down in chunks while the host threads materialise them back into
+//      unordered_map<Key, unordered_map<Key,double>> (download_materialize).
 // Results vs the reference (INTEGRATION.md "Numerical contract"):
 //   default (exact sum)  every score within 1e-12 relative of the reference's: each basket value is
 //                        the exact sum of the rounded products, rounded once (the reference rounds
@@ -336,17 +337,76 @@ struct Outer {
   }
 };
 
-// inner maps from the device's top-K rows (independent per source: all host threads)
+// inner maps from one chunk of the device's top-K rows [v0, v0 + cnt) (independent per source)
+template <typename Key>
+inline void materialize_rows(const Flat<Key>& f, Outer<Key>& o, size_t K, size_t v0, size_t cnt,
+                             const int32_t* ids, const double* sc, const int32_t* len) {
+  for (size_t r = 0; r < cnt; r++) {
+    std::unordered_map<Key, double>& m = *o.row[v0 + r];
+    m.reserve((size_t)len[r]);
+    for (int32_t i = 0; i < len[r]; i++) m.emplace(*f.keys[ids[r * K + i]], sc[r * K + i]);
+  }
+}
+
+// all rows from whole host copies (n*K ids/scores, n lengths), on nt threads
 template <typename Key>
 inline void materialize_rows(const Flat<Key>& f, Outer<Key>& o, size_t K, const std::vector<int32_t>& ids,
                              const std::vector<double>& sc, const std::vector<int32_t>& len, size_t nt) {
   parallel_ranges(f.keys.size(), nt, [&](size_t b, size_t e) {
-    for (size_t v = b; v < e; v++) {
-      std::unordered_map<Key, double>& m = *o.row[v];
-      m.reserve((size_t)len[v]);
-      for (int32_t i = 0; i < len[v]; i++) m.emplace(*f.keys[ids[v * K + i]], sc[v * K + i]);
-    }
+    materialize_rows(f, o, K, b, e - b, ids.data() + b * K, sc.data() + b * K, len.data() + b);
   });
+}
+
+// The top-K rows come down chunk by chunk into a ring of page-locked slots (DMA at link rate: the
+// whole 3.2 GB of an RMAT-22 result into fresh pageable vectors cost a zero fill, the page faults
+// and a staged copy) while nt threads materialise the chunks already down, so the download hides
+// behind the inner-map fills. The calling thread fetches, then frees the plan's device memory
+// while the fills finish; the workers take chunks in order.
+template <typename Key>
+inline int download_materialize(ppr_plan* p, const Flat<Key>& f, Outer<Key>& o, size_t K, size_t nt) {
+  const size_t n = f.keys.size(), C = 8192, nc = (n + C - 1) / C;
+  nt = std::max<size_t>(1, std::min(nt, nc));
+  const size_t S = std::min(nc, nt + 2), ids_b = C * K * 4, slot_b = C * K * 12 + C * 4;
+  void* ring = nullptr;
+  int rc = ppr_host_alloc((int64_t)(S * slot_b), &ring);
+  if (rc) { ppr_grank_plan_destroy(p); return rc; }
+  std::unique_ptr<std::atomic<uint8_t>[]> done(new std::atomic<uint8_t>[nc]);
+  for (size_t c = 0; c < nc; c++) done[c].store(0, std::memory_order_relaxed);
+  std::atomic<size_t> fetched(0), next(0);
+  std::atomic<int> err(0);
+  auto slot = [&](size_t c) { return (char*)ring + (c % S) * slot_b; };
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (size_t t = 0; t < nt; t++)
+    th.emplace_back([&] {
+      for (;;) {
+        const size_t c = next.fetch_add(1);
+        if (c >= nc) return;
+        while (fetched.load(std::memory_order_acquire) <= c) {
+          if (err.load(std::memory_order_relaxed)) return;
+          std::this_thread::yield();
+        }
+        char* b = slot(c);
+        const size_t v0 = c * C;
+        materialize_rows(f, o, K, v0, std::min(C, n - v0), (const int32_t*)b, (const double*)(b + ids_b),
+                         (const int32_t*)(b + C * K * 12));
+        done[c].store(1, std::memory_order_release);
+      }
+    });
+  for (size_t c = 0; c < nc && !rc; c++) {
+    if (c >= S)
+      while (!done[c - S].load(std::memory_order_acquire)) std::this_thread::yield();
+    char* b = slot(c);
+    const size_t v0 = c * C;
+    rc = ppr_grank_plan_fetch_rows(p, (int64_t)v0, (int64_t)std::min(n, v0 + C), (int32_t*)b,
+                                   (double*)(b + ids_b), (int32_t*)(b + C * K * 12));
+    if (rc) err.store(rc);
+    else fetched.store(c + 1, std::memory_order_release);
+  }
+  ppr_grank_plan_destroy(p);  // (beside the last fills)
+  for (auto& x : th) x.join();
+  ppr_host_free(ring);
+  return rc;
 }
 
 template <typename Key>
@@ -360,8 +420,6 @@ inline std::unordered_map<Key, std::unordered_map<Key, double>> grank_device(
   Flat<Key> f = flatten(graph, nt);
   const size_t n = f.keys.size();
   ppr_csr g{(int64_t)n, f.rp.data(), f.col.empty() ? nullptr : f.col.data()};
-  std::vector<int32_t> ids(n * K), len(n);
-  std::vector<double> sc(n * K);
   ppr_stats st;
   const auto t1 = std::chrono::steady_clock::now();
   HeapGrowth heap;  // (outer map and inner maps)
@@ -372,13 +430,19 @@ inline std::unordered_map<Key, std::unordered_map<Key, double>> grank_device(
     o.build(f);
     outer_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
   });
-  const int rc = ppr_grank_csr(&g, nullptr, (uint32_t)K, (uint32_t)L, (uint32_t)iterations, damping,
-                               tolerance, nullptr, ids.data(), sc.data(), len.data(), &st);
+  // plan (partitions, upload), device job; ppr_grank_csr's steps with the download left to the fills
+  ppr_plan* p = nullptr;
+  int rc = ppr_grank_plan_create(&g, nullptr, (uint32_t)K, (uint32_t)L, damping, nullptr, &p);
+  if (!rc) {
+    rc = ppr_grank_plan_run(p, (uint32_t)iterations, tolerance, &st);
+    if (rc) ppr_grank_plan_destroy(p);
+  }
   const auto t2 = std::chrono::steady_clock::now();
   outer.join();
   if (rc != PPR_OK) fail(rc);
   const auto t2b = std::chrono::steady_clock::now();
-  materialize_rows(f, o, K, ids, sc, len, nt);
+  rc = download_materialize(p, f, o, K, nt);
+  if (rc != PPR_OK) fail(rc);
   if (getenv("PPR_TIMING")) {  // phase breakdown of one call (stderr)
     const auto t3 = std::chrono::steady_clock::now();
     auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {

@@ -215,6 +215,14 @@ int ppr_grank_plan_unpack_host(ppr_plan* p, int32_t it, int64_t begin, int64_t e
 int ppr_grank_plan_fetch(ppr_plan* p, int32_t* out_ids, double* out_scores, int32_t* out_len);
 int ppr_grank_plan_fetch_slab(ppr_plan* p, int32_t iterations_run, int32_t* ids, double* scores,
                               int32_t* len);
+/* Rows [begin, end) of the final top-K (ids/scores (end - begin) * K, len end - begin; any may be
+ * null), synchronous. With buffers from ppr_host_alloc (page-locked host memory: DMA at link rate
+ * instead of a staged copy) the drop-in template downloads chunk by chunk while its threads
+ * materialise the chunks already down (include/ppr/grank.h; no reference counterpart). */
+int ppr_grank_plan_fetch_rows(ppr_plan* p, int64_t begin, int64_t end, int32_t* ids, double* scores,
+                              int32_t* len);
+int ppr_host_alloc(int64_t bytes, void** out);
+void ppr_host_free(void* ptr);
 /* Device stream the plan runs on (hipStream_t as void*), for event timing by the caller. Work the
  * plan puts on its internal side streams (hub bucket stage, wave tiers) is joined back into this
  * stream before each merge returns. */

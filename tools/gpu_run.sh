@@ -3,6 +3,7 @@
 # outputs under gpurun_out/TAG/ (run through gpurun: tools/gpu_run.sh is the command it executes).
 #   tests[:K]   pytest -m gpu tests (K: a -k filter)
 #   bench       bench.py default line (no cpu / e2e legs unless FULL=1)
+#   e2e         tests/cpp/_dropin_test e2e (ppr::grank through include/ppr/grank.h, PPR_TIMING split)
 #   diag        bench.py one step with PPR_DIAG=1 PPR_TIMING=1
 #   prof        rocprofv3 --kernel-trace --stats over one job (+1 warmup): kernel_stats.csv, timeline
 #   sq          two SQ counter passes (one rocprofv3 run each) over one job: sq_summary.txt
@@ -27,6 +28,10 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py --steps ${STEPS:-3} --warmup 1 $extra > "$out/bench.json" 2> "$out/bench.err" \
         || { echo "bench failed rc=$?"; tail -20 "$out/bench.err"; exit 1; }
       cat "$out/bench.json" ;;
+    e2e)
+      PPR_TIMING=1 PPR_HEAP_PAD=64 timeout -k 10 300 tests/cpp/_dropin_test e2e ${E2E_SCALE:-22} 30 > "$out/e2e.json" \
+        2> "$out/e2e.err" || { echo "e2e failed rc=$?"; tail -20 "$out/e2e.err"; exit 1; }
+      cat "$out/e2e.json"; grep ppr_timing "$out/e2e.err" ;;
     diag)
       PPR_DIAG=1 PPR_TIMING=1 timeout -k 10 300 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-e2e \
         > "$out/diag.json" 2> "$out/diag.err" || { echo "diag failed rc=$?"; tail -20 "$out/diag.err"; exit 1; }
