@@ -183,6 +183,8 @@ def lib() -> ctypes.CDLL:
         "ppr_mccp2_plan_walk": (ctypes.c_int, [vp, u32, ctypes.c_uint64, i64, i64]),
         "ppr_mccp2_plan_combine": (ctypes.c_int, [vp]),
         "ppr_mccp2_plan_run": (ctypes.c_int, [vp, u32, ctypes.c_uint64, vp]),
+        "ppr_mccp2_plan_run_sharded": (ctypes.c_int, [vp, u32, ctypes.c_uint64, vp]),
+        "ppr_mccp2_plan_run_local_group": (ctypes.c_int, [vp, i32, u32, ctypes.c_uint64, vp]),
         "ppr_exact_create": (ctypes.c_int, [vp, vp, i32, f64, vp, ctypes.POINTER(vp)]),
         "ppr_exact_run": (ctypes.c_int, [vp, u32, f64, vp]),
         "ppr_exact_topk": (ctypes.c_int, [vp, u32, vp, vp, vp]),

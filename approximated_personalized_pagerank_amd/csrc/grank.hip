@@ -2719,11 +2719,12 @@ struct LocalGroup {
   bool failed = false;
   std::vector<unsigned char*> bufs;
   std::vector<unsigned long long> md;
+  std::vector<int64_t> iv;                         // int64 all-gather (MC walk block sizes)
   std::vector<int> ok;                             // routed exchange: every rank's size check
   std::vector<std::vector<unsigned char*>> pbufs;  // routed blocks: [sender][receiver]
   std::vector<std::vector<int64_t>> psz;
   explicit LocalGroup(int n_)
-      : n(n_), bufs(n_), md(n_), ok(n_, 1), pbufs(n_, std::vector<unsigned char*>(n_)),
+      : n(n_), bufs(n_), md(n_), iv(n_), ok(n_, 1), pbufs(n_, std::vector<unsigned char*>(n_)),
         psz(n_, std::vector<int64_t>(n_)) {}
   bool barrier() {
     std::unique_lock<std::mutex> lk(mu);
@@ -3249,6 +3250,145 @@ extern "C" int ppr_grank_plan_run_local_group(ppr_plan** plans, int32_t n, uint3
     });
   for (auto& t : th) t.join();
   // the group lives on this stack frame: no plan keeps it
+  for (int i = 0; i < n; i++) { plans[i]->lgroup = nullptr; plans[i]->nranks = 1; plans[i]->rank = 0; }
+  for (int i = 0; i < n; i++)
+    if (rcs[i]) return rcs[i];
+  return PPR_OK;
+}
+
+// one int64 per rank (device word d_val) gathered on every host: out[r] = rank r's value
+static int x_allgather_i64(ppr_plan* p, const int64_t* d_val, std::vector<int64_t>& out, hipStream_t s) {
+  const int W = p->nranks;
+  out.assign(W, 0);
+  if (p->lgroup) {
+    LocalGroup& G = *p->lgroup;
+    int64_t v = 0;
+    HIP_OK(hipMemcpyAsync(&v, d_val, 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    G.iv[p->rank] = v;
+    if (!G.barrier()) return PPR_ERR_HIP;
+    out = G.iv;
+    return G.barrier() ? PPR_OK : PPR_ERR_HIP;
+  }
+  int rc = ensure_dev(&p->d_xsz, &p->xsz_bytes, 16 * (size_t)W + 8);
+  if (rc) return rc;
+  int64_t* all = reinterpret_cast<int64_t*>(p->d_xsz);
+  NCCL_OK(ncclAllGather(d_val, all, 1, ncclInt64, p->comm, s));
+  HIP_OK(hipMemcpyAsync(out.data(), all, 8 * (size_t)W, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  return PPR_OK;
+}
+
+// ---- MCCompletePathV2 on several ranks (include/mccompletepathv2.h:211-250, the whole job) ----
+// The walk set is split into W contiguous ranges of equal size (a walk's expected length is
+// 1 / (1 - d) whatever the node, so nodes cost about the same); each rank walks its range. A walk
+// basket does not depend on which rank computes it (the Philox streams are keyed by seed, step,
+// walk and source), so the job equals the one-GPU run bit for bit. The walk baskets then travel as
+// one compact block per rank (merge_glb.h format, slab slot 1): the exact block sizes are
+// all-gathered first (one int64 per rank), every rank checks them (all ranks see the same sizes,
+// so all take the same decision before any block moves), then the blocks are broadcast
+// (x_blocks). Every rank runs the combine and the top-K itself: the combine is level-sequential
+// (1,804 levels at RMAT-22), each level's time set by a lone hub's dependent chain, so splitting a
+// level's sources over ranks would not shorten it and would add two collectives per level.
+static int mc_run_sharded(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_stats* st) {
+  if (!p || !p->mc) return PPR_ERR_ARG;
+  if (walks == 0) return PPR_ERR_ITERS;
+  if (p->nranks > 1 && !p->comm && !p->lgroup) return PPR_ERR_ARG;
+  HIP_OK(hipSetDevice(p->device));
+  hipStream_t s = p->stream;
+  const int W = p->nranks, me = p->rank;
+  HIP_OK(hipMemsetAsync(p->d_stats, 0, 8 * PPR_NSTATS, s));
+  p->merge_launches = 0;
+  p->merge_ms = 0.0;
+  p->mc_walk_ms = 0.0;
+  p->mc_walks = 0;
+  p->x_bytes = 0;
+  p->x_rows_sent = 0;
+  HIP_OK(hipEventRecord(p->ev_a, s));
+  std::vector<int64_t> b(W + 1);
+  for (int r = 0; r <= W; r++) b[r] = p->mc_nwalk * r / W;
+  int rc = ppr_mccp2_plan_walk(p, walks, seed, b[me], b[me + 1]);
+  if (rc) return rc;
+  if (W > 1) {
+    int64_t rb = 0;
+    ppr_grank_plan_row_bytes(p, &rb);
+    const int64_t mine = b[me + 1] - b[me];
+    rc = ensure_dev(&p->d_xsend, &p->xsend_bytes, (size_t)(8 + mine * rb));
+    if (rc) return rc;
+    rc = ensure_dev(&p->d_xsz, &p->xsz_bytes, 16 * (size_t)W + 8);
+    if (rc) return rc;
+    int64_t* d_tot = reinterpret_cast<int64_t*>(p->d_xsz) + W;
+    rc = xpack_nodes(p, 1, p->d_mc_walk + b[me], mine, p->d_xsend, d_tot);
+    if (rc) return rc;
+    std::vector<int64_t> sz;
+    rc = x_allgather_i64(p, d_tot, sz, s);
+    if (rc) return rc;
+    for (int r = 0; r < W; r++)  // (every rank sees the same sizes: the same verdict everywhere)
+      if (b[r + 1] > b[r] && (sz[r] < 8 || sz[r] > 8 + (b[r + 1] - b[r]) * rb)) return PPR_ERR_RANGE;
+    std::vector<size_t> xo(W + 1, 0);
+    for (int r = 0; r < W; r++) xo[r + 1] = xo[r] + (r == me || b[r + 1] == b[r] ? 0 : (size_t)sz[r]);
+    rc = ensure_dev(&p->d_xrecv, &p->xrecv_bytes, std::max<size_t>(8, xo[W]));
+    if (rc) return rc;
+    p->x_bytes += (int64_t)xo[W];
+    p->x_rows_sent += mine;
+    rc = x_blocks(p, b, sz, xo, s);
+    if (rc) return rc;
+    for (int r = 0; r < W; r++) {
+      if (r == me || b[r + 1] == b[r]) continue;
+      rc = xunpack_nodes(p, 1, p->d_mc_walk + b[r], b[r + 1] - b[r], p->d_xrecv + xo[r]);
+      if (rc) return rc;
+    }
+  }
+  rc = ppr_mccp2_plan_combine(p);
+  if (rc) return rc;
+  HIP_OK(hipEventRecord(p->ev_b, s));
+  HIP_OK(hipEventSynchronize(p->ev_b));
+  if (st) {
+    std::memset(st, 0, sizeof(*st));
+    float ms = 0;
+    hipEventElapsedTime(&ms, p->ev_a, p->ev_b);
+    st->device_ms = ms;
+    st->walk_ms = p->mc_walk_ms;
+    st->combine_ms = p->merge_ms;
+    st->walk_nodes = p->mc_nwalk;
+    st->walks = p->mc_walks;
+    st->levels = (int64_t)p->mc_level_off.size() - 1;
+    st->merge_launches = p->merge_launches;
+    unsigned long long sv[2];
+    HIP_OK(hipMemcpyAsync(sv, p->d_stats, 16, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    st->candidates = (int64_t)sv[0];
+    st->algo_bytes = (int64_t)sv[1];
+  }
+  return PPR_OK;
+}
+
+extern "C" int ppr_mccp2_plan_run_sharded(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_stats* st) {
+  return mc_run_sharded(p, walks, seed, st);
+}
+
+// Test entry: the sharded MC job with n MC plans of this process as the ranks (LocalGroup)
+extern "C" int ppr_mccp2_plan_run_local_group(ppr_plan** plans, int32_t n, uint32_t walks, uint64_t seed,
+                                              ppr_mc_stats* st) {
+  if (!plans || n < 1) return PPR_ERR_ARG;
+  for (int i = 0; i < n; i++)
+    if (!plans[i] || !plans[i]->mc || plans[i]->comm || plans[i]->n != plans[0]->n ||
+        plans[i]->mc_nwalk != plans[0]->mc_nwalk)
+      return PPR_ERR_ARG;
+  LocalGroup G(n);
+  std::vector<int> rcs(n, PPR_OK);
+  for (int i = 0; i < n; i++) {
+    plans[i]->lgroup = &G;
+    plans[i]->nranks = n;
+    plans[i]->rank = i;
+  }
+  std::vector<std::thread> th;
+  for (int i = 0; i < n; i++)
+    th.emplace_back([&, i] {
+      rcs[i] = mc_run_sharded(plans[i], walks, seed, st ? st + i : nullptr);
+      if (rcs[i]) G.fail();
+    });
+  for (auto& t : th) t.join();
   for (int i = 0; i < n; i++) { plans[i]->lgroup = nullptr; plans[i]->nranks = 1; plans[i]->rank = 0; }
   for (int i = 0; i < n; i++)
     if (rcs[i]) return rcs[i];

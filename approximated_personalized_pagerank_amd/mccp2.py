@@ -106,6 +106,13 @@ class MccpPlan:
                    "mccp2_plan_run")
         return McStats.of(st)
 
+    def run_sharded(self, iterations: int, seed: int = DEFAULT_SEED) -> McStats:
+        """the whole job as this plan's rank of its RCCL group (ppr_grank_plan_comm_init first)"""
+        st = _lib.PprMcStats()
+        _lib.check(_lib.lib().ppr_mccp2_plan_run_sharded(self._p, iterations, seed & 0xFFFFFFFFFFFFFFFF,
+                                                         ctypes.byref(st)), "mccp2_plan_run_sharded")
+        return McStats.of(st)
+
     def walk(self, iterations: int, seed: int = DEFAULT_SEED, begin: int = 0, end: Optional[int] = None):
         e = self.walk_nodes if end is None else end
         _lib.check(_lib.lib().ppr_mccp2_plan_walk(self._p, iterations, seed & 0xFFFFFFFFFFFFFFFF, int(begin), int(e)),

@@ -220,6 +220,20 @@ def run_local_group(plans, iterations: int, tolerance: float):
     return list(st)
 
 
+def run_local_group_mc(plans, walks: int, seed: int):
+    """The sharded MC job (ppr_mccp2_plan_run_sharded) with these MccpPlans of one process as its
+    ranks, one thread each (tests). Returns the per-rank McStats."""
+    import ctypes
+    from . import _lib
+    from .mccp2 import McStats
+    n = len(plans)
+    arr = (ctypes.c_void_p * n)(*[pl._p for pl in plans])
+    st = (_lib.PprMcStats * n)()
+    _lib.check(_lib.lib().ppr_mccp2_plan_run_local_group(arr, n, walks, seed & 0xFFFFFFFFFFFFFFFF, st),
+               "mccp2_run_local_group")
+    return [McStats.of(s) for s in st]
+
+
 def exchange_bytes(plan):
     """(block bytes this rank received, rows it sent) in the plan's last sharded run"""
     import ctypes
@@ -287,6 +301,40 @@ class ShardedGrank:
         its = run_sharded(self.eng, self.comm, iterations, tolerance, None, bounds=weights)
         self.plan.iterations_run = its
         return its
+
+    def fetch(self):
+        return self.plan.fetch()
+
+    def close(self):
+        self.plan.close()
+
+
+class ShardedMccp:
+    """The whole MCCompletePathV2 job of this rank (one process per GPU): walks of its walk-set range,
+    walk baskets all-gathered over RCCL, the combine and top-K on every rank
+    (ppr_mccp2_plan_run_sharded). torch.distributed (gloo) only carries the RCCL unique id."""
+
+    def __init__(self, g, K, L, damping, local):
+        import torch
+        import torch.distributed as dist
+        from . import _lib
+        from .mccp2 import MccpPlan
+        self._lib, self.torch, self.dist = _lib, torch, dist
+        if not dist.is_initialized():
+            dist.init_process_group("gloo")
+        self.comm = CpuComm()
+        self.device = local % max(1, device_count())
+        self.plan = MccpPlan(g, K, L, damping, device=self.device)
+        if self.comm.world > 1:
+            uid = torch.zeros(128, dtype=torch.uint8)
+            if self.comm.rank == 0:
+                _lib.check(_lib.lib().ppr_comm_unique_id(uid.data_ptr()), "comm_unique_id")
+            dist.broadcast(uid, 0)
+            _lib.check(_lib.lib().ppr_grank_plan_comm_init(self.plan._p, uid.data_ptr(), self.comm.world,
+                                                           self.comm.rank), "comm_init")
+
+    def run(self, walks, seed):
+        return self.plan.run_sharded(walks, seed)
 
     def fetch(self):
         return self.plan.fetch()

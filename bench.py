@@ -249,9 +249,9 @@ def cpu_baseline(g, part, slab, L, damping, iters, threads, budget, seed=0):
 
 def main_mc(args):
     """MCCompletePathV2 on RMAT (configs[4]): one step = walks of the whole walk set + the
-    level-synchronous combine + top-K, graph and plan resident. N > 1: each rank walks a contiguous
-    range of the walk set (walk-count shard, no exchange) and the value counts the walks of all
-    ranks; the combine needs every walk basket and runs on one GPU (N = 1 only)."""
+    level-synchronous combine + top-K, graph and plan resident. N > 1: the whole job on every rank
+    (ppr_mccp2_plan_run_sharded): each rank walks a contiguous range of the walk set, the walk
+    baskets are all-gathered over RCCL, and every rank runs the level-sequential combine."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -267,33 +267,41 @@ def main_mc(args):
     log(f"[rank {rank}] RMAT-{args.scale}: n={g.n} m={g.m} walk set={plan.walk_nodes} levels={plan.levels} "
         f"dangling={plan.dangling} prep {time.time() - t:.1f}s")
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-        w = plan.walk_nodes
-        b, e = w * rank // world, w * (rank + 1) // world
+        # the whole job on every step: walks of this rank's walk-set range, walk baskets all-gathered
+        # over RCCL, the combine and top-K on every rank (ppr_mccp2_plan_run_sharded)
+        from approximated_personalized_pagerank_amd.shard import ShardedMccp, exchange_bytes
+        plan.close()
+        job = ShardedMccp(g, K, L, args.damping, local)
         for _ in range(args.warmup):
-            plan.walk(args.walks, 1, b, e)
-        dist.barrier()
+            job.run(args.walks, 1)
+        job.comm.barrier()
         t0 = time.perf_counter()
+        walk_ms = comb_ms = 0.0
         for s in range(args.steps):
-            plan.walk(args.walks, 1 + s, b, e)  # synchronous (event sync)
-        elapsed = time.perf_counter() - t0
-        tt = [0.0] * world
-        dist.all_gather_object(tt, elapsed)
-        dist.barrier()
+            st = job.run(args.walks, 1 + s)
+            walk_ms += st.walk_ms
+            comb_ms += st.combine_ms
+        el = time.perf_counter() - t0
+        job.comm.barrier()
+        elapsed = job.comm.all_reduce_max(el)
+        walk_max = job.comm.all_reduce_max(walk_ms)
+        comb_max = job.comm.all_reduce_max(comb_ms)
+        xb = job.comm.all_reduce_max(float(exchange_bytes(job.plan)[0]))
+        job.close()
+        job.dist.destroy_process_group()
         if rank != 0:
             return
-        elapsed = max(tt)
-        nw = int(args.walks * args.damping)
-        value = w * nw * args.steps / elapsed
         line = {
-            "metric": "random walks/sec mccompletepathv2 walk phase on RMAT-22 (walk-count shard)",
-            "value": value, "unit": "walks/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "f64",
+            "metric": "source-nodes/sec mccompletepathv2 K=50 L=200 R=1000 on RMAT-22",
+            "value": g.n * args.steps / elapsed, "unit": "source-nodes/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic RMAT (Graph500 a=.57 b=.19 c=.19, edge factor 16, seed %d, dedup)" % args.seed,
-            "config": {"workload": f"mccompletepathv2 walks RMAT-{args.scale} L={L} R={args.walks} d={args.damping}",
-                       "walk_nodes": w, "parallelism": f"walk-shard x{world}"},
+            "config": {"workload": f"mccompletepathv2 RMAT-{args.scale} K={K} L={L} R={args.walks} d={args.damping}",
+                       "nodes": g.n, "edges": g.m, "walk_nodes": st.walk_nodes, "levels": st.levels,
+                       "parallelism": f"walk-shard x{world} + walk-basket all-gather + replicated combine"},
+            "phases": {"walk_ms_per_step": walk_max / args.steps, "combine_ms_per_step": comb_max / args.steps,
+                       "walk_basket_bytes_received_per_rank": xb},
         }
         print(json.dumps(line), flush=True)
         return

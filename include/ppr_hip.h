@@ -261,6 +261,17 @@ int ppr_mccp2_plan_info(ppr_plan* p, int64_t* walk_nodes, int64_t* levels, int64
 int ppr_mccp2_plan_walk(ppr_plan* p, uint32_t walks, uint64_t seed, int64_t begin, int64_t end);
 int ppr_mccp2_plan_combine(ppr_plan* p);
 int ppr_mccp2_plan_run(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_stats* st);
+/* The whole MC job on several ranks (one process per GPU, after ppr_grank_plan_comm_init on the MC
+ * plan): each rank walks an equal contiguous range of the walk set, the walk baskets are
+ * all-gathered as compact blocks (exact sizes all-gathered and checked first, then one grouped
+ * ncclBroadcast per rank), and every rank runs the level-sequential combine and the top-K. The
+ * result equals ppr_mccp2_plan_run with the same seed bit for bit on every rank. st: walk_ms and
+ * walks are this rank's share; ppr_grank_plan_exchange_bytes gives the walk-basket bytes it
+ * received. (Replaces the single-process sweep of include/mccompletepathv2.h:211-250.) */
+int ppr_mccp2_plan_run_sharded(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_stats* st);
+/* Tests: the same with n MC plans of this process as the ranks (device copies instead of RCCL). */
+int ppr_mccp2_plan_run_local_group(ppr_plan** plans, int32_t n, uint32_t walks, uint64_t seed,
+                                   ppr_mc_stats* st);
 
 /* ---- Exact single-source PPR, batched (the reference's quality oracle) -------------------------
  * Replaces ppr::pprInternal::pprSingleSource(graph, iterations, damping, tolerance, source)

@@ -196,3 +196,49 @@ def test_gpu_mc_exact_sum_range_guard(monkeypatch):
     assert e.value.code == 11
     monkeypatch.delenv("PPR_MC_XS_LOG2")
     ppr.mccp2_csr(g, 8, 16, 50, 0.85, seed=1, device=0)
+
+
+def _mc_local_group(g, K, L, R, d, seed, world):
+    from approximated_personalized_pagerank_amd.shard import exchange_bytes, run_local_group_mc
+    plans = [ppr.MccpPlan(g, K, L, d, device=0) for _ in range(world)]
+    st = run_local_group_mc(plans, R, seed)
+    res = [pl.fetch() for pl in plans]
+    walks = [pl.fetch_slot(1) for pl in plans]
+    xb = [exchange_bytes(pl) for pl in plans]
+    for pl in plans:
+        pl.close()
+    return st, res, walks, xb
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_gpu_mc_sharded_job_equals_one_gpu(world):
+    """The whole MC job on `world` ranks (ppr_mccp2_plan_run_sharded over the in-process LocalGroup
+    transport): each rank walks its range of the walk set, the walk baskets are all-gathered, every
+    rank combines. Every rank's top-K rows and walk baskets equal the one-GPU run bit for bit, and
+    the oracle's."""
+    g = ppr.rmat(11, seed=13)
+    one = check_vs_oracle(g, 16, 64, 200, 0.85, seed=3, walks=False)
+    st, res, walks, xb = _mc_local_group(g, 16, 64, 200, 0.85, 3, world)
+    p1 = ppr.MccpPlan(g, 16, 64, 0.85, device=0)
+    p1.run(200, 3)
+    w1 = p1.fetch_slot(1)
+    p1.close()
+    for rank in range(world):
+        assert np.array_equal(res[rank].lens, one.lens), rank
+        assert np.array_equal(res[rank].ids, one.ids), rank
+        assert np.array_equal(res[rank].scores.view(np.int64), one.scores.view(np.int64)), rank
+        assert walk_sets(*walks[rank]) == walk_sets(*w1), rank
+        assert xb[rank][0] > 0 and xb[rank][1] > 0, rank
+    assert sum(s.walks for s in st) == int(200 * 0.85) * st[0].walk_nodes
+
+
+def test_gpu_mc_sharded_job_one_rank_is_the_plain_job():
+    """ppr_mccp2_plan_run_sharded without a group (one rank) is ppr_mccp2_plan_run"""
+    g = ppr.rmat(10, seed=2)
+    plan = ppr.MccpPlan(g, 8, 32, 0.85, device=0)
+    plan.run(100, 5)
+    a = plan.fetch()
+    plan.run_sharded(100, 5)
+    b = plan.fetch()
+    plan.close()
+    assert np.array_equal(a.ids, b.ids) and np.array_equal(a.scores.view(np.int64), b.scores.view(np.int64))
