@@ -40,6 +40,7 @@ namespace pprk {
 constexpr int SV_R = 3;                       // sketch rows
 constexpr int SV_UNIT_LOG = 31;               // a counter unit is 2^-31 (GRank totals are <= 1)
 constexpr int SV_XS = 4;                      // pass-2 table slots per thread in every size class
+constexpr size_t SV_LIST_BYTES = (size_t)WAVE * 12;  // pass-2 staging list of one wave: t f64[64] | key i32[64]
 // Size classes of the one-slice workgroups (host: sieve_launch): the widest sources take 16 waves
 // and a 3 x 8192 sketch (one workgroup per CU), narrower ones 8 waves / 3 x 4096 (two per CU) or
 // 4 waves / 3 x 2048 (four per CU) -- a narrow source's few batches per wave cannot hide their HBM
@@ -52,14 +53,19 @@ struct SvGeom {
   __host__ __device__ constexpr int threads() const { return waves * WAVE; }
   __host__ __device__ constexpr int bm_words() const { return SV_R * (1 << wlog) / 64; }
   __host__ __device__ constexpr size_t sketch_bytes() const { return (size_t)SV_R * ((size_t)1 << wlog) * 4; }
+  // pass 2 holds XT (20 B a slot) and one 64-entry staging list per wave (sv_pass2) in the region
+  __host__ __device__ constexpr size_t p2_bytes() const { return (size_t)xt * 20 + (size_t)waves * SV_LIST_BYTES; }
   __host__ __device__ constexpr size_t region() const {
-    return sketch_bytes() > (size_t)xt * 20 ? sketch_bytes() : (size_t)xt * 20;
+    return sketch_bytes() > p2_bytes() ? sketch_bytes() : p2_bytes();
   }
 };
 __host__ __device__ constexpr SvGeom sv_geom(int wlog, int waves) {
   return SvGeom{wlog, waves, SV_XS * waves * WAVE, SV_XS * waves * WAVE * 85 / 100 - waves * WAVE};
 }
 constexpr SvGeom SV_LARGE = sv_geom(13, 16), SV_MID = sv_geom(12, 8), SV_SMALL = sv_geom(11, 4);
+// (the staging lists fit beside XT in the sketch's bytes: no class grows)
+static_assert(SV_LARGE.region() == SV_LARGE.sketch_bytes() && SV_MID.region() == SV_MID.sketch_bytes() &&
+              SV_SMALL.region() == SV_SMALL.sketch_bytes(), "sieve LDS per class");
 constexpr int SV_THREADS = 16 * WAVE;         // the widest class (multi-slice kernels)
 constexpr int SV_XT_BUDGET = SV_LARGE.budget;
 constexpr int SVF_CAP = 4096;                 // k_svF: dense entries at or above the bound
@@ -483,9 +489,37 @@ __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, co
 }
 
 // pass 2 over successors [b0, b1): keys outside PT that pass the sieve, exactly into XT (budget
-// checked before every group that inserts; past it the workgroup only flags the overflow). Per
-// group the sieve test (three bitmap words) for every lane without a branch; a group with a
-// passing lane (a small minority) then checks PT, loads the passing scores and inserts.
+// checked before every insert step; past it the workgroup only flags the overflow). Per group the
+// sieve test (three bitmap words) for every lane without a branch. A passing lane is rare -- but
+// about half of the groups hold one (RMAT-22: 8.2e8 of 1.66e9 groups per job), and inserting
+// group by group ran the PT check, the find-or-insert and the adds with one or two live lanes of
+// 64. So the passing candidates (key, p * 2^61) are appended to the wave's 64-entry staging list
+// in LDS (one ballot and a store per group) and inserted 64 at a time, every lane busy
+// (sv_list_flush). A batch with more passing lanes than the list holds inserts group by group
+// (PPR_SV_LIST=0: always).
+#ifndef PPR_SV_LIST
+#define PPR_SV_LIST 1
+#endif
+// insert `n` (<= 64) candidates (key, t = p * 2^61) of the wave into XT: PT keys skipped
+__device__ __forceinline__ void sv_insert(const SvLds& x, const X2Table& xt, const IterArgs& a, bool live, int key,
+                                          double t, int budget) {
+  const int lane = lane_id();
+  const bool w = live && svpt_slot(x.pt, key, sv_mix((uint32_t)key), live) < 0;
+  if (!__ballot(w)) return;
+  if (a.diag && lane == 0) diag_add(a.diag, 148, 1ull);
+  if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
+    if (lane == 0) x.misc[SVM_OVF] = 1;
+    return;
+  }
+  bool ins = false;
+  int hs = -1;
+  if (w) hs = x2_slot(xt, key, ins);
+  const int nins = __popcll(__ballot(ins));
+  if (nins && lane == 0) atomicAdd(&x.misc[SVM_FILL], nins);
+  if (__ballot(w && hs < 0) && lane == 0) x.misc[SVM_OVF] = 1;
+  if (hs >= 0) sv_split_add_t(xt.a, xt.b, hs, t);
+  if (a.diag && lane == 0) diag_add(a.diag, 138, (unsigned long long)__popcll(__ballot(w)));
+}
 __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, const IterArgs& a, const SvLds& x,
                                          const X2Table& xt, int64_t b0, int64_t b1, double factor, int budget) {
   int64_t c0, c1;
@@ -493,50 +527,67 @@ __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, co
   const uint32_t* bm32 = reinterpret_cast<const uint32_t*>(x.bm);
   const double f61 = factor * 0x1p61;
   const int lane = lane_id();
+  const uint64_t lt = lanemask_lt();
+  // the wave's staging list, past XT in the region (SvGeom::p2_bytes)
+  double* lst = reinterpret_cast<double*>(x.region + (size_t)(xt.mask + 1u) * 20 + (size_t)(threadIdx.x >> 6) * SV_LIST_BYTES);
+  int* lsk = reinterpret_cast<int*>(lst + WAVE);
+  int nl = 0;  // (wave-uniform) entries in the list
+  auto flush = [&]() {
+    wave_fence();
+    const bool live = lane < nl;
+    sv_insert(x, xt, a, live, live ? lsk[lane] : 0, live ? lst[lane] : 0.0, budget);
+    nl = 0;
+    wave_fence();
+  };
   sv_rows<SV_P2_SCORES, SV_NS2>(g, s, a, c0, c1, [&](const SvBatch<SV_NS2>& bt) {
     constexpr int NG = 2 * SV_NS2;
     bool want[NG];
-    bool any = false;
+    int tot = 0;
 #pragma unroll
     for (int k = 0; k < NG; k++) want[k] = false;
     sv_groups(bt, [&](int k, int key, double, bool valid, int64_t) {
       // (PPR_WHATIF 1024, timing only: the walk alone, every key fails the test)
       want[k] = valid && ((a.whatif & 1024u) ? key == -7 : sv_passes(bm32, sv_mix((uint32_t)key), x.wlog));
-      any = any || want[k];
+      tot += __popcll(__ballot(want[k]));
     });
-    if (a.diag && lane == 0) {  // (PPR_DIAG: groups walked, groups with a lane past the bitmap test)
-      int ng = 0, np = 0;
+    if (a.diag && lane == 0) {  // (PPR_DIAG: groups walked)
+      int ng = 0;
 #pragma unroll
       for (int k = 0; k < NG; k++) { ng += ((k & 1) ? bt.rl[k >> 1] > WAVE : bt.rl[k >> 1] > 0) ? 1 : 0; }
       diag_add(a.diag, 190, (unsigned long long)ng);
-      (void)np;
     }
-    if (__builtin_expect(__ballot(any) == 0ull, 1)) return;
+    if (__builtin_expect(tot == 0, 1)) return;
     if (a.whatif & 512u) return;  // (timing only: no insert path)
-    // the few groups with a passing lane: PT check, score, insert
+    if (a.diag && lane == 0) {
+      int np = 0;
+#pragma unroll
+      for (int k = 0; k < NG; k++) np += __ballot(want[k]) ? 1 : 0;
+      diag_add(a.diag, 147, (unsigned long long)np);
+    }
+    if (PPR_SV_LIST && tot <= WAVE) {
+      if (nl + tot > WAVE) flush();
+#pragma unroll
+      for (int k = 0; k < NG; k++) {
+        const uint64_t m = __ballot(want[k]);
+        if (!m) continue;
+        if (want[k]) {
+          const int pos = nl + __popcll(m & lt);
+          lsk[pos] = bt.key[k];
+          lst[pos] = (SV_P2_SCORES ? bt.sv[k] : s.sc[bt.base[k >> 1] + (k & 1) * WAVE + lane]) * f61;
+        }
+        nl += __popcll(m);
+      }
+      return;
+    }
+    // a batch with more passing lanes than the list holds: group by group
 #pragma unroll
     for (int k = 0; k < NG; k++) {
       if (!__ballot(want[k])) continue;
-      const int key = bt.key[k];
-      const bool w = want[k] && svpt_slot(x.pt, key, sv_mix((uint32_t)key), want[k]) < 0;
-      if (a.diag && lane == 0) diag_add(a.diag, 147, 1ull);
-      if (!__ballot(w)) continue;
-      if (a.diag && lane == 0) diag_add(a.diag, 148, 1ull);
-      const double sc = SV_P2_SCORES ? bt.sv[k] : (w ? s.sc[bt.base[k >> 1] + (k & 1) * WAVE + lane] : 0.0);
-      if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
-        if (lane == 0) x.misc[SVM_OVF] = 1;
-        return;
-      }
-      bool ins = false;
-      int hs = -1;
-      if (w) hs = x2_slot(xt, key, ins);
-      const int nins = __popcll(__ballot(ins));
-      if (nins && lane == 0) atomicAdd(&x.misc[SVM_FILL], nins);
-      if (__ballot(w && hs < 0) && lane == 0) x.misc[SVM_OVF] = 1;
-      if (hs >= 0) sv_split_add_t(xt.a, xt.b, hs, sc * f61);
-      if (a.diag && lane == 0) diag_add(a.diag, 138, (unsigned long long)__popcll(__ballot(w)));
+      const double sc = SV_P2_SCORES ? bt.sv[k] : (want[k] ? s.sc[bt.base[k >> 1] + (k & 1) * WAVE + lane] : 0.0);
+      sv_insert(x, xt, a, want[k], bt.key[k], sc * f61, budget);
     }
   });
+  if (nl) flush();
 }
 
 // the self seed (1 - d) of v: into PT when v is a prev key, else into the sketch (pass 1; one thread)

@@ -372,8 +372,9 @@ inline void plan_free(ppr_plan* p) {
                 "row below the bound) %llu, sources with no new key (U = L) %llu\n", h[135], h[137], h[149],
                 (double)h[136], (double)h[138], (double)h[139], h[145], h[146]);
       if (h[190])
-        fprintf(stderr, "ppr_diag sieve pass 2: %.3e groups walked, %.3e with a lane past the bitmap test, %.3e with a "
-                "non-prev key past it (inserts)\n", (double)h[190], (double)h[147], (double)h[148]);
+        fprintf(stderr, "ppr_diag sieve pass 2: %.3e groups walked, %.3e with a lane past the bitmap test; %.3e insert "
+                "steps (staging-list flushes or groups) inserting %.3e non-prev candidates\n", (double)h[190],
+                (double)h[147], (double)h[148], (double)h[138]);
       if (h[280])
         fprintf(stderr, "ppr_diag wave tier: %llu sources, %.1f kept entries each; kcycles per source (lane 0): "
                 "setup+walk %.2f settle %.2f select %.2f row write %.2f norm1 %.2f\n", h[280],
