@@ -632,16 +632,8 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     if (i < nt) {
       const unsigned long long w = word[listed[i]];
       const int c = (int)((w >> 32) & 0xffffu), b = (int)(w >> 48);
-      double x = ((int)(uint32_t)w == W.seed) ? W.selfval : 0.0;
-      int j = b;
       const int e = b + c;
-      for (; j + 8 <= e; j += 8) {
-        const double v0 = vals[j], v1 = vals[j + 1], v2 = vals[j + 2], v3 = vals[j + 3];
-        const double v4 = vals[j + 4], v5 = vals[j + 5], v6 = vals[j + 6], v7 = vals[j + 7];
-        x = fma(v0, f, x); x = fma(v1, f, x); x = fma(v2, f, x); x = fma(v3, f, x);
-        x = fma(v4, f, x); x = fma(v5, f, x); x = fma(v6, f, x); x = fma(v7, f, x);
-      }
-      for (; j < e; j++) x = fma(vals[j], f, x);
+      const double x = fma_chain_lds(vals, b, e, f, ((int)(uint32_t)w == W.seed) ? W.selfval : 0.0);
       if (c > 0) vals[e - 1] = x;  // (a slot without occurrences is the seed key: its total is selfval)
     }
   }

@@ -226,6 +226,33 @@ __device__ __forceinline__ void diag_lap(unsigned long long* ph, int k, long lon
   t = t2;
 }
 
+// x = fma(vals[j], f, x) for j = b .. e-1, in that order (one key's ordered chain). The next 8
+// values are loaded while the current 8 are folded in, so the dependent fma chain -- not the LDS
+// read latency after every few loads -- sets the pace (tools/fma_chain.hip: ~12.5 cycles per fma
+// fed this way against ~35-50 for load-4-then-fold-4)
+__device__ __forceinline__ double fma_chain_lds(const double* vals, int b, int e, double f, double x) {
+  int j = b;
+  if (e - j >= 16) {
+    double v0 = vals[j], v1 = vals[j + 1], v2 = vals[j + 2], v3 = vals[j + 3];
+    double v4 = vals[j + 4], v5 = vals[j + 5], v6 = vals[j + 6], v7 = vals[j + 7];
+    for (j += 8; j + 8 <= e; j += 8) {
+      const double w0 = vals[j], w1 = vals[j + 1], w2 = vals[j + 2], w3 = vals[j + 3];
+      const double w4 = vals[j + 4], w5 = vals[j + 5], w6 = vals[j + 6], w7 = vals[j + 7];
+      x = fma(v0, f, x); x = fma(v1, f, x); x = fma(v2, f, x); x = fma(v3, f, x);
+      x = fma(v4, f, x); x = fma(v5, f, x); x = fma(v6, f, x); x = fma(v7, f, x);
+      v0 = w0; v1 = w1; v2 = w2; v3 = w3; v4 = w4; v5 = w5; v6 = w6; v7 = w7;
+    }
+    x = fma(v0, f, x); x = fma(v1, f, x); x = fma(v2, f, x); x = fma(v3, f, x);
+    x = fma(v4, f, x); x = fma(v5, f, x); x = fma(v6, f, x); x = fma(v7, f, x);
+  }
+  for (; j + 4 <= e; j += 4) {
+    const double v0 = vals[j], v1 = vals[j + 1], v2 = vals[j + 2], v3 = vals[j + 3];
+    x = fma(v0, f, x); x = fma(v1, f, x); x = fma(v2, f, x); x = fma(v3, f, x);
+  }
+  for (; j < e; j++) x = fma(vals[j], f, x);
+  return x;
+}
+
 template <int NG>
 __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c, int nbits,
                                                  const bool (&valid)[NG], const uint32_t (&slot)[NG],
@@ -294,17 +321,7 @@ __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c,
   for (int i = lane_id(); i < nt; i += WAVE) {
     const uint32_t sl = c.touched[i];
     const int b = c.tof[i], e = c.tof[i + 1];
-    double x = acc[sl];
-    int j = b;
-    for (; j + 4 <= e; j += 4) {
-      const double v0 = c.vals[j], v1 = c.vals[j + 1], v2 = c.vals[j + 2], v3 = c.vals[j + 3];
-      x = fma(v0, factor, x);
-      x = fma(v1, factor, x);
-      x = fma(v2, factor, x);
-      x = fma(v3, factor, x);
-    }
-    for (; j < e; j++) x = fma(c.vals[j], factor, x);
-    acc[sl] = x;
+    acc[sl] = fma_chain_lds(c.vals, b, e, factor, acc[sl]);
     c.cnt[sl] = 0;
   }
   wave_fence();
