@@ -461,6 +461,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       if (s6) p->sv_mid = std::max<int64_t>(0, atoll(s6));
       const char* s7 = getenv("PPR_SV_REDO");
       p->sv_redo_mid = !(s7 && atoi(s7) == 0);
+      const char* s8 = getenv("PPR_SV_REDO_LARGE");
+      p->sv_redo_large = !(s8 && atoi(s8) == 0);
       const char* s3 = getenv("PPR_SV_BUDGET");
       if (s3) p->sv_budget = std::max(0, std::min(SV_XT_BUDGET, atoi(s3)));
       // Streams of the exact sum: a process has 4 hardware queues (HIP's default), and streams
@@ -511,6 +513,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         {(const void*)k_xfinal<HubDesc>, "k_xfinal<HubDesc>"},
         {(const void*)k_sv1, "k_sv1"},
         {(const void*)k_sv1_redo, "k_sv1_redo"},
+        {(const void*)k_sv1_list, "k_sv1_list"},
         {(const void*)k_svA, "k_svA"},
         {(const void*)k_svB, "k_svB"},
         {(const void*)k_svF, "k_svF"},
@@ -1649,6 +1652,7 @@ struct SvRun {
   std::vector<int32_t> pos;  // index into the caller's source list of each descriptor
   size_t o_ovl = 0;          // offset of the overflow list in d_sv
   size_t o_os = 0;           // ... and of the small class's first overflows (redone on the device)
+  size_t o_om = 0;           // ... and of the mid class's (redone on the device, large geometry)
   bool live = false;
 };
 
@@ -1717,6 +1721,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   const size_t o_z = off;
   const size_t o_ov = off; off = al(off + 4 * (1 + nx));
   const size_t o_os = off; off = al(off + 4 * (1 + nx));  // small class's first overflows (device redo)
+  const size_t o_om = off; off = al(off + 4 * (1 + nx));  // mid class's first overflows (device redo)
   const size_t o_sn = off; off = al(off + 4 * nx);
   const size_t o_of = off; off = al(off + 4 * (nm + 1));
   const size_t o_pt = off; off = al(off + 8 * 2 * (size_t)Lp * nm);
@@ -1746,6 +1751,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   const SvTask* d_t = (const SvTask*)(b + o_t);
   int32_t* d_ov = (int32_t*)(b + o_ov);
   int32_t* d_os = (int32_t*)(b + o_os);
+  int32_t* d_om = (int32_t*)(b + o_om);
   int32_t* d_of = (int32_t*)(b + o_of);
   unsigned long long* d_pt = (unsigned long long*)(b + o_pt);
   uint32_t* d_sk = (uint32_t*)(b + o_gs);
@@ -1774,9 +1780,20 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
       // the small class's overflows are redone at once with the mid geometry (it hands back ~7 % of
       // its sources, the mid class < 0.5 %); only a second overflow reaches the host
       const bool redo = c == 2 && p->sv_redo_mid;
+      // the mid class's overflows (< 10 % of its sources; with the small class's second ones, most
+      // of the host hand-backs) are redone at once with the large geometry
+      const bool redo_l = c == 1 && p->sv_redo_large;
       hipLaunchKernelGGL(k_sv1, dim3((unsigned)cnt_c), dim3(G.threads()), sv_lds_bytes(Lp, G), cs[c], g, s, a, d_v, d0,
-                         Lp, G, std::min(p->sv_budget, G.budget), redo ? d_os : d_ov, d_ok, d_ovv, d_on);
+                         Lp, G, std::min(p->sv_budget, G.budget), redo ? d_os : redo_l ? d_om : d_ov, d_ok, d_ovv,
+                         d_on);
       HIP_OK(hipGetLastError());
+      if (redo_l) {
+        hipLaunchKernelGGL(k_sv1_list, dim3((unsigned)cnt_c), dim3(SV_LARGE.threads()), sv_lds_bytes(Lp, SV_LARGE), cs[c],
+                           g, s, a, d_v, d_om, Lp, SV_LARGE, std::min(p->sv_budget, SV_LARGE.budget), d_ov, d_ok, d_ovv,
+                           d_on);
+        HIP_OK(hipGetLastError());
+        p->merge_launches++;
+      }
       if (redo) {
         hipLaunchKernelGGL(k_sv1_redo, dim3((unsigned)std::min<size_t>(cnt_c, 512)), dim3(SV_MID.threads()),
                            sv_lds_bytes(Lp, SV_MID), cs[c], g, s, a, d_v, d_os, Lp, SV_MID,
@@ -1809,6 +1826,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   p->sv_sources += (int64_t)nx;
   run.o_ovl = o_ov;
   run.o_os = o_os;
+  run.o_om = o_om;
   run.live = true;
   return PPR_OK;
 }
@@ -1826,11 +1844,12 @@ static int sieve_collect(ppr_plan* p, SvRun& run, std::vector<int32_t>& back) {
     HIP_OK(hipEventRecord(p->ev_sv, p->stream_sv3));
     HIP_OK(hipStreamWaitEvent(p->stream_sv, p->ev_sv, 0));
   }
-  int32_t novf = 0, nsm = 0;
+  int32_t novf = 0, nsm = 0, nmd = 0;
   HIP_OK(hipMemcpyAsync(&novf, p->d_sv + run.o_ovl, 4, hipMemcpyDeviceToHost, p->stream_sv));
   HIP_OK(hipMemcpyAsync(&nsm, p->d_sv + run.o_os, 4, hipMemcpyDeviceToHost, p->stream_sv));
+  HIP_OK(hipMemcpyAsync(&nmd, p->d_sv + run.o_om, 4, hipMemcpyDeviceToHost, p->stream_sv));
   HIP_OK(hipStreamSynchronize(p->stream_sv));
-  p->sv_redo_dev += nsm;
+  p->sv_redo_dev += nsm + nmd;
   for (int g = 1; g < ppr_plan::NKST; g++) kst_fold(p, g);
   if (!novf) return PPR_OK;
   std::vector<int32_t> od(novf);

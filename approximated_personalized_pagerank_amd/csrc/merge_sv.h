@@ -813,6 +813,20 @@ __global__ void __launch_bounds__(8 * WAVE) k_sv1_redo(DevGraph g, DevSlab s, It
   }
 }
 
+// the sources a class handed back (`list`: [0] count, [1..] descriptors) again with a larger
+// geometry G, one workgroup each (a grid of the class's size, blocks past the count leave at
+// once); a second overflow goes to `ovl` (the host's hand-back list). It runs on the class's
+// stream right after it: the mid class's overflows take the large geometry (twice the pass-2
+// table, a 3 x 8192 sketch) without a host round trip.
+__global__ void __launch_bounds__(SV_THREADS) k_sv1_list(DevGraph g, DevSlab s, IterArgs a, const int32_t* vid,
+                                                         const int32_t* list, int Lp, SvGeom G, int budget,
+                                                         int32_t* ovl, int32_t* out_k, double* out_v,
+                                                         int32_t* out_n) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  if ((int)blockIdx.x >= list[0]) return;
+  sv1_source(smem, g, s, a, vid, list[1 + blockIdx.x], Lp, G, budget, ovl, out_k, out_v, out_n);
+}
+
 // the row of a one-slice source from its selected entries (k_sv1): one wave per source -- sort in
 // hash order, write, range index, norm1 against the old row, maxDiff (finish_source)
 __host__ __device__ constexpr size_t svfin_lds_bytes(int Lp) { return (size_t)Lp * 12 + 1024 + (size_t)Lp * 20; }

@@ -200,7 +200,7 @@ struct ppr_plan {
   int32_t* d_dlast = nullptr;         // [n] distinct keys of each source's last merge (hub planning)
   int xr_T = 8192, xr_W = 16;         // PPR_XR_T: range / bucket workgroup table slots (waves = T / 512)
   int xr_rmax = 3;                    // PPR_XR_RMAX: most key ranges a source is walked in (beyond: partition)
-  int xr_fill = 80;                   // PPR_XR_FILL: planned distinct keys per table, % of its slots
+  int xr_fill = 85;                   // PPR_XR_FILL: planned distinct keys per table, % of its slots (round-5 sweep: 80 -> 85, -0.3-0.6 %)
   int xf_stage = 4096;                // k_xfinal entries staged in LDS
   int xr_dscale = 100;                // PPR_XR_DSCALE (tests): distinct-key estimates scaled, % (forces overflows)
   unsigned char* d_xs = nullptr;      // range-workgroup scratch (descriptors, tasks, lists)
@@ -224,11 +224,12 @@ struct ppr_plan {
   int xg_cap = 1 << 16;               // dense list of the selection (PPR_XG_CAP, tests: L <= cap <= XG_CAP)
   // sieve merge of the wide exact-sum sources (merge_sv.h): PPR_SV=0 turns it off
   bool sv_enabled = false;
-  int64_t sv_slice = 1LL << 18;       // PPR_SV_SLICE: candidates per slice workgroup
+  int64_t sv_slice = 1LL << 19;       // PPR_SV_SLICE: candidates per slice workgroup (round-5 sweep: 2^18 -> 2^19, -1.6 %)
   int64_t sv_min = 4096;              // PPR_SV_MIN: sources with fewer candidates keep the range engines
                                       // (measured: 4096 beats 0 by 2-3 % -- the smallest sources overflow the
                                       // 4-wave class's sketch and were handed back -- and 16384 by 5 %)
   bool sv_redo_mid = true;            // PPR_SV_REDO=0: small-class overflows go straight to the host hand-back
+  bool sv_redo_large = true;          // PPR_SV_REDO_LARGE=0: mid-class overflows go straight to the host hand-back
   int sv_budget = 2457;               // PPR_SV_BUDGET (tests): passing keys a table takes (<= SV_XT_BUDGET)
   int64_t sv_small = 32768, sv_mid = 65536;  // PPR_SV_SMALL / PPR_SV_MID: one-slice size classes by candidates
                                       // (same-box sweep of SV_SMALL 16 K / 32 K / 48 K / 64 K: 1632 / 1589-1594 /
@@ -241,7 +242,7 @@ struct ppr_plan {
   void* h_sv_pin = nullptr;           // pinned staging of descriptors and tasks, overflow count
   size_t h_sv_bytes = 0;
   int64_t sv_sources = 0, sv_redo = 0;  // sieved sources, handed back after an overflow (PPR_TIMING)
-  int64_t sv_redo_dev = 0;            // small-class overflows redone on the device (mid geometry)
+  int64_t sv_redo_dev = 0;            // small / mid-class overflows redone on the device (mid / large geometry)
   double xh_s[8] = {};                // run_xhubs host sections, s (PPR_TIMING at destroy)
   // MCCompletePathV2 (mccp2.hip)
   bool mc = false;

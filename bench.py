@@ -456,7 +456,9 @@ def main():
                                f"damping={args.damping} tol={args.tol}",
                    "nodes": g.n, "edges": g.m, "iterations_run": stats["iterations"],
                    "parallelism": f"source-shard x{world}" if world > 1 else "1 GPU",
-                   "sum": sum_mode()},
+                   "sum": sum_mode(),
+                   "step": "cold call: every run resets its per-job planning state (distinct-key estimates, "
+                           "hot set) in ppr_grank_plan_init; graph and slab resident"},
         "roofline": {"bound": "hbm",
                      "kernel": ("basket-merge phase, exact sum: k_classify + k_merge_lds_x (wave tier) + sieve "
                                 "(k_sv1 + k_svfin in three size classes, k_svA + k_svB + k_svF for multi-slice "
