@@ -1788,7 +1788,9 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
                          d_on);
       HIP_OK(hipGetLastError());
       if (redo_l) {
-        hipLaunchKernelGGL(k_sv1_list, dim3((unsigned)cnt_c), dim3(SV_LARGE.threads()), sv_lds_bytes(Lp, SV_LARGE), cs[c],
+        // (grid: the class overflows ~7 % of its sources at RMAT-22; past the grid the host takes them)
+        const unsigned gl = (unsigned)std::min<size_t>(cnt_c, cnt_c / 8 + 64);
+        hipLaunchKernelGGL(k_sv1_list, dim3(gl), dim3(SV_LARGE.threads()), sv_lds_bytes(Lp, SV_LARGE), cs[c],
                            g, s, a, d_v, d_om, Lp, SV_LARGE, std::min(p->sv_budget, SV_LARGE.budget), d_ov, d_ok, d_ovv,
                            d_on);
         HIP_OK(hipGetLastError());

@@ -534,6 +534,18 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
                                                const HubRec* st, const IterArgs& a, int Lw, uint32_t* pt_cnt_d,
                                                int32_t* pt_key, double* pt_sc) {
   const int l = lane_id();
+  // (-DPPR_PHASE_TIMING builds, PPR_DIAG: lane-0 cycles per phase into slots 288.., buckets in 296)
+#if defined(PPR_PHASE_TIMING)
+  long long tq = a.diag ? (long long)clock64() : 0;
+  auto lap = [&](int k) {
+    if (!a.diag) return;
+    const long long t2 = (long long)clock64();
+    if (l == 0) diag_add(a.diag, 288 + k, (unsigned long long)(t2 - tq));
+    tq = t2;
+  };
+#else
+  auto lap = [](int) {};
+#endif
   unsigned long long* word = reinterpret_cast<unsigned long long*>(base);
   double* vals = reinterpret_cast<double*>(base + (size_t)T * 8);
   uint16_t* listed = reinterpret_cast<uint16_t*>(base + (size_t)T * 8 + (size_t)BW2_CAP * 8);
@@ -563,6 +575,13 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     nt = 1;
     wave_fence();
   }
+  {  // (timing: wait for the record loads)
+    int z = 0;
+#pragma unroll
+    for (int k = 0; k < BW2_GROUPS; k++) z += kk[k];
+    if (z == 0x7ffffff1) wave_fence();
+  }
+  lap(0);  // loads + table clear
   const uint64_t lt = lanemask_lt();
   uint32_t sl[BW2_GROUPS], occ[BW2_GROUPS];
   unsigned long long c0[BW2_GROUPS];
@@ -606,6 +625,7 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     nt += __popcll(fm);
     wave_fence();
   }
+  lap(1);  // P1
   // P2: run bases (listed order)
   int run = 0;
   for (int i0 = 0; i0 < nt; i0 += WAVE) {
@@ -618,6 +638,7 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     run += __builtin_amdgcn_readlane(incl, WAVE - 1);
   }
   wave_fence();
+  lap(2);
   // P3: values grouped by key
 #pragma unroll
   for (int k = 0; k < BW2_GROUPS; k++) {
@@ -625,6 +646,7 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     if (k * WAVE + l < nb) vals[(uint32_t)(word[sl[k]] >> 48) + occ[k]] = cs[k];
   }
   wave_fence();
+  lap(3);
   // P4: one chain per listed slot
   const double f = W.factor;
   for (int i0 = 0; i0 < nt; i0 += WAVE) {
@@ -638,6 +660,7 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     }
   }
   wave_fence();
+  lap(4);
   // P5: keys reaching tau, at most L of them, appended
   auto total_of = [&](int i) {
     const unsigned long long w = word[listed[i]];
@@ -654,16 +677,18 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     diag_add(a.diag, 64 + (31 - __clz(nt | 1)), 1ull);
     diag_add(a.diag, 96 + (31 - __clz(kept | 1)), 1ull);
   }
-  if (kept == 0) return true;
+  if (kept == 0) { lap(5); return true; }
   const int cnt = kept <= Lw ? kept : Lw;
   SelCrit c;
   const uint32_t ts = W.ts;
   const double tau = W.tau;
   if (kept > Lw)  // keys below tau rank as 0 (every kept total is >= tau > 0 here)
     c = select_top(nt, Lw, key_of, [&](int i) { const double x = total_of(i); return x >= tau ? x : 0.0; }, hist, ts);
+  lap(5);  // kept count + select
   int at = 0;
   if (l == 0) at = (int)atomicAdd(pt_cnt_d, (uint32_t)cnt);
   at = __builtin_amdgcn_readlane(at, 0);
+  lap(6);  // appending atomic
   int pos0 = 0;
   for (int i0 = 0; i0 < nt; i0 += WAVE) {
     const int i = i0 + l;
@@ -679,6 +704,10 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     if (sel) { const int pos = at + pos0 + __popcll(m & lt); pt_key[pos] = key; pt_sc[pos] = x; }
     pos0 += __popcll(m);
   }
+  lap(7);  // emission
+#if defined(PPR_PHASE_TIMING)
+  if (a.diag && l == 0) diag_add(a.diag, 296, 1ull);
+#endif
   return true;
 }
 

@@ -814,8 +814,10 @@ __global__ void __launch_bounds__(8 * WAVE) k_sv1_redo(DevGraph g, DevSlab s, It
 }
 
 // the sources a class handed back (`list`: [0] count, [1..] descriptors) again with a larger
-// geometry G, one workgroup each (a grid of the class's size, blocks past the count leave at
-// once); a second overflow goes to `ovl` (the host's hand-back list). It runs on the class's
+// geometry G, one workgroup each, over a grid sized for the expected overflows (a workgroup of
+// the large geometry holds 113 KB of LDS, so even a block that leaves at once occupies a CU; a
+// grid-stride loop spills at the 16-wave VGPR cap). Overflows beyond the grid, and second
+// overflows, go to `ovl` (the host's hand-back list). It runs on the class's
 // stream right after it: the mid class's overflows take the large geometry (twice the pass-2
 // table, a 3 x 8192 sketch) without a host round trip.
 __global__ void __launch_bounds__(SV_THREADS) k_sv1_list(DevGraph g, DevSlab s, IterArgs a, const int32_t* vid,
@@ -823,7 +825,10 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1_list(DevGraph g, DevSlab s, 
                                                          int32_t* ovl, int32_t* out_k, double* out_v,
                                                          int32_t* out_n) {
   extern __shared__ __align__(16) unsigned char smem[];
-  if ((int)blockIdx.x >= list[0]) return;
+  const int n = list[0];
+  if (blockIdx.x == 0)  // more overflows than blocks: the rest go to the host hand-back at once
+    for (int k = (int)gridDim.x + (int)threadIdx.x; k < n; k += (int)blockDim.x) ovl[1 + atomicAdd(&ovl[0], 1)] = list[1 + k];
+  if ((int)blockIdx.x >= n) return;
   sv1_source(smem, g, s, a, vid, list[1 + blockIdx.x], Lp, G, budget, ovl, out_k, out_v, out_n);
 }
 

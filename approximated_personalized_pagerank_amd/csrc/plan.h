@@ -337,6 +337,14 @@ inline void plan_free(ppr_plan* p) {
       if (p->diag_cap_src > 0)
         fprintf(stderr, "ppr_diag sources beyond the bucket cap %.0f, candidates %.3e of %.3e\n", p->diag_cap_src,
                 p->diag_cap_cand, p->diag_hub_cand);
+      if (h[296]) {  // (-DPPR_PHASE_TIMING builds) one-shot bucket phases, lane 0
+        const double tot = (double)(h[288] + h[289] + h[290] + h[291] + h[292] + h[293] + h[294] + h[295]);
+        fprintf(stderr, "ppr_diag one-shot buckets %llu, %.1f K cycles each: loads+clear %.1f %% P1 %.1f %% P2 %.1f %% "
+                "P3 %.1f %% P4 %.1f %% count+select %.1f %% append atomic %.1f %% emit %.1f %%\n", h[296],
+                tot / 1e3 / (double)h[296], 100.0 * h[288] / tot, 100.0 * h[289] / tot, 100.0 * h[290] / tot,
+                100.0 * h[291] / tot, 100.0 * h[292] / tot, 100.0 * h[293] / tot, 100.0 * h[294] / tot,
+                100.0 * h[295] / tot);
+      }
       if (h[152])
         fprintf(stderr, "ppr_diag spilled buckets %llu, records %llu (%.1f per bucket)\n", h[152], h[153],
                 (double)h[153] / (double)h[152]);

@@ -27,7 +27,7 @@ constexpr int PPR_NSTATS = 8;         // device counters: candidates, algorithmi
 // PPR_DIAG counters (u64, printed at plan destruction, plan.h): PPR_DIAG_BASE counters, plus as
 // many per shard -- per-wave counters go to a shard picked by block and wave, so hundreds of
 // millions of waves do not serialise on a few addresses (that contention distorted the timings)
-constexpr int PPR_DIAG_BASE = 288;  // (256..279: the sieve's size classes, merge_sv.h)
+constexpr int PPR_DIAG_BASE = 304;  // (256..279: the sieve's size classes, merge_sv.h; 288..296: one-shot bucket phases)
 constexpr int PPR_DIAG_SHARDS = 256;
 constexpr int PPR_DIAG_SLOTS = PPR_DIAG_BASE * (1 + PPR_DIAG_SHARDS);
 __device__ __forceinline__ void diag_add(unsigned long long* d, int idx, unsigned long long v) {

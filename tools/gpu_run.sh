@@ -62,6 +62,13 @@ for step in "$@"; do
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run -f csv -- python3 bench.py $P1 > "$out/write.json" 2> "$out/write.err" || { echo "write failed"; exit 1; }
       python3 tools/pmc_summary.py $(find "$out/fetch" -name "*counter_collection.csv") $(find "$out/write" -name "*counter_collection.csv") 1 exact > "$out/pmc.json"
       python3 tools/stamp_build.py "$out/pmc.json"
+      # per-kernel roofline join (needs the prof step's stats of this session; sq optional)
+      if [ -f "$out/kernel_stats.csv" ]; then
+        sqf=-; [ -f "$out/sq_summary.txt" ] && sqf="$out/sq_summary.txt"
+        python3 tools/kernel_roofline.py "$out/kernel_stats.csv" $(find "$out/fetch" -name "*counter_collection.csv" | head -1) \
+          $(find "$out/write" -name "*counter_collection.csv" | head -1) 2 1 "$sqf" "$out/prof.json" > "$out/kernel_roofline.json" \
+          || echo "kernel_roofline failed"
+      fi
       find "$out/fetch" "$out/write" -name "*counter_collection.csv" -size +20M -delete
       head -c 1500 "$out/pmc.json" ;;
     mctrace)
