@@ -461,11 +461,12 @@ __device__ __forceinline__ void sv_chunk(int64_t b0, int64_t b1, int64_t& c0, in
 #define PPR_SV_NS2 4
 #endif
 #ifndef PPR_SV_P2_SCORES
-#define PPR_SV_P2_SCORES 1
+#define PPR_SV_P2_SCORES 0
 #endif
-// pass 2 loads every candidate's score with its key (8 B more per candidate): the few groups with
-// a passing lane then insert without a dependent HBM round trip (PPR_WHATIF 512 / 1024 timings:
-// that round trip per group was 2/3 of pass 2)
+// pass 2 loads keys only (4 B per candidate): the staging list keeps a passing candidate's slab
+// index and its score is gathered when the list is flushed, one memory latency per 64 passing
+// candidates (round 5: 1344-1355 -> 1337-1338 ms per job against loading every score with its key,
+// which paid before the list, when each inserting group waited for its own score)
 constexpr bool SV_P2_SCORES = PPR_SV_P2_SCORES != 0;
 // rows per batch in pass 1 (keys and scores) and pass 2 (keys only: a lighter group, so more rows
 // in flight to cover the gather latency); build-time knobs for A/B variants (tools/build_variant.py)
@@ -535,7 +536,11 @@ __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, co
   auto flush = [&]() {
     wave_fence();
     const bool live = lane < nl;
-    sv_insert(x, xt, a, live, live ? lsk[lane] : 0, live ? lst[lane] : 0.0, budget);
+    // (without the pass's score loads the list holds each entry's slab index; its score is
+    // gathered here, one memory latency per 64 passing candidates)
+    double t = 0.0;
+    if (live) t = SV_P2_SCORES ? lst[lane] : s.sc[__double_as_longlong(lst[lane])] * f61;
+    sv_insert(x, xt, a, live, live ? lsk[lane] : 0, t, budget);
     nl = 0;
     wave_fence();
   };
@@ -573,7 +578,8 @@ __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, co
         if (want[k]) {
           const int pos = nl + __popcll(m & lt);
           lsk[pos] = bt.key[k];
-          lst[pos] = (SV_P2_SCORES ? bt.sv[k] : s.sc[bt.base[k >> 1] + (k & 1) * WAVE + lane]) * f61;
+          lst[pos] = SV_P2_SCORES ? bt.sv[k] * f61
+                                  : __longlong_as_double((long long)(bt.base[k >> 1] + (k & 1) * WAVE + lane));
         }
         nl += __popcll(m);
       }
