@@ -462,7 +462,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       const char* s7 = getenv("PPR_SV_REDO");
       p->sv_redo_mid = !(s7 && atoi(s7) == 0);
       const char* s8 = getenv("PPR_SV_REDO_LARGE");
-      p->sv_redo_large = !(s8 && atoi(s8) == 0);
+      p->sv_redo_large = s8 && atoi(s8) != 0;
       const char* s3 = getenv("PPR_SV_BUDGET");
       if (s3) p->sv_budget = std::max(0, std::min(SV_XT_BUDGET, atoi(s3)));
       // Streams of the exact sum: a process has 4 hardware queues (HIP's default), and streams

@@ -229,7 +229,9 @@ struct ppr_plan {
                                       // (measured: 4096 beats 0 by 2-3 % -- the smallest sources overflow the
                                       // 4-wave class's sketch and were handed back -- and 16384 by 5 %)
   bool sv_redo_mid = true;            // PPR_SV_REDO=0: small-class overflows go straight to the host hand-back
-  bool sv_redo_large = true;          // PPR_SV_REDO_LARGE=0: mid-class overflows go straight to the host hand-back
+  bool sv_redo_large = false;         // PPR_SV_REDO_LARGE=1: mid-class overflows redone on the device (k_sv1_list;
+                                      // off by default: at RMAT-22 the mid class now overflows ~1 source per job,
+                                      // and the redo grid's 113-KB workgroups still pass through the CUs)
   int sv_budget = 2457;               // PPR_SV_BUDGET (tests): passing keys a table takes (<= SV_XT_BUDGET)
   int64_t sv_small = 32768, sv_mid = 65536;  // PPR_SV_SMALL / PPR_SV_MID: one-slice size classes by candidates
                                       // (same-box sweep of SV_SMALL 16 K / 32 K / 48 K / 64 K: 1632 / 1589-1594 /

@@ -324,10 +324,10 @@ def test_gpu_exact_sum_init_hubs_and_damping():
     ({"PPR_SV_SMALL": "1000000000", "PPR_SV_MID": "1000000000", "PPR_TIER_MASK": "0x0", "PPR_SV_REDO": "0"}, "redo"),
     # both geometries overflow: device redo, then the host hand-back
     ({"PPR_SV_SMALL": "1000000000", "PPR_SV_MID": "1000000000", "PPR_SV_BUDGET": "8"}, "devredo+redo"),
-    # every one-slice source in the 8-wave class: its overflows are redone on the device with the
-    # 16-wave geometry (k_sv1_list); with that off they go to the host
-    ({"PPR_SV_SMALL": "0", "PPR_SV_MID": "1000000000", "PPR_TIER_MASK": "0x0"}, "devredo"),
-    ({"PPR_SV_SMALL": "0", "PPR_SV_MID": "1000000000", "PPR_TIER_MASK": "0x0", "PPR_SV_REDO_LARGE": "0"}, "redo"),
+    # every one-slice source in the 8-wave class: with PPR_SV_REDO_LARGE=1 its overflows are redone
+    # on the device with the 16-wave geometry (k_sv1_list); by default they go to the host
+    ({"PPR_SV_SMALL": "0", "PPR_SV_MID": "1000000000", "PPR_TIER_MASK": "0x0", "PPR_SV_REDO_LARGE": "1"}, "devredo"),
+    ({"PPR_SV_SMALL": "0", "PPR_SV_MID": "1000000000", "PPR_TIER_MASK": "0x0"}, "redo"),
     ({"PPR_SV": "0"}, None),                                  # off: range / partition engines only
 ])
 def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):
@@ -360,8 +360,8 @@ def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):
         assert redo > 0
     if "devredo" in (want or "").split("+"):
         assert redo_dev > 0
-    if senv.get("PPR_SV_REDO") == "0" or senv.get("PPR_SV_REDO_LARGE") == "0":
-        assert redo_dev == 0 or senv.get("PPR_SV_SMALL") != "0"
+    if senv.get("PPR_SV_REDO") == "0" or (senv.get("PPR_SV_SMALL") == "0" and "PPR_SV_REDO_LARGE" not in senv):
+        assert redo_dev == 0
 
 
 @pytest.mark.parametrize("henv", [

@@ -88,7 +88,7 @@ def main():
            "kernels": rows}
     if bench:
         # kernel groups of the bench line (bench.py KERNEL_GROUPS): their kernels by name
-        members = {"wave tier": ["k_merge_lds_x"], "sieve one-slice": ["k_sv1", "k_sv1_redo", "k_svfin"],
+        members = {"wave tier": ["k_merge_lds_x"], "sieve one-slice": ["k_sv1", "k_sv1_redo", "k_sv1_list", "k_svfin"],
                    "sieve multi-slice": ["k_svA", "k_svB", "k_svF"]}
         kb = bench["roofline"].get("kernels", {})
         algo = {"wave tier": sum(v["algo_bytes_per_step"] for k, v in kb.items() if k.startswith("wave tier")),
