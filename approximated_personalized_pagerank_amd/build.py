@@ -24,6 +24,11 @@ def build(force: bool = False, verbose: bool = False, out: str | None = None, de
     (tools/build_variant.py)."""
     out = out or LIB_PATH
     src_dir = csrc or CSRC
+    # a variant loaded for an A/B (PPR_LIB_VARIANT: LIB_PATH is the variant) is prebuilt by
+    # tools/build_variant.py with its own defines or sources: never rebuild it from these sources
+    # without them (that silently turned variant A/Bs into product-vs-product runs)
+    if out == LIB_PATH and os.environ.get("PPR_LIB_VARIANT") and not force:
+        return LIB_PATH
     if out == LIB_PATH and not force and not _stale():
         return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
