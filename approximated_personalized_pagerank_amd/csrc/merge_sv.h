@@ -219,8 +219,8 @@ __device__ __forceinline__ uint32_t sv_units_t(double t) {
 // (one ds_read_b128 from the key's home group: load 1/4, so a home group rarely fills). A key that
 // found its home group full sits in the next group with room, and bit 31 of the home group's first
 // tag word says so -- a lookup continues past its home group only then (< 1 % of the groups; keys
-// and their tags (key + 1) stay below 2^31). Accumulators are indexed by slot; slots T .. T + 63 are
-// per-lane dummies, so a lane whose key is not in PT adds there instead of branching around the add.
+// and their tags (key + 1) stay below 2^31). Accumulators are indexed by slot (slots T .. T + 63: the
+// per-lane dummies of the round-4 branch-free pass 1, kept in the layout, no longer written).
 struct SvPt {
   uint32_t* keys;            // [T] key + 1 (0 = empty); bit 31 of word 4 g: home group g overflowed
   unsigned long long* a;     // [T + 64] split accumulators (A: low 32 bits of each X_i; B: X_i >> 32)
@@ -452,8 +452,8 @@ __device__ __forceinline__ void sv_chunk(int64_t b0, int64_t b1, int64_t& c0, in
 }
 
 // pass 1 over successors [b0, b1): prev keys exactly into PT, every other key into the sketch.
-// Branch-free per group: the PT probe for every lane, the split add to the key's PT slot or the
-// lane's dummy slot, the sketch adds with 0 units for PT keys and masked lanes.
+// Per group: the PT probe for every lane, then the split add for the PT lanes and the sketch adds
+// for the others, each under its lane mask.
 #ifndef PPR_SV_NS1
 #define PPR_SV_NS1 4
 #endif
@@ -475,7 +475,6 @@ __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, co
                                          int64_t b0, int64_t b1, double factor, uint32_t* sk) {
   int64_t c0, c1;
   sv_chunk(b0, b1, c0, c1);
-  const int dummy = x.pt.T + lane_id();
   const double f61 = factor * 0x1p61;
   sv_rows<true, SV_NS1>(g, s, a, c0, c1, [&](const SvBatch<SV_NS1>& bt) {
     sv_groups(bt, [&](int, int key, double sc, bool valid, int64_t) {
@@ -483,8 +482,10 @@ __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, co
       const int slot = svpt_slot(x.pt, key, h, valid);
       const bool inpt = valid && slot >= 0;
       const double t = sc * f61;  // p * 2^61, exact (sv_split_t)
-      sv_split_add_t(x.pt.a, x.pt.b, inpt ? slot : dummy, t);
-      sv_sketch_add(sk, h, (valid && !inpt) ? sv_units_t(t) : 0u, x.wlog);
+      // exec-masked adds (round 5: 1335-1341 -> 1320-1324 ms per job against the branch-free form
+      // that sent non-PT lanes to per-lane dummy slots and PT lanes' zero units to the sketch)
+      if (inpt) sv_split_add_t(x.pt.a, x.pt.b, slot, t);
+      if (valid && !inpt) sv_sketch_add(sk, h, sv_units_t(t), x.wlog);
     });
   });
 }

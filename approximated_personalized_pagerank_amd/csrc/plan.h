@@ -315,6 +315,8 @@ inline void plan_free(ppr_plan* p) {
   if (getenv("PPR_TIMING") && p->spec_redo)
     fprintf(stderr, "ppr_timing spec_redo_sources %lld\n", (long long)p->spec_redo);
   if (getenv("PPR_TIMING") && p->host_plan_calls)
+    fprintf(stderr, "ppr_timing hub_paths lds_rank %u one_shot %d\n", p->lds_rank, (int)p->hub_bw2);
+  if (getenv("PPR_TIMING") && p->host_plan_calls)
     fprintf(stderr, "ppr_timing hub_planning host_s %.4f calls %lld hubs %lld order_s %.4f batches_s %.4f\n",
             p->host_plan_s, (long long)p->host_plan_calls, (long long)p->host_plan_hubs, p->host_plan_part[0],
             p->host_plan_part[1]);
