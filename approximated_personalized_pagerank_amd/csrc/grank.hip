@@ -61,7 +61,9 @@ namespace pprk {
 // of lower lanes on the same counter, for every collision pattern tried. It runs at the bucket
 // waves' own launch shape: the same grid (every CU filled to its LDS limit), the same waves per
 // block, the same per-wave LDS footprint and the counters at the same offset inside it (the
-// T-slot table, ChunkLds::cnt at 12 T). *ok stays 1 only if no lane of any wave ever disagrees.
+// T-slot table, ChunkLds::cnt at 12 T). ok[0] (the 32-bit add ranks: the scatter and the chunked
+// bucket accumulation) and ok[1] (the 64-bit CAS / add of the one-shot buckets, below) are probed
+// separately: each stays 1 only if no lane of any wave ever disagrees.
 __global__ void __launch_bounds__(256) k_probe_lds_rank(int* ok, int trials, int T, int wave_bytes) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6, l = lane_id();
@@ -89,6 +91,8 @@ __global__ void __launch_bounds__(256) k_probe_lds_rank(int* ok, int trials, int
     bad |= act && got != want;
     wave_fence();
   }
+  if (bad) atomicAnd(&ok[0], 0);
+  bad = 0;
   // the one-shot bucket path (merge_hub.h bucket_oneshot) relies on the same order for the 64-bit
   // add and for the 64-bit CAS on its slot words (table at offset 0): the lowest lane of a slot
   // wins the CAS, and every later add returns the count of lower lanes (plus the winner's 1)
@@ -108,7 +112,7 @@ __global__ void __launch_bounds__(256) k_probe_lds_rank(int* ok, int trials, int
     else bad |= (uint32_t)prev == 0xffffffffu || got != below;
     wave_fence();
   }
-  if (bad) atomicAnd(ok, 0);
+  if (bad) atomicAnd(&ok[1], 0);
 }
 
 }  // namespace pprk
@@ -363,23 +367,24 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     // in lane order: probe it once on this device, fall back to ballot ranks otherwise
     const char* e = getenv("PPR_LDS_RANK");
     int* d_ok = nullptr;
-    int ok = 0;
-    if ((!e || atoi(e) != 0) && hipMalloc(&d_ok, sizeof(int)) == hipSuccess) {
-      ok = 1;
-      if (hipMemcpy(d_ok, &ok, sizeof(int), hipMemcpyHostToDevice) == hipSuccess) {
+    int ok[2] = {0, 0};
+    if ((!e || atoi(e) != 0) && hipMalloc(&d_ok, sizeof(ok)) == hipSuccess) {
+      ok[0] = ok[1] = 1;
+      if (hipMemcpy(d_ok, ok, sizeof(ok), hipMemcpyHostToDevice) == hipSuccess) {
         hipFuncSetAttribute((const void*)k_probe_lds_rank, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipLaunchKernelGGL(k_probe_lds_rank, dim3((unsigned)p->hub_bw_blocks), dim3(64 * p->hub_bw_waves),
                            p->hub_lds_wave, p->stream, d_ok, 64, p->hub_wave_t,
                            p->hub_wave_stride);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(p->stream) != hipSuccess ||
-            hipMemcpy(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
-          ok = 0;
+            hipMemcpy(ok, d_ok, sizeof(ok), hipMemcpyDeviceToHost) != hipSuccess)
+          ok[0] = ok[1] = 0;
       } else {
-        ok = 0;
+        ok[0] = ok[1] = 0;
       }
       hipFree(d_ok);
     }
-    p->lds_rank = ok ? 1u : 0u;
+    p->lds_rank = ok[0] ? 1u : 0u;
+    p->lds_rank64 = ok[1] ? 1u : 0u;
   }
   // exact-sum GRank (merge_xs.h): the default outside the MC combine; PPR_FLAG_CHAIN_SUM or
   // PPR_SUM=chain keep the reference's in-order fma chains (and the hub pipeline of merge_hub.h)
@@ -1156,7 +1161,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       // present in most successor baskets) still has few distinct keys, and its sequential fma
       // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
       const int wpb = p->hub_bw_waves;
-      const int cap2 = (p->hub_bw2 && p->lds_rank) ? BW2_CAP : 0;
+      const int cap2 = (p->hub_bw2 && p->lds_rank && p->lds_rank64) ? BW2_CAP : 0;
       const int64_t blocks = (nbuck + wpb - 1) / wpb;
       const dim3 grid((unsigned)blocks), blk(64 * wpb);
       if (p->hub_range > 0) {

@@ -112,7 +112,8 @@ struct ppr_plan {
   size_t gath_bytes = 0;
   int num_cus = 256;
   int hub_bw_blocks = 0;           // persistent k_hub_bucket_w grid
-  uint32_t lds_rank = 0;           // k_probe_lds_rank passed (PPR_LDS_RANK=0 forces the ballot path)
+  uint32_t lds_rank = 0;           // k_probe_lds_rank: 32-bit add ranks in lane order (PPR_LDS_RANK=0 forces the ballot path)
+  uint32_t lds_rank64 = 0;         // ... and the 64-bit CAS / add order the one-shot buckets need
   bool seg_enabled = false;        // segmented hub buckets (k_hub_seg, PPR_HUB_SEG=1)
   int seg_bucket = 256, seg_t = 512, seg_wpb = 1;
   int hub_bw_ng = 2;               // PPR_BW_NG: groups per chunk (1, 2, 4 or 8)
@@ -315,7 +316,8 @@ inline void plan_free(ppr_plan* p) {
   if (getenv("PPR_TIMING") && p->spec_redo)
     fprintf(stderr, "ppr_timing spec_redo_sources %lld\n", (long long)p->spec_redo);
   if (getenv("PPR_TIMING") && p->host_plan_calls)
-    fprintf(stderr, "ppr_timing hub_paths lds_rank %u one_shot %d\n", p->lds_rank, (int)p->hub_bw2);
+    fprintf(stderr, "ppr_timing hub_paths lds_rank %u lds_rank64 %u one_shot %d\n", p->lds_rank, p->lds_rank64,
+            (int)p->hub_bw2);
   if (getenv("PPR_TIMING") && p->host_plan_calls)
     fprintf(stderr, "ppr_timing hub_planning host_s %.4f calls %lld hubs %lld order_s %.4f batches_s %.4f\n",
             p->host_plan_s, (long long)p->host_plan_calls, (long long)p->host_plan_hubs, p->host_plan_part[0],
