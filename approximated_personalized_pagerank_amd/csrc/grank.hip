@@ -93,9 +93,9 @@ __global__ void __launch_bounds__(256) k_probe_lds_rank(int* ok, int trials, int
   }
   if (bad) atomicAnd(&ok[0], 0);
   bad = 0;
-  // the one-shot bucket path (merge_hub.h bucket_oneshot) relies on the same order for the 64-bit
-  // add and for the 64-bit CAS on its slot words (table at offset 0): the lowest lane of a slot
-  // wins the CAS, and every later add returns the count of lower lanes (plus the winner's 1)
+  // (informational since round 5: the round-2 one-shot bucket path relied on the same order for
+  // the 64-bit add and the 64-bit CAS on its slot words; the current one needs only the 32-bit add
+  // order above. ok[1] is reported by PPR_TIMING as lds_rank64.)
   unsigned long long* w64 = reinterpret_cast<unsigned long long*>(smem + (size_t)wv * wave_bytes);
   for (int t = 0; t < trials; t++) {
     const uint32_t r = hash32(t * 7727u + blockIdx.x * 104723u + wv * 37u + 3u);
@@ -1161,7 +1161,7 @@ static int run_hubs(ppr_plan* p, const IterArgs& a, const int32_t* big,
       // present in most successor baskets) still has few distinct keys, and its sequential fma
       // chain must not hold a whole workgroup. Only table overflows move to the workgroup kernel.
       const int wpb = p->hub_bw_waves;
-      const int cap2 = (p->hub_bw2 && p->lds_rank && p->lds_rank64) ? BW2_CAP : 0;
+      const int cap2 = (p->hub_bw2 && p->lds_rank) ? BW2_CAP : 0;
       const int64_t blocks = (nbuck + wpb - 1) / wpb;
       const dim3 grid((unsigned)blocks), blk(64 * wpb);
       if (p->hub_range > 0) {

@@ -505,23 +505,27 @@ struct BucketWave {
 // ---------------------------------------------------------------------------------------------
 // One-shot bucket (default for buckets of at most BW2_CAP records, with lane-ordered LDS atomics):
 // the whole bucket is loaded into registers at once and accumulated in one pass instead of chunk
-// by chunk, with one 64-bit LDS word per table slot, key | occurrences << 32 | run base << 48:
-//   P1  per group, in stream order: find-or-insert with the occurrence index in the same atomic
-//       (a key's first record claims an empty slot by CAS with count 1, later ones add 1 << 32;
-//       same-address lanes of one instruction are served in lane order -- probed per plan, both
-//       for the 64-bit add and the 64-bit CAS -- and the groups go in order), new slots listed;
-//   P2  exclusive scan of the listed slots' counts -> each slot's run base (into its word);
+// by chunk. Per table slot a 32-bit key and a 32-bit counter:
+//   P1  per group, in stream order: find-or-insert every key (32-bit CAS; which lane of a group
+//       wins an empty slot does not matter), then one returning 32-bit add on the key's counter
+//       for every lane at once -- same-address lanes of one instruction are served in lane order
+//       (probed per plan, k_probe_lds_rank ok[0]) and the groups go in order, so the returned
+//       value is the record's occurrence index in stream order; new slots listed;
+//   P2  exclusive scan of the listed slots' counts -> each slot's run base (over its counter);
 //   P3  every record's value to vals[base + occurrence]: the bucket's values grouped by key, in
 //       stream order inside a key;
 //   P4  one lane per listed slot: the key's fma chain over its run, seeded with the source's own
 //       value for the seed key (include/grank.h:103-116 order); the total overwrites the run's
 //       last value;
 //   P5  totals >= tau (at most L by (score desc, tie_w desc)) appended to the source's list.
+// (Round 5: the round-2 form kept key, count and base in one 64-bit word and needed the 64-bit
+// CAS and add in lane order too; on the round-5 MI355X boxes only the 32-bit order held, which
+// had switched this path and the ordered ranks of the scatter and the chunks off.)
 // The chunked path needs ~10 dependent LDS round trips per 128 records plus a 512-slot compaction
 // per bucket; this one ~20 per bucket. Buckets it cannot take (more records) use the chunked path.
 constexpr int BW2_GROUPS = 8;
 constexpr int BW2_CAP = BW2_GROUPS * WAVE;  // records
-__host__ __device__ constexpr size_t bw2_lds(int T) {  // words | vals | listed slots | select histogram
+__host__ __device__ constexpr size_t bw2_lds(int T) {  // keys | counters | vals | listed slots | select histogram
   return ((size_t)T * 8 + (size_t)BW2_CAP * 8 + (size_t)BW2_CAP * 2 + 1024 + 15) & ~(size_t)15;
 }
 
@@ -546,12 +550,12 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
 #else
   auto lap = [](int) {};
 #endif
-  unsigned long long* word = reinterpret_cast<unsigned long long*>(base);
+  uint32_t* keys = reinterpret_cast<uint32_t*>(base);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(base + (size_t)T * 4);
   double* vals = reinterpret_cast<double*>(base + (size_t)T * 8);
   uint16_t* listed = reinterpret_cast<uint16_t*>(base + (size_t)T * 8 + (size_t)BW2_CAP * 8);
   uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 8 + (size_t)BW2_CAP * 10);
-  constexpr unsigned long long EMPTYW = 0xffffffffull;  // key EMPTY, count 0
-  constexpr unsigned long long ONE = 1ull << 32;
+  constexpr uint32_t EMPTYK = 0xffffffffu;  // (keys are >= 0)
   const int ng = (nb + WAVE - 1) / WAVE;  // (uniform) groups holding records
   int kk[BW2_GROUPS];
   double cs[BW2_GROUPS];
@@ -563,13 +567,13 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     kk[k] = rec_key(r);
     cs[k] = rec_sc(r);
   }
-  for (int i = l; i < T; i += WAVE) word[i] = EMPTYW;
+  for (int i = l; i < T; i += WAVE) { keys[i] = EMPTYK; cnt[i] = 0u; }
   wave_fence();
   int nt = 0;
   if (W.seed >= 0) {  // the source's own key: listed, no occurrence yet (its chain starts at selfval)
     if (l == 0) {
       const uint32_t h = bw2_slot(W.seed, T);
-      word[h] = (unsigned long long)(uint32_t)W.seed;
+      keys[h] = (uint32_t)W.seed;
       listed[0] = (uint16_t)h;
     }
     nt = 1;
@@ -583,12 +587,11 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
   }
   lap(0);  // loads + table clear
   const uint64_t lt = lanemask_lt();
-  uint32_t sl[BW2_GROUPS], occ[BW2_GROUPS];
-  unsigned long long c0[BW2_GROUPS];
+  uint32_t sl[BW2_GROUPS], occ[BW2_GROUPS], c0[BW2_GROUPS];
 #pragma unroll
   for (int k = 0; k < BW2_GROUPS; k++) {  // first probes up front (a stale EMPTY is caught by the CAS)
     sl[k] = bw2_slot(kk[k], T);
-    c0[k] = (k < ng && k * WAVE + l < nb) ? word[sl[k]] : EMPTYW;
+    c0[k] = (k < ng && k * WAVE + l < nb) ? keys[sl[k]] : EMPTYK;
   }
   // P1
 #pragma unroll
@@ -596,78 +599,78 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     if (k >= ng) break;  // uniform
     const bool v = k * WAVE + l < nb;
     // at most the lanes whose early probe did not show their key bring a new key
-    const int maybe_new = __popcll(__ballot(v && (uint32_t)c0[k] != (uint32_t)kk[k]));
+    const int maybe_new = __popcll(__ballot(v && c0[k] != (uint32_t)kk[k]));
     if (nt + maybe_new > budget) return false;
-    uint32_t h = sl[k], o = 0;
+    uint32_t h = sl[k];
     bool fresh = false;
     bool lost = false;
     if (v) {
-      unsigned long long w = c0[k];
-      lost = true;  // (bounded probe: a full table fails the pass, the caller takes more passes)
+      uint32_t w = c0[k];
+      lost = true;  // (bounded probe: a full table fails the pass, the caller spills the bucket)
       for (int n = 0; n < 2 * T; n++) {
-        const uint32_t wk = (uint32_t)w;
-        if (wk == (uint32_t)kk[k]) { o = (uint32_t)(atomicAdd(&word[h], ONE) >> 32) & 0xffffu; lost = false; break; }
-        if (wk == 0xffffffffu) {
-          const unsigned long long prev = atomicCAS(&word[h], EMPTYW, ONE | (uint32_t)kk[k]);
-          if (prev == EMPTYW) { fresh = true; lost = false; break; }  // occurrence 0
-          w = prev;  // taken meanwhile (a lower lane or an earlier group): test the same slot again
+        if (w == (uint32_t)kk[k]) { lost = false; break; }
+        if (w == EMPTYK) {
+          const uint32_t prev = atomicCAS(&keys[h], EMPTYK, (uint32_t)kk[k]);
+          if (prev == EMPTYK) { fresh = true; lost = false; break; }
+          w = prev;  // taken meanwhile (another lane or an earlier group): test the same slot again
           continue;
         }
         h = (h + 1 == (uint32_t)T) ? 0u : h + 1;
-        w = word[h];
+        w = keys[h];
       }
     }
     if (__ballot(lost)) return false;
+    wave_fence();
+    // occurrence indices: one returning add for the whole group, same-slot lanes in lane order
+    occ[k] = v ? atomicAdd(&cnt[h], 1u) : 0u;
     sl[k] = h;
-    occ[k] = o;
     const uint64_t fm = __ballot(fresh);
     if (fresh) listed[nt + __popcll(fm & lt)] = (uint16_t)h;
     nt += __popcll(fm);
     wave_fence();
   }
   lap(1);  // P1
-  // P2: run bases (listed order)
+  // P2: run bases (listed order) over the counters; the total after the last run
   int run = 0;
   for (int i0 = 0; i0 < nt; i0 += WAVE) {
     const int i = i0 + l;
-    unsigned long long w = 0;
     int c = 0;
-    if (i < nt) { w = word[listed[i]]; c = (int)((w >> 32) & 0xffffu); }
+    if (i < nt) c = (int)cnt[listed[i]];
     const int incl = wave_incl_scan(c);
-    if (i < nt) word[listed[i]] = (w & 0x0000ffffffffffffull) | ((unsigned long long)(run + incl - c) << 48);
+    if (i < nt) cnt[listed[i]] = (uint32_t)(run + incl - c);
     run += __builtin_amdgcn_readlane(incl, WAVE - 1);
   }
+  const int total = run;
   wave_fence();
   lap(2);
   // P3: values grouped by key
 #pragma unroll
   for (int k = 0; k < BW2_GROUPS; k++) {
     if (k >= ng) break;
-    if (k * WAVE + l < nb) vals[(uint32_t)(word[sl[k]] >> 48) + occ[k]] = cs[k];
+    if (k * WAVE + l < nb) vals[cnt[sl[k]] + occ[k]] = cs[k];
   }
   wave_fence();
   lap(3);
+  // run of listed slot i: [cnt[listed[i]], next run's base or the total)
+  auto run_end = [&](int i) { return i + 1 < nt ? (int)cnt[listed[i + 1]] : total; };
   // P4: one chain per listed slot
   const double f = W.factor;
   for (int i0 = 0; i0 < nt; i0 += WAVE) {
     const int i = i0 + l;
     if (i < nt) {
-      const unsigned long long w = word[listed[i]];
-      const int c = (int)((w >> 32) & 0xffffu), b = (int)(w >> 48);
-      const int e = b + c;
-      const double x = fma_chain_lds(vals, b, e, f, ((int)(uint32_t)w == W.seed) ? W.selfval : 0.0);
-      if (c > 0) vals[e - 1] = x;  // (a slot without occurrences is the seed key: its total is selfval)
+      const int b = (int)cnt[listed[i]], e = run_end(i);
+      const double x = fma_chain_lds(vals, b, e, f, ((int)keys[listed[i]] == W.seed) ? W.selfval : 0.0);
+      if (e > b) vals[e - 1] = x;
     }
   }
   wave_fence();
   lap(4);
   // P5: keys reaching tau, at most L of them, appended
   auto total_of = [&](int i) {
-    const unsigned long long w = word[listed[i]];
-    const int c = (int)((w >> 32) & 0xffffu);
-    return c > 0 ? vals[(int)(w >> 48) + c - 1] : W.selfval;
+    const int b = (int)cnt[listed[i]], e = run_end(i);
+    return e > b ? vals[e - 1] : W.selfval;  // (a slot without occurrences is the seed key)
   };
-  auto key_of = [&](int i) { return (int)(uint32_t)word[listed[i]]; };
+  auto key_of = [&](int i) { return (int)keys[listed[i]]; };
   int kept = 0;
   for (int i0 = 0; i0 < nt; i0 += WAVE) {
     const int i = i0 + l;
@@ -678,7 +681,7 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     diag_add(a.diag, 96 + (31 - __clz(kept | 1)), 1ull);
   }
   if (kept == 0) { lap(5); return true; }
-  const int cnt = kept <= Lw ? kept : Lw;
+  const int cntk = kept <= Lw ? kept : Lw;
   SelCrit c;
   const uint32_t ts = W.ts;
   const double tau = W.tau;
@@ -686,7 +689,7 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     c = select_top(nt, Lw, key_of, [&](int i) { const double x = total_of(i); return x >= tau ? x : 0.0; }, hist, ts);
   lap(5);  // kept count + select
   int at = 0;
-  if (l == 0) at = (int)atomicAdd(pt_cnt_d, (uint32_t)cnt);
+  if (l == 0) at = (int)atomicAdd(pt_cnt_d, (uint32_t)cntk);
   at = __builtin_amdgcn_readlane(at, 0);
   lap(6);  // appending atomic
   int pos0 = 0;
