@@ -133,7 +133,7 @@ struct ppr_plan {
   unsigned char* d_xsz = nullptr;     // int64 block size per rank (all-gathered)
   unsigned char* d_xtmp = nullptr;    // scan temporary of the block offsets
   size_t xsend_bytes = 0, xrecv_bytes = 0, xsz_bytes = 0, xtmp_bytes = 0;
-  int64_t fused_max = 16384;          // PPR_FUSED_MAX: MC levels up to this many sources take one host sync
+  int64_t fused_max = 65536;          // PPR_FUSED_MAX: MC levels up to this many sources take one host sync (round 5: 16384 -> 65536, combine 926 -> 909 ms)
   int64_t last_nbig = 0, last_maxneed = 0;
   double host_plan_s = 0.0;                  // host time planning hub batches (PPR_TIMING, at destroy)
   int64_t host_plan_calls = 0, host_plan_hubs = 0;
