@@ -466,6 +466,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       if (s6) p->sv_mid = std::max<int64_t>(0, atoll(s6));
       const char* s7 = getenv("PPR_SV_REDO");
       p->sv_redo_mid = !(s7 && atoi(s7) == 0);
+      const char* s9 = getenv("PPR_SV_P2SKIP");
+      p->sv_p2skip = !(s9 && atoi(s9) == 0);
       const char* s8 = getenv("PPR_SV_REDO_LARGE");
       p->sv_redo_large = s8 && atoi(s8) != 0;
       const char* s3 = getenv("PPR_SV_BUDGET");
@@ -746,7 +748,7 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   a.stats = (p->flags & PPR_FLAG_STATS) ? 1u : 0u;
   a.lds_rank = p->lds_rank;
   a.nt = (uint32_t)p->nt_loads;
-  a.whatif = (uint32_t)p->whatif & 0xffffu;
+  a.whatif = ((uint32_t)p->whatif & 0xffffu) | (p->sv_p2skip ? 0u : WI_SV_NO_P2SKIP);
   a.iter = unit ? -1 : it;
   a.spec = (unit || p->hot_cap > 0 || it < p->spec_from) ? 0.0 : p->spec_ratio;
   a.xs = p->xsum ? 1u : 0u;

@@ -704,7 +704,7 @@ __device__ __forceinline__ void sv1_source(unsigned char* smem, DevGraph g, DevS
   sv_lap(a, dg + 2, tph);
   // a sketch row with no counter at or above thr: no key outside PT can pass, pass 2 would insert
   // nothing (exact skip)
-  if (sv_rows_all(x)) {
+  if (sv_rows_all(x) || (a.whatif & WI_SV_NO_P2SKIP)) {
     if (threadIdx.x == 0) sv_seed2(x, xt, v, 1.0 - a.damping);
     sv_pass2(g, s, a, x, xt, b, e, factor, budget);
     __syncthreads();

@@ -230,6 +230,7 @@ struct ppr_plan {
                                       // (measured: 4096 beats 0 by 2-3 % -- the smallest sources overflow the
                                       // 4-wave class's sketch and were handed back -- and 16384 by 5 %)
   bool sv_redo_mid = true;            // PPR_SV_REDO=0: small-class overflows go straight to the host hand-back
+  bool sv_p2skip = true;             // PPR_SV_P2SKIP=0: pass 2 runs even when a sketch row proves it inserts nothing
   bool sv_redo_large = false;         // PPR_SV_REDO_LARGE=1: mid-class overflows redone on the device (k_sv1_list;
                                       // off by default: at RMAT-22 the mid class now overflows ~1 source per job,
                                       // and the redo grid's 113-KB workgroups still pass through the CUs)

@@ -176,6 +176,8 @@ struct IterArgs {
 // with 8, plan.h): never set from the environment, so the real pass can not inherit them
 constexpr uint32_t WI_SCAT_COALESCED = 1u << 20, WI_SCAT_NOSTORE = 1u << 21, WI_SCAT_NOSCORE = 1u << 22,
                    WI_SCAT_COUNT = 1u << 23, WI_SCAT_WALK = 1u << 24;
+// the sieve's exact pass-2 skip turned off (PPR_SV_P2SKIP=0, tests: the skip must not change a bit)
+constexpr uint32_t WI_SV_NO_P2SKIP = 1u << 25;
 
 // Speculative top-L pruning bound of a hub source (GRank iterations): spec x the smallest score of
 // the source's previous row when that row was full. Bucket waves then emit only keys whose exact

@@ -328,6 +328,7 @@ def test_gpu_exact_sum_init_hubs_and_damping():
     # on the device with the 16-wave geometry (k_sv1_list); by default they go to the host
     ({"PPR_SV_SMALL": "0", "PPR_SV_MID": "1000000000", "PPR_TIER_MASK": "0x0", "PPR_SV_REDO_LARGE": "1"}, "devredo"),
     ({"PPR_SV_SMALL": "0", "PPR_SV_MID": "1000000000", "PPR_TIER_MASK": "0x0"}, "redo"),
+    ({"PPR_SV_P2SKIP": "0"}, "sieve"),                        # pass 2 even where a sketch row rules it out
     ({"PPR_SV": "0"}, None),                                  # off: range / partition engines only
 ])
 def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):
@@ -500,3 +501,30 @@ def test_gpu_partitions_match_host():
     r = ppr.grank_csr(path, 4, 8, 3, 0.85, -1.0, part="plan", device=0)  # (device declines, host BFS)
     o = oracle.grank(path.row_ptr, path.col, path.partitions(), 4, 8, 3, 0.85, -1.0)
     assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])
+
+
+@pytest.mark.parametrize("skip", ["1", "0"])
+def test_gpu_sieve_pass2_skip_forced(skip, monkeypatch, capfd):
+    """the exact pass-2 skip (a sketch row without a counter at the bound
+    proves that no key outside PT can pass) fires on these graphs, and turning it off
+    (PPR_SV_P2SKIP=0) leaves every bit of the result -- both runs equal the oracle's exact sum"""
+    monkeypatch.setenv("PPR_SV_MIN", "0")
+    monkeypatch.setenv("PPR_TIER_MASK", "0x0")  # every source with a full row through the sieve
+    monkeypatch.setenv("PPR_SV_P2SKIP", skip)
+    monkeypatch.setenv("PPR_DIAG", "1")
+    skipped = 0
+    for scale, K, L, it in [(11, 16, 32, 8), (12, 32, 128, 6)]:
+        g = ppr.rmat(scale, seed=191 + scale)
+        part = g.partitions()
+        r = ppr.grank_csr(g, K, L, it, 0.85, -1.0, part=part, device=0)
+        o = oracle.grank(g.row_ptr, g.col, part, K, L, it, 0.85, -1.0)
+        assert np.array_equal(r.max_diff, o["max_diff"])
+        assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])
+        err = capfd.readouterr().err
+        for ln in err.splitlines():
+            if "pass 2 skipped" in ln:
+                skipped += int(ln.split("pass 2 skipped (a sketch row below the bound)")[1].split(",")[0])
+    if skip == "1":
+        assert skipped > 0
+    else:
+        assert skipped == 0
