@@ -365,6 +365,29 @@ def test_gpu_sieve_bit_exact(senv, want, monkeypatch, capfd):
         assert redo_dev == 0
 
 
+@pytest.mark.parametrize("L,sieved_want", [(128, True), (129, False), (256, False), (512, False)])
+def test_gpu_sieve_basket_width_limit(L, sieved_want, monkeypatch, capfd):
+    """the sieve takes baskets of at most 128 entries (grank.hip sv_enabled; merge_sv.h walks a row
+    as two 64-entry groups): at L = 128 it runs, past it every source takes the range / partition
+    engines -- exact either way, with the sieve's size-class knobs forced on (no sieve
+    path past L = 128 runs without parity)"""
+    monkeypatch.setenv("PPR_SV_MIN", "0")
+    monkeypatch.setenv("PPR_SV_SLICE", "256")  # multi-slice too, were the sieve on
+    monkeypatch.setenv("PPR_TIER_MASK", "0x0")  # every source with a full row offered to the sieve
+    monkeypatch.setenv("PPR_TIMING", "1")
+    g = ppr.rmat(12, seed=517)
+    part = g.partitions()
+    r = ppr.grank_csr(g, 32, L, 3, 0.85, -1.0, part=part, device=0)
+    o = oracle.grank(g.row_ptr, g.col, part, 32, L, 3, 0.85, -1.0)
+    assert np.array_equal(r.max_diff, o["max_diff"])
+    assert np.array_equal(r.lens, o["lens"])
+    assert np.array_equal(r.ids, o["ids"])
+    assert np.array_equal(r.scores, o["scores"])
+    err = capfd.readouterr().err
+    sieved = sum(int(x.split()[2]) for x in err.splitlines() if x.startswith("ppr_timing sieve_sources"))
+    assert (sieved > 0) == sieved_want
+
+
 @pytest.mark.parametrize("henv", [
     # the bucket partition limited to 2 buckets of 819 keys: every source expected beyond them
     # goes to the HBM table (merge_xg.h); the selection list at its largest (all keys at once)
