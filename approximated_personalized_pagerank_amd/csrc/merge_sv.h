@@ -140,32 +140,25 @@ __device__ __forceinline__ int x2_slot(const X2Table& t, int key, bool& ins) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// One cheap hash per key (full-rate 24-bit multiplies: v_mul_lo_u32 is a quarter-rate VALU op,
-// and the walk hashes every candidate twice). Its low bits place the key in PT, three bit fields
-// give its sketch cells. (Independent of hash_b, which orders the stored rows; the quality only
-// moves the false-positive rate, never the result.)
-__device__ __forceinline__ uint32_t sv_mix(uint32_t x) {
-  x ^= x >> 16;                    // (bits 24-31 reach the 24-bit multiply through bits 8-15)
-  x = __umul24(x, 0x9E3779u);
-  x ^= x >> 13;
-  x = __umul24(x, 0x5BD1E9u) ^ (x >> 24);
-  x ^= x >> 15;
-  return x;
+// Three multiplicative hashes of a key (Knuth: the top bits of key * an odd constant mix every key
+// bit; v_mul_lo_u32 issues at the VALU's full rate on gfx950, tools/valu_rates.hip). h0's top bits
+// place the key in PT (a multiply-high by the group count); the top wlog bits of h0, h1 and h2 are its
+// three sketch cells -- one shift each, no bit-field mixing (round 6: the old 24-bit mixer and its
+// three bit fields took 16 VALU instructions of a pass-1 group, these take 6). Independent of hash_b,
+// which orders the stored rows; the hashes' quality only moves the false-positive rate, never the
+// result.
+struct SvHash {
+  uint32_t h0, h1, h2;
+};
+__device__ __forceinline__ SvHash sv_hash(int key) {
+  const uint32_t k = (uint32_t)key;
+  return SvHash{k * 0x9E3779B1u, k * 0x85EBCA77u, k * 0xC2B2AE3Du};
 }
-// sketch cell of row j (rows of 2^wlog counters, wlog <= 13): bits 0.., bits 13.., and a 24-bit
-// product of the rest
-__device__ __forceinline__ uint32_t sv_cell(uint32_t h, int j, int wlog) {
-  const uint32_t m = (1u << wlog) - 1u;
-  const uint32_t c = j == 0 ? (h & m) : j == 1 ? ((h >> 13) & m) : ((uint32_t)__umul24(h ^ (h >> 19), 0x2C1B3Du) >> (32 - wlog));
-  return ((uint32_t)j << wlog) + c;
-}
-// an upper bound of p * 2^31 in counter units: fl(p) is within 2^-24 relative of p, the factor
-// 2^31 (1 + 2^-20) -- exact in single precision -- and the +1 after the truncation cover that and
-// the product's rounding (f >= p 2^31 (1 + 2^-20)(1 - 2^-24)^2 > p 2^31)
-__device__ __forceinline__ uint32_t sv_units(double p) {
-  const float f = (float)p * 2147485696.0f;
-  return f >= 4294967040.0f ? 0xffffffffu : (uint32_t)f + 1u;
-}
+// an upper bound of p * 2^31 in counter units, from fl(p * 2^31) = fl(s * (f * 2^31)) (a
+// power-of-two scale commutes with the rounding; below the normal range both round to < 1 unit):
+// floor + 1 > p * 2^31. GRank contributions are <= 1: no saturation.
+__device__ __forceinline__ uint32_t sv_units31(double p31) { return (uint32_t)p31 + 1u; }
+__device__ __forceinline__ uint32_t sv_units(double p) { return sv_units31(p * 0x1p31); }
 // counter threshold of the bound theta: a key whose total reaches theta has every counter >=
 // 2^31 * theta * (1 - 2^-52) (its stored value rounds up by at most half an ulp); the margin
 // below makes the test conservative (a counter at the threshold passes)
@@ -173,17 +166,23 @@ __device__ __forceinline__ uint32_t sv_thr(double theta) {
   const double x = floor(ldexp(theta, SV_UNIT_LOG) * (1.0 - 0x1p-40));
   return x <= 0.0 ? 0u : x >= 4294967295.0 ? 0xffffffffu : (uint32_t)x;
 }
-__device__ __forceinline__ void sv_sketch_add(uint32_t* sk, uint32_t h, uint32_t u, int wlog) {
-#pragma unroll
-  for (int j = 0; j < SV_R; j++) atomicAdd(&sk[sv_cell(h, j, wlog)], u);
+// the key's three counters (row j: counters (j << wlog) + top wlog bits of h_j)
+__device__ __forceinline__ void sv_sketch_add(uint32_t* sk, const SvHash& hs, uint32_t u, int wlog) {
+  const int sh = 32 - wlog;
+  atomicAdd(&sk[hs.h0 >> sh], u);
+  atomicAdd(&sk[(1u << wlog) + (hs.h1 >> sh)], u);
+  atomicAdd(&sk[(2u << wlog) + (hs.h2 >> sh)], u);
 }
 // every counter of the key at or above the threshold (bitmap of the counters that are; the three
-// words are read together)
-__device__ __forceinline__ bool sv_passes(const uint32_t* bm, uint32_t h, int wlog) {
-  uint32_t w[SV_R], c[SV_R];
-#pragma unroll
-  for (int j = 0; j < SV_R; j++) { c[j] = sv_cell(h, j, wlog); w[j] = bm[c[j] >> 5]; }
-  return ((w[0] >> (c[0] & 31u)) & (w[1] >> (c[1] & 31u)) & (w[2] >> (c[2] & 31u)) & 1u) != 0u;
+// words are read together). Counter c = h >> sh is bit c & 31 of word c >> 5 = h >> (sh + 5); the
+// 32-bit shift by c takes its low five bits by itself.
+__device__ __forceinline__ bool sv_passes(const uint32_t* bm, const SvHash& hs, int wlog) {
+  const int sh = 32 - wlog;
+  const int rw = (1 << wlog) >> 5;  // bitmap words per row
+  const uint32_t w0 = bm[hs.h0 >> (sh + 5)];
+  const uint32_t w1 = bm[rw + (hs.h1 >> (sh + 5))];
+  const uint32_t w2 = bm[2 * rw + (hs.h2 >> (sh + 5))];
+  return ((w0 >> ((hs.h0 >> sh) & 31u)) & (w1 >> ((hs.h1 >> sh) & 31u)) & (w2 >> ((hs.h2 >> sh) & 31u)) & 1u) != 0u;
 }
 // The split accumulator's two addends of one contribution p = fl(s * f), from t = p * 2^61:
 // X = floor(p * 2^93) (merge_xs.h xs_conv), A = X mod 2^32, B = X >> 32 = floor(t). t is exact
@@ -192,12 +191,22 @@ __device__ __forceinline__ bool sv_passes(const uint32_t* bm, uint32_t h, int wl
 // integer shifts and no branches: B's words are two truncating conversions, and t - B < 2^32 and
 // its fraction are exact (they are multiples of ulp(t)), so A = trunc(frac(t) * 2^32).
 __device__ __forceinline__ void sv_split_t(double t, unsigned long long& A, unsigned long long& B) {
-  const uint32_t bh = (uint32_t)(t * 0x1p-32);             // t < 2^63 (p < 4)
-  const double r = t - (double)bh * 0x1p32;                // [0, 2^32), exact
-  const uint32_t bl = (uint32_t)r;
-  A = (unsigned long long)(uint32_t)((r - (double)bl) * 0x1p32);
+  const uint32_t bh = (uint32_t)(t * 0x1p-32);                    // t <= 2^61 (p <= 1)
+  const uint32_t bl = (uint32_t)fma(-(double)bh, 0x1p32, t);      // t - bh 2^32 in [0, 2^32), exact
+  A = (unsigned long long)(uint32_t)(__builtin_amdgcn_fract(t) * 0x1p32);  // frac(t) 2^32 < 2^32
   B = ((unsigned long long)bh << 32) | bl;
 }
+// accumulators of slot i at ab[2 i] (A) and ab[2 i + 1] (B): one address, the second add at +8
+__device__ __forceinline__ void sv_split_add_t(unsigned long long* ab, int i, double t) {
+  unsigned long long A, B;
+  sv_split_t(t, A, B);
+  atomicAdd(&ab[2 * i], A);
+  atomicAdd(&ab[2 * i + 1], B);
+}
+__device__ __forceinline__ void sv_split_add(unsigned long long* ab, int i, double p) {
+  sv_split_add_t(ab, i, p * 0x1p61);
+}
+// (XT: separate A and B arrays)
 __device__ __forceinline__ void sv_split_add_t(unsigned long long* a, unsigned long long* b, int i, double t) {
   unsigned long long A, B;
   sv_split_t(t, A, B);
@@ -206,12 +215,6 @@ __device__ __forceinline__ void sv_split_add_t(unsigned long long* a, unsigned l
 }
 __device__ __forceinline__ void sv_split_add(unsigned long long* a, unsigned long long* b, int i, double p) {
   sv_split_add_t(a, b, i, p * 0x1p61);
-}
-// counter units of t = p * 2^61: an upper bound of p * 2^31 (sv_units). GRank contributions are
-// <= 1, so f < 2^31 + 2^12 and the conversion never saturates.
-__device__ __forceinline__ uint32_t sv_units_t(double t) {
-  const float f = (float)t * 0x1.00001p-30f;
-  return (uint32_t)f + 1u;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -223,8 +226,8 @@ __device__ __forceinline__ uint32_t sv_units_t(double t) {
 // per-lane dummies of the round-4 branch-free pass 1, kept in the layout, no longer written).
 struct SvPt {
   uint32_t* keys;            // [T] key + 1 (0 = empty); bit 31 of word 4 g: home group g overflowed
-  unsigned long long* a;     // [T + 64] split accumulators (A: low 32 bits of each X_i; B: X_i >> 32)
-  unsigned long long* b;     // [T + 64]
+  unsigned long long* ab;    // [2 (T + 64)] split accumulators of slot i: A at 2 i (low 32 bits of each
+                             // X_i), B at 2 i + 1 (X_i >> 32)
   int* pos;                  // [T] row position of the slot's key
   int T;
   uint32_t gmask;            // T / 4 - 1
@@ -233,14 +236,16 @@ __host__ __device__ constexpr size_t svpt_bytes(int Lp) { return (size_t)4 * Lp 
 __device__ __forceinline__ SvPt svpt_carve(unsigned char* p, int Lp) {
   SvPt t;
   t.T = 4 * Lp;
-  t.a = reinterpret_cast<unsigned long long*>(p); p += (size_t)(t.T + 64) * 8;
-  t.b = reinterpret_cast<unsigned long long*>(p); p += (size_t)(t.T + 64) * 8;
+  t.ab = reinterpret_cast<unsigned long long*>(p); p += (size_t)(t.T + 64) * 16;
   t.keys = reinterpret_cast<uint32_t*>(p); p += (size_t)t.T * 4;
   t.pos = reinterpret_cast<int*>(p);
   t.gmask = (uint32_t)(t.T / 4) - 1u;
   return t;
 }
 constexpr uint32_t SV_OVF_BIT = 0x80000000u;
+// first slot of the home group of a key with hash h0: its top bits times the slot count, rounded
+// down to the group (a multiply-high and a mask)
+__device__ __forceinline__ uint32_t svpt_home(const SvPt& t, uint32_t h0) { return __umulhi(h0, (uint32_t)t.T) & ~3u; }
 // the slot of tag past its home group g4 (the group overflowed): groups in order until the tag or
 // an empty slot (the key would have taken it)
 __device__ __forceinline__ int svpt_find_from(const SvPt& t, uint32_t tag, uint32_t g4) {
@@ -260,7 +265,7 @@ __device__ __forceinline__ int svpt_find_from(const SvPt& t, uint32_t tag, uint3
 // every lane of the wave must call it (one ballot).
 __device__ __forceinline__ int svpt_slot(const SvPt& t, int key, uint32_t h, bool active) {
   const uint32_t tag = (uint32_t)key + 1u;
-  const uint32_t g4 = (h & t.gmask) << 2;
+  const uint32_t g4 = svpt_home(t, h);
   const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g4);
   int m = q.w == tag ? 3 : -1;
   m = q.z == tag ? 2 : m;
@@ -328,7 +333,7 @@ __device__ __forceinline__ void sv_lap(const IterArgs& a, int slot, long long& t
 __device__ __forceinline__ void sv_build_pt(const SvLds& x, const DevSlab& s, const IterArgs& a, int v, int Lp) {
   const SvPt& t = x.pt;
   for (int i = threadIdx.x; i < t.T; i += blockDim.x) t.keys[i] = 0u;
-  for (int i = threadIdx.x; i < t.T + 64; i += blockDim.x) { t.a[i] = 0ull; t.b[i] = 0ull; }
+  for (int i = threadIdx.x; i < 2 * (t.T + 64); i += blockDim.x) t.ab[i] = 0ull;
   if (threadIdx.x < 64) x.misc[threadIdx.x] = 0;
   __syncthreads();
   const int cur = (a.active == 1) ? a.sB : a.sA;
@@ -337,7 +342,7 @@ __device__ __forceinline__ void sv_build_pt(const SvLds& x, const DevSlab& s, co
   for (int i = threadIdx.x; i < len; i += blockDim.x) {
     const int key = s.key(s.ids[r + i]);
     const uint32_t tag = (uint32_t)key + 1u;
-    const uint32_t home = (sv_mix((uint32_t)key) & t.gmask) << 2;
+    const uint32_t home = svpt_home(t, sv_hash(key).h0);
     uint32_t g4 = home;
     for (int n = 0; n <= (int)t.gmask; n++) {  // (T = 4 L slots: a free slot always exists)
       int got = -1;
@@ -387,6 +392,9 @@ __device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, con
                                         FB fb) {
   const int lane = lane_id();
   const int lcl = lane < s.L ? lane : 0;  // (rows narrower than a wave: stay inside the row slot)
+  // second-half lane, clamped inside the row slot (L < 128: lanes past L would read the next row,
+  // past the slab's end for its last row)
+  const int lhi = WAVE + lane < s.L ? WAVE + lane : lcl;
   auto colx_at = [&](int64_t w0) { return w0 + lane < c1 ? g.colx[w0 + lane] : (int32_t)-1; };
   auto len_of = [&](int32_t cx) { return cx == -1 ? 0 : s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)]; };
   auto base_of = [&](int32_t cx) { return cx == -1 ? (int64_t)0 : s.row(read_slot(a, cx), cx & 0x7fffffff); };
@@ -410,27 +418,31 @@ __device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, con
         bt.base[q] = has ? sv_readlane64(base, qq) : (int64_t)0;  // (row 0: a valid address)
         bt.key[2 * q] = s.ids[bt.base[q] + lcl];
         if (kScores) bt.sv[2 * q] = s.sc[bt.base[q] + lcl];
-        if (bt.rl[q] > WAVE) {
-          bt.key[2 * q + 1] = s.ids[bt.base[q] + WAVE + lane];
-          if (kScores) bt.sv[2 * q + 1] = s.sc[bt.base[q] + WAVE + lane];
-        } else {
-          bt.key[2 * q + 1] = 0;
-          if (kScores) bt.sv[2 * q + 1] = 0.0;
-        }
+        // the second half is loaded unconditionally (a row of <= 64 entries re-reads its first
+        // half's lines, and sv_groups skips it): with a load count that does not depend on the
+        // row lengths the compiler's vmcnt waits can count the next batch's loads exactly (a
+        // branch around the load made it merge both paths and wait for half of the prefetch)
+        const int i2 = bt.rl[q] > WAVE ? lhi : lcl;
+        bt.key[2 * q + 1] = s.ids[bt.base[q] + i2];
+        if (kScores) bt.sv[2 * q + 1] = s.sc[bt.base[q] + i2];
       }
     };
     auto run = [&](const SvBatch<NS>& bt) { fb(bt); };
     // two batch buffers in turn (no per-batch copy of one into the other); sched_barrier keeps the
     // next batch's loads ahead of this batch's work without pulling its first uses up
+    // The loads are issued unconditionally (a batch past the window's rows loads row 0 of the slab
+    // and has no valid lane): every path through the loop issues the same loads in the same order,
+    // so the compiler's vmcnt waits count the batch in flight exactly instead of merging in a path
+    // without it (which made it wait for the whole prefetch before the last groups of a batch).
     SvBatch<NS> ba, bb;
     load(0, ba);
     for (int q0 = 0; q0 < nrows; q0 += 2 * NS) {
-      if (q0 + NS < nrows) load(q0 + NS, bb);
+      load(q0 + NS, bb);
       __builtin_amdgcn_sched_barrier(0);
       run(ba);
       __builtin_amdgcn_sched_barrier(0);
       if (q0 + NS >= nrows) break;
-      if (q0 + 2 * NS < nrows) load(q0 + 2 * NS, ba);
+      load(q0 + 2 * NS, ba);
       __builtin_amdgcn_sched_barrier(0);
       run(bb);
       __builtin_amdgcn_sched_barrier(0);
@@ -468,6 +480,14 @@ __device__ __forceinline__ void sv_chunk(int64_t b0, int64_t b1, int64_t& c0, in
 // candidates (round 5: 1344-1355 -> 1337-1338 ms per job against loading every score with its key,
 // which paid before the list, when each inserting group waited for its own score)
 constexpr bool SV_P2_SCORES = PPR_SV_P2_SCORES != 0;
+// timing-only build switches (tools/build_variant.py; round 6: build-time instead of PPR_WHATIF bits,
+// whose per-group test cost pass 2 a branch in every group)
+#ifndef PPR_SV_WALK_ONLY
+#define PPR_SV_WALK_ONLY 0
+#endif
+#ifndef PPR_SV_NO_INSERT
+#define PPR_SV_NO_INSERT 0
+#endif
 // rows per batch in pass 1 (keys and scores) and pass 2 (keys only: a lighter group, so more rows
 // in flight to cover the gather latency); build-time knobs for A/B variants (tools/build_variant.py)
 constexpr int SV_NS1 = PPR_SV_NS1, SV_NS2 = PPR_SV_NS2;
@@ -475,17 +495,16 @@ __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, co
                                          int64_t b0, int64_t b1, double factor, uint32_t* sk) {
   int64_t c0, c1;
   sv_chunk(b0, b1, c0, c1);
-  const double f61 = factor * 0x1p61;
+  const double f61 = factor * 0x1p61, f31 = factor * 0x1p31;
   sv_rows<true, SV_NS1>(g, s, a, c0, c1, [&](const SvBatch<SV_NS1>& bt) {
     sv_groups(bt, [&](int, int key, double sc, bool valid, int64_t) {
-      const uint32_t h = sv_mix((uint32_t)key);
-      const int slot = svpt_slot(x.pt, key, h, valid);
+      const SvHash hs = sv_hash(key);
+      const int slot = svpt_slot(x.pt, key, hs.h0, valid);
       const bool inpt = valid && slot >= 0;
-      const double t = sc * f61;  // p * 2^61, exact (sv_split_t)
       // exec-masked adds (round 5: 1335-1341 -> 1320-1324 ms per job against the branch-free form
       // that sent non-PT lanes to per-lane dummy slots and PT lanes' zero units to the sketch)
-      if (inpt) sv_split_add_t(x.pt.a, x.pt.b, slot, t);
-      if (valid && !inpt) sv_sketch_add(sk, h, sv_units_t(t), x.wlog);
+      if (inpt) sv_split_add_t(x.pt.ab, slot, sc * f61);  // (t = p * 2^61, exact: sv_split_t)
+      if (valid && !inpt) sv_sketch_add(sk, hs, sv_units31(sc * f31), x.wlog);
     });
   });
 }
@@ -506,7 +525,7 @@ __device__ __forceinline__ void sv_pass1(const DevGraph& g, const DevSlab& s, co
 __device__ __forceinline__ void sv_insert(const SvLds& x, const X2Table& xt, const IterArgs& a, bool live, int key,
                                           double t, int budget) {
   const int lane = lane_id();
-  const bool w = live && svpt_slot(x.pt, key, sv_mix((uint32_t)key), live) < 0;
+  const bool w = live && svpt_slot(x.pt, key, sv_hash(key).h0, live) < 0;
   if (!__ballot(w)) return;
   if (a.diag && lane == 0) diag_add(a.diag, 148, 1ull);
   if (__hip_atomic_load(&x.misc[SVM_FILL], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > budget) {
@@ -534,26 +553,40 @@ __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, co
   double* lst = reinterpret_cast<double*>(x.region + (size_t)(xt.mask + 1u) * 20 + (size_t)(threadIdx.x >> 6) * SV_LIST_BYTES);
   int* lsk = reinterpret_cast<int*>(lst + WAVE);
   int nl = 0;  // (wave-uniform) entries in the list
-  auto flush = [&]() {
+  // A full list is flushed in two steps. `issue` moves it into registers (key, and the score gather
+  // from its slab index, in flight) and frees the list; `complete` inserts those entries at the top
+  // of the next batch, after that batch's successor loads were issued. The gather is then never the
+  // youngest load when its result is used, so its wait leaves the walk's prefetch in flight (used
+  // at once, it was: in-order vmcnt made every flush drain the pipeline).
+  int pn = 0;        // (wave-uniform) entries pending
+  int pk = 0;        // this lane's pending key
+  double pt = 0.0;   // its score (or t, with the pass's score loads)
+  auto issue = [&]() {
     wave_fence();
     const bool live = lane < nl;
-    // (without the pass's score loads the list holds each entry's slab index; its score is
-    // gathered here, one memory latency per 64 passing candidates)
-    double t = 0.0;
-    if (live) t = SV_P2_SCORES ? lst[lane] : s.sc[__double_as_longlong(lst[lane])] * f61;
-    sv_insert(x, xt, a, live, live ? lsk[lane] : 0, t, budget);
+    pk = live ? lsk[lane] : 0;
+    if (SV_P2_SCORES) pt = lst[lane];
+    else pt = s.sc[live ? __double_as_longlong(lst[lane]) : 0ll];  // (dead lanes: slab entry 0)
+    pn = nl;
     nl = 0;
     wave_fence();
   };
+  auto complete = [&]() {
+    if (pn) {
+      sv_insert(x, xt, a, lane < pn, pk, SV_P2_SCORES ? pt : pt * f61, budget);
+      pn = 0;
+    }
+  };
   sv_rows<SV_P2_SCORES, SV_NS2>(g, s, a, c0, c1, [&](const SvBatch<SV_NS2>& bt) {
     constexpr int NG = 2 * SV_NS2;
+    complete();
     bool want[NG];
     int tot = 0;
 #pragma unroll
     for (int k = 0; k < NG; k++) want[k] = false;
     sv_groups(bt, [&](int k, int key, double, bool valid, int64_t) {
-      // (PPR_WHATIF 1024, timing only: the walk alone, every key fails the test)
-      want[k] = valid && ((a.whatif & 1024u) ? key == -7 : sv_passes(bm32, sv_mix((uint32_t)key), x.wlog));
+      // (PPR_SV_WALK_ONLY build, timing only: the walk alone, every key fails the test)
+      want[k] = valid && (PPR_SV_WALK_ONLY ? key == -7 : sv_passes(bm32, sv_hash(key), x.wlog));
       tot += __popcll(__ballot(want[k]));
     });
     if (a.diag && lane == 0) {  // (PPR_DIAG: groups walked)
@@ -563,7 +596,7 @@ __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, co
       diag_add(a.diag, 190, (unsigned long long)ng);
     }
     if (__builtin_expect(tot == 0, 1)) return;
-    if (a.whatif & 512u) return;  // (timing only: no insert path)
+    if (PPR_SV_NO_INSERT) return;  // (timing-only build: no insert path)
     if (a.diag && lane == 0) {
       int np = 0;
 #pragma unroll
@@ -571,7 +604,7 @@ __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, co
       diag_add(a.diag, 147, (unsigned long long)np);
     }
     if (PPR_SV_LIST && tot <= WAVE) {
-      if (nl + tot > WAVE) flush();
+      if (nl + tot > WAVE) issue();  // (nothing pending: complete() ran at the top of this batch)
 #pragma unroll
       for (int k = 0; k < NG; k++) {
         const uint64_t m = __ballot(want[k]);
@@ -594,13 +627,17 @@ __device__ __forceinline__ void sv_pass2(const DevGraph& g, const DevSlab& s, co
       sv_insert(x, xt, a, want[k], bt.key[k], sc * f61, budget);
     }
   });
-  if (nl) flush();
+  complete();
+  if (nl) {
+    issue();
+    complete();
+  }
 }
 
 // the self seed (1 - d) of v: into PT when v is a prev key, else into the sketch (pass 1; one thread)
 __device__ __forceinline__ int svpt_slot1(const SvPt& t, int key) {
   const uint32_t tag = (uint32_t)key + 1u;
-  const uint32_t g4 = (sv_mix((uint32_t)key) & t.gmask) << 2;
+  const uint32_t g4 = svpt_home(t, sv_hash(key).h0);
   const uint4 q = *reinterpret_cast<const uint4*>(t.keys + g4);
   if ((q.x & ~SV_OVF_BIT) == tag) return (int)g4;
   if (q.y == tag) return (int)g4 + 1;
@@ -610,12 +647,12 @@ __device__ __forceinline__ int svpt_slot1(const SvPt& t, int key) {
 }
 __device__ __forceinline__ void sv_seed1(const SvLds& x, int v, double seed, uint32_t* sk) {
   const int h = svpt_slot1(x.pt, v);
-  if (h >= 0) sv_split_add(x.pt.a, x.pt.b, h, seed);
-  else sv_sketch_add(sk, sv_mix((uint32_t)v), sv_units(seed), x.wlog);
+  if (h >= 0) sv_split_add(x.pt.ab, h, seed);
+  else sv_sketch_add(sk, sv_hash(v), sv_units(seed), x.wlog);
 }
 // ... and into XT in pass 2 when v is not a prev key and passes
 __device__ __forceinline__ void sv_seed2(const SvLds& x, const X2Table& xt, int v, double seed) {
-  if (svpt_slot1(x.pt, v) >= 0 || !sv_passes(reinterpret_cast<const uint32_t*>(x.bm), sv_mix((uint32_t)v), x.wlog)) return;
+  if (svpt_slot1(x.pt, v) >= 0 || !sv_passes(reinterpret_cast<const uint32_t*>(x.bm), sv_hash(v), x.wlog)) return;
   bool ins;
   const int h = x2_slot(xt, v, ins);
   if (h < 0) { x.misc[SVM_OVF] = 1; return; }
@@ -693,7 +730,7 @@ __device__ __forceinline__ void sv1_source(unsigned char* smem, DevGraph g, DevS
   // bound: the smallest exact total of the L prev keys
   const int Tpt = x.pt.T;
   const double theta = sv_theta(x, Tpt, [&](int i) {
-    return (x.pt.keys[i] & ~SV_OVF_BIT) ? x2_value(x.pt.a[i], x.pt.b[i]) : bitsd(~0ull >> 1);  // (empty: above every value)
+    return (x.pt.keys[i] & ~SV_OVF_BIT) ? x2_value(x.pt.ab[2 * i], x.pt.ab[2 * i + 1]) : bitsd(~0ull >> 1);  // (empty: above every value)
   });
   const uint32_t thr = sv_thr(theta);
   sv_bitmap(x, thr, [&](int c) { return sk[c]; });
@@ -752,7 +789,7 @@ __device__ __forceinline__ void sv1_source(unsigned char* smem, DevGraph g, DevS
     int b0 = 0;
     if (m && lane_id() == 0) b0 = atomicAdd(&x.misc[SVM_U], __popcll(m));
     b0 = __shfl(b0, 0) + __popcll(m & lanemask_lt());
-    if (has) { dv[b0] = x2_value(x.pt.a[i], x.pt.b[i]); dk[b0] = (int)kt - 1; }
+    if (has) { dv[b0] = x2_value(x.pt.ab[2 * i], x.pt.ab[2 * i + 1]); dk[b0] = (int)kt - 1; }
   }
   __syncthreads();
   const int U = x.misc[SVM_U];
@@ -897,7 +934,7 @@ __global__ void __launch_bounds__(SV_THREADS) k_svA(DevGraph g, DevSlab s, IterA
   unsigned long long* gp = gpt + sd.gpt;
   for (int i = threadIdx.x; i < x.pt.T; i += blockDim.x) {
     if (!(x.pt.keys[i] & ~SV_OVF_BIT)) continue;
-    const unsigned long long A = x.pt.a[i], B = x.pt.b[i];
+    const unsigned long long A = x.pt.ab[2 * i], B = x.pt.ab[2 * i + 1];
     const int r = x.pt.pos[i];
     if (A) atomicAdd(&gp[2 * r], A);
     if (B) atomicAdd(&gp[2 * r + 1], B);
