@@ -308,6 +308,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     if (exr && atoi(exr) == 0) p->xroute = false;
     const char* exb = getenv("PPR_XTEST_BADSIZE");
     if (exb) p->xtest_badsize = atoi(exb);
+    const char* exf = getenv("PPR_XTEST_FAIL");
+    if (exf && sscanf(exf, "%d,%d", &p->xtest_fail_rank, &p->xtest_fail_it) != 2) p->xtest_fail_rank = -1;
+    const char* ext = getenv("PPR_XTIMEOUT");
+    if (ext) p->x_timeout_s = std::max(1.0, atof(ext));
     const char* e9e = getenv("PPR_WG_PASSES");  // tests: force workgroup-tier overflows
     if (e9e) p->wg_max_passes = std::max(1, std::min(WG_MAX_PASSES, atoi(e9e)));
     const char* e9d = getenv("PPR_FUSED_MAX");
@@ -409,6 +413,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       const double seed = damping > 0.0 ? (double)std::max<int64_t>(1, maxdeg) / damping : 1.0;
       if ((double)maxdeg + seed >= lim) { plan_free(p); return PPR_ERR_RANGE; }
     }
+    const char* ee = getenv("PPR_XSHARD_ENDS");  // (any summation mode)
+    p->xshard_ends = !(ee && atoi(ee) == 0);
     if (p->xsum) {
       // the order-bound alternatives of the chain path do not apply: no hot pass, no speculative
       // bound, no workgroup tier (its overflow would fall to the chain-order HBM table)
@@ -464,6 +470,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       const char* s6 = getenv("PPR_SV_MID");
       if (s5) p->sv_small = std::max<int64_t>(0, atoll(s5));
       if (s6) p->sv_mid = std::max<int64_t>(0, atoll(s6));
+      const char* ex = getenv("PPR_XR_ORDER");
+      p->xr_big_first = ex && atoi(ex) == 1;
+      const char* eh = getenv("PPR_XH_FIRST");
+      p->xh_first = !(eh && atoi(eh) == 0);
       const char* s7 = getenv("PPR_SV_REDO");
       p->sv_redo_mid = !(s7 && atoi(s7) == 0);
       const char* s9 = getenv("PPR_SV_P2SKIP");
@@ -1527,7 +1537,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       kst_begin(p, 5, sw);
       p->kst_pend_bytes[5] = bytes;
     }
-    static const bool big_first = getenv("PPR_XR_ORDER") && atoi(getenv("PPR_XR_ORDER")) == 1;  // (experiment)
+    const bool big_first = p->xr_big_first;  // (experiment)
     for (int c0 = 0; c0 < 3; c0++) {
       const int c = big_first ? 2 - c0 : c0;
       if (tasks[c].empty()) continue;
@@ -1950,9 +1960,8 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
   // the larger of the two host plannings goes second: when the range engines take more sources
   // than the sieve (the big partition's iterations: ~258 K mid-sized sources at RMAT-22), they are
   // planned and queued first and collected after the sieve's launches (PPR_XH_FIRST=0: sieve first)
-  static const int xh_first = getenv("PPR_XH_FIRST") ? atoi(getenv("PPR_XH_FIRST")) : 1;
   XhDefer df;
-  df.want = xh_first != 0 && src.size() > ssrc.size();
+  df.want = p->xh_first && src.size() > ssrc.size();
   if (df.want) { int r = run_xhubs_list(p, a, src, cand, deg, dest, maxdiff, 0, &df); if (r) return r; }
   if (!ssrc.empty()) { int r = sieve_launch(p, a, ssrc, scand, sdeg, maxdiff, run); if (r) return r; }
   lap(2, tl);  // sieve planning + launches
@@ -2282,8 +2291,8 @@ static int init_dangling(ppr_plan* p, const int32_t* list, int64_t cnt) {
   if (cnt <= 0) return PPR_OK;
   const int64_t th = cnt * NRANGE;
   const double seed = p->xsum ? xs_single_host(1.0 - p->damping, XS_F) : 1.0 - p->damping;
-  hipLaunchKernelGGL(k_init_dangling, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, p->stream, dev_slab(p), list, cnt,
-                     seed);
+  hipLaunchKernelGGL(k_init_dangling, dim3((unsigned)std::min<int64_t>((th + 255) / 256, 1 << 20)), dim3(256), 0,
+                     p->stream, dev_slab(p), list, cnt, seed);
   HIP_OK(hipGetLastError());
   return PPR_OK;
 }
@@ -2768,6 +2777,42 @@ struct LocalGroup {
   void fail() { std::lock_guard<std::mutex> lk(mu); failed = true; cv.notify_all(); }
 };
 
+// Waits of the sharded loops. With an RCCL communicator a peer that failed never posts its side of
+// a collective, and the RCCL kernels waiting for it would spin forever (a blocking sync with them):
+// these waits poll instead and give up when RCCL reports an asynchronous error or after
+// x_timeout_s seconds (PPR_XTIMEOUT) without the stream finishing. The loops' error path then
+// aborts the communicator (x_abort), which also releases this rank's RCCL kernels; every peer
+// leaves the same way, by its own error or its own time limit. Without a communicator (one rank,
+// or the in-process LocalGroup, whose barriers carry the failure) a wait is a plain sync.
+static int x_sync(ppr_plan* p, hipStream_t s) {
+  if (!p->comm) { HIP_OK(hipStreamSynchronize(s)); return PPR_OK; }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return PPR_OK;
+    if (e != hipErrorNotReady) return PPR_ERR_HIP;
+    ncclResult_t ae = ncclSuccess;
+    if (ncclCommGetAsyncError(p->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+      return PPR_ERR_HIP;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > p->x_timeout_s)
+      return PPR_ERR_HIP;
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+static int x_sync_event(ppr_plan* p, hipEvent_t ev) {
+  if (!p->comm) { HIP_OK(hipEventSynchronize(ev)); return PPR_OK; }
+  HIP_OK(hipStreamWaitEvent(p->stream, ev, 0));
+  return x_sync(p, p->stream);
+}
+// a failed sharded run on an RCCL communicator: abort it (its peers' waits end by their own error
+// or time limit); the plan needs ppr_grank_plan_comm_init again before the next sharded run
+static void x_abort(ppr_plan* p) {
+  if (p->comm) {
+    ncclCommAbort(p->comm);
+    p->comm = nullptr;
+  }
+}
+
 // every non-empty rank's block (its d_xsend, sz[r] bytes) into d_xrecv + xo[r] of every other rank
 static int x_blocks(ppr_plan* p, const std::vector<int64_t>& b, const std::vector<int64_t>& sz,
                     const std::vector<size_t>& xo, hipStream_t s) {
@@ -2997,7 +3042,8 @@ static int x_exchange_routed(ppr_plan* p, uint32_t it, const XRoute& xr, int slo
     const ncclResult_t ne = ncclGroupEnd();  // (always closed, whatever failed inside)
     if (nr != ncclSuccess || ne != ncclSuccess) return PPR_ERR_HIP;
     HIP_OK(hipMemcpyAsync(hsz.data(), tx, 16 * (size_t)W, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
+    rc = x_sync(p, s);
+    if (rc) return rc;
     int32_t* okd = reinterpret_cast<int32_t*>(rx + W);  // (d_xsz holds 2 W + 1 words)
     int32_t mine_ok = 1;
     for (int d = 0; d < W; d++)
@@ -3005,7 +3051,8 @@ static int x_exchange_routed(ppr_plan* p, uint32_t it, const XRoute& xr, int slo
     HIP_OK(hipMemcpyAsync(okd, &mine_ok, 4, hipMemcpyHostToDevice, s));
     NCCL_OK(ncclAllReduce(okd, okd, 1, ncclInt32, ncclMin, p->comm, s));
     HIP_OK(hipMemcpyAsync(&mine_ok, okd, 4, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
+    rc = x_sync(p, s);
+    if (rc) return rc;
     if (!mine_ok) return PPR_ERR_RANGE;  // every rank saw the same minimum: none posts a block
     nr = ncclGroupStart();
     for (int d = 0; d < W && nr == ncclSuccess; d++) {
@@ -3154,9 +3201,7 @@ extern "C" int ppr_grank_plan_ends_time(ppr_plan* p, int32_t world, int32_t rank
   return probe_take();
 }
 
-extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance,
-                                          ppr_stats* st) {
-  if (!p) return PPR_ERR_ARG;
+static int run_sharded_impl(ppr_plan* p, uint32_t iterations, double tolerance, ppr_stats* st) {
   if (iterations == 0) return PPR_ERR_ITERS;
   if (p->nranks > 1 && !p->comm && !p->lgroup) return PPR_ERR_ARG;
   HIP_OK(hipSetDevice(p->device));
@@ -3177,8 +3222,7 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
   // and the K-wide rows are all-gathered. Without them every rank inits every source, and the
   // result rows of both partitions are broadcast L-wide so that every rank's top-K reads every row.
   const bool route = p->nranks > 1 && p->nranks <= 32 && p->xroute;
-  static const bool ends_env = !(getenv("PPR_XSHARD_ENDS") && atoi(getenv("PPR_XSHARD_ENDS")) == 0);
-  const bool shard_ends = route && ends_env;
+  const bool shard_ends = route && p->xshard_ends;
   XRoute xr;
   int rc = PPR_OK;
   if (route) { rc = xroute_build(p, bd, xr); if (rc) return rc; }
@@ -3190,11 +3234,14 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
     const std::vector<int64_t>& b = bd[it & 1];
     rc = ppr_grank_plan_iterate(p, (int32_t)it, b[p->rank], b[p->rank + 1]);
     if (rc) return rc;
+    if (p->rank == p->xtest_fail_rank && (int)it == p->xtest_fail_it) return PPR_ERR_HIP;  // (tests)
     unsigned long long* mdp = p->d_maxdiff + (it < PPR_MAX_ITER_STATS ? it : PPR_MAX_ITER_STATS);
     if (p->nranks > 1) {
       rc = route ? x_exchange_routed(p, it, xr) : x_exchange_bulk(p, it, bd[it & 1]);
       if (rc) return rc;
       rc = x_allreduce_max(p, mdp, s);
+      if (rc) return rc;
+      rc = x_sync(p, s);  // (a stuck collective is found here, before any blocking wait of the next merge)
       if (rc) return rc;
     }
     if (tolerance > 0) {  // (the all-reduced value: every rank takes the same stop decision)
@@ -3206,6 +3253,8 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
     }
   }
   if (shard_ends) {
+    rc = x_sync(p, s);  // (init / last exchange)
+    if (rc) return rc;
     rc = launch_topk(p, ((it + 1) / 2) & 1, (it / 2) & 1, p->d_xowner, p->rank);
     if (rc) return rc;
     for (int q = 0; q < 2; q++) {
@@ -3222,11 +3271,14 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
         rc = x_exchange_bulk(p, (uint32_t)last, bd[q]);
         if (rc) return rc;
       }
+    rc = x_sync(p, s);
+    if (rc) return rc;
     rc = ppr_grank_plan_finish(p, (int32_t)it);
     if (rc) return rc;
   }
   HIP_OK(hipEventRecord(p->ev_b, s));
-  HIP_OK(hipEventSynchronize(p->ev_b));
+  rc = x_sync_event(p, p->ev_b);
+  if (rc) return rc;
   if (st) {
     rc = read_maxdiff_history(p, it, st);
     if (rc) return rc;
@@ -3243,6 +3295,16 @@ extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, doub
     st->merge_launches = p->merge_launches;
   }
   return PPR_OK;
+}
+
+// A failing rank aborts its RCCL communicator (x_abort): its peers' waits end by their own errors or
+// time limits (x_sync) instead of waiting forever for a rank that left
+extern "C" int ppr_grank_plan_run_sharded(ppr_plan* p, uint32_t iterations, double tolerance,
+                                          ppr_stats* st) {
+  if (!p) return PPR_ERR_ARG;
+  const int rc = run_sharded_impl(p, iterations, tolerance, st);
+  if (rc) x_abort(p);
+  return rc;
 }
 
 extern "C" int ppr_grank_plan_exchange_bytes(ppr_plan* p, int64_t* recv_bytes, int64_t* rows_sent) {
@@ -3303,7 +3365,8 @@ static int x_allgather_i64(ppr_plan* p, const int64_t* d_val, std::vector<int64_
   int64_t* all = reinterpret_cast<int64_t*>(p->d_xsz);
   NCCL_OK(ncclAllGather(d_val, all, 1, ncclInt64, p->comm, s));
   HIP_OK(hipMemcpyAsync(out.data(), all, 8 * (size_t)W, hipMemcpyDeviceToHost, s));
-  HIP_OK(hipStreamSynchronize(s));
+  rc = x_sync(p, s);
+  if (rc) return rc;
   return PPR_OK;
 }
 
@@ -3337,6 +3400,7 @@ static int mc_run_sharded(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_sta
   for (int r = 0; r <= W; r++) b[r] = p->mc_nwalk * r / W;
   int rc = ppr_mccp2_plan_walk(p, walks, seed, b[me], b[me + 1]);
   if (rc) return rc;
+  if (me == p->xtest_fail_rank && p->xtest_fail_it == 0) return PPR_ERR_HIP;  // (tests)
   if (W > 1) {
     int64_t rb = 0;
     ppr_grank_plan_row_bytes(p, &rb);
@@ -3360,6 +3424,8 @@ static int mc_run_sharded(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_sta
     p->x_bytes += (int64_t)xo[W];
     p->x_rows_sent += mine;
     rc = x_blocks(p, b, sz, xo, s);
+    if (rc) return rc;
+    rc = x_sync(p, s);
     if (rc) return rc;
     for (int r = 0; r < W; r++) {
       if (r == me || b[r + 1] == b[r]) continue;
@@ -3392,7 +3458,9 @@ static int mc_run_sharded(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_sta
 }
 
 extern "C" int ppr_mccp2_plan_run_sharded(ppr_plan* p, uint32_t walks, uint64_t seed, ppr_mc_stats* st) {
-  return mc_run_sharded(p, walks, seed, st);
+  const int rc = mc_run_sharded(p, walks, seed, st);
+  if (rc && p) x_abort(p);
+  return rc;
 }
 
 // Test entry: the sharded MC job with n MC plans of this process as the ranks (LocalGroup)

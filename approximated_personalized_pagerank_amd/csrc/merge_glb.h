@@ -176,9 +176,7 @@ __global__ void __launch_bounds__(256) k_topk(DevSlab s, const uint8_t* part, in
 // (finish_source, unit mode), with its row minimum and 64-range index. One thread per (node,
 // range): no table, no select -- the merge engines spent as long on these 52 % of RMAT-22's nodes
 // as on all the others' init.
-__global__ void k_init_dangling(DevSlab s, const int32_t* list, int64_t cnt, double seed) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= cnt * NRANGE) return;
+__device__ __forceinline__ void init_dangling_one(DevSlab s, const int32_t* list, int64_t t, double seed) {
   const int64_t v = list[t / NRANGE];
   const int q = (int)(t % NRANGE);
   const uint16_t x = row_range((int)v) <= (uint32_t)q ? 1 : 0;
@@ -193,6 +191,12 @@ __global__ void k_init_dangling(DevSlab s, const int32_t* list, int64_t cnt, dou
       s.rmin[s.lrow(sl, v)] = seed;
     }
   }
+}
+// (grid-stride: cnt * NRANGE work items pass 2^32 at 2^26 nodes)
+__global__ void k_init_dangling(DevSlab s, const int32_t* list, int64_t cnt, double seed) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < cnt * NRANGE;
+       t += (int64_t)gridDim.x * blockDim.x)
+    init_dangling_one(s, list, t, seed);
 }
 
 // Row exchange for source sharding: one compact block per active-list range of `count` rows (the

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -58,11 +59,12 @@ __global__ void k_cc_jump(int32_t* lab, int64_t n) {
   lab[v] = l;
 }
 
-// source node of every edge (for the one-thread-per-edge passes)
+// source node of every edge (for the one-thread-per-edge passes): one wave per node, grid-stride
+// (a wave per node in one grid passed the 2^32 work-item limit at n >= 2^26)
 __global__ void k_edge_src(const int64_t* rp, int64_t n, int32_t* src) {
-  const int64_t v = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  if (v >= n) return;
-  for (int64_t e = rp[v] + (threadIdx.x & 63); e < rp[v + 1]; e += 64) src[e] = (int32_t)v;
+  const int64_t W = (int64_t)gridDim.x * (blockDim.x / 64);
+  for (int64_t v = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); v < n; v += W)
+    for (int64_t e = rp[v] + (threadIdx.x & 63); e < rp[v + 1]; e += 64) src[e] = (int32_t)v;
 }
 
 __global__ void k_bfs_roots(const int32_t* lab, int64_t n, int32_t* depth) {
@@ -118,9 +120,13 @@ __global__ void k_col_mark(int32_t* col, int64_t m, const uint8_t* part) {
 int partitions_core(const int64_t* d_rp, int32_t* d_col, int64_t n, int64_t m, uint8_t* d_part, uint8_t* h_part,
                     bool mark, int32_t* d_src, int32_t* d_lab, int32_t* d_depth, int32_t* d_flag, hipStream_t st) {
   constexpr int CC_ROUNDS = 64, BFS_LEVELS = 512;
+  // one thread per node / edge in the passes below: past 2^32 work items the launches would fail,
+  // so such graphs take the host BFS (PPR_ERR_RANGE, like a graph that needs too many rounds)
+  if (n > (int64_t)UINT32_MAX - 256 || m > (int64_t)UINT32_MAX - 256) return PPR_ERR_RANGE;
   const unsigned bn = (unsigned)((n + 255) / 256), bm = (unsigned)((m + 255) / 256);
   int32_t h[2] = {0, 0};
-  hipLaunchKernelGGL(k_edge_src, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, d_rp, n, d_src);
+  hipLaunchKernelGGL(k_edge_src, dim3((unsigned)std::min<int64_t>((n + 3) / 4, 1 << 16)), dim3(256), 0, st, d_rp, n,
+                     d_src);
   hipLaunchKernelGGL(k_cc_init, dim3(bn), dim3(256), 0, st, d_lab, n);
   PP_OK(hipGetLastError());
   {

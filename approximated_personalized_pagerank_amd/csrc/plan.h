@@ -125,6 +125,8 @@ struct ppr_plan {
   int hub_slice = 8192;            // PPR_HUB_SLICE: k_hub_reduce slice (>= L)
   // source sharding (ppr_grank_plan_comm_init / ppr_grank_plan_run_sharded)
   ncclComm_t comm = nullptr;
+  double x_timeout_s = 600.0;        // PPR_XTIMEOUT: seconds an RCCL wait may go without progress (x_sync)
+  int xtest_fail_rank = -1, xtest_fail_it = -1;  // PPR_XTEST_FAIL="rank,it" (tests): that rank fails there
   struct LocalGroup* lgroup = nullptr;  // tests: the ranks are plans of this process (grank.hip)
   int nranks = 1, rank = 0;
   std::vector<double> work[2];        // per active source: merge work estimate (list order)
@@ -226,6 +228,10 @@ struct ppr_plan {
   // sieve merge of the wide exact-sum sources (merge_sv.h): PPR_SV=0 turns it off
   bool sv_enabled = false;
   int64_t sv_slice = 1LL << 19;       // PPR_SV_SLICE: candidates per slice workgroup (round-5 sweep: 2^18 -> 2^19, -1.6 %)
+  // read per plan in plan_alloc (a process may switch them between plans; tests cover both ways)
+  bool xr_big_first = false;          // PPR_XR_ORDER=1: range tasks largest source first (experiment)
+  bool xh_first = true;               // PPR_XH_FIRST: range engines planned and queued before the sieve
+  bool xshard_ends = true;            // PPR_XSHARD_ENDS: sharded init and K-wide top-K (routed exchange)
   int64_t sv_min = 4096;              // PPR_SV_MIN: sources with fewer candidates keep the range engines
                                       // (measured: 4096 beats 0 by 2-3 % -- the smallest sources overflow the
                                       // 4-wave class's sketch and were handed back -- and 16384 by 5 %)

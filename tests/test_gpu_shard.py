@@ -223,3 +223,79 @@ def test_gpu_routed_exchange_size_mismatch_fails_every_rank(bad, monkeypatch):
     assert time.time() - t0 < 60.0
     for pl in plans:
         pl.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rank,it", [(1, 0), (2, 5), (0, 11)])
+def test_gpu_failing_rank_releases_every_rank(rank, it, monkeypatch):
+    """a rank that fails inside the sharded loop (PPR_XTEST_FAIL="rank,it": that
+    rank returns an error right after its merge of iteration it, before the exchange) must not
+    strand its peers: every rank returns, promptly and with an error. Over RCCL the failing rank
+    aborts its communicator and the peers' polling waits end (x_sync); in the in-process group the
+    failure releases the barriers. Then the same plans run a clean job again, bit-exact."""
+    import time
+    import approximated_personalized_pagerank_amd as ppr
+    from approximated_personalized_pagerank_amd.shard import run_local_group
+    g = ppr.rmat(12, seed=5)
+    part = g.partitions()
+    monkeypatch.setenv("PPR_XTEST_FAIL", f"{rank},{it}")
+    plans = [ppr.GrankPlan(g, 16, 32, 0.85, part=part, device=0) for _ in range(3)]
+    t0 = time.time()
+    with pytest.raises(ppr.PprError):
+        run_local_group(plans, 16, -1.0)
+    assert time.time() - t0 < 60.0
+    for pl in plans:
+        pl.close()
+    monkeypatch.delenv("PPR_XTEST_FAIL")
+    ref = ppr.GrankPlan(g, 16, 32, 0.85, part=part, device=0)
+    ref.run(16, -1.0)
+    one = ref.fetch()
+    ref.close()
+    plans = [ppr.GrankPlan(g, 16, 32, 0.85, part=part, device=0) for _ in range(3)]
+    run_local_group(plans, 16, -1.0)
+    for pl in plans:
+        r = pl.fetch()
+        assert np.array_equal(r.ids, one.ids) and np.array_equal(r.scores.view(np.int64), one.scores.view(np.int64))
+        pl.close()
+
+
+@pytest.mark.gpu
+def test_gpu_failing_rank_releases_every_rank_mc(monkeypatch):
+    """The MC job's sharded loop likewise: rank 1 fails after its walks, before the walk-basket
+    all-gather; every rank returns with an error instead of waiting for it."""
+    import time
+    import approximated_personalized_pagerank_amd as ppr
+    from approximated_personalized_pagerank_amd.shard import run_local_group_mc
+    g = ppr.rmat(10, seed=2)
+    monkeypatch.setenv("PPR_XTEST_FAIL", "1,0")
+    plans = [ppr.MccpPlan(g, 8, 32, 0.85, device=0) for _ in range(3)]
+    t0 = time.time()
+    with pytest.raises(ppr.PprError):
+        run_local_group_mc(plans, 100, 5)
+    assert time.time() - t0 < 60.0
+    for pl in plans:
+        pl.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("var", ["PPR_XSHARD_ENDS", "PPR_XH_FIRST"])
+def test_gpu_local_group_knobs_off_bit_exact(var, monkeypatch):
+    """the non-sharded ends (x_exchange_bulk + a full top-K on every rank) and the
+    sieve-first ordering are read per plan now, so a process can switch them: each off, LocalGroup
+    world 3 equals the one-GPU run bit for bit."""
+    import approximated_personalized_pagerank_amd as ppr
+    from approximated_personalized_pagerank_amd.shard import run_local_group
+    g = ppr.rmat(13, seed=7)
+    part = g.partitions()
+    ref = ppr.GrankPlan(g, 32, 64, 0.85, part=part, device=0)
+    ref.run(12, -1.0)
+    one = ref.fetch()
+    ref.close()
+    monkeypatch.setenv(var, "0")
+    plans = [ppr.GrankPlan(g, 32, 64, 0.85, part=part, device=0) for _ in range(3)]
+    run_local_group(plans, 12, -1.0)
+    for pl in plans:
+        r = pl.fetch()
+        assert np.array_equal(r.lens, one.lens)
+        assert np.array_equal(r.ids, one.ids) and np.array_equal(r.scores.view(np.int64), one.scores.view(np.int64))
+        pl.close()
