@@ -48,6 +48,7 @@
 #include "merge_hot.h"
 #include "merge_xs.h"
 #include "merge_sv.h"
+#include "merge_xm.h"
 #include "merge_xg.h"
 
 using namespace pprk;
@@ -308,6 +309,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     if (exr && atoi(exr) == 0) p->xroute = false;
     const char* exb = getenv("PPR_XTEST_BADSIZE");
     if (exb) p->xtest_badsize = atoi(exb);
+    const char* erp = getenv("PPR_TEST_RANK_PERMUTE");
+    p->rank_permute = erp && atoi(erp) != 0;
     const char* exf = getenv("PPR_XTEST_FAIL");
     if (exf && sscanf(exf, "%d,%d", &p->xtest_fail_rank, &p->xtest_fail_it) != 2) p->xtest_fail_rank = -1;
     const char* ext = getenv("PPR_XTIMEOUT");
@@ -470,6 +473,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       const char* s6 = getenv("PPR_SV_MID");
       if (s5) p->sv_small = std::max<int64_t>(0, atoll(s5));
       if (s6) p->sv_mid = std::max<int64_t>(0, atoll(s6));
+      const char* exm = getenv("PPR_XM");  // one-range sources of the smallest class: k_xm (1) or k_xr (0, default:
+      p->xm = exm && atoi(exm) == 1;       // k_xm measured 2.8 % slower per job)
       const char* ex = getenv("PPR_XR_ORDER");
       p->xr_big_first = ex && atoi(ex) == 1;
       const char* eh = getenv("PPR_XH_FIRST");
@@ -525,6 +530,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         {(const void*)k_hub_join, "k_hub_join"},
         {(const void*)k_merge_lds_x, "k_merge_lds_x"},
         {(const void*)k_xr, "k_xr"},
+        {(const void*)k_xm<4>, "k_xm<4>"},
         {(const void*)k_xb, "k_xb"},
         {(const void*)k_xfinal<XDesc>, "k_xfinal<XDesc>"},
         {(const void*)k_xfinal<HubDesc>, "k_xfinal<HubDesc>"},
@@ -758,7 +764,8 @@ static IterArgs iter_args(const ppr_plan* p, int it, bool unit) {
   a.stats = (p->flags & PPR_FLAG_STATS) ? 1u : 0u;
   a.lds_rank = p->lds_rank;
   a.nt = (uint32_t)p->nt_loads;
-  a.whatif = ((uint32_t)p->whatif & 0xffffu) | (p->sv_p2skip ? 0u : WI_SV_NO_P2SKIP);
+  a.whatif = ((uint32_t)p->whatif & 0xffffu) | (p->sv_p2skip ? 0u : WI_SV_NO_P2SKIP) |
+             (p->rank_permute ? WI_RANK_PERMUTE : 0u);
   a.iter = unit ? -1 : it;
   a.spec = (unit || p->hot_cap > 0 || it < p->spec_from) ? 0.0 : p->spec_ratio;
   a.xs = p->xsum ? 1u : 0u;
@@ -1473,6 +1480,18 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
   int64_t nmulti = 0;
   for (const XDesc& x : xd) nmulti += x.R > 1;
   const size_t nx = xd.size();
+  // the 2048-slot class's one-range sources on k_xm (merge_xm.h): self-contained task records;
+  // init (unit) merges and baskets wider than 128 keep k_xr
+  const bool use_xm = p->xm && !a.unit && p->Lp <= 2 * WAVE && xm_lds_bytes(cls[0].T) <= 160 * 1024;
+  std::vector<XmTask> xmt;
+  if (use_xm) {
+    xmt.reserve(tasks[0].size());
+    for (const XTask& t : tasks[0]) {
+      const XDesc& x = xd[(size_t)t.d];
+      xmt.push_back(XmTask{x.pt_off, x.factor, x.selfval, t.d, x.v});
+    }
+    tasks[0].clear();
+  }
   size_t ntask = 0;
   for (int c = 0; c < 3; c++) ntask += tasks[c].size();
   // device scratch: descriptors | tasks | list keys | list scores | pc | dsum | oflag | ovl | xtau
@@ -1480,6 +1499,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
   size_t off = 0;
   const size_t o_d = off;  off = al(off + sizeof(XDesc) * (nx + 1));
   const size_t o_t = off;  off = al(off + sizeof(XTask) * (ntask + 1));
+  const size_t o_m = off;  off = al(off + sizeof(XmTask) * (xmt.size() + 1));
   const size_t o_k = off;  off = al(off + 4 * (size_t)(pt + 1));
   const size_t o_s = off;  off = al(off + 8 * (size_t)(pt + 1));
   const size_t o_z = off;  // zeroed together: pc | dsum | oflag | ovl | xtau
@@ -1506,7 +1526,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
     int32_t* d_ov = (int32_t*)(b + o_ov);
     unsigned long long* d_xt = (unsigned long long*)(b + o_xt);
     // descriptors and tasks through the pinned staging buffer (one upload)
-    const size_t up = o_t + sizeof(XTask) * ntask;
+    const size_t up = o_m + sizeof(XmTask) * xmt.size();
     {
       // (its own pinned buffer: run_hubs below restages h_desc_pin while this upload may be pending;
       // the previous upload from it completed at the last call's closing sync of sw)
@@ -1515,6 +1535,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
     }
     unsigned char* hb = (unsigned char*)p->h_xs_pin;
     std::memcpy(hb + o_d, xd.data(), sizeof(XDesc) * nx);
+    if (!xmt.empty()) std::memcpy(hb + o_m, xmt.data(), sizeof(XmTask) * xmt.size());
     size_t tofs[3];
     {
       size_t k = 0;
@@ -1538,6 +1559,15 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       p->kst_pend_bytes[5] = bytes;
     }
     const bool big_first = p->xr_big_first;  // (experiment)
+    if (!xmt.empty()) {
+      const int T = cls[0].T, W = cls[0].W;
+      const int budget = p->xr_budget_over ? 2 * T : std::min(T * 85 / 100, T - W * WAVE - WAVE);
+      // (4 waves: 8 waves at 3 workgroups per CU would need more than 80 VGPRs)
+      hipLaunchKernelGGL(k_xm<4>, dim3((unsigned)xmt.size()), dim3(64 * 4), xm_lds_bytes(T), sw, g, s, a,
+                         (const XmTask*)(b + o_m), T, budget, d_pk, d_ps, d_pc, d_ds, d_of, d_ov);
+      HIP_OK(hipGetLastError());
+      p->merge_launches++;
+    }
     for (int c0 = 0; c0 < 3; c0++) {
       const int c = big_first ? 2 - c0 : c0;
       if (tasks[c].empty()) continue;

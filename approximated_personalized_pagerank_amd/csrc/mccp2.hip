@@ -179,7 +179,7 @@ extern "C" int ppr_mccp2_plan_combine(ppr_plan* p) {
   a.diag = p->d_diag;
   a.lds_rank = p->lds_rank;
   a.nt = (uint32_t)p->nt_loads;
-  a.whatif = (uint32_t)p->whatif & 0xffffu;
+  a.whatif = ((uint32_t)p->whatif & 0xffffu) | (p->rank_permute ? WI_RANK_PERMUTE : 0u);
   a.iter = -1;
   a.spec = 0.0;
   const int64_t nl = (int64_t)p->mc_level_off.size() - 1;

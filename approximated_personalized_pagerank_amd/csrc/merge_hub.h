@@ -44,9 +44,9 @@ constexpr int HUB_SLICE = 8192;       // k_hub_reduce: appended entries per redu
 
 
 // wave bucket LDS: acc f64[T] | keys i32[T] | cnt u16[T] | vals f64[CHUNK] | touched u16[CHUNK] |
-// tof u16[CHUNK + 2]; the radix histogram of the final select (1 KB) aliases vals
+// tof u16[CHUNK + 2] | ord u32[CHUNK]; the radix histogram of the final select (1 KB) aliases vals
 __host__ __device__ constexpr size_t hub_wave_lds(int T, int ng) {  // 16-B multiple: acc stays aligned
-  return ((size_t)T * 16 + ((size_t)(ng * WAVE) * 12 > 1024 ? (size_t)(ng * WAVE) * 12 : 1024) + 4 + 15) & ~(size_t)15;
+  return ((size_t)T * 16 + ((size_t)(ng * WAVE) * 16 > 1024 ? (size_t)(ng * WAVE) * 16 : 1024) + 4 + 15) & ~(size_t)15;
 }
 
 struct HubDesc {
@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(256) k_hub_count(DevGraph g, DevSlab s, IterAr
 }
 
 template <bool HK>
-__global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, IterArgs a,
+__global__ void __launch_bounds__(256, 5) k_hub_scatter(DevGraph g, DevSlab s, IterArgs a,
                                                      const HubDesc* desc, const HubTask* tasks,
                                                      int64_t ntasks, int maxP, const int32_t* cm,
                                                      HubRec* st) {
@@ -235,8 +235,18 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
   HubRec* stv = st + base0;
   uint8_t* fl = smem + (size_t)(blockDim.x >> 6) * maxP * 4 + (size_t)wv * HUB_WALK_FLAGS;
   const bool hotp = d.hot >= 0;
-  const bool ordered = a.lds_rank != 0;
-  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid0, int id, double sv, bool) {
+#ifndef PPR_SCATTER_ORDERED
+#define PPR_SCATTER_ORDERED 1
+#endif
+#ifndef PPR_SCATTER_ANYROW
+#define PPR_SCATTER_ANYROW 0  // (A/B timing only: one add for every group, as before round 6)
+#endif
+#ifndef PPR_SCATTER_ROWS
+#define PPR_SCATTER_ROWS 4
+#endif
+  constexpr int SCAT_ROWS = PPR_SCATTER_ROWS;  // most baskets a group may span and still take the adds
+  const bool ordered = PPR_SCATTER_ORDERED && a.lds_rank != 0;
+  hub_tile_walk(g, s, a, d.v, tk.x, d.tw, fl, [&](bool valid0, int id, double sv, bool one_row, int rr, int nr) {
     const bool valid = valid0 && (id >= 0 || !hotp);  // with a hot pass: cold keys only
     const int key = valid ? s.keyd<HK>(id) : 0;
     const uint32_t dg = valid ? hub_digit(key, d.logP) : 0u;
@@ -245,10 +255,26 @@ __global__ void __launch_bounds__(256) k_hub_scatter(DevGraph g, DevSlab s, Iter
       if (valid && key == -5 && sv == -1.0) stv[0] = hub_rec(key, sv);
       return;
     }
-    if (ordered) {
-      // lane-ordered LDS atomics (probed per plan, k_probe_lds_rank): same-digit lanes get their
-      // run positions in lane order, i.e. stream order -- the stable rank in one instruction
-      uint32_t pos = valid ? atomicAdd(&run[dg], 1u) : 0u;
+    // The atomic ranks need no particular service order among lanes whose keys are distinct: a
+    // stable partition only has to keep each KEY's contributions in stream order, and across
+    // instructions program order does. The candidates of one successor basket have distinct keys,
+    // so a group spanning up to SCAT_ROWS baskets takes one returning add per basket (exec-masked,
+    // in basket order); wider groups take the ballot ranks. No result depends on the order in
+    // which the LDS serves same-address atomics (round 6; before, on the per-plan probe alone).
+    if (ordered && (nr <= SCAT_ROWS || PPR_SCATTER_ANYROW)) {
+      uint32_t pos = 0u;
+      const int nrr = PPR_SCATTER_ANYROW ? 1 : nr;
+      for (int r = 0; r < nrr; r++) {
+        const bool mine = valid && (PPR_SCATTER_ANYROW || rr == r);
+        if (!(a.whatif & WI_RANK_PERMUTE)) {
+          if (mine) pos = atomicAdd(&run[dg], 1u);
+        } else {  // (tests: odd lanes first)
+          if (mine && (lane_id() & 1)) pos = atomicAdd(&run[dg], 1u);
+          wave_fence();
+          if (mine && !(lane_id() & 1)) pos = atomicAdd(&run[dg], 1u);
+        }
+        wave_fence();
+      }
       if (a.whatif & WI_SCAT_COALESCED) {  // (timing only: the same records stored lane-contiguously)
         const uint64_t vm = __ballot(valid);
         if (!vm) return;
@@ -343,12 +369,15 @@ struct BucketWave {
   uint32_t* hist;
   int T, budget, fill;
   bool overflow;
-  bool ordered;  // lane-ordered LDS atomics (IterArgs::lds_rank)
+  bool ordered;  // lane-ordered LDS atomics (IterArgs::lds_rank), verified where used (chunk_accumulate)
+  bool permute;  // (tests) WI_RANK_PERMUTE
 
   // T: any multiple of 64 (slots by multiply-shift of the key hash, linear probing with wrap)
-  __device__ __forceinline__ void setup(unsigned char* base, int T_, int NG, bool ordered_, int budget_ = -1) {
+  __device__ __forceinline__ void setup(unsigned char* base, int T_, int NG, bool ordered_, int budget_ = -1,
+                                        bool permute_ = false) {
     T = T_;
     ordered = ordered_;
+    permute = permute_;
     t.acc = reinterpret_cast<double*>(base);
     t.keys = reinterpret_cast<int*>(base + (size_t)T * 8);
     t.mask = (uint32_t)T - 1;
@@ -357,6 +386,7 @@ struct BucketWave {
     ck.vals = reinterpret_cast<double*>(base + (size_t)T * 16);
     ck.touched = reinterpret_cast<uint16_t*>(base + (size_t)T * 16 + (size_t)(NG * WAVE) * 8);
     ck.tof = ck.touched + NG * WAVE;
+    ck.ord = ck.tof + NG * WAVE + 2;  // (tof holds NG * 64 + 1)
     hist = reinterpret_cast<uint32_t*>(ck.vals);  // final select only (after accumulation)
     budget = budget_ > 0 ? budget_ : T / 4 * 3;
     fill = 0;
@@ -434,7 +464,7 @@ struct BucketWave {
       t1 = (long long)clock64();
       ph[2] += (unsigned long long)(t1 - (long long)ph[8]);
     }
-    chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor, ordered, ph);
+    chunk_accumulate<NG>(t.acc, ck, t.nbits, cv, sl, cs, factor, ordered, ph, permute);
     if (ph) {
       const int z = t.keys[0];  // wait for the chains' LDS traffic before reading the clock
       if (z == 0x7ffffffe) wave_fence();
@@ -555,6 +585,10 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
   double* vals = reinterpret_cast<double*>(base + (size_t)T * 8);
   uint16_t* listed = reinterpret_cast<uint16_t*>(base + (size_t)T * 8 + (size_t)BW2_CAP * 8);
   uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 8 + (size_t)BW2_CAP * 10);
+  // stream positions of the values (P3, P4: verifies the occurrence order; the select's histogram,
+  // used only after P4, occupies the same 1 KB)
+  uint16_t* ord = reinterpret_cast<uint16_t*>(hist);
+  static_assert(BW2_CAP * 2 <= 1024, "one-shot positions alias the select histogram");
   constexpr uint32_t EMPTYK = 0xffffffffu;  // (keys are >= 0)
   const int ng = (nb + WAVE - 1) / WAVE;  // (uniform) groups holding records
   int kk[BW2_GROUPS];
@@ -621,8 +655,16 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     }
     if (__ballot(lost)) return false;
     wave_fence();
-    // occurrence indices: one returning add for the whole group, same-slot lanes in lane order
-    occ[k] = v ? atomicAdd(&cnt[h], 1u) : 0u;
+    // occurrence indices: one returning add for the whole group, same-slot lanes in the hardware's
+    // order (lane order where probed; P4 verifies it)
+    occ[k] = 0u;
+    if (!(a.whatif & WI_RANK_PERMUTE)) {
+      if (v) occ[k] = atomicAdd(&cnt[h], 1u);
+    } else {  // (tests: odd lanes first)
+      if (v && (l & 1)) occ[k] = atomicAdd(&cnt[h], 1u);
+      wave_fence();
+      if (v && !(l & 1)) occ[k] = atomicAdd(&cnt[h], 1u);
+    }
     sl[k] = h;
     const uint64_t fm = __ballot(fresh);
     if (fresh) listed[nt + __popcll(fm & lt)] = (uint16_t)h;
@@ -643,13 +685,27 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
   const int total = run;
   wave_fence();
   lap(2);
-  // P3: values grouped by key
+  // P3: values grouped by key, each with its stream position; then the order check (ppr_device.h
+  // chunk_accumulate: a record with occurrence index > 0 must come after its left neighbour)
+  uint32_t qq[BW2_GROUPS];
+#pragma unroll
+  for (int k = 0; k < BW2_GROUPS; k++) {
+    qq[k] = 0u;
+    if (k >= ng) break;
+    if (k * WAVE + l < nb) {
+      qq[k] = cnt[sl[k]] + occ[k];
+      vals[qq[k]] = cs[k];
+      ord[qq[k]] = (uint16_t)(k * WAVE + l);
+    }
+  }
+  wave_fence();
+  bool bad = false;
 #pragma unroll
   for (int k = 0; k < BW2_GROUPS; k++) {
     if (k >= ng) break;
-    if (k * WAVE + l < nb) vals[cnt[sl[k]] + occ[k]] = cs[k];
+    if (k * WAVE + l < nb && occ[k] > 0u) bad = bad || (int)ord[qq[k] - 1] > k * WAVE + l;
   }
-  wave_fence();
+  const bool sorted_path = __ballot(bad) != 0ull;
   lap(3);
   // run of listed slot i: [cnt[listed[i]], next run's base or the total)
   auto run_end = [&](int i) { return i + 1 < nt ? (int)cnt[listed[i + 1]] : total; };
@@ -659,7 +715,10 @@ __device__ __forceinline__ bool bucket_oneshot(unsigned char* base, int T, int b
     const int i = i0 + l;
     if (i < nt) {
       const int b = (int)cnt[listed[i]], e = run_end(i);
-      const double x = fma_chain_lds(vals, b, e, f, ((int)keys[listed[i]] == W.seed) ? W.selfval : 0.0);
+      const double x0 = ((int)keys[listed[i]] == W.seed) ? W.selfval : 0.0;
+      const double x = __builtin_expect(sorted_path, 0)
+                           ? fma_chain_sorted(vals, [&](int j) { return (int)ord[j]; }, b, e, f, x0)
+                           : fma_chain_lds(vals, b, e, f, x0);
       if (e > b) vals[e - 1] = x;
     }
   }
@@ -760,7 +819,7 @@ __global__ void __launch_bounds__(256) k_hub_bucket_w(DevSlab s, IterArgs a, con
     return;
   }
   BucketWave B;
-  B.setup(smem + (size_t)wv * wbytes, T, NG, a.lds_rank != 0, budget);
+  B.setup(smem + (size_t)wv * wbytes, T, NG, a.lds_rank != 0, budget, (a.whatif & WI_RANK_PERMUTE) != 0);
   if (W.seed >= 0) B.seed(W.seed, W.selfval);
   if (ph) { ph[8] = (unsigned long long)clock64(); ph[0] = ph[8] - (unsigned long long)t_start; }
   // the next chunk's records are loaded while the current chunk is accumulated (MC combine
@@ -872,7 +931,7 @@ __global__ void __launch_bounds__(256) k_hub_range(DevGraph g, DevSlab s, IterAr
   const int seed_x = (d.hot >= 0 && H.has(v)) ? -1 : (int)hub_digit(v, d.logP);
   BucketWave B;
   unsigned char* base = smem + (size_t)wv * hub_wave_lds(T, NG);
-  B.setup(base, T, NG, a.lds_rank != 0, budget);
+  B.setup(base, T, NG, a.lds_rank != 0, budget, (a.whatif & WI_RANK_PERMUTE) != 0);
   auto bstart = [&](int x) { return (int64_t)__shfl((long long)bs, x - x0); };
   bool cv[NG], nv[NG];
   int kk[NG], nk[NG];
@@ -944,7 +1003,7 @@ __global__ void __launch_bounds__(256) k_hub_seg(DevGraph g, DevSlab s, IterArgs
     if (dg) { const long long t2 = (long long)clock64(); ph[k] += (unsigned long long)(t2 - tc); tc = t2; }
   };
   BucketWave B;
-  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0);
+  B.setup(smem + (size_t)wv * hub_wave_lds(T, NG), T, NG, a.lds_rank != 0, -1, (a.whatif & WI_RANK_PERMUTE) != 0);
   {
     const int rg = (int)row_range(v);
     if (rg >= r0 && rg < r1) B.seed(v, self_seed(a, e - b));

@@ -387,9 +387,11 @@ __device__ __forceinline__ int64_t sv_readlane64(int64_t x, int lane) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), lane);
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-template <bool kScores, int NS, class FB>
+// `succ(ln, rmin_bits)` (optional, merge_wave.h WalkRowMin) sees every successor's basket length and
+// row minimum once (the minimum loaded beside the length, one window ahead)
+template <bool kScores, int NS, class FB, class RM = WalkNoSucc>
 __device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, const IterArgs& a, int64_t c0, int64_t c1,
-                                        FB fb) {
+                                        FB fb, RM succ = RM{}) {
   const int lane = lane_id();
   const int lcl = lane < s.L ? lane : 0;  // (rows narrower than a wave: stay inside the row slot)
   // second-half lane, clamped inside the row slot (L < 128: lanes past L would read the next row,
@@ -398,16 +400,22 @@ __device__ __forceinline__ void sv_rows(const DevGraph& g, const DevSlab& s, con
   auto colx_at = [&](int64_t w0) { return w0 + lane < c1 ? g.colx[w0 + lane] : (int32_t)-1; };
   auto len_of = [&](int32_t cx) { return cx == -1 ? 0 : s.len[s.lrow(read_slot(a, cx), cx & 0x7fffffff)]; };
   auto base_of = [&](int32_t cx) { return cx == -1 ? (int64_t)0 : s.row(read_slot(a, cx), cx & 0x7fffffff); };
+  auto rmin_of = [&](int32_t cx) {
+    return cx == -1 ? 0ull : dbits(s.rmin[s.lrow(read_slot(a, cx), cx & 0x7fffffff)]);
+  };
   int32_t ncx = colx_at(c0);
   int32_t nncx = c0 + WAVE < c1 ? colx_at(c0 + WAVE) : -1;
   int nln = len_of(ncx);
+  unsigned long long nrm = RM::kWant ? rmin_of(ncx) : 0ull;
   for (int64_t w0 = c0; w0 < c1; w0 += WAVE) {
     const int32_t cx = ncx;
     const int ln = nln;
+    if (RM::kWant) succ(ln, nrm);
     const int64_t base = base_of(cx);
     ncx = nncx;
     if (w0 + 2 * WAVE < c1) nncx = colx_at(w0 + 2 * WAVE);
     nln = len_of(ncx);
+    if (RM::kWant) nrm = rmin_of(ncx);
     const int nrows = (int)min((int64_t)WAVE, c1 - w0);
     auto load = [&](int q0, SvBatch<NS>& bt) {
 #pragma unroll

@@ -10,6 +10,8 @@
 //                  accumulation, so the next batch's HBM gathers overlap the current LDS work.
 //   k_stat_written SURVEY s8d bytes of the rows an iteration wrote (12 * len + 4 per source).
 #pragma once
+#include <type_traits>
+
 #include "ppr_common.h"
 
 namespace pprk {
@@ -213,7 +215,10 @@ __device__ __forceinline__ void hub_window_walk_part(const DevGraph& g, const De
   const int64_t i = i0 + lane_id();
   if (a.unit) {  // init: every successor contributes {u: 1.0}
     const bool valid = i < e;
-    f(valid, valid ? (g.colx[i] & 0x7fffffff) : 0, 1.0, false);
+    if constexpr (std::is_invocable_v<F, bool, int, double, bool, int, int>)
+      f(valid, valid ? (g.colx[i] & 0x7fffffff) : 0, 1.0, false, lane_id(), WAVE);  // (one successor a lane)
+    else
+      f(valid, valid ? (g.colx[i] & 0x7fffffff) : 0, 1.0, false);
     return;
   }
   int u = 0, sl = 0, ln = 0;
@@ -235,7 +240,15 @@ __device__ __forceinline__ void hub_window_walk_part(const DevGraph& g, const De
   // HUB_TW_BATCH groups of 64 candidates are gathered together (one memory latency per batch),
   // and the next batch is in flight while f consumes the current one; f still sees the
   // candidates in stream order
-  auto load = [&](int g0, int (&key)[HUB_TW_BATCH], double (&sv)[HUB_TW_BATCH], bool (&one)[HUB_TW_BATCH]) {
+  // (f may also take the lane's row within the group and the group's row count: rr, nr)
+  constexpr bool kRows = std::is_invocable_v<F, bool, int, double, bool, int, int>;
+  // (rr: 8 bits per group, 4 groups per word; nr: wave-uniform)
+  constexpr int RW = (HUB_TW_BATCH + 3) / 4;
+  auto load = [&](int g0, int (&key)[HUB_TW_BATCH], double (&sv)[HUB_TW_BATCH], bool (&one)[HUB_TW_BATCH],
+                  uint32_t (&rr)[RW], int (&nr)[HUB_TW_BATCH]) {
+    if (kRows)
+#pragma unroll
+      for (int q = 0; q < RW; q++) rr[q] = 0u;
     if (flags) {
 #pragma unroll
       for (int q = 0; q < HUB_TW_BATCH / 4; q++)  // WAVE * HUB_TW_BATCH flag bytes
@@ -263,6 +276,12 @@ __device__ __forceinline__ void hub_window_walk_part(const DevGraph& g, const De
       const int jj = j < WAVE ? j : WAVE - 1;
       // every candidate of the group from one successor basket: its keys are distinct
       one[k] = !__ballot(valid && jj != __builtin_amdgcn_readlane(jj, 0));
+      if (kRows) {
+        const uint64_t vm = __ballot(valid);
+        const int j0 = __builtin_amdgcn_readlane(jj, 0);
+        rr[k / 4] |= (uint32_t)min(jj - j0, 255) << (8 * (k % 4));
+        nr[k] = __builtin_amdgcn_readfirstlane(vm ? __shfl(jj, 63 - __clzll((long long)vm)) - j0 + 1 : 1);
+      }
       const int exv = __shfl(incl, jj > 0 ? jj - 1 : 0);
       const int ex = jj > 0 ? exv : 0;
       const int uj = __shfl(u, jj);
@@ -279,17 +298,28 @@ __device__ __forceinline__ void hub_window_walk_part(const DevGraph& g, const De
   int key[HUB_TW_BATCH], nkey[HUB_TW_BATCH];
   double sv[HUB_TW_BATCH], nsv[HUB_TW_BATCH];
   bool one[HUB_TW_BATCH], none[HUB_TW_BATCH];
+  uint32_t rr[RW], nrr[RW];
+  int nr[HUB_TW_BATCH], nnr[HUB_TW_BATCH];
   const int step = WAVE * HUB_TW_BATCH * nparts;
   const int gs = WAVE * HUB_TW_BATCH * part;
-  if (gs < total) load(gs, nkey, nsv, none);
+  if (gs < total) load(gs, nkey, nsv, none, nrr, nnr);
   for (int g0 = gs; g0 < total; g0 += step) {
 #pragma unroll
-    for (int k = 0; k < HUB_TW_BATCH; k++) { key[k] = nkey[k]; sv[k] = nsv[k]; one[k] = none[k]; }
-    if (g0 + step < total) load(g0 + step, nkey, nsv, none);
+    for (int k = 0; k < HUB_TW_BATCH; k++) {
+      key[k] = nkey[k]; sv[k] = nsv[k]; one[k] = none[k];
+      if (kRows) nr[k] = nnr[k];
+    }
+    if (kRows)
+#pragma unroll
+      for (int q = 0; q < RW; q++) rr[q] = nrr[q];
+    if (g0 + step < total) load(g0 + step, nkey, nsv, none, nrr, nnr);
 #pragma unroll
     for (int k = 0; k < HUB_TW_BATCH; k++) {
       if (g0 + k * WAVE >= total) break;  // uniform
-      f(g0 + k * WAVE + lane_id() < total, key[k], sv[k], one[k]);
+      if constexpr (kRows)
+        f(g0 + k * WAVE + lane_id() < total, key[k], sv[k], one[k], (int)((rr[k / 4] >> (8 * (k % 4))) & 255u), nr[k]);
+      else
+        f(g0 + k * WAVE + lane_id() < total, key[k], sv[k], one[k]);
     }
   }
 }

@@ -536,6 +536,10 @@ __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, 
   unsigned long long mb = 0;
   uint8_t* fl = x.fl + (size_t)wv * HUB_WALK_FLAGS;
   auto fn = [&](bool valid, int id, double sv, bool) {
+#if defined(PPR_XR_WALK_ONLY)  // (timing-only build: the walk alone, no table work)
+    if (valid && id == -9 && sv == -1.0) x.w.misc[XM_FILL] = 1;
+    return;
+#endif
     if (xr_stop(x, budget)) return;  // (uniform per wave: one LDS read per group)
     xr_apply(x, valid && xr_in(id, r, R), id, sv * factor, budget, a.xsf);
   };

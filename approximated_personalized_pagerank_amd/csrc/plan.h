@@ -112,6 +112,7 @@ struct ppr_plan {
   size_t gath_bytes = 0;
   int num_cus = 256;
   int hub_bw_blocks = 0;           // persistent k_hub_bucket_w grid
+  bool rank_permute = false;       // PPR_TEST_RANK_PERMUTE (tests): IterArgs WI_RANK_PERMUTE
   uint32_t lds_rank = 0;           // k_probe_lds_rank: 32-bit add ranks in lane order (PPR_LDS_RANK=0 forces the ballot path)
   uint32_t lds_rank64 = 0;         // ... and the 64-bit CAS / add order the one-shot buckets need
   bool seg_enabled = false;        // segmented hub buckets (k_hub_seg, PPR_HUB_SEG=1)
@@ -229,6 +230,7 @@ struct ppr_plan {
   bool sv_enabled = false;
   int64_t sv_slice = 1LL << 19;       // PPR_SV_SLICE: candidates per slice workgroup (round-5 sweep: 2^18 -> 2^19, -1.6 %)
   // read per plan in plan_alloc (a process may switch them between plans; tests cover both ways)
+  bool xm = false;                    // PPR_XM=1: k_xm for the one-range sources of the 2048-slot class
   bool xr_big_first = false;          // PPR_XR_ORDER=1: range tasks largest source first (experiment)
   bool xh_first = true;               // PPR_XH_FIRST: range engines planned and queued before the sieve
   bool xshard_ends = true;            // PPR_XSHARD_ENDS: sharded init and K-wide top-K (routed exchange)

@@ -178,6 +178,11 @@ constexpr uint32_t WI_SCAT_COALESCED = 1u << 20, WI_SCAT_NOSTORE = 1u << 21, WI_
                    WI_SCAT_COUNT = 1u << 23, WI_SCAT_WALK = 1u << 24;
 // the sieve's exact pass-2 skip turned off (PPR_SV_P2SKIP=0, tests: the skip must not change a bit)
 constexpr uint32_t WI_SV_NO_P2SKIP = 1u << 25;
+// (tests, PPR_TEST_RANK_PERMUTE=1) the ordered paths take their same-address LDS atomics odd lanes
+// first, then even lanes: the occurrence order a device without lane-ordered atomics could return.
+// The results must not change (ppr_device.h chunk_accumulate, merge_hub.h bucket_oneshot verify the
+// order they got and fall back to stream order).
+constexpr uint32_t WI_RANK_PERMUTE = 1u << 26;
 
 // Speculative top-L pruning bound of a hub source (GRank iterations): spec x the smallest score of
 // the source's previous row when that row was full. Bucket waves then emit only keys whose exact

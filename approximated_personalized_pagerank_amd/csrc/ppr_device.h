@@ -210,6 +210,7 @@ struct ChunkLds {
   double* vals;       // [NG * 64]
   uint16_t* touched;  // [NG * 64]
   uint16_t* tof;      // [NG * 64 + 1]
+  uint16_t* ord;      // [NG * 64] (ordered mode) stream position of vals[j]: the order is verified
 };
 
 // With `ordered` (lane-ordered LDS atomics, verified on the device at plan creation: see
@@ -226,6 +227,27 @@ __device__ __forceinline__ void diag_lap(unsigned long long* ph, int k, long lon
   t = t2;
 }
 
+// The ordered mode's occurrence indices come from the hardware's order of same-address LDS atomics.
+// Nothing documents that order, so it is verified where it is used: every value's stream position
+// goes beside it (ord), every value with an occurrence index > 0 is compared with its left neighbour
+// (the same key's previous occurrence: its position must be smaller -- sorted runs are exactly those
+// whose adjacent pairs are), and if any pair is out of order the wave's chains are recomputed in
+// stream order (fma_chain_sorted). The result does not depend on the
+// hardware order. (Round 6; PPR_TEST_RANK_PERMUTE forces a permuted order in the tests.)
+template <class Ord>
+__device__ __forceinline__ double fma_chain_sorted(const double* vals, Ord ord, int b, int e, double f, double x) {
+  int last = -1;
+  for (int n = b; n < e; n++) {  // the next position: the smallest one past the last (O(n^2), rare)
+    int best = b, bo = 0x10000;
+    for (int j = b; j < e; j++) {
+      const int o = ord(j);
+      if (o > last && o < bo) { bo = o; best = j; }
+    }
+    x = fma(vals[best], f, x);
+    last = bo;
+  }
+  return x;
+}
 // x = fma(vals[j], f, x) for j = b .. e-1, in that order (one key's ordered chain). The next 8
 // values are loaded while the current 8 are folded in, so the dependent fma chain -- not the LDS
 // read latency after every few loads -- sets the pace (tools/fma_chain.hip: ~12.5 cycles per fma
@@ -257,7 +279,7 @@ template <int NG>
 __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c, int nbits,
                                                  const bool (&valid)[NG], const uint32_t (&slot)[NG],
                                                  const double (&val)[NG], double factor, bool ordered,
-                                                 unsigned long long* ph = nullptr) {
+                                                 unsigned long long* ph = nullptr, bool permute = false) {
   const uint64_t lt = lanemask_lt();
   uint32_t occ[NG];
   int nt = 0;
@@ -265,7 +287,14 @@ __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c,
   if (ordered) {
 #pragma unroll
     for (int k = 0; k < NG; k++) {
-      const uint32_t o = valid[k] ? atomicAdd(&c.cnt[slot[k]], 1u) : 1u;
+      uint32_t o = 1u;
+      if (!permute) {
+        if (valid[k]) o = atomicAdd(&c.cnt[slot[k]], 1u);
+      } else {  // (tests: odd lanes first -- the order a device without lane-ordered atomics may return)
+        if (valid[k] && (lane_id() & 1)) o = atomicAdd(&c.cnt[slot[k]], 1u);
+        wave_fence();
+        if (valid[k] && !(lane_id() & 1)) o = atomicAdd(&c.cnt[slot[k]], 1u);
+      }
       const bool fresh = valid[k] && o == 0;
       const uint64_t fm = __ballot(fresh);
       if (fresh) c.touched[nt + __popcll(fm & lt)] = (uint16_t)slot[k];
@@ -311,17 +340,37 @@ __device__ __forceinline__ void chunk_accumulate(double* acc, const ChunkLds& c,
   if (lane_id() == 0) c.tof[nt] = (uint16_t)run;
   wave_fence();
   diag_lap(ph, 12, tph, c.cnt);
-  // C: values grouped by slot, stream order inside a slot
+  // C: values grouped by slot, stream order inside a slot (ordered mode: with the stream position)
+  uint32_t qq[NG];
 #pragma unroll
-  for (int k = 0; k < NG; k++)
-    if (valid[k]) c.vals[c.cnt[slot[k]] + occ[k]] = val[k];
+  for (int k = 0; k < NG; k++) {
+    qq[k] = valid[k] ? c.cnt[slot[k]] + occ[k] : 0u;
+    if (valid[k]) {
+      c.vals[qq[k]] = val[k];
+      if (ordered) c.ord[qq[k]] = (uint16_t)(k * WAVE + lane_id());
+    }
+  }
   wave_fence();
+  // (ordered) the order check, every record at once, off the chains' path: a record with an
+  // occurrence index > 0 has its slot's previous occurrence just before it, which must come earlier
+  // in the stream (across groups program order guarantees it; only same-instruction lanes can fail)
+  bool sorted_path = false;
+  if (ordered) {
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < NG; k++)
+      if (valid[k] && occ[k] > 0u) bad = bad || (int)c.ord[qq[k] - 1] > k * WAVE + lane_id();
+    sorted_path = __ballot(bad) != 0ull;
+  }
   diag_lap(ph, 13, tph, c.cnt);
   // D: one lane per touched slot
   for (int i = lane_id(); i < nt; i += WAVE) {
     const uint32_t sl = c.touched[i];
     const int b = c.tof[i], e = c.tof[i + 1];
-    acc[sl] = fma_chain_lds(c.vals, b, e, factor, acc[sl]);
+    if (__builtin_expect(sorted_path, 0))
+      acc[sl] = fma_chain_sorted(c.vals, [&](int j) { return (int)c.ord[j]; }, b, e, factor, acc[sl]);
+    else
+      acc[sl] = fma_chain_lds(c.vals, b, e, factor, acc[sl]);
     c.cnt[sl] = 0;
   }
   wave_fence();
@@ -443,9 +492,101 @@ __device__ __forceinline__ void radix_kth_desc(int n, int& k, GetV getv, Filt fi
   }
 }
 
+// Top-`need` of at most 4 * 64 entries with the values in registers (round 6): the need-th largest
+// value is found bit by bit from the highest varying bit, each step one compare and one ballot per
+// register and scalar popcounts -- no LDS histogram, no fence -- and the search stops as soon as the
+// entries at or above the current bound are exactly `need`. Exact ties at the cut are broken by the
+// largest tie_w the same way. The selected set is radix_kth_desc's: {v > v*} plus, at v = v*, all
+// of them or those with tie_w >= w* (w* the k-th largest tie_w there).
+struct SelAll {
+  __device__ bool operator()(int) const { return true; }
+};
+#ifndef PPR_SEL_REG
+#define PPR_SEL_REG 1  // (A/B only: 0 = the histogram passes for every size)
+#endif
+template <class KeyAt, class ValAt, class Occ = SelAll>
+__device__ __forceinline__ SelCrit select_top_reg(int n, int need, KeyAt keyat, ValAt valat, uint32_t ts,
+                                                  Occ occ = Occ{}) {
+  constexpr int R = 4;
+  uint64_t v[R];
+  bool ok[R];
+  uint64_t lor = 0, land = ~0ull;
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    const int i = j * WAVE + lane_id();
+    ok[j] = i < n && occ(i);
+    v[j] = ok[j] ? dbits(valat(i)) : 0ull;
+    if (ok[j]) { lor |= v[j]; land &= v[j]; }
+  }
+  lor = wave_or(lor);
+  land = wave_and(land);
+  auto count_ge = [&](uint64_t x) {
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < R; j++) c += __popcll(__ballot(ok[j] && v[j] >= x));
+    return c;
+  };
+  SelCrit c;
+  c.tie = false; c.pb = 0; c.mb = 0; c.ma = ~0ull;
+  const uint64_t diff = lor ^ land;
+  uint64_t x = land;  // every value equal: the bound is that value
+  int cx = 0;         // entries >= x
+#pragma unroll
+  for (int j = 0; j < R; j++) cx += __popcll(__ballot(ok[j]));
+  if (diff) {
+    const int top = 63 - __clzll((long long)diff);
+    x = land & (top == 63 ? 0ull : ~((2ull << top) - 1ull));  // the shared high bits, zeros below
+    for (int b = top; b >= 0 && cx != need; b--) {
+      const uint64_t cand = x | (1ull << b);
+      const int cnt = count_ge(cand);
+      if (cnt >= need) { x = cand; cx = cnt; }
+    }
+  }
+  c.pa = x;  // v >= x selects cx entries; cx == need unless values equal to x straddle the cut
+  if (cx > need) {
+    // exact ties at x: the (need - #{v > x}) largest tie_w among them
+    int gt = 0;
+#pragma unroll
+    for (int j = 0; j < R; j++) gt += __popcll(__ballot(ok[j] && v[j] > x));
+    const int k2 = need - gt;
+    uint32_t w[R];
+    bool eq[R];
+    uint32_t wor = 0, wand = ~0u;
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      eq[j] = ok[j] && v[j] == x;
+      w[j] = eq[j] ? tie_w(keyat(j * WAVE + lane_id()), ts) : 0u;
+      if (eq[j]) { wor |= w[j]; wand &= w[j]; }
+    }
+    wor = (uint32_t)wave_or(wor);
+    wand = (uint32_t)wave_and(wand);
+    const uint32_t wd = wor ^ wand;
+    uint32_t y = wand;
+    int cy = 0;
+#pragma unroll
+    for (int j = 0; j < R; j++) cy += __popcll(__ballot(eq[j]));
+    if (wd) {
+      const int top = 31 - __clz(wd);
+      y = wand & (top == 31 ? 0u : ~((2u << top) - 1u));
+      for (int b = top; b >= 0 && cy != k2; b--) {
+        const uint32_t cand = y | (1u << b);
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < R; j++) cnt += __popcll(__ballot(eq[j] && w[j] >= cand));
+        if (cnt >= k2) { y = cand; cy = cnt; }
+      }
+    }
+    c.tie = true;
+    c.pb = y;
+    c.mb = 0xffffffffull;
+  }
+  return c;
+}
+
 template <class KeyAt, class ValAt>
 __device__ __forceinline__ SelCrit select_top(int n, int need, KeyAt keyat, ValAt valat,
                                               uint32_t* hist, uint32_t ts) {
+  if (PPR_SEL_REG && n <= 4 * WAVE) return select_top_reg(n, need, keyat, valat, ts);
   SelCrit c;
   c.tie = false; c.pb = 0; c.mb = 0;
   int k = need;

@@ -225,6 +225,19 @@ template <class KeyAt, class ValAt, class Occ>
 __device__ __forceinline__ SelCrit wg_select_top(const WgLds& w, int n, int need, KeyAt keyat,
                                                  ValAt valat, Occ occ, uint32_t ts) {
   SelCrit c;
+  if (PPR_SEL_REG && n <= 4 * WAVE) {
+    // (round 6) few entries: one wave selects with the values in registers (ppr_device.h
+    // select_top_reg, no histogram passes) and publishes the criterion
+    uint64_t* pub = reinterpret_cast<uint64_t*>(w.hist);
+    if (threadIdx.x < WAVE) {
+      c = select_top_reg(n, need, keyat, valat, ts, occ);
+      if (threadIdx.x == 0) { pub[0] = c.pa; pub[1] = c.ma; pub[2] = c.pb; pub[3] = c.mb; pub[4] = c.tie ? 1ull : 0ull; }
+    }
+    __syncthreads();
+    c.pa = pub[0]; c.ma = pub[1]; c.pb = pub[2]; c.mb = pub[3]; c.tie = pub[4] != 0ull;
+    __syncthreads();  // (ends on a barrier like the radix path: the histogram region is free again)
+    return c;
+  }
   c.tie = false; c.pb = 0; c.mb = 0;
   int k = need;
   bool tie = false;
