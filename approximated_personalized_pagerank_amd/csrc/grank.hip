@@ -453,6 +453,10 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         }
       TRY(dalloc(&p->d_dlast, n));
       TRY(dalloc(&p->d_wovl, n + 1));
+      const char* ews = getenv("PPR_WAVE_SPLIT");
+      if (ews) p->wave_split_T = std::max(0, atoi(ews));
+      const char* ewc = getenv("PPR_WAVE_CAP");
+      if (ewc) p->wave_cap = std::max(0, atoi(ewc));
       const char* e9 = getenv("PPR_XR_BUDGET");
       p->xr_budget_over = e9 && strcmp(e9, "over") == 0;
       if (hipMemset(p->d_dlast, 0, 4 * (size_t)(n > 0 ? n : 1)) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
@@ -529,6 +533,7 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         {(const void*)k_hub_hot, "k_hub_hot"},
         {(const void*)k_hub_join, "k_hub_join"},
         {(const void*)k_merge_lds_x, "k_merge_lds_x"},
+        {(const void*)k_wfin, "k_wfin"},
         {(const void*)k_xr, "k_xr"},
         {(const void*)k_xm<4>, "k_xm<4>"},
         {(const void*)k_xb, "k_xb"},
@@ -1810,10 +1815,12 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   unsigned long long* d_gb = (unsigned long long*)(b + o_gb);
   const size_t lds = sv_lds_bytes(Lp, SV_LARGE);
   {
-    // one-slice classes beside the multi-slice chain (stream_sv): large then small on stream_sv2,
-    // mid on stream_sv3, so each class's tail overlaps another's work
+    // one-slice classes beside the multi-slice chain (stream_sv): large on stream_sv2, mid then
+    // small on stream_sv3 (the mid class ends long before the large one; the small class's 40-KB
+    // workgroups fill the LDS the 116-KB ones leave; behind the large class it ran alone at the end
+    // of the iteration: round 6, -0.5 % per job)
     const SvGeom geo[3] = {SV_LARGE, SV_MID, SV_SMALL};
-    hipStream_t cs[3] = {s2, s3, s2};
+    hipStream_t cs[3] = {s2, s3, s3};
     size_t c0 = nm;
     for (int c = 0; c < 3; c++) {
       const size_t cnt_c = cls_end[c] - c0;
@@ -2206,9 +2213,29 @@ reclassify:
       if (!p->wave_x_launched) HIP_OK(hipMemsetAsync(p->d_wovl, 0, 4, sw));
       p->wave_x_launched = true;
       const int Tw = std::max(64, p->tierT[t] >> p->wave_tdiv);  // (PPR_WAVE_TDIV: tests of the overflow redo)
-      hipLaunchKernelGGL(k_merge_lds_x, dim3((unsigned)blocks), dim3(64 * wpb), lds_wave_bytes_x(Tw, p->Lp) * wpb,
-                         sw, g, s, a, p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], Tw, p->Lp, maxdiff,
-                         p->d_stats, p->d_dlast, p->d_wovl);
+      // the largest tables end after their compaction: the row in k_wfin (merge_xs.h WList)
+      WList wl{nullptr, nullptr, nullptr, 0};
+      const bool split = !a.unit && p->wave_split_T > 0 && Tw >= p->wave_split_T;
+      if (split) {
+        const int cap = p->wave_cap ? std::max<int>((int)p->L, p->wave_cap) : 2 * p->Lp;
+        const size_t nk = (size_t)cnt[t] * (size_t)cap;
+        const size_t need = nk * 12 + 4 * (size_t)cnt[t] + 512;
+        int rc = ensure_dev(&p->d_wl, &p->wl_bytes, need);
+        if (rc) return rc;
+        wl.v = reinterpret_cast<double*>(p->d_wl);
+        wl.k = reinterpret_cast<int32_t*>(p->d_wl + nk * 8);
+        wl.n = reinterpret_cast<int32_t*>(p->d_wl + nk * 12);
+        wl.cap = cap;
+      }
+      const int32_t* tl = p->d_tier_lists + (int64_t)t * p->n;
+      const size_t wlds = split ? lds_wave_bytes_xs(Tw) : lds_wave_bytes_x(Tw, p->Lp);
+      hipLaunchKernelGGL(k_merge_lds_x, dim3((unsigned)blocks), dim3(64 * wpb), wlds * wpb, sw, g, s, a, tl, (int64_t)cnt[t], Tw, p->Lp, maxdiff, p->d_stats, p->d_dlast, p->d_wovl, wl);
+      if (split) {
+        HIP_OK(hipGetLastError());
+        hipLaunchKernelGGL(k_wfin, dim3((unsigned)(((int64_t)cnt[t] + 3) / 4)), dim3(256), wfin_lds_bytes(p->Lp) * 4, sw,
+                           s, a, tl, (int64_t)cnt[t], wl, p->Lp, maxdiff, p->d_stats);
+        p->merge_launches++;
+      }
     } else {
       const int Tw = std::max(64, p->tierT[t] >> p->wave_tdiv);  // (PPR_WAVE_TDIV: tests of the bounded probes)
       const size_t bytes = lds_wave_bytes(Tw, p->Lp) * wpb;

@@ -150,28 +150,42 @@ __device__ __forceinline__ XTable xt_carve(unsigned char* p, int T) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// wave tier: layout table (16 T) | rv u64[Lp] | rk i32[Lp] | hist u32[256] | hk i32[2Lp] |
-// hv i32[2Lp] | mf i32[Lp]
+// wave tier: layout table (16 T) | hist u32[256] | rv u64[Lp] | rk i32[Lp] | hk i32[2Lp] |
+// hv i32[2Lp] | mf i32[Lp]; a split wave (WList) has no row epilogue: table and hist only
 __host__ __device__ constexpr size_t lds_wave_bytes_x(int T, int Lp) {
   return (size_t)T * 16 + (size_t)Lp * 12 + 1024 + (size_t)Lp * 20;
 }
+__host__ __device__ constexpr size_t lds_wave_bytes_xs(int T) { return (size_t)T * 16 + 1024; }
+
+// Split epilogue (round 6, the tiers with the largest tables): the wave stops after the compaction
+// and writes its kept entries (at most `cap`, the common case by far: ~150 of them) to a list in
+// HBM; k_wfin (below) then selects, writes the row and its norm1 with one 5-KB wave per source. A
+// 2048-slot table costs 38 KB of LDS per wave: holding it through the select, the row write and
+// norm1 (more than half of the wave's time, PPR_DIAG) kept the tier at 4 waves per CU.
+struct WList {
+  int32_t* k;  // [count * cap] keys
+  double* v;   // [count * cap] values
+  int32_t* n;  // [count] entries (-1: the table ran out, the host redoes the source)
+  int cap;     // 0: no split; else >= L
+};
 
 // (a table that runs out -- never, at T >= 4/3 of the tier's candidate cap, unless PPR_WAVE_TDIV
 // shrinks it for the tests -- writes no row: the source goes to `wovl` ([0] count, then sources)
 // and the host merges it again with the workgroup engines)
 __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, IterArgs a, const int32_t* list,
                                                      int64_t count, int T, int Lp, unsigned long long* maxdiff,
-                                                     unsigned long long* stats, int32_t* dlast, int32_t* wovl) {
+                                                     unsigned long long* stats, int32_t* dlast, int32_t* wovl,
+                                                     WList wl) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (w >= count) return;
-  unsigned char* base = smem + (size_t)wv * lds_wave_bytes_x(T, Lp);
+  unsigned char* base = smem + (size_t)wv * (wl.cap ? lds_wave_bytes_xs(T) : lds_wave_bytes_x(T, Lp));
   const XTable t = xt_carve(base, T);
-  uint64_t* rv = reinterpret_cast<uint64_t*>(base + (size_t)T * 16);
-  int* rk = reinterpret_cast<int*>(base + (size_t)T * 16 + (size_t)Lp * 8);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 16 + (size_t)Lp * 12);
-  int* hk = reinterpret_cast<int*>(base + (size_t)T * 16 + (size_t)Lp * 12 + 1024);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 16);
+  uint64_t* rv = reinterpret_cast<uint64_t*>(base + (size_t)T * 16 + 1024);
+  int* rk = reinterpret_cast<int*>(base + (size_t)T * 16 + 1024 + (size_t)Lp * 8);
+  int* hk = reinterpret_cast<int*>(base + (size_t)T * 16 + 1024 + (size_t)Lp * 12);
   int* hv = hk + 2 * Lp;
   int* mf = hv + 2 * Lp;
 
@@ -213,7 +227,10 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   }
   wave_fence();
   if (__ballot(bad)) {  // table ran out: no row, the host redoes the source
-    if (lane_id() == 0) wovl[1 + atomicAdd(&wovl[0], 1)] = v;
+    if (lane_id() == 0) {
+      wovl[1 + atomicAdd(&wovl[0], 1)] = v;
+      if (wl.cap) wl.n[w] = -1;
+    }
     return;
   }
   fs_lap(a, 280, 1, tl);  // (slot 281: setup + walk)
@@ -271,8 +288,57 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   if (dlast && !a.unit && lane_id() == 0) dlast[v] = D;  // (init counts predict nothing)
   fs_lap(a, 280, 2, tl);  // (slot 282: settle + compact)
   if (a.diag && !a.unit && lane_id() == 0) { diag_add(a.diag, 280, 1ull); diag_add(a.diag, 287, (unsigned long long)U); }
+  if (wl.cap) {  // the list for k_wfin: every kept entry, or the top-L of more than cap (cap >= L)
+    U = __builtin_amdgcn_readfirstlane(U);
+    const int64_t o = w * (int64_t)wl.cap;
+    if (U <= wl.cap) {
+      for (int i = lane_id(); i < U; i += WAVE) { wl.k[o + i] = keys[i]; wl.v[o + i] = vals[i]; }
+      if (lane_id() == 0) wl.n[w] = U;
+      return;
+    }
+    const uint32_t ts = tie_salt(v);
+    const SelCrit c = select_top(U, (int)s.L, [&](int i) { return keys[i]; }, [&](int i) { return vals[i]; }, hist, ts);
+    int nb = 0;
+    for (int i0 = 0; i0 < U; i0 += WAVE) {
+      const int i = i0 + lane_id();
+      const bool sel = i < U && sel_test(c, dbits(vals[i]), tie_w(keys[i], ts));
+      const uint64_t m = __ballot(sel);
+      if (sel) {
+        const int64_t q = o + nb + __popcll(m & lanemask_lt());
+        wl.k[q] = keys[i];
+        wl.v[q] = vals[i];
+      }
+      nb += __popcll(m);
+    }
+    if (lane_id() == 0) wl.n[w] = nb;
+    return;
+  }
   finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return vals[i]; }, s, a, hist, rv, rk, Lp, hk, hv,
                 mf, maxdiff, stats, a.unit ? -1 : 283);  // (283 select, 284 row write, 285 norm1)
+}
+
+// the row of a split wave-tier source from its list (one wave per source, 4 per block)
+__host__ __device__ constexpr size_t wfin_lds_bytes(int Lp) { return (size_t)Lp * 12 + 1024 + (size_t)Lp * 20; }
+__global__ void __launch_bounds__(256) k_wfin(DevSlab s, IterArgs a, const int32_t* list, int64_t count, WList wl,
+                                              int Lp, unsigned long long* maxdiff, unsigned long long* stats) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int wv = threadIdx.x >> 6;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (w >= count) return;
+  const int n = wl.n[w];
+  if (n < 0) return;  // finished by the wave itself, or overflowed
+  unsigned char* base = smem + (size_t)wv * wfin_lds_bytes(Lp);
+  uint64_t* rv = reinterpret_cast<uint64_t*>(base);
+  int* rk = reinterpret_cast<int*>(base + (size_t)Lp * 8);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)Lp * 12);
+  int* hk = reinterpret_cast<int*>(base + (size_t)Lp * 12 + 1024);
+  int* hv = hk + 2 * Lp;
+  int* mf = hv + 2 * Lp;
+  const int64_t o = w * (int64_t)wl.cap;
+  const int32_t* lk = wl.k + o;
+  const double* lv = wl.v + o;
+  finish_source(list[w], n, [&](int i) { return lk[i]; }, [&](int i) { return lv[i]; }, s, a, hist, rv, rk, Lp, hk,
+                hv, mf, maxdiff, stats, 283);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -220,6 +220,10 @@ struct ppr_plan {
   int64_t xg_sources = 0;             // sources merged there (PPR_TIMING at destroy)
   // bounded probes (tests force them to run out): exact wave-tier overflow list and knobs
   int32_t* d_wovl = nullptr;          // [1 + n]: count, sources whose wave-tier table ran out
+  int wave_split_T = 256;             // PPR_WAVE_SPLIT: wave tiers with T >= this end in k_wfin (0: none)
+  int wave_cap = 0;                   // (tests) PPR_WAVE_CAP: list entries per split source (>= L; 0: 2 Lp)
+  unsigned char* d_wl = nullptr;      // their lists (merge_xs.h WList)
+  size_t wl_bytes = 0;
   bool wave_x_launched = false;
   int wave_tdiv = 0;                  // PPR_WAVE_TDIV (tests): wave-tier tables T >> this
   bool wave_by_d = false;             // PPR_WAVE_BY_D: exact-sum wave tiers by last distinct keys
@@ -307,6 +311,7 @@ inline void plan_free(ppr_plan* p) {
   hipFree(p->d_sv);
   hipFree(p->d_xg);
   hipFree(p->d_wovl);
+  hipFree(p->d_wl);
   if (p->h_sv_pin) hipHostFree(p->h_sv_pin);
   if (p->ev_sv) hipEventDestroy(p->ev_sv);
   if (getenv("PPR_TIMING") && p->sv_sources)

@@ -263,6 +263,10 @@ def test_gpu_speculative_bound_bit_exact(env, want_redo, monkeypatch, capfd, cha
     {"PPR_WAVE_WPB": "4"},                                        # 4-wave blocks in the wave tier
     {"PPR_WAVE_BY_D": "1"},                                       # wave tiers sized by last distinct keys
     {"PPR_WAVE_BY_D": "1", "PPR_XR_DSCALE": "5"},                 # ... with every overflow path busy
+    {"PPR_WAVE_SPLIT": "0"},                                      # every wave-tier row written by its wave
+    {"PPR_WAVE_SPLIT": "256"},                                    # ... by k_wfin from the wave's list, all tiers
+    {"PPR_WAVE_SPLIT": "256", "PPR_WAVE_TDIV": "2"},              # ... with table overflows beside them
+    {"PPR_WAVE_SPLIT": "256", "PPR_WAVE_CAP": "1"},               # ... lists of L: the wave selects first
     {"PPR_XM": "1"},                                              # one-range sources of the smallest class
     {"PPR_XM": "1", "PPR_SV": "0", "PPR_TIER_MASK": "0x20"},      # through k_xm (merge_xm.h, opt-in) ...
     {"PPR_XM": "1", "PPR_XR_DSCALE": "5", "PPR_SV": "0"},         # ... overflowing: redone as from k_xr
