@@ -455,6 +455,9 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       TRY(dalloc(&p->d_wovl, n + 1));
       const char* ews = getenv("PPR_WAVE_SPLIT");
       if (ews) p->wave_split_T = std::max(0, atoi(ews));
+      p->xr_cap = 2 * p->Lp;
+      const char* exc = getenv("PPR_XR_LISTCAP");  // (0: k_xr selects every one-range source itself)
+      if (exc) p->xr_cap = atoi(exc) <= 0 ? 0 : std::max<int>((int)L, atoi(exc));
       const char* ewc = getenv("PPR_WAVE_CAP");
       if (ewc) p->wave_cap = std::max(0, atoi(ewc));
       const char* e9 = getenv("PPR_XR_BUDGET");
@@ -1478,7 +1481,9 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       // (merge_factor / self_seed of ppr_common.h: GRank d/deg and 1 - d, the MC combine 1 and 1/f)
       x.factor = a.mc ? 1.0 : p->damping / (double)deg[i];
       x.selfval = a.mc ? 1.0 / (p->damping / (double)deg[i]) : 1.0 - p->damping;
-      pt += (int64_t)rng[i] * L;  // every range appends at most L entries (one range: the whole top-L)
+      // every range of a multi-range source appends at most L entries; a one-range source its whole
+      // top-L, or up to xr_cap unselected entries (k_xfin1 selects)
+      pt += rng[i] == 1 ? (int64_t)std::max<int64_t>(L, p->xr_cap) : (int64_t)rng[i] * L;
       xd.push_back(x);
       for (int r = 0; r < rng[i]; r++) tasks[ci[i]].push_back(XTask{d, r});
     }
@@ -1581,7 +1586,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       // out, which must end in the overflow redo)
       const int budget = p->xr_budget_over ? 2 * T : std::min(T * 85 / 100, T - W * WAVE - WAVE);
       hipLaunchKernelGGL(k_xr, dim3((unsigned)tasks[c].size()), dim3(64 * W), xr_lds_bytes(T, W, p->Lp), sw, g, s, a,
-                         d_xd, d_tk + tofs[c], T, budget, p->Lp, d_xt, d_pk, d_ps, d_pc, d_ds, d_of, d_ov);
+                         d_xd, d_tk + tofs[c], T, budget, p->Lp, d_xt, d_pk, d_ps, d_pc, d_ds, d_of, d_ov, p->xr_cap);
       HIP_OK(hipGetLastError());
       p->merge_launches++;
     }
@@ -1768,8 +1773,8 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   const size_t o_d = off; off = al(off + sizeof(SvDesc) * (nm + 1));
   const size_t o_t = off; off = al(off + sizeof(SvTask) * (nt + 1));
   const size_t up = off;
-  const size_t o_sk = off; off = al(off + 4 * (size_t)Lp * nx);
-  const size_t o_sv = off; off = al(off + 8 * (size_t)Lp * nx);
+  const size_t o_sk = off; off = al(off + 4 * (size_t)sv_ostride(Lp) * nx);
+  const size_t o_sv = off; off = al(off + 8 * (size_t)sv_ostride(Lp) * nx);
   const size_t o_z = off;
   const size_t o_ov = off; off = al(off + 4 * (1 + nx));
   const size_t o_os = off; off = al(off + 4 * (1 + nx));  // small class's first overflows (device redo)

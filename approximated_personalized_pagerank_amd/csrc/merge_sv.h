@@ -704,6 +704,14 @@ __device__ __forceinline__ void sv_clear_region(const SvLds& x, size_t bytes) {
   for (size_t i = threadIdx.x; i < bytes / 16; i += blockDim.x) r[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
+// entries per one-slice source in the k_sv1 -> k_svfin lists: a source with at most this many
+// kept entries emits them unselected and k_svfin (one 5-KB wave) selects its top-L, so the
+// workgroup's table is released before the select (round 6, as the wave tier's k_wfin)
+#ifndef PPR_SV_OSTRIDE_X
+#define PPR_SV_OSTRIDE_X 2
+#endif
+__host__ __device__ constexpr int sv_ostride(int Lp) { return PPR_SV_OSTRIDE_X * Lp; }
+
 // ---------------------------------------------------------------------------------------------
 // one source (descriptor d) of a one-slice class, the whole workgroup; a source that overflows
 // (or has no full row) goes to `ovl` and writes nothing
@@ -812,7 +820,7 @@ __device__ __forceinline__ void sv1_source(unsigned char* smem, DevGraph g, DevS
   const uint32_t ts = tie_salt(v);
   SelCrit sc;
   sc.tie = false; sc.pa = 0; sc.ma = 0; sc.pb = 0; sc.mb = 0;
-  const bool cut = U > L;
+  const bool cut = U > sv_ostride(Lp);  // (else k_svfin selects: every kept entry goes to the list)
   if (cut) {
     WgLds w = WgLds{};
     w.hist = x.hist;
@@ -821,8 +829,8 @@ __device__ __forceinline__ void sv1_source(unsigned char* smem, DevGraph g, DevS
   }
   if (threadIdx.x == 0) x.misc[SVM_PT] = 0;
   __syncthreads();
-  int32_t* ok = out_k + (int64_t)d * Lp;
-  double* ov = out_v + (int64_t)d * Lp;
+  int32_t* ok = out_k + (int64_t)d * sv_ostride(Lp);
+  double* ov = out_v + (int64_t)d * sv_ostride(Lp);
   for (int i0 = 0; i0 < U; i0 += blockDim.x) {
     const int i = i0 + threadIdx.x;
     const bool sel = i < U && (!cut || sel_test(sc, dbits(dv[i]), tie_w(dk[i], ts)));
@@ -884,8 +892,9 @@ __global__ void __launch_bounds__(SV_THREADS) k_sv1_list(DevGraph g, DevSlab s, 
   sv1_source(smem, g, s, a, vid, list[1 + blockIdx.x], Lp, G, budget, ovl, out_k, out_v, out_n);
 }
 
-// the row of a one-slice source from its selected entries (k_sv1): one wave per source -- sort in
-// hash order, write, range index, norm1 against the old row, maxDiff (finish_source)
+// the row of a one-slice source from its entries (k_sv1; more than L: the top-L first): one wave
+// per source -- sort in hash order, write, range index, norm1 against the old row, maxDiff
+// (finish_source)
 __host__ __device__ constexpr size_t svfin_lds_bytes(int Lp) { return (size_t)Lp * 12 + 1024 + (size_t)Lp * 20; }
 __global__ void __launch_bounds__(64) k_svfin(DevSlab s, IterArgs a, const int32_t* vid, int d0, const int32_t* in_k,
                                               const double* in_v, const int32_t* in_n, int Lp,
@@ -901,12 +910,10 @@ __global__ void __launch_bounds__(64) k_svfin(DevSlab s, IterArgs a, const int32
   int* hk = reinterpret_cast<int*>(smem + (size_t)Lp * 12 + 1024);
   int* hv = hk + 2 * Lp;
   int* mf = hv + 2 * Lp;
-  const int32_t* ik = in_k + (int64_t)d * Lp;
-  const double* iv = in_v + (int64_t)d * Lp;
-  for (int i = lane_id(); i < n; i += WAVE) { rk[i] = ik[i]; rv[i] = dbits(iv[i]); }
-  wave_fence();
-  finish_source(v, n, [&](int i) { return rk[i]; }, [&](int i) { return bitsd(rv[i]); }, s, a, hist, rv, rk, Lp, hk, hv,
-                mf, maxdiff, stats);
+  const int32_t* ik = in_k + (int64_t)d * sv_ostride(Lp);
+  const double* iv = in_v + (int64_t)d * sv_ostride(Lp);
+  finish_source(v, n, [&](int i) { return ik[i]; }, [&](int i) { return iv[i]; }, s, a, hist, rv, rk, Lp, hk, hv, mf,
+                maxdiff, stats);
 }
 
 // slice k of S of the successor list [b, e)

@@ -431,7 +431,7 @@ constexpr int XR_SLOTS = 8;  // table slots per thread (T <= 8 * blockDim: T / W
 __device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& s, const IterArgs& a,
                                           const XDesc& xd, int d, bool publish, double tau0, double tau_spec,
                                           unsigned long long* xtau, int32_t* pk, double* ps, uint32_t* pc,
-                                          uint32_t* dsum, long long* tph = nullptr, int slot = 0) {
+                                          uint32_t* dsum, long long* tph = nullptr, int slot = 0, int cap = 0) {
   const int L = s.L;
   const int v = xd.v;
   // a list range may already filter by the bound the source's other ranges published
@@ -493,7 +493,9 @@ __device__ __forceinline__ void xr_finish(const XrLds& x, int T, const DevSlab& 
   auto valat = [&](int i) { return dv[i]; };
   SelCrit sc;
   sc.tie = false; sc.pa = 0; sc.ma = 0; sc.pb = 0; sc.mb = 0;
-  const bool cut = U > L;
+  // (a one-range source with at most `cap` kept entries emits them all: k_xfin1 selects, with a
+  // 5-KB wave instead of this workgroup's table -- round 6, as the wave tier's k_wfin)
+  const bool cut = U > L && !(cap && !publish && U <= cap);
   if (tph) xr_lap(a, slot, *tph);  // settle + compact
   if (cut) sc = wg_select_top(x.w, U, L, keyat, valat, [](int) { return true; }, ts);
   // (wg_select_top ends on a barrier)
@@ -557,12 +559,12 @@ __global__ void __launch_bounds__(64) k_xfin1(DevSlab s, IterArgs a, const XDesc
   int* hk = reinterpret_cast<int*>(smem + (size_t)Lp * 12 + 1024);
   int* hv = hk + 2 * Lp;
   int* mf = hv + 2 * Lp;
-  const int n = (int)pc[d];
-  for (int i = lane_id(); i < n; i += WAVE) { rk[i] = pk[xd.pt_off + i]; rv[i] = dbits(ps[xd.pt_off + i]); }
-  wave_fence();
+  const int n = (int)pc[d];  // (<= L, or <= the k_xr list cap: finish_source selects then)
   if (dlast && !a.unit && lane_id() == 0) dlast[xd.v] = (int32_t)dsum[d];
-  finish_source(xd.v, n, [&](int i) { return rk[i]; }, [&](int i) { return bitsd(rv[i]); }, s, a, hist, rv, rk, Lp,
-                hk, hv, mf, maxdiff, stats);
+  const int32_t* lk = pk + xd.pt_off;
+  const double* lv = ps + xd.pt_off;
+  finish_source(xd.v, n, [&](int i) { return lk[i]; }, [&](int i) { return lv[i]; }, s, a, hist, rv, rk, Lp, hk, hv, mf,
+                maxdiff, stats);
 }
 
 // range r of R of a hub source: key k belongs to range ((hash_b(k) * R) >> 32) -- hash_b orders the
@@ -578,7 +580,7 @@ struct XTask { int32_t d; int32_t r; };
 __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, const XDesc* xdesc,
                                              const XTask* tasks, int T, int budget, int Lp, unsigned long long* xtau,
                                              int32_t* pk, double* ps, uint32_t* pc, uint32_t* dsum,
-                                             int32_t* oflag, int32_t* ovl) {
+                                             int32_t* oflag, int32_t* ovl, int xcap) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int W = blockDim.x >> 6, wv = threadIdx.x >> 6;
   const XrLds x = xr_carve(smem, T, W, Lp);
@@ -650,7 +652,7 @@ __global__ void __launch_bounds__(1024) k_xr(DevGraph g, DevSlab s, IterArgs a, 
     const int64_t cr = s.lrow((a.active == 1) ? a.sB : a.sA, v);
     if (s.len[cr] == s.L) tau_spec = XR_SPEC * s.rmin[cr];
   }
-  xr_finish(x, T, s, a, xd, tk.d, R > 1, tau_rows, tau_spec, xtau, pk, ps, pc, dsum, a.diag ? &tph : nullptr, 185);
+  xr_finish(x, T, s, a, xd, tk.d, R > 1, tau_rows, tau_spec, xtau, pk, ps, pc, dsum, a.diag ? &tph : nullptr, 185, xcap);
 }
 
 // One workgroup per staged bucket of a partitioned hub source: the bucket's records are

@@ -221,6 +221,8 @@ struct ppr_plan {
   // bounded probes (tests force them to run out): exact wave-tier overflow list and knobs
   int32_t* d_wovl = nullptr;          // [1 + n]: count, sources whose wave-tier table ran out
   int wave_split_T = 256;             // PPR_WAVE_SPLIT: wave tiers with T >= this end in k_wfin (0: none)
+  int xr_cap = 0;                     // PPR_XR_LISTCAP: one-range k_xr sources emit up to this many unselected
+                                      // entries for k_xfin1 (set to 2 Lp at plan creation; 0: k_xr selects)
   int wave_cap = 0;                   // (tests) PPR_WAVE_CAP: list entries per split source (>= L; 0: 2 Lp)
   unsigned char* d_wl = nullptr;      // their lists (merge_xs.h WList)
   size_t wl_bytes = 0;

@@ -263,6 +263,8 @@ def test_gpu_speculative_bound_bit_exact(env, want_redo, monkeypatch, capfd, cha
     {"PPR_WAVE_WPB": "4"},                                        # 4-wave blocks in the wave tier
     {"PPR_WAVE_BY_D": "1"},                                       # wave tiers sized by last distinct keys
     {"PPR_WAVE_BY_D": "1", "PPR_XR_DSCALE": "5"},                 # ... with every overflow path busy
+    {"PPR_XR_LISTCAP": "0"},                                      # k_xr selects every one-range source itself
+    {"PPR_XR_LISTCAP": "1", "PPR_SV": "0"},                       # ... k_xfin1 gets lists of <= L only
     {"PPR_WAVE_SPLIT": "0"},                                      # every wave-tier row written by its wave
     {"PPR_WAVE_SPLIT": "256"},                                    # ... by k_wfin from the wave's list, all tiers
     {"PPR_WAVE_SPLIT": "256", "PPR_WAVE_TDIV": "2"},              # ... with table overflows beside them
