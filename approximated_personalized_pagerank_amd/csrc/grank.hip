@@ -535,7 +535,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         {(const void*)k_hub_scatter<true>, "k_hub_scatter<true>"},
         {(const void*)k_hub_hot, "k_hub_hot"},
         {(const void*)k_hub_join, "k_hub_join"},
-        {(const void*)k_merge_lds_x, "k_merge_lds_x"},
+        {(const void*)k_merge_lds_x<false>, "k_merge_lds_x"},
+        {(const void*)k_merge_lds_x<true>, "k_merge_lds_x<split>"},
         {(const void*)k_wfin, "k_wfin"},
         {(const void*)k_xr, "k_xr"},
         {(const void*)k_xm<4>, "k_xm<4>"},
@@ -1414,10 +1415,21 @@ struct XhDefer {
   bool live = false;   // launches queued, not yet collected
   int depth = 0;
   size_t o_ov = 0;
-  std::vector<int32_t> src, cand, deg, xv;
-  std::vector<int64_t> dest;
+  // the caller's lists (run_xhubs keeps them alive and unchanged until xhubs_finish)
+  const std::vector<int32_t>* src = nullptr;
+  const std::vector<int32_t>* cand = nullptr;
+  const std::vector<int32_t>* deg = nullptr;
+  const std::vector<int64_t>* dest = nullptr;
+  std::vector<int32_t> xv;
 };
 static int xhubs_finish(ppr_plan* p, const IterArgs& a, XhDefer& df, unsigned long long* maxdiff);
+
+// (PPR_SV_LOG) host planning sub-phase laps: xh_sub[k] += seconds since t
+static inline void sub_lap(ppr_plan* p, int k, std::chrono::steady_clock::time_point& t) {
+  const auto t2 = std::chrono::steady_clock::now();
+  p->xh_sub[k] += std::chrono::duration<double>(t2 - t).count();
+  t = t2;
+}
 
 static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int32_t>& src,
                           const std::vector<int32_t>& cand, const std::vector<int32_t>& deg,
@@ -1425,6 +1437,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
                           XhDefer* defer = nullptr) {
   const size_t n = src.size();
   if (!n) return PPR_OK;
+  auto tsub = std::chrono::steady_clock::now();
   hipStream_t st = p->stream;
   hipStream_t sw = p->stream3 ? p->stream3 : st;
   DevGraph g{p->d_rp, p->d_colx, p->n};
@@ -1437,8 +1450,14 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
                       {std::min(4096, p->xr_T), std::min(4096, p->xr_T) / 512},
                       {p->xr_T, p->xr_T / 512}};
   auto cap_of = [&](int T) { return (int64_t)T * p->xr_fill / 100; };
-  std::vector<int32_t> rng;            // ranges per walked source (0: partitioned, -1: HBM table)
-  std::vector<uint8_t> ci;             // table class of a walked source
+  // (per-thread scratch kept across calls: no page faults on fresh vectors each iteration; a call's
+  // lists are dead before the nested redo call of its tail or of xhubs_finish reuses them)
+  static thread_local std::vector<int32_t> rng_tl;
+  static thread_local std::vector<uint8_t> ci_tl;
+  static thread_local std::vector<XDesc> xd_tl;
+  static thread_local std::vector<XTask> tasks_tl[3];
+  std::vector<int32_t>& rng = rng_tl;  // ranges per walked source (0: partitioned, -1: HBM table)
+  std::vector<uint8_t>& ci = ci_tl;    // table class of a walked source
   rng.resize(n);
   ci.resize(n);
   std::vector<int32_t> bsrc, bcand;    // partitioned: sources | candidate counts, then degrees
@@ -1466,9 +1485,14 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       bdest.push_back((int32_t)std::min<int64_t>(dest[i], INT32_MAX));
     }
   }
+  sub_lap(p, 0, tsub);  // range planning: classes
   // ranged sources: multi-range ones first (k_xfinal covers descriptors [0, nmulti))
-  std::vector<XDesc> xd;
-  std::vector<XTask> tasks[3];
+  std::vector<XDesc>& xd = xd_tl;
+  std::vector<XTask>* tasks = tasks_tl;
+  xd.clear();
+  for (int c = 0; c < 3; c++) tasks[c].clear();
+  xd.reserve(n);
+  tasks[0].reserve(n);
   int64_t pt = 0;
   for (int pass = 0; pass < 2; pass++)
     for (size_t i = 0; i < n; i++) {
@@ -1487,6 +1511,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
       xd.push_back(x);
       for (int r = 0; r < rng[i]; r++) tasks[ci[i]].push_back(XTask{d, r});
     }
+  sub_lap(p, 1, tsub);  // range planning: descriptors
   int64_t nmulti = 0;
   for (const XDesc& x : xd) nmulti += x.R > 1;
   const size_t nx = xd.size();
@@ -1555,6 +1580,7 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
         k += tasks[c].size();
       }
     }
+    sub_lap(p, 2, tsub);  // range planning: staging
     HIP_OK(hipMemcpyAsync(b, hb, up, hipMemcpyHostToDevice, sw));
     HIP_OK(hipMemsetAsync(b + o_z, 0, total - o_z, sw));
     // kernel-stat group 5: the range engines (k_xr, k_xfinal, k_xfin1) of this call on sw; SURVEY
@@ -1604,13 +1630,14 @@ static int run_xhubs_list(ppr_plan* p, const IterArgs& a, const std::vector<int3
     }
     if (!a.unit && !a.mc) kst_end(p, 5, sw, p->kst_pend_bytes[5]);
   }
+  sub_lap(p, 3, tsub);  // range planning: launches
   // deferred completion (no partitioned or HBM-table source in this call: those plan on the host
   // from device counts and would serialise behind the range engines here anyway)
   if (defer && defer->want && nx && bsrc.empty() && xgs.empty()) {
     defer->live = true;
     defer->depth = depth;
     defer->o_ov = o_ov;
-    defer->src = src; defer->cand = cand; defer->deg = deg; defer->dest = dest;
+    defer->src = &src; defer->cand = &cand; defer->deg = &deg; defer->dest = &dest;
     defer->xv.resize(nx);
     for (size_t i = 0; i < nx; i++) defer->xv[i] = xd[i].v;
     return PPR_OK;
@@ -1682,8 +1709,12 @@ static int xhubs_finish(ppr_plan* p, const IterArgs& a, XhDefer& df, unsigned lo
   HIP_OK(hipMemcpyAsync(od.data(), p->d_xs + df.o_ov + 4, 4 * (size_t)novf, hipMemcpyDeviceToHost, sw));
   HIP_OK(hipStreamSynchronize(sw));
   p->xr_redo += novf;
-  std::vector<std::pair<int32_t, int32_t>> idx(df.src.size());
-  for (size_t i = 0; i < df.src.size(); i++) idx[i] = {df.src[i], (int32_t)i};
+  const std::vector<int32_t>& dsrc = *df.src;
+  const std::vector<int32_t>& dcand = *df.cand;
+  const std::vector<int32_t>& ddeg = *df.deg;
+  const std::vector<int64_t>& ddest = *df.dest;
+  std::vector<std::pair<int32_t, int32_t>> idx(dsrc.size());
+  for (size_t i = 0; i < dsrc.size(); i++) idx[i] = {dsrc[i], (int32_t)i};
   std::sort(idx.begin(), idx.end());
   std::vector<int32_t> rsrc, rcand, rdeg;
   std::vector<int64_t> rdest;
@@ -1692,11 +1723,11 @@ static int xhubs_finish(ppr_plan* p, const IterArgs& a, XhDefer& df, unsigned lo
     auto it = std::lower_bound(idx.begin(), idx.end(), std::make_pair(v, (int32_t)-1));
     if (it == idx.end() || it->first != v) return PPR_ERR_HIP;
     const size_t i = (size_t)it->second;
-    rsrc.push_back(df.src[i]);
-    rcand.push_back(df.cand[i]);
-    rdeg.push_back(df.deg[i]);
-    const int64_t grown = 4 * df.dest[i] + 64;
-    rdest.push_back(df.dest[i] >= (int64_t)df.cand[i] ? grown : std::min<int64_t>((int64_t)df.cand[i], grown));
+    rsrc.push_back(dsrc[i]);
+    rcand.push_back(dcand[i]);
+    rdeg.push_back(ddeg[i]);
+    const int64_t grown = 4 * ddest[i] + 64;
+    rdest.push_back(ddest[i] >= (int64_t)dcand[i] ? grown : std::min<int64_t>((int64_t)dcand[i], grown));
   }
   return run_xhubs_list(p, a, rsrc, rcand, rdeg, rdest, maxdiff, df.depth + 1);
 }
@@ -1719,6 +1750,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   const size_t n = src.size();
   run.live = false;
   if (!n) return PPR_OK;
+  auto tsub = std::chrono::steady_clock::now();
   DevGraph g{p->d_rp, p->d_colx, p->n};
   const DevSlab s = dev_slab(p);
   const int Lp = p->Lp;
@@ -1729,8 +1761,10 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   auto klass = [&](int64_t c) { return c > p->sv_slice ? 0 : c >= p->sv_mid ? 1 : c >= p->sv_small ? 2 : 3; };
   auto step = [](int64_t c) { return std::min(255, (int)(8.0 * std::log2((double)std::max<int64_t>(1, c)))); };
   constexpr int NKEY = 4 * 256;
-  std::vector<uint32_t> cnt(NKEY + 1, 0u);
-  std::vector<uint16_t> key(n);
+  std::vector<uint32_t>& cnt = p->xhs.svcnt;
+  cnt.assign(NKEY + 1, 0u);
+  std::vector<uint16_t>& key = p->xhs.svkey;
+  key.resize(n);
   for (size_t i = 0; i < n; i++) {
     key[i] = (uint16_t)(klass(cand[i]) * 256 + (255 - step(cand[i])));
     cnt[key[i] + 1]++;
@@ -1745,6 +1779,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   auto sv_algo_bytes = [&](size_t i) {
     return 8.0 + 8.0 * deg[i] + 12.0 * ((double)cand[i] - 1.0) + 24.0 * (double)p->L + 4.0;
   };
+  sub_lap(p, 4, tsub);  // sieve planning: order
   std::vector<SvDesc> desc(nm);
   std::vector<SvTask> tasks;
   int64_t tg_total = 0;
@@ -1798,6 +1833,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
   hipStream_t s1 = p->stream_sv, s2 = p->stream_sv2, s3 = p->stream_sv3;
   // descriptors up and the zeroed region cleared on the mid class's stream (the plan stream: idle
   // once the classification is read), the other sieve streams wait for it
+  sub_lap(p, 5, tsub);  // sieve planning: descriptors + staging
   HIP_OK(hipMemcpyAsync(b, hb, up, hipMemcpyHostToDevice, s3));
   HIP_OK(hipMemsetAsync(b + o_z, 0, total - o_z, s3));
   HIP_OK(hipEventRecord(p->ev_sv, s3));
@@ -1884,6 +1920,7 @@ static int sieve_launch(ppr_plan* p, const IterArgs& a, const std::vector<int32_
     kst_end(p, 4, s1, bytes);
     p->merge_launches += 3;
   }
+  sub_lap(p, 6, tsub);  // sieve planning: launches
   p->sv_sources += (int64_t)nx;
   run.o_ovl = o_ov;
   run.o_os = o_os;
@@ -1940,15 +1977,20 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
   auto tl = now();
   const auto t_in = tl;
   struct LapLog {  // PPR_SV_LOG: this call's host phases (ms), printed when it returns
-    const IterArgs& a; double* v; std::chrono::steady_clock::time_point t0;
+    ppr_plan* p; const IterArgs& a; double* v; std::chrono::steady_clock::time_point t0;
     ~LapLog() {
       if (!getenv("PPR_SV_LOG")) return;
       const double tot = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       fprintf(stderr, "ppr_xh_laps it %d total %.2f gather %.2f classify %.2f sieve_launch %.2f engines %.2f "
               "sieve_wait %.2f handback %.2f\n", a.iter, 1e3 * tot, 1e3 * v[0], 1e3 * v[1], 1e3 * v[2], 1e3 * v[3],
               1e3 * v[4], 1e3 * (v[5] + v[6]));
+      const double* u = p->xh_sub;
+      fprintf(stderr, "ppr_xh_sub it %d range classes %.2f descriptors %.2f staging %.2f launches %.2f sieve order %.2f "
+              "descriptors+staging %.2f launches %.2f\n", a.iter, 1e3 * u[0], 1e3 * u[1], 1e3 * u[2], 1e3 * u[3],
+              1e3 * u[4], 1e3 * u[5], 1e3 * u[6]);
+      for (int k = 0; k < 8; k++) p->xh_sub[k] = 0.0;
     }
-  } laplog{a, lapv, t_in};
+  } laplog{p, a, lapv, t_in};
   hipStream_t st = p->stream;
   const size_t nh = (size_t)count;
   {
@@ -1968,12 +2010,17 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
   HIP_OK(hipGetLastError());
   HIP_OK(hipMemcpyAsync(h + nh, d_g, 16 * nh, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
-  std::vector<int32_t> hcopy(h, h + 5 * nh);  // (the pinned buffer is restaged by later calls)
+  std::vector<int32_t>& hcopy = p->xhs.h;  // (the pinned buffer is restaged by later calls)
+  hcopy.assign(h, h + 5 * nh);
   h = hcopy.data();
   lap(0, tl);  // gather + copy back
   const bool sieve = p->sv_enabled && a.xs && !a.unit && !a.mc && p->hot_n == 0;
-  std::vector<int32_t> src, cand, deg, ssrc, scand, sdeg, sidx;
-  std::vector<int64_t> dest;
+  std::vector<int32_t>& src = p->xhs.src; std::vector<int32_t>& cand = p->xhs.cand;
+  std::vector<int32_t>& deg = p->xhs.deg; std::vector<int32_t>& ssrc = p->xhs.ssrc;
+  std::vector<int32_t>& scand = p->xhs.scand; std::vector<int32_t>& sdeg = p->xhs.sdeg;
+  std::vector<int32_t>& sidx = p->xhs.sidx;
+  std::vector<int64_t>& dest = p->xhs.dest;
+  src.clear(); cand.clear(); deg.clear(); ssrc.clear(); scand.clear(); sdeg.clear(); sidx.clear(); dest.clear();
   // distinct keys expected: the last merge's count (rows change little between updates) plus a
   // margin, else (first merge) 60 % of the candidates; never more than the candidates + 1
   auto estimate = [&](size_t i) {
@@ -1983,6 +2030,8 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
     if (p->xr_dscale != 100) x = std::max<int64_t>(1, x * p->xr_dscale / 100);
     return x;
   };
+  src.reserve(nh); cand.reserve(nh); deg.reserve(nh); dest.reserve(nh);
+  if (sieve) { ssrc.reserve(nh); scand.reserve(nh); sdeg.reserve(nh); sidx.reserve(nh); }
   for (size_t i = 0; i < nh; i++) {
     const int32_t c = h[nh + i];
     if (sieve && h[4 * nh + i] == (int32_t)p->L && c >= p->sv_min && c < (1 << 30)) {
@@ -2015,7 +2064,8 @@ static int run_xhubs(ppr_plan* p, const IterArgs& a, const int32_t* d_list, int6
     if (r) return r;
   }
   lap(3, tl);  // range / partition engines (their syncs included)
-  std::vector<int32_t> back;
+  std::vector<int32_t>& back = p->xhs.back;
+  back.clear();
   const int64_t dev0 = p->sv_redo_dev;
   { int r = sieve_collect(p, run, back); if (r) return r; }
   lap(4, tl);  // waiting for the sieve
@@ -2234,7 +2284,8 @@ reclassify:
       }
       const int32_t* tl = p->d_tier_lists + (int64_t)t * p->n;
       const size_t wlds = split ? lds_wave_bytes_xs(Tw) : lds_wave_bytes_x(Tw, p->Lp);
-      hipLaunchKernelGGL(k_merge_lds_x, dim3((unsigned)blocks), dim3(64 * wpb), wlds * wpb, sw, g, s, a, tl, (int64_t)cnt[t], Tw, p->Lp, maxdiff, p->d_stats, p->d_dlast, p->d_wovl, wl);
+      hipLaunchKernelGGL(split ? k_merge_lds_x<true> : k_merge_lds_x<false>, dim3((unsigned)blocks), dim3(64 * wpb),
+                         wlds * wpb, sw, g, s, a, tl, (int64_t)cnt[t], Tw, p->Lp, maxdiff, p->d_stats, p->d_dlast, p->d_wovl, wl);
       if (split) {
         HIP_OK(hipGetLastError());
         hipLaunchKernelGGL(k_wfin, dim3((unsigned)(((int64_t)cnt[t] + 3) / 4)), dim3(256), wfin_lds_bytes(p->Lp) * 4, sw,

@@ -172,7 +172,11 @@ struct WList {
 // (a table that runs out -- never, at T >= 4/3 of the tier's candidate cap, unless PPR_WAVE_TDIV
 // shrinks it for the tests -- writes no row: the source goes to `wovl` ([0] count, then sources)
 // and the host merges it again with the workgroup engines)
-__global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, IterArgs a, const int32_t* list,
+#ifndef PPR_WX_WAVES
+#define PPR_WX_WAVES 1  // (A/B: waves per SIMD the compiler sizes the split k_merge_lds_x's registers for)
+#endif
+template <bool kSplit>
+__global__ void __launch_bounds__(256, kSplit ? PPR_WX_WAVES : 1) k_merge_lds_x(DevGraph g, DevSlab s, IterArgs a, const int32_t* list,
                                                      int64_t count, int T, int Lp, unsigned long long* maxdiff,
                                                      unsigned long long* stats, int32_t* dlast, int32_t* wovl,
                                                      WList wl) {
@@ -180,7 +184,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   const int wv = threadIdx.x >> 6;
   const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (w >= count) return;
-  unsigned char* base = smem + (size_t)wv * (wl.cap ? lds_wave_bytes_xs(T) : lds_wave_bytes_x(T, Lp));
+  unsigned char* base = smem + (size_t)wv * (kSplit ? lds_wave_bytes_xs(T) : lds_wave_bytes_x(T, Lp));
   const XTable t = xt_carve(base, T);
   uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 16);
   uint64_t* rv = reinterpret_cast<uint64_t*>(base + (size_t)T * 16 + 1024);
@@ -229,7 +233,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   if (__ballot(bad)) {  // table ran out: no row, the host redoes the source
     if (lane_id() == 0) {
       wovl[1 + atomicAdd(&wovl[0], 1)] = v;
-      if (wl.cap) wl.n[w] = -1;
+      if (kSplit) wl.n[w] = -1;
     }
     return;
   }
@@ -288,7 +292,7 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
   if (dlast && !a.unit && lane_id() == 0) dlast[v] = D;  // (init counts predict nothing)
   fs_lap(a, 280, 2, tl);  // (slot 282: settle + compact)
   if (a.diag && !a.unit && lane_id() == 0) { diag_add(a.diag, 280, 1ull); diag_add(a.diag, 287, (unsigned long long)U); }
-  if (wl.cap) {  // the list for k_wfin: every kept entry, or the top-L of more than cap (cap >= L)
+  if (kSplit) {  // the list for k_wfin: every kept entry, or the top-L of more than cap (cap >= L)
     U = __builtin_amdgcn_readfirstlane(U);
     const int64_t o = w * (int64_t)wl.cap;
     if (U <= wl.cap) {
@@ -311,10 +315,10 @@ __global__ void __launch_bounds__(256) k_merge_lds_x(DevGraph g, DevSlab s, Iter
       nb += __popcll(m);
     }
     if (lane_id() == 0) wl.n[w] = nb;
-    return;
+  } else {
+    finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return vals[i]; }, s, a, hist, rv, rk, Lp, hk, hv,
+                  mf, maxdiff, stats, a.unit ? -1 : 283);  // (283 select, 284 row write, 285 norm1)
   }
-  finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return vals[i]; }, s, a, hist, rv, rk, Lp, hk, hv,
-                mf, maxdiff, stats, a.unit ? -1 : 283);  // (283 select, 284 row write, 285 norm1)
 }
 
 // the row of a split wave-tier source from its list (one wave per source, 4 per block)

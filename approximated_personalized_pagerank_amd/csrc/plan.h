@@ -221,6 +221,15 @@ struct ppr_plan {
   // bounded probes (tests force them to run out): exact wave-tier overflow list and knobs
   int32_t* d_wovl = nullptr;          // [1 + n]: count, sources whose wave-tier table ran out
   int wave_split_T = 256;             // PPR_WAVE_SPLIT: wave tiers with T >= this end in k_wfin (0: none)
+  // run_xhubs's per-call host lists, kept across iterations (capacity only): fresh vectors of a
+  // few hundred thousand entries each cost the planning their page faults every iteration
+  struct XhScratch {
+    std::vector<int32_t> h, src, cand, deg, ssrc, scand, sdeg, sidx, back;
+    std::vector<int64_t> dest;
+    std::vector<uint16_t> svkey;
+    std::vector<uint32_t> svcnt;
+  } xhs;
+  double xh_sub[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (PPR_SV_LOG) host planning sub-phases, seconds
   int xr_cap = 0;                     // PPR_XR_LISTCAP: one-range k_xr sources emit up to this many unselected
                                       // entries for k_xfin1 (set to 2 Lp at plan creation; 0: k_xr selects)
   int wave_cap = 0;                   // (tests) PPR_WAVE_CAP: list entries per split source (>= L; 0: 2 Lp)
