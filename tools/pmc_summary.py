@@ -19,7 +19,7 @@ import json
 import sys
 
 MERGE_KERNELS = ("k_classify", "k_merge_lds", "k_merge_wg", "k_merge_glb", "k_hub_", "rocprim", "k_stat", "k_xr", "k_xb",
-                 "k_xfin", "k_gather", "k_sv", "k_xg_")
+                 "k_xfin", "k_gather", "k_sv", "k_xg_", "k_wfin", "k_xm")
 
 
 def per_kernel(path):
