@@ -458,6 +458,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       p->xr_cap = 2 * p->Lp;
       const char* exc = getenv("PPR_XR_LISTCAP");  // (0: k_xr selects every one-range source itself)
       if (exc) p->xr_cap = atoi(exc) <= 0 ? 0 : std::max<int>((int)L, atoi(exc));
+      const char* ewm = getenv("PPR_WL_MAX_MB");  // (tests: a small bound forces the chunked lists)
+      if (ewm) p->wl_max = std::max<size_t>(1, (size_t)atoll(ewm)) << 20;
       const char* ewc = getenv("PPR_WAVE_CAP");
       if (ewc) p->wave_cap = std::max(0, atoi(ewc));
       const char* e9 = getenv("PPR_XR_BUDGET");
@@ -2258,6 +2260,40 @@ reclassify:
   // the classification is complete (host sync): the wave tiers need no event to start on their stream
   hipStream_t sw = p->stream_wave ? p->stream_wave : st;
   bool wave_ev = false;
+  // split wave tiers (exact sum): every tier's lists in one region, reused tier after tier (walk,
+  // then its rows); a tier whose lists would pass wl_max bytes goes in chunks. (Queueing every
+  // tier's walk before the first row kernel, one region per tier, measured neutral: round 6.)
+  WList wls[NT];
+  const int wcap = p->wave_cap ? std::max<int>((int)p->L, p->wave_cap) : 2 * p->Lp;
+  const size_t wrec = (size_t)wcap * 12 + 4;  // list bytes per source
+  const int64_t wchunk = std::max<int64_t>(1, (int64_t)((p->wl_max - 512) / wrec));  // sources per chunk
+  {
+    int64_t most = 0;
+    for (int t = 0; t < NT; t++) {
+      wls[t] = WList{nullptr, nullptr, nullptr, 0};
+      if (!cnt[t] || !p->tierT[t] || !a.xs || a.unit || p->wave_split_T <= 0 ||
+          std::max(64, p->tierT[t] >> p->wave_tdiv) < p->wave_split_T)
+        continue;
+      wls[t].cap = wcap;
+      most = std::max<int64_t>(most, std::min<int64_t>((int64_t)cnt[t], wchunk));
+    }
+    if (most) {
+      int rc = ensure_dev(&p->d_wl, &p->wl_bytes, (size_t)most * wrec + 512);
+      if (rc) return rc;
+      const size_t nk = (size_t)most * (size_t)wcap;
+      for (int t = 0; t < NT; t++)
+        if (wls[t].cap) {
+          wls[t].v = reinterpret_cast<double*>(p->d_wl);
+          wls[t].k = reinterpret_cast<int32_t*>(p->d_wl + nk * 8);
+          wls[t].n = reinterpret_cast<int32_t*>(p->d_wl + nk * 12);
+        }
+    }
+  }
+  auto launch_wfin = [&](const int32_t* tl, int64_t c, const WList& wl) {
+    hipLaunchKernelGGL(k_wfin, dim3((unsigned)((c + 3) / 4)), dim3(256), wfin_lds_bytes(p->Lp) * 4, sw, s, a, tl, c, wl,
+                       p->Lp, maxdiff, p->d_stats);
+    p->merge_launches++;
+  };
   for (int t = 0; t < NT; t++) {
     if (!cnt[t] || !p->tierT[t]) continue;
     if (!wave_ev && !a.unit && !a.mc) { kst_begin(p, 0, sw); wave_ev = true; }
@@ -2268,29 +2304,21 @@ reclassify:
       if (!p->wave_x_launched) HIP_OK(hipMemsetAsync(p->d_wovl, 0, 4, sw));
       p->wave_x_launched = true;
       const int Tw = std::max(64, p->tierT[t] >> p->wave_tdiv);  // (PPR_WAVE_TDIV: tests of the overflow redo)
-      // the largest tables end after their compaction: the row in k_wfin (merge_xs.h WList)
-      WList wl{nullptr, nullptr, nullptr, 0};
-      const bool split = !a.unit && p->wave_split_T > 0 && Tw >= p->wave_split_T;
-      if (split) {
-        const int cap = p->wave_cap ? std::max<int>((int)p->L, p->wave_cap) : 2 * p->Lp;
-        const size_t nk = (size_t)cnt[t] * (size_t)cap;
-        const size_t need = nk * 12 + 4 * (size_t)cnt[t] + 512;
-        int rc = ensure_dev(&p->d_wl, &p->wl_bytes, need);
-        if (rc) return rc;
-        wl.v = reinterpret_cast<double*>(p->d_wl);
-        wl.k = reinterpret_cast<int32_t*>(p->d_wl + nk * 8);
-        wl.n = reinterpret_cast<int32_t*>(p->d_wl + nk * 12);
-        wl.cap = cap;
-      }
+      // the tables end after their compaction: the row in k_wfin (merge_xs.h WList)
+      const WList wl = wls[t];
+      const bool split = wl.cap != 0;
       const int32_t* tl = p->d_tier_lists + (int64_t)t * p->n;
       const size_t wlds = split ? lds_wave_bytes_xs(Tw) : lds_wave_bytes_x(Tw, p->Lp);
-      hipLaunchKernelGGL(split ? k_merge_lds_x<true> : k_merge_lds_x<false>, dim3((unsigned)blocks), dim3(64 * wpb),
-                         wlds * wpb, sw, g, s, a, tl, (int64_t)cnt[t], Tw, p->Lp, maxdiff, p->d_stats, p->d_dlast, p->d_wovl, wl);
-      if (split) {
-        HIP_OK(hipGetLastError());
-        hipLaunchKernelGGL(k_wfin, dim3((unsigned)(((int64_t)cnt[t] + 3) / 4)), dim3(256), wfin_lds_bytes(p->Lp) * 4, sw,
-                           s, a, tl, (int64_t)cnt[t], wl, p->Lp, maxdiff, p->d_stats);
-        p->merge_launches++;
+      const int64_t step = split ? wchunk : (int64_t)cnt[t];
+      for (int64_t c0 = 0; c0 < (int64_t)cnt[t]; c0 += step) {
+        const int64_t c = std::min<int64_t>(step, (int64_t)cnt[t] - c0);
+        hipLaunchKernelGGL(split ? k_merge_lds_x<true> : k_merge_lds_x<false>, dim3((unsigned)((c + wpb - 1) / wpb)),
+                           dim3(64 * wpb), wlds * wpb, sw, g, s, a, tl + c0, c, Tw, p->Lp, maxdiff, p->d_stats,
+                           p->d_dlast, p->d_wovl, wl);
+        if (split) {
+          HIP_OK(hipGetLastError());
+          launch_wfin(tl + c0, c, wl);
+        }
       }
     } else {
       const int Tw = std::max(64, p->tierT[t] >> p->wave_tdiv);  // (PPR_WAVE_TDIV: tests of the bounded probes)
@@ -3117,6 +3145,7 @@ static int x_exchange_routed(ppr_plan* p, uint32_t it, const XRoute& xr, int slo
   auto size_ok = [&](int r, int64_t z) { return z >= 8 && (size_t)z <= ro[r + 1] - ro[r]; };
   if (p->lgroup) {
     LocalGroup& G = *p->lgroup;
+    G.ok[me] = 1;  // (this call's verdict only: written again below, before the second barrier)
     HIP_OK(hipMemcpyAsync(hsz.data(), tx, 8 * (size_t)W, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));  // this rank's blocks are complete
     for (int d = 0; d < W; d++) {

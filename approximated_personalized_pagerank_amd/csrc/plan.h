@@ -114,7 +114,9 @@ struct ppr_plan {
   int hub_bw_blocks = 0;           // persistent k_hub_bucket_w grid
   bool rank_permute = false;       // PPR_TEST_RANK_PERMUTE (tests): IterArgs WI_RANK_PERMUTE
   uint32_t lds_rank = 0;           // k_probe_lds_rank: 32-bit add ranks in lane order (PPR_LDS_RANK=0 forces the ballot path)
-  uint32_t lds_rank64 = 0;         // ... and the 64-bit CAS / add order the one-shot buckets need
+  uint32_t lds_rank64 = 0;         // ... and the 64-bit add order (reported by PPR_TIMING only; round 6:
+                                   // the ordered paths check every chain's order themselves, so no
+                                   // result depends on either probe)
   bool seg_enabled = false;        // segmented hub buckets (k_hub_seg, PPR_HUB_SEG=1)
   int seg_bucket = 256, seg_t = 512, seg_wpb = 1;
   int hub_bw_ng = 2;               // PPR_BW_NG: groups per chunk (1, 2, 4 or 8)
@@ -234,6 +236,7 @@ struct ppr_plan {
                                       // entries for k_xfin1 (set to 2 Lp at plan creation; 0: k_xr selects)
   int wave_cap = 0;                   // (tests) PPR_WAVE_CAP: list entries per split source (>= L; 0: 2 Lp)
   unsigned char* d_wl = nullptr;      // their lists (merge_xs.h WList)
+  size_t wl_max = (size_t)4 << 30;    // PPR_WL_MAX_MB: most list bytes of one split-tier launch (else chunks)
   size_t wl_bytes = 0;
   bool wave_x_launched = false;
   int wave_tdiv = 0;                  // PPR_WAVE_TDIV (tests): wave-tier tables T >> this

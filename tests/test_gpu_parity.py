@@ -269,6 +269,7 @@ def test_gpu_speculative_bound_bit_exact(env, want_redo, monkeypatch, capfd, cha
     {"PPR_WAVE_SPLIT": "256"},                                    # ... by k_wfin from the wave's list, all tiers
     {"PPR_WAVE_SPLIT": "256", "PPR_WAVE_TDIV": "2"},              # ... with table overflows beside them
     {"PPR_WAVE_SPLIT": "256", "PPR_WAVE_CAP": "1"},               # ... lists of L: the wave selects first
+    {"PPR_WL_MAX_MB": "1"},                                       # ... lists bounded: tiers in chunks
     {"PPR_XM": "1"},                                              # one-range sources of the smallest class
     {"PPR_XM": "1", "PPR_SV": "0", "PPR_TIER_MASK": "0x20"},      # through k_xm (merge_xm.h, opt-in) ...
     {"PPR_XM": "1", "PPR_XR_DSCALE": "5", "PPR_SV": "0"},         # ... overflowing: redone as from k_xr
