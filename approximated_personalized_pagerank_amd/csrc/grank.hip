@@ -230,6 +230,8 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
       if (bytes > 64 * 1024) {
         hipFuncSetAttribute((const void*)k_merge_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_merge_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_merge_lds<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_merge_lds<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       }
     }
   if (p->tierCap[NT])
@@ -418,6 +420,18 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
     }
     const char* ee = getenv("PPR_XSHARD_ENDS");  // (any summation mode)
     p->xshard_ends = !(ee && atoi(ee) == 0);
+    {  // split wave tiers, any summation mode
+      const char* ews = getenv("PPR_WAVE_SPLIT");
+      if (ews) p->wave_split_T = std::max(0, atoi(ews));
+      const char* ewsc = getenv("PPR_WAVE_SPLIT_CHAIN");
+      if (ewsc) p->wave_split_chain = std::max(0, atoi(ewsc));
+      const char* ewsm = getenv("PPR_WAVE_SPLIT_MC");
+      if (ewsm) p->wave_split_mc = std::max(0, atoi(ewsm));
+      const char* ewm = getenv("PPR_WL_MAX_MB");  // (tests: a small bound forces the chunked lists)
+      if (ewm) p->wl_max = std::max<size_t>(1, (size_t)atoll(ewm)) << 20;
+      const char* ewc = getenv("PPR_WAVE_CAP");
+      if (ewc) p->wave_cap = std::max(0, atoi(ewc));
+    }
     if (p->xsum) {
       // the order-bound alternatives of the chain path do not apply: no hot pass, no speculative
       // bound, no workgroup tier (its overflow would fall to the chain-order HBM table)
@@ -453,15 +467,9 @@ int plan_alloc(int64_t n, const int64_t* row_ptr, const int32_t* colx, uint32_t 
         }
       TRY(dalloc(&p->d_dlast, n));
       TRY(dalloc(&p->d_wovl, n + 1));
-      const char* ews = getenv("PPR_WAVE_SPLIT");
-      if (ews) p->wave_split_T = std::max(0, atoi(ews));
       p->xr_cap = 2 * p->Lp;
       const char* exc = getenv("PPR_XR_LISTCAP");  // (0: k_xr selects every one-range source itself)
       if (exc) p->xr_cap = atoi(exc) <= 0 ? 0 : std::max<int>((int)L, atoi(exc));
-      const char* ewm = getenv("PPR_WL_MAX_MB");  // (tests: a small bound forces the chunked lists)
-      if (ewm) p->wl_max = std::max<size_t>(1, (size_t)atoll(ewm)) << 20;
-      const char* ewc = getenv("PPR_WAVE_CAP");
-      if (ewc) p->wave_cap = std::max(0, atoi(ewc));
       const char* e9 = getenv("PPR_XR_BUDGET");
       p->xr_budget_over = e9 && strcmp(e9, "over") == 0;
       if (hipMemset(p->d_dlast, 0, 4 * (size_t)(n > 0 ? n : 1)) != hipSuccess) { plan_free(p); return PPR_ERR_HIP; }
@@ -2271,8 +2279,8 @@ reclassify:
     int64_t most = 0;
     for (int t = 0; t < NT; t++) {
       wls[t] = WList{nullptr, nullptr, nullptr, 0};
-      if (!cnt[t] || !p->tierT[t] || !a.xs || a.unit || p->wave_split_T <= 0 ||
-          std::max(64, p->tierT[t] >> p->wave_tdiv) < p->wave_split_T)
+      const int split_T = a.xs ? p->wave_split_T : a.mc ? p->wave_split_mc : p->wave_split_chain;
+      if (!cnt[t] || !p->tierT[t] || a.unit || split_T <= 0 || std::max(64, p->tierT[t] >> p->wave_tdiv) < split_T)
         continue;
       wls[t].cap = wcap;
       most = std::max<int64_t>(most, std::min<int64_t>((int64_t)cnt[t], wchunk));
@@ -2322,11 +2330,23 @@ reclassify:
       }
     } else {
       const int Tw = std::max(64, p->tierT[t] >> p->wave_tdiv);  // (PPR_WAVE_TDIV: tests of the bounded probes)
-      const size_t bytes = lds_wave_bytes(Tw, p->Lp) * wpb;
-      hipLaunchKernelGGL(p->hot_n > 0 ? k_merge_lds<true> : k_merge_lds<false>, dim3((unsigned)blocks), dim3(64 * wpb),
-                         bytes, sw, g, s, a,
-                         p->d_tier_lists + (int64_t)t * p->n, (int64_t)cnt[t], Tw, p->Lp,
-                         maxdiff, p->d_stats);
+      const WList wl = wls[t];
+      const bool split = wl.cap != 0;
+      const int32_t* tl = p->d_tier_lists + (int64_t)t * p->n;
+      const size_t bytes = (split ? lds_wave_bytes_s(Tw) : lds_wave_bytes(Tw, p->Lp)) * wpb;
+      const bool hk = p->hot_n > 0;
+      const int64_t step = split ? wchunk : (int64_t)cnt[t];
+      for (int64_t c0 = 0; c0 < (int64_t)cnt[t]; c0 += step) {
+        const int64_t c = std::min<int64_t>(step, (int64_t)cnt[t] - c0);
+        hipLaunchKernelGGL(split ? (hk ? k_merge_lds<true, true> : k_merge_lds<false, true>)
+                                 : (hk ? k_merge_lds<true, false> : k_merge_lds<false, false>),
+                           dim3((unsigned)((c + wpb - 1) / wpb)), dim3(64 * wpb), bytes, sw, g, s, a, tl + c0, c, Tw,
+                           p->Lp, maxdiff, p->d_stats, wl);
+        if (split) {
+          HIP_OK(hipGetLastError());
+          launch_wfin(tl + c0, c, wl);
+        }
+      }
     }
     HIP_OK(hipGetLastError());
     p->merge_launches++;

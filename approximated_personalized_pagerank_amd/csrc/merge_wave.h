@@ -187,9 +187,7 @@ __global__ void __launch_bounds__(256) k_stat_written(DevSlab s, IterArgs a, con
   }
 }
 
-// per-wave LDS bytes for table size T and padded width Lp
-// layout: acc f64[T] | keys i32[T] | rv u64[Lp] | rk i32[Lp] | hist u32[256] | hk i32[2Lp] |
-//         hv i32[2Lp] | mf i32[Lp] | own u8[T]
+// per-wave LDS bytes for table size T and padded width Lp (layout: k_merge_lds below)
 __host__ __device__ constexpr size_t lds_wave_bytes(int T, int Lp) {
   return (size_t)T * 13 + (size_t)Lp * 12 + 1024 + (size_t)Lp * 20;
 }
@@ -349,28 +347,68 @@ __device__ __forceinline__ void hub_window_walk(const DevGraph& g, const DevSlab
 // flag bytes per wave of hub_window_walk
 constexpr int HUB_WALK_FLAGS = WAVE * HUB_TW_BATCH;
 
-template <bool HK>
+// Split epilogue of the wave tiers (round 6): the wave stops after its compaction
+// and writes its kept entries to a list in HBM; k_wfin (merge_xs.h) selects, writes the row and its
+// norm1 with a 5-KB wave, so the table's LDS is held for the walk only.
+struct WList {
+  int32_t* k;  // [count * cap] keys
+  double* v;   // [count * cap] values
+  int32_t* n;  // [count] entries (-1: the table ran out, the host redoes the source)
+  int cap;     // 0: no split; else >= L
+};
+// source w's list: every one of its U kept entries, or the top-L of more than cap (cap >= L)
+template <class K, class V>
+__device__ __forceinline__ void wave_emit_list(const WList& wl, int64_t w, int U, const K* keys, const V* vals, int v,
+                                               int L, uint32_t* hist) {
+  U = __builtin_amdgcn_readfirstlane(U);
+  const int64_t o = w * (int64_t)wl.cap;
+  if (U <= wl.cap) {
+    for (int i = lane_id(); i < U; i += WAVE) { wl.k[o + i] = (int32_t)keys[i]; wl.v[o + i] = (double)vals[i]; }
+    if (lane_id() == 0) wl.n[w] = U;
+    return;
+  }
+  const uint32_t ts = tie_salt(v);
+  const SelCrit c = select_top(U, L, [&](int i) { return (int)keys[i]; }, [&](int i) { return (double)vals[i]; }, hist, ts);
+  int nb = 0;
+  for (int i0 = 0; i0 < U; i0 += WAVE) {
+    const int i = i0 + lane_id();
+    const bool sel = i < U && sel_test(c, dbits((double)vals[i]), tie_w((int)keys[i], ts));
+    const uint64_t m = __ballot(sel);
+    if (sel) {
+      const int64_t q = o + nb + __popcll(m & lanemask_lt());
+      wl.k[q] = (int32_t)keys[i];
+      wl.v[q] = (double)vals[i];
+    }
+    nb += __popcll(m);
+  }
+  if (lane_id() == 0) wl.n[w] = nb;
+}
+
+// chain-order wave tier. LDS: acc f64[T] | keys i32[T] | own u8[T] | hist u32[256] | rv u64[Lp] |
+// rk i32[Lp] | hk i32[2Lp] | hv i32[2Lp] | mf i32[Lp]; split (kSplit): up to hist
+__host__ __device__ constexpr size_t lds_wave_bytes_s(int T) { return (size_t)T * 13 + 1024; }
+template <bool HK, bool kSplit = false>
 __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterArgs a,
                                                    const int32_t* list, int64_t count, int T,
                                                    int Lp, unsigned long long* maxdiff,
-                                                   unsigned long long* stats) {
+                                                   unsigned long long* stats, WList wl = WList{}) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int wv = threadIdx.x >> 6;
   const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (w >= count) return;
-  unsigned char* base = smem + (size_t)wv * lds_wave_bytes(T, Lp);
+  unsigned char* base = smem + (size_t)wv * (kSplit ? lds_wave_bytes_s(T) : lds_wave_bytes(T, Lp));
   LdsTable t;
   t.acc = reinterpret_cast<double*>(base);
   t.keys = reinterpret_cast<int*>(base + (size_t)T * 8);
   t.mask = (uint32_t)T - 1;
   t.nbits = 31 - __clz(T);
-  uint64_t* rv = reinterpret_cast<uint64_t*>(base + (size_t)T * 12);
-  int* rk = reinterpret_cast<int*>(base + (size_t)T * 12 + (size_t)Lp * 8);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 12 + (size_t)Lp * 12);
-  int* hk = reinterpret_cast<int*>(base + (size_t)T * 12 + (size_t)Lp * 12 + 1024);
+  uint8_t* own = base + (size_t)T * 12;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(base + (size_t)T * 13);  // (T: a multiple of 64)
+  uint64_t* rv = reinterpret_cast<uint64_t*>(base + (size_t)T * 13 + 1024);
+  int* rk = reinterpret_cast<int*>(base + (size_t)T * 13 + 1024 + (size_t)Lp * 8);
+  int* hk = reinterpret_cast<int*>(base + (size_t)T * 13 + 1024 + (size_t)Lp * 12);
   int* hv = hk + 2 * Lp;
   int* mf = hv + 2 * Lp;
-  uint8_t* own = reinterpret_cast<uint8_t*>(mf + Lp);
 
   const int v = list[w];
   const int64_t b = g.rp[v], e = g.rp[v + 1];
@@ -404,8 +442,11 @@ __global__ void __launch_bounds__(256) k_merge_lds(DevGraph g, DevSlab s, IterAr
   const int U = table_compact_min(t, tau);
   const int* keys = t.keys;
   const double* acc = t.acc;
-  finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, s, a, hist,
-                rv, rk, Lp, hk, hv, mf, maxdiff, stats);
+  if (kSplit)
+    wave_emit_list(wl, w, U, keys, acc, v, (int)s.L, hist);
+  else
+    finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return acc[i]; }, s, a, hist,
+                  rv, rk, Lp, hk, hv, mf, maxdiff, stats);
 }
 
 }  // namespace pprk

@@ -162,12 +162,7 @@ __host__ __device__ constexpr size_t lds_wave_bytes_xs(int T) { return (size_t)T
 // HBM; k_wfin (below) then selects, writes the row and its norm1 with one 5-KB wave per source. A
 // 2048-slot table costs 38 KB of LDS per wave: holding it through the select, the row write and
 // norm1 (more than half of the wave's time, PPR_DIAG) kept the tier at 4 waves per CU.
-struct WList {
-  int32_t* k;  // [count * cap] keys
-  double* v;   // [count * cap] values
-  int32_t* n;  // [count] entries (-1: the table ran out, the host redoes the source)
-  int cap;     // 0: no split; else >= L
-};
+// (WList, wave_emit_list: merge_wave.h)
 
 // (a table that runs out -- never, at T >= 4/3 of the tier's candidate cap, unless PPR_WAVE_TDIV
 // shrinks it for the tests -- writes no row: the source goes to `wovl` ([0] count, then sources)
@@ -293,28 +288,7 @@ __global__ void __launch_bounds__(256, kSplit ? PPR_WX_WAVES : 1) k_merge_lds_x(
   fs_lap(a, 280, 2, tl);  // (slot 282: settle + compact)
   if (a.diag && !a.unit && lane_id() == 0) { diag_add(a.diag, 280, 1ull); diag_add(a.diag, 287, (unsigned long long)U); }
   if (kSplit) {  // the list for k_wfin: every kept entry, or the top-L of more than cap (cap >= L)
-    U = __builtin_amdgcn_readfirstlane(U);
-    const int64_t o = w * (int64_t)wl.cap;
-    if (U <= wl.cap) {
-      for (int i = lane_id(); i < U; i += WAVE) { wl.k[o + i] = keys[i]; wl.v[o + i] = vals[i]; }
-      if (lane_id() == 0) wl.n[w] = U;
-      return;
-    }
-    const uint32_t ts = tie_salt(v);
-    const SelCrit c = select_top(U, (int)s.L, [&](int i) { return keys[i]; }, [&](int i) { return vals[i]; }, hist, ts);
-    int nb = 0;
-    for (int i0 = 0; i0 < U; i0 += WAVE) {
-      const int i = i0 + lane_id();
-      const bool sel = i < U && sel_test(c, dbits(vals[i]), tie_w(keys[i], ts));
-      const uint64_t m = __ballot(sel);
-      if (sel) {
-        const int64_t q = o + nb + __popcll(m & lanemask_lt());
-        wl.k[q] = keys[i];
-        wl.v[q] = vals[i];
-      }
-      nb += __popcll(m);
-    }
-    if (lane_id() == 0) wl.n[w] = nb;
+    wave_emit_list(wl, w, U, keys, vals, v, (int)s.L, hist);
   } else {
     finish_source(v, U, [&](int i) { return keys[i]; }, [&](int i) { return vals[i]; }, s, a, hist, rv, rk, Lp, hk, hv,
                   mf, maxdiff, stats, a.unit ? -1 : 283);  // (283 select, 284 row write, 285 norm1)

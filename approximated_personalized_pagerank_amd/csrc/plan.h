@@ -223,6 +223,9 @@ struct ppr_plan {
   // bounded probes (tests force them to run out): exact wave-tier overflow list and knobs
   int32_t* d_wovl = nullptr;          // [1 + n]: count, sources whose wave-tier table ran out
   int wave_split_T = 256;             // PPR_WAVE_SPLIT: wave tiers with T >= this end in k_wfin (0: none)
+  int wave_split_chain = 256;         // PPR_WAVE_SPLIT_CHAIN: the same for GRank's chain-order wave tiers
+                                      // (round 6: -1.3 % per chain job)
+  int wave_split_mc = 0;              // PPR_WAVE_SPLIT_MC: ... and the MC combine's (+1.6-2 %: off)
   // run_xhubs's per-call host lists, kept across iterations (capacity only): fresh vectors of a
   // few hundred thousand entries each cost the planning their page faults every iteration
   struct XhScratch {

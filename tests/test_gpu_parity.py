@@ -561,3 +561,29 @@ def test_gpu_sieve_pass2_skip_forced(skip, monkeypatch, capfd):
         assert skipped > 0
     else:
         assert skipped == 0
+
+
+@pytest.mark.parametrize("senv", [{"PPR_WAVE_SPLIT_CHAIN": "0"}, {"PPR_WAVE_SPLIT_CHAIN": "256", "PPR_WAVE_SPLIT_MC": "256"},
+                                  {"PPR_WAVE_SPLIT_CHAIN": "256", "PPR_WAVE_SPLIT_MC": "256", "PPR_WAVE_CAP": "1",
+                                   "PPR_WL_MAX_MB": "1"}])
+def test_gpu_chain_wave_split_bit_exact(senv, monkeypatch, chain_sum):
+    """the chain-order wave tiers with and without the split epilogue (k_merge_lds<.., true> + k_wfin,
+    DESIGN.md 3.6; lists capped at L and chunked) equal the oracle's fma chains bit for bit, and the
+    MC combine through the same tiers equals the MC oracle"""
+    for k, v in senv.items():
+        monkeypatch.setenv(k, v)
+    for scale, K, L, it in [(10, 16, 32, 5), (12, 32, 128, 4)]:
+        g = ppr.rmat(scale, seed=55 + scale)
+        part = g.partitions()
+        r = ppr.grank_csr(g, K, L, it, 0.85, -1.0, part=part, device=0)
+        o = oracle.grank(g.row_ptr, g.col, part, K, L, it, 0.85, -1.0)
+        assert np.array_equal(r.max_diff, o["max_diff"])
+        assert np.array_equal(r.ids, o["ids"]) and np.array_equal(r.scores, o["scores"])
+    g = ppr.rmat(11, seed=3)
+    o = oracle.mccp2(g.row_ptr, g.col, 16, 64, 200, 0.85, 7, want_walks=False)
+    plan = ppr.MccpPlan(g, 16, 64, 0.85, device=0)
+    plan.run(200, 7)
+    m = plan.fetch()
+    plan.close()
+    assert np.array_equal(m.ids, o["ids"])
+    assert np.array_equal(m.scores.view(np.int64), o["scores"].view(np.int64))
