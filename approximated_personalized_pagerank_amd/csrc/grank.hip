@@ -2297,9 +2297,13 @@ reclassify:
         }
     }
   }
+#ifndef PPR_WFIN_WPB
+#define PPR_WFIN_WPB 1  // (round 6: one source per block, -0.2 to -0.4 % against 4 in 4 same-box pairs)
+#endif
   auto launch_wfin = [&](const int32_t* tl, int64_t c, const WList& wl) {
-    hipLaunchKernelGGL(k_wfin, dim3((unsigned)((c + 3) / 4)), dim3(256), wfin_lds_bytes(p->Lp) * 4, sw, s, a, tl, c, wl,
-                       p->Lp, maxdiff, p->d_stats);
+    constexpr int wpb = PPR_WFIN_WPB;  // sources (waves) per block
+    hipLaunchKernelGGL(k_wfin, dim3((unsigned)((c + wpb - 1) / wpb)), dim3(64 * wpb), wfin_lds_bytes(p->Lp) * wpb, sw, s,
+                       a, tl, c, wl, p->Lp, maxdiff, p->d_stats);
     p->merge_launches++;
   };
   for (int t = 0; t < NT; t++) {
