@@ -16,6 +16,11 @@ from approximated_personalized_pagerank_amd._lib import PKG_DIR  # noqa: E402
 
 args = sys.argv[1:]
 name = args.pop(0)
+# the walk clears its flag bytes a dword per lane (merge_wave.h hub_window_walk_part): a batch that is
+# not a multiple of 4 groups leaves stale flags and faults the GPU (round 6: PPR_TW_BATCH=6 did)
+for d in args:
+    if d.startswith("PPR_TW_BATCH=") and (int(d.split("=")[1]) % 4 or int(d.split("=")[1]) < 4):
+        sys.exit("PPR_TW_BATCH must be a multiple of 4")
 csrc = None
 if args and args[0] == "--rev":
     rev = args[1]
